@@ -1,0 +1,98 @@
+/* picotron_hip.h -- C ABI of the picotron_amd gfx950 (MI355X) kernels.
+ *
+ * Every entry point takes plain device pointers, element counts / strides (in ELEMENTS, not
+ * bytes) and a hipStream_t, launches asynchronously on that stream, never allocates, and returns
+ * 0 on success, a negative PT_E* code for an argument error detected before launch, or a
+ * positive hipError_t from the launch.  bf16 tensors are passed as raw 16-bit storage.
+ *
+ * Each function names the reference interface it replaces (paths relative to the reference
+ * checkout, okoge-kaz/picotron @ 2025-03-02).  The Python host layer (picotron_amd/_C.py) binds
+ * these with ctypes; INTEGRATION.md shows the binding a picotron maintainer would add.
+ */
+#ifndef PICOTRON_HIP_H
+#define PICOTRON_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* hipStream_t;
+
+#define PT_OK 0
+#define PT_EINVAL (-1)
+#define PT_EALIGN (-2)
+#define PT_EUNSUPPORTED (-3)
+
+/* ---- RMSNorm ------------------------------------------------------------------------------
+ * replaces picotron/model.py:51-65 (TritonRMSNorm -> flash-attn layer_norm_fn, mode 0) and
+ * picotron/model.py:81-86 (LlamaRMSNorm, mode 1); `residual` fuses the bf16 residual add of
+ * picotron/model.py:207-208 (z_out = bf16(x + residual) is normalised and written out).
+ * x, residual, y, z_out: [rows, cols] bf16; weight [cols] bf16; rstd [rows] f32 (saved for bwd). */
+int pt_rmsnorm_fwd(const void* x, const void* residual, const void* weight, void* y, void* z_out, float* rstd,
+                   int64_t rows, int64_t cols, float eps, int mode, hipStream_t stream);
+/* number of f32 rows of `cols` the bwd needs in dw_partial */
+int pt_rmsnorm_bwd_partials(int64_t rows, int cols);
+/* autograd backward of the above: dx = d/dz (+ dres), dweight [cols] bf16 (may be NULL) */
+int pt_rmsnorm_bwd(const void* dy, const void* z, const void* weight, const float* rstd, const void* dres,
+                   void* dx, void* dweight, float* dw_partial, int64_t rows, int64_t cols, int mode,
+                   hipStream_t stream);
+
+/* ---- RoPE (rotate-half, non-interleaved) --------------------------------------------------
+ * replaces picotron/model.py:136-137 (flash-attn apply_rotary_emb) and model.py:12-19
+ * (apply_rotary_pos_emb).  In place on the first `nheads` heads of every row of x
+ * ([rows, row_stride] bf16); row r has position r % seq_len in the [seq_len, table_stride]
+ * cos/sin tables of get_cos_sin (model.py:21-31).  inverse = 1 rotates by -theta (backward). */
+int pt_rope(void* x, int64_t rows, int64_t row_stride, int64_t nheads, int64_t head_dim, const void* cos_table,
+            const void* sin_table, int64_t seq_len, int64_t table_stride, int inverse, hipStream_t stream);
+
+/* ---- SwiGLU: h = silu(g) * u --------------------------------------------------------------
+ * replaces picotron/model.py:186 F.silu(gate_proj(x)) * up_proj(x) (fwd and autograd bwd). */
+int pt_swiglu_fwd(const void* g, int64_t g_stride, const void* u, int64_t u_stride, void* h, int64_t h_stride,
+                  int64_t rows, int64_t cols, hipStream_t stream);
+int pt_swiglu_bwd(const void* dh, int64_t dh_stride, const void* g, int64_t g_stride, const void* u,
+                  int64_t u_stride, void* dg, int64_t dg_stride, void* du, int64_t du_stride, int64_t rows,
+                  int64_t cols, hipStream_t stream);
+
+/* ---- fused cross-entropy forward + backward -----------------------------------------------
+ * replaces train.py:49 F.cross_entropy(logits, targets, 'mean') / grad_acc (+ autograd bwd) and
+ * pipeline_parallel.py:103,153.  row_loss[r] = lse - logit[target]; dlogits (may alias logits) =
+ * (softmax - onehot) * scale * (*inv_count if non-NULL).  targets int64, ignore_index rows -> 0. */
+int pt_cross_entropy_fwd_bwd(const void* logits, int64_t logits_stride, const int64_t* targets, void* dlogits,
+                             int64_t dlogits_stride, float* row_loss, int64_t rows, int64_t vocab, float scale,
+                             const float* inv_count, int64_t ignore_index, hipStream_t stream);
+
+/* ---- bf16 GEMM, f32 accumulate -------------------------------------------------------------
+ * replaces every F.linear / matmul of the layer: model.py:124-126,161,186,270,
+ * tensor_parallel.py:186, tp_communications.py:79,93,98,105.
+ * C[M,N] (op)= A[M,K] B[K,N].  a_kcontig: A stored [M,K] (else [K,M]); b_kcontig: B stored
+ * [N,K] (weights; else [K,N]).  B may be split into nb pointer segments along N (b_seg_dim 0)
+ * or K (1), C into nc segments along M; *_bounds hold n+1 boundaries (NULL = one segment).
+ * epilogue 0: C bf16 = acc, 1: C bf16 += acc, 2: C f32 = acc, 3: C f32 += acc.  tile -1 = auto. */
+int pt_gemm(const void* A, int64_t lda, int a_kcontig, const void* const* B, const int64_t* ldb,
+            const int64_t* b_bounds, int nb, int b_kcontig, int b_seg_dim, void* const* C, const int64_t* ldc,
+            const int64_t* c_bounds, int nc, int64_t M, int64_t N, int64_t K, int epilogue, int tile,
+            hipStream_t stream);
+int pt_gemm_pick_tile(int64_t M, int64_t N, const int64_t* mseg, int nmseg, const int64_t* nseg, int nnseg);
+
+/* ---- flash attention ----------------------------------------------------------------------
+ * replaces model.py:33-37,154 flash_attn_func(causal=True) / model.py:157 SDPA, and the ring
+ * blocks context_parallel.py:112-155 with update_out_and_lse (:157-187) fused (merge = 1).
+ * q/k/v/o/dout/dq/dk/dv: token-major [B, S, H, D] views given as base + 3 strides
+ * {batch, seq, head} (elements; d contiguous).  lse, delta: f32 [B, H, Sq].  D in {64, 128},
+ * Sq % 128 == 0, Sk % 64 == 0 (bwd: Sk % 128 == 0).  causal: key j visible to query i iff j <= i. */
+int pt_attn_fwd(const void* q, const int64_t* q_str, const void* k, const int64_t* k_str, const void* v,
+                const int64_t* v_str, void* o, const int64_t* o_str, float* lse, int64_t B, int64_t H, int64_t HKV,
+                int64_t Sq, int64_t Sk, int64_t D, float scale, int causal, int merge, hipStream_t stream);
+int pt_attn_bwd_delta(const void* dout, const int64_t* do_str, const void* o, const int64_t* o_str, float* delta,
+                      int64_t B, int64_t H, int64_t Sq, int64_t D, hipStream_t stream);
+int pt_attn_bwd(const void* q, const int64_t* q_str, const void* k, const int64_t* k_str, const void* v,
+                const int64_t* v_str, const void* dout, const int64_t* do_str, const float* lse, const float* delta,
+                void* dq, const int64_t* dq_str, void* dk, const int64_t* dk_str, void* dv, const int64_t* dv_str,
+                int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int64_t D, float scale, int causal,
+                int grad_f32, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PICOTRON_HIP_H */

@@ -1,0 +1,92 @@
+"""ctypes binding of the C ABI in include/picotron_hip.h (libpicotron_hip.so, built in-tree).
+
+There is deliberately no fallback: if the library is missing, or no HIP device is visible,
+every op raises.  torch must be imported (and its HIP runtime initialised) before the library is
+loaded so that both share one runtime (see build.py).
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libpicotron_hip.so")
+
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int
+_f32 = ctypes.c_float
+_vp = ctypes.c_void_p
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_vpp = ctypes.POINTER(ctypes.c_void_p)
+
+# name -> (restype, argtypes); mirrors include/picotron_hip.h one to one
+SIGNATURES = {
+    "pt_rmsnorm_fwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _f32, _i32, _vp]),
+    "pt_rmsnorm_bwd_partials": (_i32, [_i64, _i32]),
+    "pt_rmsnorm_bwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp]),
+    "pt_rope": (_i32, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _i32, _vp]),
+    "pt_swiglu_fwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp]),
+    "pt_swiglu_bwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp]),
+    "pt_cross_entropy_fwd_bwd": (_i32, [_vp, _i64, _vp, _vp, _i64, _vp, _i64, _i64, _f32, _vp, _i64, _vp]),
+    "pt_gemm": (_i32, [_vp, _i64, _i32, _vpp, _i64p, _i64p, _i32, _i32, _i32, _vpp, _i64p, _i64p, _i32,
+                       _i64, _i64, _i64, _i32, _i32, _vp]),
+    "pt_gemm_pick_tile": (_i32, [_i64, _i64, _i64p, _i32, _i64p, _i32]),
+    "pt_attn_fwd": (_i32, [_vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _i64, _i64, _i64, _i64, _i64,
+                           _i64, _f32, _i32, _i32, _vp]),
+    "pt_attn_bwd_delta": (_i32, [_vp, _i64p, _vp, _i64p, _vp, _i64, _i64, _i64, _i64, _vp]),
+    "pt_attn_bwd": (_i32, [_vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _vp, _vp, _i64p, _vp, _i64p,
+                           _vp, _i64p, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _i32, _i32, _vp]),
+}
+
+ERRORS = {-1: "PT_EINVAL (bad size or null pointer)", -2: "PT_EALIGN (misaligned pointer/stride)",
+          -3: "PT_EUNSUPPORTED (shape outside the kernel's tiling)"}
+
+_lib = None
+
+
+class HipKernelError(RuntimeError):
+    pass
+
+
+def load_library(path=LIB_PATH):
+    """dlopen the kernel library and bind every symbol; does not touch the GPU."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise HipKernelError(f"picotron_amd HIP library not built: {path} (run python -m picotron_amd.build)")
+    import torch  # noqa: F401  -- its HIP runtime must be the one our SONAME binds to
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def lib():
+    """The bound library, for compute calls: requires a visible HIP device."""
+    if _lib is None:
+        load_library()
+    if not torch.cuda.is_available():
+        raise HipKernelError("picotron_amd kernels need a HIP device (MI355X / gfx950); none is visible")
+    return _lib
+
+
+def check(rc, name):
+    if rc != 0:
+        msg = ERRORS.get(rc, f"hipError {rc}")
+        raise HipKernelError(f"{name} failed: {msg}")
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def i64arr(vals):
+    return (ctypes.c_int64 * len(vals))(*[int(v) for v in vals])
+
+
+def ptrarr(vals):
+    return (ctypes.c_void_p * len(vals))(*[int(v) for v in vals])

@@ -1,0 +1,611 @@
+// Flash attention forward / backward for gfx950 (MFMA 32x32x16 bf16, f32 softmax), with the
+// ring-attention LSE merge fused into the forward epilogue.
+//
+// Replaces (reference, /root/reference):
+//   * picotron/model.py:33-37,154   flash_attention -> flash_attn_func(q, k, v, causal=True)  (fwd + FA2 bwd)
+//   * picotron/model.py:157         F.scaled_dot_product_attention(q, k, v, is_causal=True)   (FLASH_ATTEN=0)
+//   * picotron/context_parallel/context_parallel.py:112-128  ring_attention_forward (block attention + LSE)
+//   * context_parallel.py:130-155   ring_attention_backward (block bwd from the global out/LSE)
+//   * context_parallel.py:157-187   update_out_and_lse (fused: merge=1 epilogue)
+//   * model.py:142-143              repeat_interleave for GQA (elided: kv head = q head / group)
+//
+// Layout: q/k/v/o are token-major [B, S, H, D] strided views (d contiguous), e.g. slices of the
+// fused [T, (h + 2*hkv) * D] projection output -- no transposes, no copies.  lse is f32 [B, H, Sq].
+// mask: 0 = full, 1 = causal (key j visible to query i iff j <= i; Sq == Sk).
+//
+// Fragment scheme (all v_mfma_f32_32x32x16_bf16): scores are computed "key on the row",
+// S^T = K . Q^T, so a lane owns one query column and softmax statistics are lane-local (plus one
+// lane^32 exchange).  The S^T / dS^T accumulators are re-used directly as the B operand of the
+// next product (O^T += V^T P^T, dQ^T += K^T dS^T); the matching A operands come from
+// ds_read_b64_tr_b16 transposed reads of the row-major K/V tiles.  The dK/dV kernel uses the
+// mirror scheme (S = Q . K^T, key on the lane) so dV^T += dO^T P and dK^T += Q^T dS take their
+// B operands from accumulators as well.  One LDS image per tile serves both the row reads and
+// the transposed reads (XOR swizzle from tools/lds_swizzle_search.py, conflict-free for both).
+// K/V (fwd, dq) and Q/dO (dkdv) tiles arrive by global_load_lds_dwordx4 into a 2-deep ring.
+#include "common.h"
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short short4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+
+namespace {
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+constexpr int KT = 64;  // rows per staged K/V (or Q/dO) tile
+constexpr int NW = 4;   // waves per workgroup, 32 rows each
+
+struct AttnArgs {
+  const uint16_t* q; int64_t q_sb, q_ss, q_sh;
+  const uint16_t* k; int64_t k_sb, k_ss, k_sh;
+  const uint16_t* v; int64_t v_sb, v_ss, v_sh;
+  void* o; int64_t o_sb, o_ss, o_sh;            // bf16 output, or f32 accumulator when merge
+  float* lse;                                    // [B, H, Sq]
+  const uint16_t* dout; int64_t do_sb, do_ss, do_sh;
+  const float* delta;                            // [B, H, Sq] rowsum(dO * O)
+  void* dq; int64_t dq_sb, dq_ss, dq_sh;
+  void* dk; int64_t dk_sb, dk_ss, dk_sh;
+  void* dv; int64_t dv_sb, dv_ss, dv_sh;
+  int B, H, HKV, Sq, Sk;
+  float scale;
+  int causal;
+  int merge;      // fwd: merge into (o f32, lse) accumulators
+  int grad_f32;   // bwd: dq/dk/dv are f32 accumulators (+=) instead of bf16 stores
+};
+
+template <int D>
+__device__ __forceinline__ int aswz(int r) {
+  if (D == 64) return (((r >> 1) & 1) << 2) | ((r >> 3) & 1) | (((r >> 4) & 1) << 1);
+  return ((r & 1) << 2) | (((r >> 1) & 1) << 3) | ((r >> 3) & 1) | (((r >> 4) & 1) << 1);
+}
+
+__device__ __forceinline__ void glds16(const void* gsrc, lds_u8* lds_base) {
+  __builtin_amdgcn_global_load_lds(gsrc, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+// stage a [KT][D] bf16 tile (rows `row_stride` elements apart) into a swizzled LDS image
+template <int D>
+__device__ __forceinline__ void stage_rows(const uint16_t* __restrict__ g, int64_t row_stride, lds_u8* dst,
+                                           int wave, int lane) {
+  constexpr int RB = D * 2, RC = RB / 16, RPI = 1024 / RB;  // rows per 1 KiB wave instruction
+  constexpr int NI = KT * RB / 1024;
+#pragma unroll
+  for (int it = 0; it < NI / NW; ++it) {
+    const int i = it * NW + wave;
+    const int r = i * RPI + lane / RC, c = lane % RC;
+    glds16(g + (int64_t)r * row_stride + 8 * (c ^ aswz<D>(r)), dst + i * 1024);
+  }
+}
+
+// A operand (rows of the tile): lane -> row row0 + (lane & 31), k = 16 ks + 8 (lane >> 5) + j
+template <int D>
+__device__ __forceinline__ bf16x8_t rd_row(const lds_u8* t, int row0, int ks, int lane) {
+  const int r = row0 + (lane & 31), ch = 2 * ks + (lane >> 5);
+  return *(const __attribute__((address_space(3))) bf16x8_t*)(t + r * (D * 2) + 16 * (ch ^ aswz<D>(r)));
+}
+
+// A operand X^T (sum over tile rows) for 16-row step s and 32-column tile dt:
+// element j <-> tile row 16 s + 8 (j >> 2) + 4 (lane >> 5) + (j & 3), column 32 dt + (lane & 31)
+template <int D>
+__device__ __forceinline__ bf16x8_t rd_tr(const lds_u8* t, int s, int dt, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int col = 32 * dt + 16 * (g & 1) + 4 * p;
+  bf16x8_t out;
+#pragma unroll
+  for (int sec = 0; sec < 2; ++sec) {
+    const int r = 16 * s + 8 * sec + 4 * (g >> 1) + q;
+    const int off = r * (D * 2) + 16 * ((col >> 3) ^ aswz<D>(r)) + 8 * ((col >> 2) & 1);
+    short4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(t + off));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) out[4 * sec + j] = __builtin_bit_cast(__bf16, v[j]);
+  }
+  return out;
+}
+
+// B operand from a C-layout 32x32 accumulator, k-step s (rows 16 s .. 16 s + 15)
+__device__ __forceinline__ bf16x8_t acc_as_b(const f32x16_t& x, int s) {
+  bf16x8_t out;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[j] = (__bf16)x[8 * s + j];
+  return out;
+}
+
+// B operand straight from a global row: lane -> row (lane & 31) of `base`, k = 16 ks + 8 (lane >> 5) + j
+__device__ __forceinline__ bf16x8_t ld_row_frag(const uint16_t* row_ptr, int ks, int lane) {
+  return *(const bf16x8_t*)(row_ptr + 16 * ks + 8 * (lane >> 5));
+}
+
+// C layout row index of register r for this lane
+__device__ __forceinline__ int crow(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+__device__ __forceinline__ f32x16_t zero16() {
+  f32x16_t z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+__device__ __forceinline__ f32x16_t mfma(const bf16x8_t& a, const bf16x8_t& b, const f32x16_t& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// store a 32(d) x 32(row) C-layout tile transposed into row-major memory: lane owns row
+// (lane & 31), d = 32 dt + crow(r); 4 consecutive d per 8-byte store
+__device__ __forceinline__ void store_T_bf16(uint16_t* row_ptr, int dt, const f32x16_t& x, float mul, int lane) {
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4) {
+    const int d = 32 * dt + 8 * g4 + 4 * (lane >> 5);
+    uint2 w;
+    w.x = pack_bf2(x[4 * g4 + 0] * mul, x[4 * g4 + 1] * mul);
+    w.y = pack_bf2(x[4 * g4 + 2] * mul, x[4 * g4 + 3] * mul);
+    *(uint2*)(row_ptr + d) = w;
+  }
+}
+__device__ __forceinline__ void accum_T_f32(float* row_ptr, int dt, const f32x16_t& x, float mul, int lane) {
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4) {
+    const int d = 32 * dt + 8 * g4 + 4 * (lane >> 5);
+    float4 o = *(float4*)(row_ptr + d);
+    o.x += x[4 * g4 + 0] * mul; o.y += x[4 * g4 + 1] * mul;
+    o.z += x[4 * g4 + 2] * mul; o.w += x[4 * g4 + 3] * mul;
+    *(float4*)(row_ptr + d) = o;
+  }
+}
+
+// ============================================================================ forward
+template <int D>
+__global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
+  constexpr int DT = D / 32, KS = D / 16;
+  constexpr int TILE_B = KT * D * 2;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+  lds_u8* smem = (lds_u8*)smem_raw;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nqb = a.Sq / (NW * 32);
+  const int qb = a.causal ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;  // heavy blocks first
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int hk = h / (a.H / a.HKV);
+  const int q0 = qb * NW * 32 + wave * 32;
+  const int myq = q0 + (lane & 31);
+
+  const uint16_t* qrow = a.q + b * a.q_sb + (int64_t)myq * a.q_ss + h * a.q_sh;
+  bf16x8_t qf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) qf[ks] = ld_row_frag(qrow, ks, lane);
+
+  const uint16_t* kbase = a.k + b * a.k_sb + hk * a.k_sh;
+  const uint16_t* vbase = a.v + b * a.v_sb + hk * a.v_sh;
+  const int kv_end = a.causal ? (qb + 1) * NW * 32 : a.Sk;
+  const int nkt = kv_end / KT;
+  const float c2 = a.scale * kLog2e;
+
+  f32x16_t o[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) o[i] = zero16();
+  float m = -INFINITY, l = 0.f;
+
+  auto stage = [&](int kt, int buf) {
+    lds_u8* sk = smem + buf * 2 * TILE_B;
+    stage_rows<D>(kbase + (int64_t)kt * KT * a.k_ss, a.k_ss, sk, wave, lane);
+    stage_rows<D>(vbase + (int64_t)kt * KT * a.v_ss, a.v_ss, sk + TILE_B, wave, lane);
+  };
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nkt) stage(kt + 1, buf ^ 1);
+    const lds_u8* sk = smem + buf * 2 * TILE_B;
+    const lds_u8* sv = sk + TILE_B;
+    const int kv0 = kt * KT;
+    if (!a.causal || kv0 <= q0 + 31) {  // wave-uniform: skip tiles fully above the diagonal
+      f32x16_t s[2];
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        s[kh] = zero16();
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) s[kh] = mfma(rd_row<D>(sk, 32 * kh, ks, lane), qf[ks], s[kh]);
+      }
+      const bool diag = a.causal && (kv0 + KT - 1 > q0);
+      float mt = -INFINITY;
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float x = s[kh][r] * c2;
+          if (diag && kv0 + 32 * kh + crow(r, lane) > myq) x = -INFINITY;
+          s[kh][r] = x;
+          mt = fmaxf(mt, x);
+        }
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float mn = fmaxf(m, mt);
+      const float alpha = exp2f(m - mn);
+      m = mn;
+      float ls = 0.f;
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = exp2f(s[kh][r] - mn);
+          s[kh][r] = p;
+          ls += p;
+        }
+      l = l * alpha + ls;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const bf16x8_t pb = acc_as_b(s[st >> 1], st & 1);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) o[dt] = mfma(rd_tr<D>(sv, st, dt, lane), pb, o[dt]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  l += __shfl_xor(l, 32, 64);
+  const float inv_l = 1.0f / l;
+  const float lse = m * kLn2 + __logf(l);
+  float* lse_p = a.lse + ((int64_t)b * a.H + h) * a.Sq + myq;
+  if (!a.merge) {
+    uint16_t* orow = (uint16_t*)a.o + b * a.o_sb + (int64_t)myq * a.o_ss + h * a.o_sh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) store_T_bf16(orow, dt, o[dt], inv_l, lane);
+    if (lane < 32) *lse_p = lse;
+  } else {
+    // update_out_and_lse: out <- out*exp(lse_old - lse_new) + blk*exp(lse_blk - lse_new)
+    float* orow = (float*)a.o + b * a.o_sb + (int64_t)myq * a.o_ss + h * a.o_sh;
+    const float lold = *lse_p;
+    const float lnew = fmaxf(lold, lse) + log1pf(__expf(-fabsf(lold - lse)));
+    const float wold = lold == -INFINITY ? 0.f : __expf(lold - lnew);
+    const float wblk = __expf(lse - lnew) * inv_l;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = 32 * dt + 8 * g4 + 4 * (lane >> 5);
+        float4 ov = *(float4*)(orow + d);
+        ov.x = ov.x * wold + o[dt][4 * g4 + 0] * wblk;
+        ov.y = ov.y * wold + o[dt][4 * g4 + 1] * wblk;
+        ov.z = ov.z * wold + o[dt][4 * g4 + 2] * wblk;
+        ov.w = ov.w * wold + o[dt][4 * g4 + 3] * wblk;
+        *(float4*)(orow + d) = ov;
+      }
+    __syncthreads();  // both lane halves have read lse_old before it is overwritten
+    if (lane < 32) *lse_p = lnew;
+  }
+}
+
+// ======================================================================= delta = rowsum(dO * O)
+// one thread per (b, h, q) row; d in 16-byte chunks.  D is passed in a.dq_sh.
+__global__ __launch_bounds__(256) void attn_delta_kernel(AttnArgs a, const uint16_t* __restrict__ o) {
+  const int64_t total = (int64_t)a.B * a.H * a.Sq;
+  const int Dh = (int)a.dq_sh;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int qq = (int)(i % a.Sq);
+    const int h = (int)((i / a.Sq) % a.H);
+    const int b = (int)(i / ((int64_t)a.Sq * a.H));
+    const uint16_t* dr = a.dout + b * a.do_sb + (int64_t)qq * a.do_ss + h * a.do_sh;
+    const uint16_t* orow = o + b * a.o_sb + (int64_t)qq * a.o_ss + h * a.o_sh;
+    float acc = 0.f;
+    for (int d = 0; d < Dh; d += 8) {
+      float x[8], y[8];
+      unpack8(ld8(dr + d), x);
+      unpack8(ld8(orow + d), y);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += x[j] * y[j];
+    }
+    a.lse[i] = acc;  // the delta buffer travels in the lse slot
+  }
+}
+
+// ============================================================================ dK / dV
+template <int D>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv_kernel(AttnArgs a) {
+  constexpr int DT = D / 32, KS = D / 16;
+  constexpr int TILE_B = KT * D * 2;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+  lds_u8* smem = (lds_u8*)smem_raw;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kb = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  const int k0 = kb * NW * 32 + wave * 32;
+  const int mykey = k0 + (lane & 31);
+  const int group = a.H / a.HKV;
+
+  const uint16_t* krow = a.k + b * a.k_sb + (int64_t)mykey * a.k_ss + hk * a.k_sh;
+  const uint16_t* vrow = a.v + b * a.v_sb + (int64_t)mykey * a.v_ss + hk * a.v_sh;
+  bf16x8_t kf[KS], vf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    kf[ks] = ld_row_frag(krow, ks, lane);
+    vf[ks] = ld_row_frag(vrow, ks, lane);
+  }
+  f32x16_t dk[DT], dv[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) { dk[i] = zero16(); dv[i] = zero16(); }
+  const float c2 = a.scale * kLog2e;
+
+  // q tiles: causal -> only those that can see this block's keys
+  const int qt_begin = a.causal ? (kb * NW * 32) / KT : 0;
+  const int nqt = a.Sq / KT;
+  const int n_iter = (nqt - qt_begin) * group;
+  // LDS: 2 x {Q tile, dO tile, lse[64], delta[64]}
+  constexpr int STAGE_B = 2 * TILE_B + 2 * KT * 4;
+
+  auto stage = [&](int it, int buf) {
+    const int hq = hk * group + it / (nqt - qt_begin);
+    const int qt = qt_begin + it % (nqt - qt_begin);
+    lds_u8* sq = smem + buf * STAGE_B;
+    stage_rows<D>(a.q + b * a.q_sb + (int64_t)qt * KT * a.q_ss + hq * a.q_sh, a.q_ss, sq, wave, lane);
+    stage_rows<D>(a.dout + b * a.do_sb + (int64_t)qt * KT * a.do_ss + hq * a.do_sh, a.do_ss, sq + TILE_B, wave, lane);
+    if (wave == 0) {  // 64 lse + 64 delta floats = 2 x 256 B: one 4-byte DMA per lane each
+      const int64_t ro = ((int64_t)b * a.H + hq) * a.Sq + qt * KT;
+      __builtin_amdgcn_global_load_lds(a.lse + ro + lane, (__attribute__((address_space(3))) void*)(sq + 2 * TILE_B), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds(a.delta + ro + lane, (__attribute__((address_space(3))) void*)(sq + 2 * TILE_B + KT * 4), 4, 0, 0);
+    }
+  };
+  if (n_iter > 0) stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int it = 0; it < n_iter; ++it) {
+    const int buf = it & 1;
+    if (it + 1 < n_iter) stage(it + 1, buf ^ 1);
+    const int qt = qt_begin + it % (nqt - qt_begin);
+    const lds_u8* sq = smem + buf * STAGE_B;
+    const lds_u8* sdo = sq + TILE_B;
+    const float* slse = (const float*)(sq + 2 * TILE_B);
+    const float* sdel = slse + KT;
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      const int qs = qt * KT + 32 * qh;
+      if (a.causal && qs + 31 < k0) continue;  // wave-uniform: all these queries precede my keys
+      // S = Q K^T and dP = dO V^T  (C layout: col = key = lane, row = query)
+      f32x16_t s = zero16(), dp = zero16();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        s = mfma(rd_row<D>(sq, 32 * qh, ks, lane), kf[ks], s);
+        dp = mfma(rd_row<D>(sdo, 32 * qh, ks, lane), vf[ks], dp);
+      }
+      const bool diag = a.causal && (qs < k0 + 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qi = 32 * qh + crow(r, lane);
+        float p = exp2f(s[r] * c2 - slse[qi] * kLog2e);
+        if (diag && mykey > qt * KT + qi) p = 0.f;
+        s[r] = p;                             // P
+        dp[r] = p * (dp[r] - sdel[qi]);       // dS
+      }
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const bf16x8_t pb = acc_as_b(s, st), db = acc_as_b(dp, st);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          dv[dt] = mfma(rd_tr<D>(sdo, 2 * qh + st, dt, lane), pb, dv[dt]);
+          dk[dt] = mfma(rd_tr<D>(sq, 2 * qh + st, dt, lane), db, dk[dt]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  if (!a.grad_f32) {
+    uint16_t* dkr = (uint16_t*)a.dk + b * a.dk_sb + (int64_t)mykey * a.dk_ss + hk * a.dk_sh;
+    uint16_t* dvr = (uint16_t*)a.dv + b * a.dv_sb + (int64_t)mykey * a.dv_ss + hk * a.dv_sh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      store_T_bf16(dkr, dt, dk[dt], a.scale, lane);
+      store_T_bf16(dvr, dt, dv[dt], 1.0f, lane);
+    }
+  } else {
+    float* dkr = (float*)a.dk + b * a.dk_sb + (int64_t)mykey * a.dk_ss + hk * a.dk_sh;
+    float* dvr = (float*)a.dv + b * a.dv_sb + (int64_t)mykey * a.dv_ss + hk * a.dv_sh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      accum_T_f32(dkr, dt, dk[dt], a.scale, lane);
+      accum_T_f32(dvr, dt, dv[dt], 1.0f, lane);
+    }
+  }
+}
+
+// ============================================================================ dQ
+template <int D>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnArgs a) {
+  constexpr int DT = D / 32, KS = D / 16;
+  constexpr int TILE_B = KT * D * 2;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+  lds_u8* smem = (lds_u8*)smem_raw;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nqb = a.Sq / (NW * 32);
+  const int qb = a.causal ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int hk = h / (a.H / a.HKV);
+  const int q0 = qb * NW * 32 + wave * 32;
+  const int myq = q0 + (lane & 31);
+
+  const uint16_t* qrow = a.q + b * a.q_sb + (int64_t)myq * a.q_ss + h * a.q_sh;
+  const uint16_t* dorow = a.dout + b * a.do_sb + (int64_t)myq * a.do_ss + h * a.do_sh;
+  bf16x8_t qf[KS], dof[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    qf[ks] = ld_row_frag(qrow, ks, lane);
+    dof[ks] = ld_row_frag(dorow, ks, lane);
+  }
+  const int64_t ri = ((int64_t)b * a.H + h) * a.Sq + myq;
+  const float lse2 = a.lse[ri] * kLog2e;
+  const float del = a.delta[ri];
+  const float c2 = a.scale * kLog2e;
+
+  const uint16_t* kbase = a.k + b * a.k_sb + hk * a.k_sh;
+  const uint16_t* vbase = a.v + b * a.v_sb + hk * a.v_sh;
+  const int kv_end = a.causal ? (qb + 1) * NW * 32 : a.Sk;
+  const int nkt = kv_end / KT;
+  f32x16_t dq[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) dq[i] = zero16();
+
+  auto stage = [&](int kt, int buf) {
+    lds_u8* sk = smem + buf * 2 * TILE_B;
+    stage_rows<D>(kbase + (int64_t)kt * KT * a.k_ss, a.k_ss, sk, wave, lane);
+    stage_rows<D>(vbase + (int64_t)kt * KT * a.v_ss, a.v_ss, sk + TILE_B, wave, lane);
+  };
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nkt) stage(kt + 1, buf ^ 1);
+    const lds_u8* sk = smem + buf * 2 * TILE_B;
+    const lds_u8* sv = sk + TILE_B;
+    const int kv0 = kt * KT;
+    if (!a.causal || kv0 <= q0 + 31) {
+      const bool diag = a.causal && (kv0 + KT - 1 > q0);
+      f32x16_t ds[2];
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        f32x16_t s = zero16(), dp = zero16();
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          s = mfma(rd_row<D>(sk, 32 * kh, ks, lane), qf[ks], s);
+          dp = mfma(rd_row<D>(sv, 32 * kh, ks, lane), dof[ks], dp);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float p = exp2f(s[r] * c2 - lse2);
+          if (diag && kv0 + 32 * kh + crow(r, lane) > myq) p = 0.f;
+          s[r] = p * (dp[r] - del);
+        }
+        ds[kh] = s;
+      }
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const bf16x8_t db = acc_as_b(ds[st >> 1], st & 1);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) dq[dt] = mfma(rd_tr<D>(sk, st, dt, lane), db, dq[dt]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  if (!a.grad_f32) {
+    uint16_t* dqr = (uint16_t*)a.dq + b * a.dq_sb + (int64_t)myq * a.dq_ss + h * a.dq_sh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) store_T_bf16(dqr, dt, dq[dt], a.scale, lane);
+  } else {
+    float* dqr = (float*)a.dq + b * a.dq_sb + (int64_t)myq * a.dq_ss + h * a.dq_sh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) accum_T_f32(dqr, dt, dq[dt], a.scale, lane);
+  }
+}
+
+template <typename K>
+void set_smem(K kern, int bytes) {
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
+int check_common(const AttnArgs& a, int D) {
+  if (D != 64 && D != 128) return PT_EUNSUPPORTED;
+  if (a.B <= 0 || a.H <= 0 || a.HKV <= 0 || a.H % a.HKV) return PT_EINVAL;
+  if (a.Sq % (NW * 32) || a.Sk % KT) return PT_EUNSUPPORTED;
+  if (a.causal && a.Sq != a.Sk) return PT_EUNSUPPORTED;
+  return PT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// q/k/v/o: base pointer + (batch, seq, head) strides in elements; d contiguous.
+// merge = 0: o is bf16, lse written.  merge = 1: o is an f32 accumulator and lse holds the running
+// LSE (initialise o = 0, lse = -inf); this block's result is merged in (update_out_and_lse).
+int pt_attn_fwd(const void* q, const int64_t* q_str, const void* k, const int64_t* k_str, const void* v,
+                const int64_t* v_str, void* o, const int64_t* o_str, float* lse, int64_t B, int64_t H, int64_t HKV,
+                int64_t Sq, int64_t Sk, int64_t D, float scale, int causal, int merge, hipStream_t stream) {
+  if (!q || !k || !v || !o || !lse) return PT_EINVAL;
+  AttnArgs a{};
+  a.q = (const uint16_t*)q; a.q_sb = q_str[0]; a.q_ss = q_str[1]; a.q_sh = q_str[2];
+  a.k = (const uint16_t*)k; a.k_sb = k_str[0]; a.k_ss = k_str[1]; a.k_sh = k_str[2];
+  a.v = (const uint16_t*)v; a.v_sb = v_str[0]; a.v_ss = v_str[1]; a.v_sh = v_str[2];
+  a.o = o; a.o_sb = o_str[0]; a.o_ss = o_str[1]; a.o_sh = o_str[2];
+  a.lse = lse;
+  a.B = (int)B; a.H = (int)H; a.HKV = (int)HKV; a.Sq = (int)Sq; a.Sk = (int)Sk;
+  a.scale = scale; a.causal = causal; a.merge = merge;
+  int rc = check_common(a, (int)D);
+  if (rc) return rc;
+  const dim3 grid((unsigned)(Sq / (NW * 32)), (unsigned)H, (unsigned)B);
+  const int smem = 2 * 2 * KT * (int)D * 2;
+  if (D == 64) { set_smem(attn_fwd_kernel<64>, smem); attn_fwd_kernel<64><<<grid, NW * 64, smem, stream>>>(a); }
+  else { set_smem(attn_fwd_kernel<128>, smem); attn_fwd_kernel<128><<<grid, NW * 64, smem, stream>>>(a); }
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
+
+// delta[b, h, q] = sum_d dO * O   (f32, [B, H, Sq])
+int pt_attn_bwd_delta(const void* dout, const int64_t* do_str, const void* o, const int64_t* o_str, float* delta,
+                      int64_t B, int64_t H, int64_t Sq, int64_t D, hipStream_t stream) {
+  if (!dout || !o || !delta || D % 8) return PT_EINVAL;
+  AttnArgs a{};
+  a.dout = (const uint16_t*)dout; a.do_sb = do_str[0]; a.do_ss = do_str[1]; a.do_sh = do_str[2];
+  a.o_sb = o_str[0]; a.o_ss = o_str[1]; a.o_sh = o_str[2];
+  a.lse = delta;
+  a.dq_sh = D;
+  a.B = (int)B; a.H = (int)H; a.Sq = (int)Sq;
+  const int64_t total = B * H * Sq;
+  int64_t g = (total + 255) / 256;
+  if (g > PT_STREAM_GRID_CAP) g = PT_STREAM_GRID_CAP;
+  attn_delta_kernel<<<(int)g, 256, 0, stream>>>(a, (const uint16_t*)o);
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
+
+// Backward from (global) out/lse: dq, dk, dv.  grad_f32 = 1 makes dq/dk/dv f32 accumulators (+=),
+// used by the ring, where blocks of one query/key shard arrive over several steps.
+int pt_attn_bwd(const void* q, const int64_t* q_str, const void* k, const int64_t* k_str, const void* v,
+                const int64_t* v_str, const void* dout, const int64_t* do_str, const float* lse, const float* delta,
+                void* dq, const int64_t* dq_str, void* dk, const int64_t* dk_str, void* dv, const int64_t* dv_str,
+                int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int64_t D, float scale, int causal,
+                int grad_f32, hipStream_t stream) {
+  if (!q || !k || !v || !dout || !lse || !delta || !dq || !dk || !dv) return PT_EINVAL;
+  AttnArgs a{};
+  a.q = (const uint16_t*)q; a.q_sb = q_str[0]; a.q_ss = q_str[1]; a.q_sh = q_str[2];
+  a.k = (const uint16_t*)k; a.k_sb = k_str[0]; a.k_ss = k_str[1]; a.k_sh = k_str[2];
+  a.v = (const uint16_t*)v; a.v_sb = v_str[0]; a.v_ss = v_str[1]; a.v_sh = v_str[2];
+  a.dout = (const uint16_t*)dout; a.do_sb = do_str[0]; a.do_ss = do_str[1]; a.do_sh = do_str[2];
+  a.lse = (float*)lse; a.delta = delta;
+  a.dq = dq; a.dq_sb = dq_str[0]; a.dq_ss = dq_str[1]; a.dq_sh = dq_str[2];
+  a.dk = dk; a.dk_sb = dk_str[0]; a.dk_ss = dk_str[1]; a.dk_sh = dk_str[2];
+  a.dv = dv; a.dv_sb = dv_str[0]; a.dv_ss = dv_str[1]; a.dv_sh = dv_str[2];
+  a.B = (int)B; a.H = (int)H; a.HKV = (int)HKV; a.Sq = (int)Sq; a.Sk = (int)Sk;
+  a.scale = scale; a.causal = causal; a.grad_f32 = grad_f32;
+  int rc = check_common(a, (int)D);
+  if (rc) return rc;
+  if (Sk % (NW * 32)) return PT_EUNSUPPORTED;
+  const int smem_kv = 2 * 2 * KT * (int)D * 2;
+  const int smem_q = 2 * (2 * KT * (int)D * 2 + 2 * KT * 4);
+  const dim3 gq((unsigned)(Sq / (NW * 32)), (unsigned)H, (unsigned)B);
+  const dim3 gk((unsigned)(Sk / (NW * 32)), (unsigned)HKV, (unsigned)B);
+  if (D == 64) {
+    set_smem(attn_bwd_dkdv_kernel<64>, smem_q);
+    set_smem(attn_bwd_dq_kernel<64>, smem_kv);
+    attn_bwd_dkdv_kernel<64><<<gk, NW * 64, smem_q, stream>>>(a);
+    PT_CHECK_LAUNCH();
+    attn_bwd_dq_kernel<64><<<gq, NW * 64, smem_kv, stream>>>(a);
+  } else {
+    set_smem(attn_bwd_dkdv_kernel<128>, smem_q);
+    set_smem(attn_bwd_dq_kernel<128>, smem_kv);
+    attn_bwd_dkdv_kernel<128><<<gk, NW * 64, smem_q, stream>>>(a);
+    PT_CHECK_LAUNCH();
+    attn_bwd_dq_kernel<128><<<gq, NW * 64, smem_kv, stream>>>(a);
+  }
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,70 @@
+// Shared device helpers for the picotron_amd gfx950 (CDNA4 / MI355X) kernels.
+//
+// Everything in csrc/ is plain HIP written for gfx950 only: 64-lane wavefronts,
+// MFMA bf16 tiles, LDS staging.  Host entry points are `extern "C"` and take
+// plain device pointers, sizes and a hipStream_t (see include/picotron_hip.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PT_WAVE 64
+
+// The C ABI (and the PT_* error codes: 0 ok, negative = argument error found before launch,
+// positive = hipError_t of the launch).  Included here so every definition is checked against it.
+#include "../../include/picotron_hip.h"
+
+#define PT_CHECK_LAUNCH()                          \
+  do {                                             \
+    hipError_t _e = hipGetLastError();             \
+    if (_e != hipSuccess) return (int)_e;          \
+  } while (0)
+
+// ---- bf16 <-> f32 -----------------------------------------------------------
+// bf16 is carried as raw uint16 bits.  f32->bf16 is round-to-nearest-even via
+// the native __bf16 cast (hipcc emits v_cvt_pk_bf16_f32, NaN-preserving).
+__device__ __forceinline__ float bf2f(uint16_t u) { return __uint_as_float((uint32_t)u << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+// round an f32 through bf16 and back (models a bf16 storage round trip)
+__device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
+
+__device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+__device__ __forceinline__ float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+// 8 x bf16 in one 16-byte vector
+struct __attribute__((aligned(16))) bf16x8 { uint32_t w[4]; };
+
+__device__ __forceinline__ void unpack8(const bf16x8& v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { f[2 * i] = lo_bf(v.w[i]); f[2 * i + 1] = hi_bf(v.w[i]); }
+}
+__device__ __forceinline__ bf16x8 pack8(const float* f) {
+  bf16x8 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v.w[i] = pack_bf2(f[2 * i], f[2 * i + 1]);
+  return v;
+}
+__device__ __forceinline__ bf16x8 ld8(const uint16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
+__device__ __forceinline__ void st8(uint16_t* p, const bf16x8& v) { *reinterpret_cast<bf16x8*>(p) = v; }
+
+// ---- wave reductions (64 lanes) ---------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+static inline bool pt_aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// Grid cap for streaming (HBM-bound) kernels: 256 CUs x 8 blocks.
+static constexpr int PT_STREAM_GRID_CAP = 2048;

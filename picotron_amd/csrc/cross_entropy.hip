@@ -1,0 +1,172 @@
+// Fused cross-entropy forward + backward over bf16 logits (one read, one in-place write).
+//
+// Replaces (reference, /root/reference): train.py:48-49
+//   loss = F.cross_entropy(logits.view(-1, V), targets, reduction='mean') / grad_acc_steps
+// and its autograd backward (softmax - onehot), and the PP variant pipeline_parallel.py:103,153.
+//
+//   row_loss[r] = lse_r - x[r, t_r]            (0 for t_r == ignore_index)
+//   dlogits[r,:] = (softmax(x[r,:]) - onehot(t_r)) * scale * (*inv_count if given)
+// where the caller sets scale = 1/grad_acc and inv_count = 1/#valid rows (on device, so the
+// host never synchronises).  dlogits may alias logits (in place: the logits are dead after the
+// loss, which saves a 384 MiB buffer at SmolLM-1.7B mbs4 seq1024).
+//
+// One 256-thread workgroup per row; the row is held in registers (NC 16-byte chunks per
+// thread) so HBM sees exactly one read and one write of the logits: 4*V bytes per row, the
+// roofline figure in DESIGN.md.  Rows longer than 256*8*32 elements take the two-pass variant.
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ float block_reduce(float v, float* red, bool is_max) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  v = is_max ? wave_max(v) : wave_sum(v);
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float r = red[0];
+#pragma unroll
+  for (int i = 1; i < kThreads / 64; ++i) r = is_max ? fmaxf(r, red[i]) : r + red[i];
+  __syncthreads();
+  return r;
+}
+
+template <int NC>
+__global__ __launch_bounds__(kThreads) void ce_kernel(const uint16_t* __restrict__ logits, int64_t ls,
+                                                      const int64_t* __restrict__ tgt, uint16_t* dlogits,
+                                                      int64_t ds, float* __restrict__ row_loss, int V,
+                                                      float scale, const float* __restrict__ inv_count,
+                                                      int64_t ignore_index) {
+  __shared__ float red[kThreads / 64];
+  const int64_t row = blockIdx.x;
+  const uint16_t* x = logits + row * ls;
+  const int nch = V >> 3;
+  const int64_t t = tgt[row];
+  const bool valid = t != ignore_index;
+  // read the target logit before any barrier: later writes may overwrite x in place
+  const float xt = (threadIdx.x == 0 && valid) ? bf2f(x[t]) : 0.f;
+  bf16x8 v[NC];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int c = threadIdx.x + i * kThreads;
+    if (c < nch) {
+      v[i] = ld8(x + c * 8);
+      float f[8];
+      unpack8(v[i], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mx = fmaxf(mx, f[j]);
+    }
+  }
+  mx = block_reduce(mx, red, true);
+  float se = 0.f;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int c = threadIdx.x + i * kThreads;
+    if (c < nch) {
+      float f[8];
+      unpack8(v[i], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) se += __expf(f[j] - mx);
+    }
+  }
+  se = block_reduce(se, red, false);
+  const float lse = mx + __logf(se);
+  const float g = valid ? scale * (inv_count ? *inv_count : 1.0f) : 0.f;
+  if (threadIdx.x == 0) row_loss[row] = valid ? lse - xt : 0.f;
+  uint16_t* d = dlogits + row * ds;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int c = threadIdx.x + i * kThreads;
+    if (c < nch) {
+      float f[8];
+      unpack8(v[i], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float p = __expf(f[j] - lse);
+        f[j] = (p - ((int64_t)(c * 8 + j) == t ? 1.f : 0.f)) * g;
+      }
+      st8(d + c * 8, pack8(f));
+    }
+  }
+}
+
+// long rows: online max/sum in one read, gradient in a second read
+__global__ __launch_bounds__(kThreads) void ce_kernel_2pass(const uint16_t* __restrict__ logits, int64_t ls,
+                                                            const int64_t* __restrict__ tgt, uint16_t* dlogits,
+                                                            int64_t ds, float* __restrict__ row_loss, int V,
+                                                            float scale, const float* __restrict__ inv_count,
+                                                            int64_t ignore_index) {
+  __shared__ float red[kThreads / 64];
+  __shared__ float red2[kThreads / 64];
+  const int64_t row = blockIdx.x;
+  const uint16_t* x = logits + row * ls;
+  const int nch = V >> 3;
+  float m = -INFINITY, s = 0.f;
+  for (int c = threadIdx.x; c < nch; c += kThreads) {
+    float f[8];
+    unpack8(ld8(x + c * 8), f);
+    float cm = m;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cm = fmaxf(cm, f[j]);
+    s *= __expf(m - cm);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += __expf(f[j] - cm);
+    m = cm;
+  }
+  // combine (m, s) pairs across the block
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64), os = __shfl_xor(s, o, 64);
+    const float nm = fmaxf(m, om);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (om == -INFINITY ? 0.f : os * __expf(om - nm));
+    m = nm;
+  }
+  if (lane == 0) { red[wid] = m; red2[wid] = s; }
+  __syncthreads();
+  float M = red[0];
+  for (int i = 1; i < kThreads / 64; ++i) M = fmaxf(M, red[i]);
+  float S = 0.f;
+  for (int i = 0; i < kThreads / 64; ++i) S += red2[i] * __expf(red[i] - M);
+  const float lse = M + __logf(S);
+  const int64_t t = tgt[row];
+  const bool valid = t != ignore_index;
+  const float g = valid ? scale * (inv_count ? *inv_count : 1.0f) : 0.f;
+  if (threadIdx.x == 0) row_loss[row] = valid ? lse - bf2f(x[t]) : 0.f;
+  __syncthreads();  // x[t] read before any in-place write
+  uint16_t* d = dlogits + row * ds;
+  for (int c = threadIdx.x; c < nch; c += kThreads) {
+    float f[8];
+    unpack8(ld8(x + c * 8), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (__expf(f[j] - lse) - ((int64_t)(c * 8 + j) == t ? 1.f : 0.f)) * g;
+    st8(d + c * 8, pack8(f));
+  }
+}
+
+}  // namespace
+
+extern "C" int pt_cross_entropy_fwd_bwd(const void* logits, int64_t logits_stride, const int64_t* targets,
+                                        void* dlogits, int64_t dlogits_stride, float* row_loss, int64_t rows,
+                                        int64_t vocab, float scale, const float* inv_count, int64_t ignore_index,
+                                        hipStream_t stream) {
+  if (!logits || !targets || !dlogits || !row_loss || rows <= 0 || vocab <= 0) return PT_EINVAL;
+  if ((vocab & 7) || (logits_stride & 7) || (dlogits_stride & 7)) return PT_EALIGN;
+  if (!pt_aligned16(logits) || !pt_aligned16(dlogits)) return PT_EALIGN;
+  const auto* L = (const uint16_t*)logits;
+  auto* D = (uint16_t*)dlogits;
+  const int nc = (int)((vocab / 8 + kThreads - 1) / kThreads);
+  const dim3 grid((unsigned)rows);
+#define PT_CE(N) ce_kernel<N><<<grid, kThreads, 0, stream>>>(L, logits_stride, targets, D, dlogits_stride, row_loss, (int)vocab, scale, inv_count, ignore_index)
+  if (nc <= 4) PT_CE(4);
+  else if (nc <= 8) PT_CE(8);
+  else if (nc <= 16) PT_CE(16);
+  else if (nc <= 24) PT_CE(24);
+  else if (nc <= 32) PT_CE(32);
+  else ce_kernel_2pass<<<grid, kThreads, 0, stream>>>(L, logits_stride, targets, D, dlogits_stride, row_loss,
+                                                      (int)vocab, scale, inv_count, ignore_index);
+#undef PT_CE
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}

@@ -1,0 +1,233 @@
+"""Tensor-level wrappers over the C ABI: validation, output allocation (by torch's caching
+allocator -- kernels never allocate) and launch on torch's current stream.
+
+Every function here runs the gfx950 kernels and nothing else; there is no CPU or eager
+fallback.  Shapes/dtypes/strides are validated in Python before the call, as the reference
+validates with asserts (e.g. picotron/model.py:95-96, tensor_parallel.py:81,151,226).
+"""
+import math
+
+import torch
+
+from . import _C
+
+BF16 = torch.bfloat16
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _req(cond, msg):
+    if not cond:
+        raise ValueError(msg)
+
+
+def _bf16_rowmajor(t, name):
+    _req(t.dtype == BF16, f"{name}: expected bfloat16, got {t.dtype}")
+    _req(t.is_cuda, f"{name}: expected a device tensor")
+    _req(t.dim() == 2 and t.stride(1) == 1, f"{name}: expected a 2-D row-major view")
+
+
+# --------------------------------------------------------------------------------- RMSNorm
+MODE_TRITON = 0   # flash-attn layer_norm_fn(is_rms_norm=True): bf16(x * rstd * w)
+MODE_LLAMA = 1    # LlamaRMSNorm: w * bf16(x * rstd)
+
+
+def rmsnorm_fwd(x, weight, eps, mode=MODE_TRITON, residual=None):
+    """x [rows, cols] bf16 contiguous.  Returns (y, rstd, z) where z = bf16(x + residual) (or None)."""
+    _bf16_rowmajor(x, "x")
+    x = x.contiguous()
+    rows, cols = x.shape
+    lib = _C.lib()
+    y = torch.empty_like(x)
+    rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+    z = None
+    if residual is not None:
+        residual = residual.contiguous()
+        _req(residual.shape == x.shape and residual.dtype == BF16, "residual shape/dtype")
+        z = torch.empty_like(x)
+    rc = lib.pt_rmsnorm_fwd(_ptr(x), _ptr(residual), _ptr(weight), _ptr(y), _ptr(z), _ptr(rstd), rows, cols,
+                            float(eps), int(mode), _C.stream_ptr())
+    _C.check(rc, "pt_rmsnorm_fwd")
+    return y, rstd, z
+
+
+def rmsnorm_bwd(dy, z, weight, rstd, mode=MODE_TRITON, dres=None):
+    """Returns (dx, dweight).  dres (same shape as dy) is added into dx when given."""
+    dy = dy.contiguous()
+    rows, cols = z.shape
+    lib = _C.lib()
+    nparts = lib.pt_rmsnorm_bwd_partials(rows, cols)
+    _C.check(0 if nparts > 0 else nparts, "pt_rmsnorm_bwd_partials")
+    partial = torch.empty(nparts, cols, dtype=torch.float32, device=z.device)
+    dx = torch.empty_like(z)
+    dw = torch.empty(cols, dtype=BF16, device=z.device)
+    if dres is not None:
+        dres = dres.contiguous()
+    rc = lib.pt_rmsnorm_bwd(_ptr(dy), _ptr(z), _ptr(weight), _ptr(rstd), _ptr(dres), _ptr(dx), _ptr(dw),
+                            _ptr(partial), rows, cols, int(mode), _C.stream_ptr())
+    _C.check(rc, "pt_rmsnorm_bwd")
+    return dx, dw
+
+
+# ------------------------------------------------------------------------------------ RoPE
+def rope_(x2d, nheads, head_dim, cos, sin, seq_len, inverse=False):
+    """In-place rotate the first `nheads` heads of every row of x2d ([rows, row_stride] view)."""
+    _req(x2d.dtype == BF16 and x2d.stride(-1) == 1, "rope: bf16 row-major view expected")
+    _req(cos.dtype == BF16 and sin.dtype == BF16 and cos.stride(-1) == 1, "rope: bf16 cos/sin tables")
+    _req(cos.shape[0] >= seq_len, "rope: table shorter than the sequence")
+    rows = x2d.shape[0]
+    rc = _C.lib().pt_rope(_ptr(x2d), rows, x2d.stride(0), nheads, head_dim, _ptr(cos), _ptr(sin), seq_len,
+                          cos.stride(0), 1 if inverse else 0, _C.stream_ptr())
+    _C.check(rc, "pt_rope")
+    return x2d
+
+
+# ---------------------------------------------------------------------------------- SwiGLU
+def swiglu_fwd(g, u, out=None):
+    rows, cols = g.shape
+    h = out if out is not None else torch.empty(rows, cols, dtype=BF16, device=g.device)
+    rc = _C.lib().pt_swiglu_fwd(_ptr(g), g.stride(0), _ptr(u), u.stride(0), _ptr(h), h.stride(0), rows, cols,
+                                _C.stream_ptr())
+    _C.check(rc, "pt_swiglu_fwd")
+    return h
+
+
+def swiglu_bwd(dh, g, u, dg=None, du=None):
+    rows, cols = g.shape
+    dh = dh if dh.stride(-1) == 1 else dh.contiguous()
+    dg = dg if dg is not None else torch.empty(rows, cols, dtype=BF16, device=g.device)
+    du = du if du is not None else torch.empty(rows, cols, dtype=BF16, device=g.device)
+    rc = _C.lib().pt_swiglu_bwd(_ptr(dh), dh.stride(0), _ptr(g), g.stride(0), _ptr(u), u.stride(0), _ptr(dg),
+                                dg.stride(0), _ptr(du), du.stride(0), rows, cols, _C.stream_ptr())
+    _C.check(rc, "pt_swiglu_bwd")
+    return dg, du
+
+
+# ---------------------------------------------------------------------------- cross entropy
+def cross_entropy_fwd_bwd(logits, targets, scale=1.0, ignore_index=-100, inplace=True):
+    """logits [rows, V] bf16, targets [rows] int64.  Returns (loss (f32 scalar tensor, mean over
+    valid rows, *not* multiplied by scale), dlogits (aliases logits when inplace), inv_count)."""
+    _bf16_rowmajor(logits, "logits")
+    targets = targets.contiguous().to(torch.int64)
+    rows, vocab = logits.shape
+    valid = (targets != ignore_index)
+    inv_count = (1.0 / valid.sum().clamp_min(1).to(torch.float32)).reshape(1)
+    row_loss = torch.empty(rows, dtype=torch.float32, device=logits.device)
+    dlogits = logits if inplace else torch.empty_like(logits)
+    rc = _C.lib().pt_cross_entropy_fwd_bwd(_ptr(logits), logits.stride(0), _ptr(targets), _ptr(dlogits),
+                                           dlogits.stride(0), _ptr(row_loss), rows, vocab, float(scale),
+                                           _ptr(inv_count), int(ignore_index), _C.stream_ptr())
+    _C.check(rc, "pt_cross_entropy_fwd_bwd")
+    loss = row_loss.sum() * inv_count[0]
+    return loss, dlogits, inv_count
+
+
+# ------------------------------------------------------------------------------------ GEMM
+EPI_BF16, EPI_BF16_ACC, EPI_F32, EPI_F32_ACC = 0, 1, 2, 3
+
+
+def _gemm(A, lda, a_kcontig, Bs, ldbs, b_bounds, b_kcontig, b_seg_dim, Cs, ldcs, c_bounds, M, N, K, epilogue,
+          tile=-1):
+    lib = _C.lib()
+    nb, nc = len(Bs), len(Cs)
+    rc = lib.pt_gemm(_ptr(A), lda, int(a_kcontig), _C.ptrarr([_ptr(b) for b in Bs]), _C.i64arr(ldbs),
+                     _C.i64arr(b_bounds), nb, int(b_kcontig), int(b_seg_dim), _C.ptrarr([_ptr(c) for c in Cs]),
+                     _C.i64arr(ldcs), _C.i64arr(c_bounds), nc, M, N, K, int(epilogue), int(tile), _C.stream_ptr())
+    _C.check(rc, f"pt_gemm(M={M}, N={N}, K={K}, a_k={a_kcontig}, b_k={b_kcontig}, epi={epilogue})")
+
+
+def _bounds(sizes):
+    out = [0]
+    for s in sizes:
+        out.append(out[-1] + int(s))
+    return out
+
+
+def linear_fwd(x2d, weights, out=None, tile=-1):
+    """Y = x . [W_0; W_1; ...]^T  -> [T, sum N_i] (one launch; F.linear of model.py:124-126,186)."""
+    _bf16_rowmajor(x2d, "x")
+    T, K = x2d.shape
+    for w in weights:
+        _req(w.dtype == BF16 and w.is_contiguous() and w.shape[1] == K, "weight must be contiguous [N, K] bf16")
+    ns = [w.shape[0] for w in weights]
+    N = sum(ns)
+    y = out if out is not None else torch.empty(T, N, dtype=BF16, device=x2d.device)
+    _req(y.stride(1) == 1 and y.shape == (T, N), "out shape")
+    _gemm(x2d, x2d.stride(0), 1, weights, [K] * len(weights), _bounds(ns), 1, 0, [y], [y.stride(0)], [0, T],
+          T, N, K, EPI_BF16, tile)
+    return y
+
+
+def linear_dgrad(dy2d, weights, out=None, accumulate=False, tile=-1):
+    """dX = dY . [W_0; W_1; ...]  where dY = [dY_0 | dY_1 | ...] is [T, sum N_i]."""
+    _bf16_rowmajor(dy2d, "dy")
+    T, N = dy2d.shape
+    Kin = weights[0].shape[1]
+    ns = [w.shape[0] for w in weights]
+    _req(sum(ns) == N, "dgrad: dY width must equal the stacked weight rows")
+    dx = out if out is not None else torch.empty(T, Kin, dtype=BF16, device=dy2d.device)
+    _gemm(dy2d, dy2d.stride(0), 1, weights, [Kin] * len(weights), _bounds(ns), 0, 1, [dx], [dx.stride(0)],
+          [0, T], T, Kin, N, EPI_BF16_ACC if accumulate else EPI_BF16, tile)
+    return dx
+
+
+def linear_wgrad(dy2d, x2d, outs, epilogue=EPI_BF16, tile=-1):
+    """dW_i = dY_i^T . X for the column segments dY_i of dY (widths = outs[i].shape[0]); one launch."""
+    _bf16_rowmajor(dy2d, "dy")
+    _bf16_rowmajor(x2d, "x")
+    T, N = dy2d.shape
+    Kin = x2d.shape[1]
+    ns = [o.shape[0] for o in outs]
+    _req(sum(ns) == N, "wgrad: output rows must cover dY's width")
+    _gemm(dy2d, dy2d.stride(0), 0, [x2d], [x2d.stride(0)], [0, Kin], 0, 0, outs, [o.stride(0) for o in outs],
+          _bounds(ns), N, Kin, T, epilogue, tile)
+    return outs
+
+
+# ------------------------------------------------------------------------------- attention
+def _str3(t):
+    _req(t.dim() == 4 and t.stride(3) == 1, "attention tensors are [B, S, H, D] views with d contiguous")
+    return _C.i64arr([t.stride(0), t.stride(1), t.stride(2)])
+
+
+def attn_fwd(q, k, v, scale, causal, out=None, lse=None, merge=False):
+    """q [B,Sq,H,D], k/v [B,Sk,Hkv,D] (token-major views).  Returns (out, lse[B,H,Sq] f32).
+    merge=True: `out` is an f32 accumulator and `lse` the running LSE; this block is merged in."""
+    B, Sq, H, D = q.shape
+    Sk, HKV = k.shape[1], k.shape[2]
+    if out is None:
+        out = torch.empty(B, Sq, H, D, dtype=BF16, device=q.device)
+    if lse is None:
+        lse = torch.empty(B, H, Sq, dtype=torch.float32, device=q.device)
+    _req(lse.is_contiguous() and lse.shape == (B, H, Sq), "lse must be contiguous [B, H, Sq] f32")
+    rc = _C.lib().pt_attn_fwd(_ptr(q), _str3(q), _ptr(k), _str3(k), _ptr(v), _str3(v), _ptr(out), _str3(out),
+                              _ptr(lse), B, H, HKV, Sq, Sk, D, float(scale), int(bool(causal)), int(bool(merge)),
+                              _C.stream_ptr())
+    _C.check(rc, "pt_attn_fwd")
+    return out, lse
+
+
+def attn_bwd(dout, q, k, v, out, lse, scale, causal, dq=None, dk=None, dv=None, grad_f32=False, delta=None):
+    B, Sq, H, D = q.shape
+    Sk, HKV = k.shape[1], k.shape[2]
+    lib = _C.lib()
+    if delta is None:
+        delta = torch.empty(B, H, Sq, dtype=torch.float32, device=q.device)
+        rc = lib.pt_attn_bwd_delta(_ptr(dout), _str3(dout), _ptr(out), _str3(out), _ptr(delta), B, H, Sq, D,
+                                   _C.stream_ptr())
+        _C.check(rc, "pt_attn_bwd_delta")
+    gdt = torch.float32 if grad_f32 else BF16
+    if dq is None:
+        dq = (torch.zeros if grad_f32 else torch.empty)(B, Sq, H, D, dtype=gdt, device=q.device)
+    if dk is None:
+        dk = (torch.zeros if grad_f32 else torch.empty)(B, Sk, HKV, D, dtype=gdt, device=q.device)
+    if dv is None:
+        dv = (torch.zeros if grad_f32 else torch.empty)(B, Sk, HKV, D, dtype=gdt, device=q.device)
+    rc = lib.pt_attn_bwd(_ptr(q), _str3(q), _ptr(k), _str3(k), _ptr(v), _str3(v), _ptr(dout), _str3(dout),
+                         _ptr(lse), _ptr(delta), _ptr(dq), _str3(dq), _ptr(dk), _str3(dk), _ptr(dv), _str3(dv),
+                         B, H, HKV, Sq, Sk, D, float(scale), int(bool(causal)), int(bool(grad_f32)),
+                         _C.stream_ptr())
+    _C.check(rc, "pt_attn_bwd")
+    return dq, dk, dv, delta

@@ -1,0 +1,282 @@
+"""Kernel parity on the GPU: each gfx950 kernel (through the C ABI) against the CPU oracle /
+torch fp32 on the same seeded inputs.  Tolerances: bf16 outputs within rel 2e-2 of the fp32
+reference (north_star), stated per test."""
+import math
+
+import pytest
+import torch
+
+from oracle import picotron_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+def rel_err(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+def maxabs(a, b):
+    return (a.float().cpu() - b.float().cpu()).abs().max().item()
+
+
+@pytest.fixture(autouse=True)
+def _seed():
+    torch.manual_seed(0)
+
+
+# --------------------------------------------------------------------------- RMSNorm
+@pytest.mark.parametrize("rows,cols", [(64, 64), (300, 2048), (128, 4096), (8, 512)])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_rmsnorm_fwd_bwd(rows, cols, mode):
+    from picotron_amd import kernels as K
+    x = torch.randn(rows, cols).to(BF)
+    w = (1 + 0.1 * torch.randn(cols)).to(BF)
+    dy = torch.randn(rows, cols).to(BF)
+    # reference in fp32 on the same bf16 inputs
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    ref = O.rmsnorm_flash_semantics(xr, wr, 1e-5) if mode == 0 else O.rmsnorm_llama(xr, wr, 1e-5)
+    ref.backward(dy.float())
+    y, rstd, _ = K.rmsnorm_fwd(x.to(DEV), w.to(DEV), 1e-5, mode)
+    dx, dw = K.rmsnorm_bwd(dy.to(DEV), x.to(DEV), w.to(DEV), rstd, mode)
+    torch.cuda.synchronize()
+    assert rel_err(y, ref) < 5e-3
+    assert rel_err(dx, xr.grad) < 1e-2
+    assert rel_err(dw, wr.grad) < 1e-2
+
+
+def test_rmsnorm_fused_residual():
+    from picotron_amd import kernels as K
+    rows, cols = 256, 2048
+    x, r = torch.randn(rows, cols).to(BF), torch.randn(rows, cols).to(BF)
+    w = torch.ones(cols).to(BF)
+    y, rstd, z = K.rmsnorm_fwd(x.to(DEV), w.to(DEV), 1e-5, 0, residual=r.to(DEV))
+    zr = (x + r)  # bf16 add, as the reference's residual (model.py:207-208)
+    assert torch.equal(z.cpu(), zr)
+    assert rel_err(y, O.rmsnorm_flash_semantics(zr, w, 1e-5)) < 5e-3
+    dy, dres = torch.randn(rows, cols).to(BF), torch.randn(rows, cols).to(BF)
+    dx, _ = K.rmsnorm_bwd(dy.to(DEV), z, w.to(DEV), rstd, 0, dres=dres.to(DEV))
+    zf = zr.float().requires_grad_(True)
+    O.rmsnorm_flash_semantics(zf, w.float(), 1e-5).backward(dy.float())
+    assert rel_err(dx, zf.grad + dres.float()) < 1e-2
+
+
+# ------------------------------------------------------------------------------ RoPE
+@pytest.mark.parametrize("d", [64, 128])
+def test_rope_fused_qk_rows(d):
+    from picotron_amd import kernels as K
+    B, S, nh, nkv = 2, 64, 4, 2
+    cos, sin = O.get_cos_sin(S, d, base=10000.0)
+    qkv = torch.randn(B * S, (nh + 2 * nkv) * d).to(BF)
+    ref = qkv.clone()
+    # reference: rotate q and k heads ([B, H, S, D] layout), flash semantics (one rounding)
+    for lo, n in ((0, nh), (nh * d, nkv)):
+        t = ref[:, lo:lo + n * d].view(B, S, n, d).transpose(1, 2)
+        t2 = O.rotary_flash_semantics(t, cos, sin)
+        ref[:, lo:lo + n * d] = t2.transpose(1, 2).reshape(B * S, n * d)
+    dq = qkv.to(DEV)
+    K.rope_(dq, nh + nkv, d, cos.to(DEV), sin.to(DEV), S)
+    torch.cuda.synchronize()
+    assert maxabs(dq, ref) <= 2 * 2 ** -7 * ref.abs().max().item()
+    assert torch.equal(dq[:, (nh + nkv) * d:].cpu(), qkv[:, (nh + nkv) * d:])  # v untouched
+    # inverse restores the input to bf16 rounding
+    K.rope_(dq, nh + nkv, d, cos.to(DEV), sin.to(DEV), S, inverse=True)
+    assert rel_err(dq, qkv) < 1e-2
+
+
+# ---------------------------------------------------------------------------- SwiGLU
+def test_swiglu_fwd_bwd_strided():
+    from picotron_amd import kernels as K
+    T, I = 512, 1024
+    gu = torch.randn(T, 2 * I).to(BF)
+    g, u = gu[:, :I], gu[:, I:]
+    dh = torch.randn(T, I).to(BF)
+    gr, ur = g.clone().requires_grad_(True), u.clone().requires_grad_(True)
+    h_ref = torch.nn.functional.silu(gr) * ur   # bf16 eager, as model.py:186
+    h_ref.backward(dh)
+    d = gu.to(DEV)
+    h = K.swiglu_fwd(d[:, :I], d[:, I:])
+    dg, du = K.swiglu_bwd(dh.to(DEV), d[:, :I], d[:, I:])
+    torch.cuda.synchronize()
+    assert maxabs(h, h_ref) <= 1e-2 * h_ref.abs().max().item()
+    assert rel_err(dg, gr.grad) < 1e-2 and rel_err(du, ur.grad) < 1e-2
+
+
+# ---------------------------------------------------------------------- cross entropy
+@pytest.mark.parametrize("V", [96, 49152, 32000, 80000])
+def test_cross_entropy_fused(V):
+    from picotron_amd import kernels as K
+    T, ga = 64, 4
+    logits = (3 * torch.randn(T, V)).to(BF)
+    tgt = torch.randint(0, V, (T,))
+    tgt[5] = -100
+    lr = logits.float().requires_grad_(True)
+    loss_ref = torch.nn.functional.cross_entropy(lr, tgt) / ga
+    loss_ref.backward()
+    dl = logits.to(DEV)
+    loss, grad, _ = K.cross_entropy_fwd_bwd(dl, tgt.to(DEV), scale=1.0 / ga, inplace=True)
+    torch.cuda.synchronize()
+    assert abs(loss.item() / ga - loss_ref.item()) < 1e-3 * max(1, abs(loss_ref.item()))
+    assert grad.data_ptr() == dl.data_ptr()
+    assert rel_err(grad, lr.grad) < 1e-2
+    assert grad[5].float().abs().max().item() == 0.0
+
+
+def test_cross_entropy_golden_vector():
+    """against the reference's own bf16 F.cross_entropy / grad_acc (tests/golden/G9)."""
+    import os
+    from picotron_amd import kernels as K
+    g = torch.load(os.path.join(os.path.dirname(__file__), "golden", "G9.pt"), weights_only=True)
+    lg = g["logits"].view(16, -1).to(DEV).clone()
+    loss, grad, _ = K.cross_entropy_fwd_bwd(lg, g["targets"].reshape(-1).to(DEV), scale=1.0 / int(g["grad_acc"]))
+    assert abs(loss.item() / int(g["grad_acc"]) - g["loss"].float().item()) < 2e-2 * abs(g["loss"].float().item())
+    assert rel_err(grad, g["dlogits"].view(16, -1)) < 2e-2
+
+
+# ------------------------------------------------------------------------------ GEMM
+def _ref_mm(a, b):
+    return a.float().cpu() @ b.float().cpu()
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 256), (4096, 2048, 2048), (128, 384, 128),
+                                   (64, 64, 128)])
+def test_gemm_fwd_nt(M, N, K):
+    from picotron_amd import kernels as K_
+    x = torch.randn(M, K).to(BF)
+    w = (torch.randn(N, K) / math.sqrt(K)).to(BF)
+    y = K_.linear_fwd(x.to(DEV), [w.to(DEV)])
+    torch.cuda.synchronize()
+    assert rel_err(y, _ref_mm(x, w.t())) < 1e-2
+
+
+@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+def test_gemm_every_tile_every_layout(tile):
+    from picotron_amd import kernels as K_
+    M, N, K = 512, 512, 256
+    a = torch.randn(M, K).to(BF)
+    b = (torch.randn(N, K) / 16).to(BF)
+    y = K_.linear_fwd(a.to(DEV), [b.to(DEV)], tile=tile)
+    assert rel_err(y, _ref_mm(a, b.t())) < 1e-2
+    # NN: dX = dY W   (dY [M, N], W [N, K])
+    dy = torch.randn(M, N).to(BF)
+    dx = K_.linear_dgrad(dy.to(DEV), [b.to(DEV)], tile=tile)
+    assert rel_err(dx, _ref_mm(dy, b)) < 1e-2
+    # TN: dW = dY^T X  (dY [M, N], X [M, K]) -> [N, K]
+    dw = torch.empty(N, K, dtype=BF, device=DEV)
+    K_.linear_wgrad(dy.to(DEV), a.to(DEV), [dw], tile=tile)
+    torch.cuda.synchronize()
+    assert rel_err(dw, _ref_mm(dy.t(), a)) < 1e-2
+
+
+def test_gemm_segmented_qkv():
+    """fused q|k|v forward, dX over stacked weights, dW into three outputs: one launch each."""
+    from picotron_amd import kernels as K_
+    T, H, nkv = 1024, 512, 256
+    x = torch.randn(T, H).to(BF)
+    ws = [(torch.randn(n, H) / math.sqrt(H)).to(BF) for n in (H, nkv, nkv)]
+    wd = [w.to(DEV) for w in ws]
+    y = K_.linear_fwd(x.to(DEV), wd)
+    ref = _ref_mm(x, torch.cat(ws).t())
+    assert rel_err(y, ref) < 1e-2
+    dy = torch.randn(T, H + 2 * nkv).to(BF)
+    dx = K_.linear_dgrad(dy.to(DEV), wd)
+    assert rel_err(dx, _ref_mm(dy, torch.cat(ws))) < 1e-2
+    outs = [torch.empty_like(w) for w in wd]
+    K_.linear_wgrad(dy.to(DEV), x.to(DEV), outs)
+    ref_w = _ref_mm(dy.t(), x)
+    lo = 0
+    for o, w in zip(outs, ws):
+        assert rel_err(o, ref_w[lo:lo + w.shape[0]]) < 1e-2
+        lo += w.shape[0]
+
+
+def test_gemm_accumulate_epilogues():
+    from picotron_amd import kernels as K_
+    T, N, K = 512, 256, 256
+    dy, x = torch.randn(T, N).to(BF), torch.randn(T, K).to(BF)
+    base = torch.randn(N, K)
+    # f32 accumulate (main_grad)
+    acc = base.clone().to(DEV)
+    K_.linear_wgrad(dy.to(DEV), x.to(DEV), [acc], epilogue=K_.EPI_F32_ACC)
+    assert rel_err(acc, base + _ref_mm(dy.t(), x)) < 1e-3
+    # bf16 accumulate (param.grad in bf16 across micro-batches)
+    accb = base.to(BF).to(DEV)
+    K_.linear_wgrad(dy.to(DEV), x.to(DEV), [accb], epilogue=K_.EPI_BF16_ACC)
+    assert rel_err(accb, base.to(BF).float() + _ref_mm(dy.t(), x)) < 1e-2
+
+
+def test_gemm_asymmetric_exact():
+    """A = I with an asymmetric B catches a transposed C write (guide §3)."""
+    from picotron_amd import kernels as K_
+    n = 256
+    eye = torch.eye(n).to(BF)
+    b = torch.arange(n * n, dtype=torch.float32).reshape(n, n).remainder(251).to(BF)
+    y = K_.linear_fwd(eye.to(DEV), [b.to(DEV)])   # y = I . b^T
+    assert torch.equal(y.cpu(), b.t().contiguous())
+
+
+# ------------------------------------------------------------------------- attention
+def _qkv(B, S, H, HKV, D, fused=True):
+    T = B * S
+    buf = torch.randn(T, (H + 2 * HKV) * D).to(BF)
+    d = buf.to(DEV)
+    q = d[:, :H * D].view(B, S, H, D)
+    k = d[:, H * D:(H + HKV) * D].view(B, S, HKV, D)
+    v = d[:, (H + HKV) * D:].view(B, S, HKV, D)
+    return q, k, v
+
+
+def _ref_attn(q, k, v, causal, scale):
+    # [B,S,H,D] -> [B,H,S,D], GQA by repeat_interleave (model.py:142-143)
+    rep = q.shape[2] // k.shape[2]
+    qq = q.float().cpu().transpose(1, 2)
+    kk = k.float().cpu().transpose(1, 2).repeat_interleave(rep, 1)
+    vv = v.float().cpu().transpose(1, 2).repeat_interleave(rep, 1)
+    return qq, kk, vv
+
+
+@pytest.mark.parametrize("B,S,H,HKV,D,causal", [(2, 128, 4, 4, 64, True), (1, 256, 4, 2, 64, True),
+                                                 (2, 256, 2, 2, 128, True), (1, 128, 2, 1, 128, False),
+                                                 (1, 512, 2, 2, 64, False), (2, 1024, 2, 2, 64, True)])
+def test_attention_fwd_bwd(B, S, H, HKV, D, causal):
+    from picotron_amd import kernels as K_
+    q, k, v = _qkv(B, S, H, HKV, D)
+    scale = 1 / math.sqrt(D)
+    o, lse = K_.attn_fwd(q, k, v, scale, causal)
+    qq, kk, vv = _ref_attn(q, k, v, causal, scale)
+    qq.requires_grad_(True); kk.requires_grad_(True); vv.requires_grad_(True)
+    o_ref, lse_ref = O.attention_lse(qq, kk, vv, scale, causal)
+    assert rel_err(o, o_ref.transpose(1, 2)) < 1e-2
+    assert maxabs(lse, lse_ref) < 1e-2
+    do = torch.randn(o.shape).to(BF)
+    (o_ref * do.float().transpose(1, 2)).sum().backward()
+    dq, dk, dv, _ = K_.attn_bwd(do.to(DEV), q, k, v, o, lse, scale, causal)
+    torch.cuda.synchronize()
+    rep = H // HKV
+    dk_ref = kk.grad.view(B, HKV, rep, S, D).sum(2).transpose(1, 2)
+    dv_ref = vv.grad.view(B, HKV, rep, S, D).sum(2).transpose(1, 2)
+    assert rel_err(dq, qq.grad.transpose(1, 2)) < 2e-2
+    assert rel_err(dk, dk_ref) < 2e-2
+    assert rel_err(dv, dv_ref) < 2e-2
+
+
+def test_attention_ring_merge_matches_full():
+    """Two key blocks merged by the fused update_out_and_lse epilogue == attention over both
+    (context_parallel.py:157-187), and the backward with the global LSE sums to the full grads."""
+    from picotron_amd import kernels as K_
+    B, S, H, D = 1, 256, 2, 64
+    q, k, v = _qkv(B, 2 * S, H, H, D)
+    scale = 1 / math.sqrt(D)
+    q2 = q[:, S:]                       # queries of the second shard
+    acc = torch.zeros(B, S, H, D, dtype=torch.float32, device=DEV)
+    lse = torch.full((B, H, S), float("-inf"), device=DEV)
+    K_.attn_fwd(q2, k[:, S:], v[:, S:], scale, True, out=acc, lse=lse, merge=True)   # diagonal block
+    K_.attn_fwd(q2, k[:, :S], v[:, :S], scale, False, out=acc, lse=lse, merge=True)  # earlier block
+    qq, kk, vv = _ref_attn(q, k, v, True, scale)
+    o_ref, lse_ref = O.attention_lse(qq, kk, vv, scale, True)
+    assert rel_err(acc, o_ref[:, :, S:].transpose(1, 2)) < 1e-2
+    assert maxabs(lse, lse_ref[:, :, S:]) < 1e-2

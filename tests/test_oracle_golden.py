@@ -1,0 +1,129 @@
+"""Pin the CPU oracle against golden vectors generated from the reference itself
+(tests/golden/make_golden.py).  CPU only."""
+import math
+import os
+
+import pytest
+import torch
+
+from oracle import picotron_oracle as O
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def load(name):
+    return torch.load(os.path.join(GOLD, f"{name}.pt"), weights_only=True)
+
+
+def close(a, b, rtol=1e-5, atol=1e-6):
+    torch.testing.assert_close(a.float(), b.float(), rtol=rtol, atol=atol)
+
+
+@pytest.mark.parametrize("tag", ["f32", "bf16"])
+def test_rmsnorm_llama_golden(tag):
+    g = load(f"G1_{tag}")
+    x = g["x"].clone().requires_grad_(True)
+    w = g["w"].clone().requires_grad_(True)
+    y = O.rmsnorm_llama(x, w, float(g["eps"]))
+    y.backward(g["dy"])
+    tol = dict(rtol=0, atol=0) if tag == "f32" else dict(rtol=1e-2, atol=1e-2)
+    close(y, g["y"], **({"rtol": 1e-6, "atol": 1e-6} if tag == "f32" else tol))
+    close(x.grad, g["dx"], rtol=1e-5 if tag == "f32" else 2e-2, atol=1e-5 if tag == "f32" else 2e-2)
+    close(w.grad, g["dw"], rtol=1e-5 if tag == "f32" else 2e-2, atol=1e-5 if tag == "f32" else 5e-2)
+
+
+def test_cos_sin_tables_golden():
+    g = load("G2_tables")
+    c, s = O.get_cos_sin(16, 32, base=10000.0)
+    assert torch.equal(c, g["cos_16_32"]) and torch.equal(s, g["sin_16_32"])
+    c, s = O.get_cos_sin(64, 128)
+    assert torch.equal(c, g["cos_64_128_default"]) and torch.equal(s, g["sin_64_128_default"])
+
+
+def test_rope_golden():
+    g = load("G2")
+    x = g["x"].clone().requires_grad_(True)
+    y = O.apply_rotary_pos_emb(x, g["cos"].float(), g["sin"].float())
+    y.backward(g["dy"])
+    close(y, g["y"])
+    close(x.grad, g["dx"])
+
+
+def test_attention_golden():
+    g = load("G3")
+    p = {k: g[k].clone().requires_grad_(True) for k in ["q_proj.weight", "k_proj.weight", "v_proj.weight",
+                                                       "out_proj.weight"]}
+    x = g["x"].clone().requires_grad_(True)
+    y = O.attention(x, p["q_proj.weight"], p["k_proj.weight"], p["v_proj.weight"], p["out_proj.weight"],
+                    g["cos"].float(), g["sin"].float(), 4, 2)
+    y.backward(g["dy"])
+    close(y, g["y"], rtol=1e-4, atol=1e-5)
+    close(x.grad, g["dx"], rtol=1e-4, atol=1e-5)
+    for k, v in p.items():
+        close(v.grad, g[f"grad.{k}"], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("tag", ["f32", "bf16"])
+def test_ring_pieces_golden(tag):
+    g = load(f"G4_{tag}")
+    sc = 1 / math.sqrt(16)
+    tol = dict(rtol=1e-5, atol=1e-6) if tag == "f32" else dict(rtol=0, atol=0)
+    o_c, l_c = O.ring_attention_forward(g["q"], g["k"], g["v"], sc, True)
+    o_f, l_f = O.ring_attention_forward(g["q"], g["k"], g["v"], sc, False)
+    close(o_c, g["o_causal"], **tol); close(l_c, g["lse_causal"], **tol)
+    close(o_f, g["o_full"], **tol); close(l_f, g["lse_full"], **tol)
+    out, lse = O.update_out_and_lse(None, None, o_c, l_c)
+    out, lse = O.update_out_and_lse(out, lse, o_f, l_f)
+    close(out, g["merged_out"], **tol); close(lse, g["merged_lse"], **tol)
+    dq, dk, dv = O.ring_attention_backward(g["dO"], g["q"], g["k"], g["v"], out.to(g["q"].dtype),
+                                           lse.squeeze(-1), sc, True)
+    close(dq, g["dq"], **tol); close(dk, g["dk"], **tol); close(dv, g["dv"], **tol)
+
+
+def test_mlp_golden():
+    g = load("G5")
+    p = {k: g[k].clone().requires_grad_(True) for k in ["up_proj.weight", "gate_proj.weight", "down_proj.weight"]}
+    x = g["x"].clone().requires_grad_(True)
+    y = O.mlp(x, p["gate_proj.weight"], p["up_proj.weight"], p["down_proj.weight"])
+    y.backward(g["dy"])
+    close(y, g["y"], rtol=1e-5, atol=1e-6)
+    close(x.grad, g["dx"], rtol=1e-5, atol=1e-6)
+    for k, v in p.items():
+        close(v.grad, g[f"grad.{k}"], rtol=1e-5, atol=1e-6)
+
+
+def test_decoder_layer_golden():
+    g = load("G6")
+    names = [k for k in g if not k.startswith("grad.") and k not in ("x", "y", "dy", "dx", "cos", "sin")]
+    p = {k: g[k].clone().requires_grad_(True) for k in names}
+    x = g["x"].clone().requires_grad_(True)
+    y = O.decoder_layer(x, p, g["cos"].float(), g["sin"].float(), 4, 2, 1e-5)
+    y.backward(g["dy"])
+    close(y, g["y"], rtol=1e-4, atol=1e-5)
+    close(x.grad, g["dx"], rtol=1e-4, atol=1e-5)
+    for k, v in p.items():
+        close(v.grad, g[f"grad.{k}"], rtol=1e-4, atol=1e-4)
+
+
+def test_cross_entropy_golden():
+    g = load("G9")
+    logits = g["logits"].clone().requires_grad_(True)
+    loss = torch.nn.functional.cross_entropy(logits.view(16, -1), g["targets"].reshape(-1)) / int(g["grad_acc"])
+    loss.backward()
+    close(loss, g["loss"], rtol=0, atol=0)
+    close(logits.grad, g["dlogits"], rtol=0, atol=0)
+    # the oracle's fp32 statement agrees with the reference's bf16 result to bf16 precision
+    lo = O.cross_entropy(g["logits"], g["targets"], int(g["grad_acc"]))
+    close(lo, g["loss"], rtol=1e-2, atol=1e-2)
+
+
+def test_llama_forward_golden():
+    g = load("G10")
+    cfg = dict(hidden_size=64, intermediate_size=128, num_attention_heads=4, num_key_value_heads=2,
+               rms_norm_eps=1e-5, vocab_size=96, num_hidden_layers=2)
+    params = {k[len("param."):]: v for k, v in g.items() if k.startswith("param.")}
+    cos, sin = O.get_cos_sin(16, 16, base=10000.0)
+    logits = O.llama_forward(g["ids"][:, :-1], params, cfg, cos.float(), sin.float())
+    close(logits, g["logits"], rtol=1e-4, atol=1e-4)
+    loss = torch.nn.functional.cross_entropy(logits.reshape(-1, 96), g["ids"][:, 1:].reshape(-1))
+    close(loss, g["loss"], rtol=1e-5, atol=1e-5)
