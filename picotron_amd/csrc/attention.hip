@@ -25,7 +25,7 @@
 #include "common.h"
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef short short4_t __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 
@@ -91,16 +91,14 @@ template <int D>
 __device__ __forceinline__ bf16x8_t rd_tr(const lds_u8* t, int s, int dt, int lane) {
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   const int col = 32 * dt + 16 * (g & 1) + 4 * p;
-  bf16x8_t out;
+  bf16x4_t v[2];  // whole-vector concat (element-wise bit_cast of short4 miscompiles, see gemm.hip)
 #pragma unroll
   for (int sec = 0; sec < 2; ++sec) {
     const int r = 16 * s + 8 * sec + 4 * (g >> 1) + q;
     const int off = r * (D * 2) + 16 * ((col >> 3) ^ aswz<D>(r)) + 8 * ((col >> 2) & 1);
-    short4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(t + off));
-#pragma unroll
-    for (int j = 0; j < 4; ++j) out[4 * sec + j] = __builtin_bit_cast(__bf16, v[j]);
+    v[sec] = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4_t*)(t + off));
   }
-  return out;
+  return __builtin_shufflevector(v[0], v[1], 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
 // B operand from a C-layout 32x32 accumulator, k-step s (rows 16 s .. 16 s + 15)

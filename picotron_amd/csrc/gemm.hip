@@ -24,7 +24,7 @@
 #include "common.h"
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef short short4_t __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 
@@ -95,16 +95,16 @@ __device__ __forceinline__ bf16x8_t read_frag(const lds_u8* lds, int rbase, int 
     constexpr int rb = ROWS * 2;
     const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
     const int col = rbase + 4 * p;
-    bf16x8_t out;
+    // NB: read as bf16x4 and concatenate whole vectors; an element-wise bit_cast of a short4
+    // result miscompiles on ROCm 7.2 (the halves were duplicated; tools/probe_tr.*)
+    bf16x4_t t[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int kr = 32 * s + 8 * g + 4 * h + q;
       const int off = kr * rb + 16 * ((col >> 3) ^ swz_mn(kr, rb)) + 8 * ((col >> 2) & 1);
-      short4_t t = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(lds + off));
-#pragma unroll
-      for (int j = 0; j < 4; ++j) out[4 * h + j] = __builtin_bit_cast(__bf16, t[j]);
+      t[h] = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4_t*)(lds + off));
     }
-    return out;
+    return __builtin_shufflevector(t[0], t[1], 0, 1, 2, 3, 4, 5, 6, 7);
   }
 }
 
