@@ -57,7 +57,8 @@ int pt_swiglu_bwd(const void* dh, int64_t dh_stride, const void* g, int64_t g_st
 /* ---- fused cross-entropy forward + backward -----------------------------------------------
  * replaces train.py:49 F.cross_entropy(logits, targets, 'mean') / grad_acc (+ autograd bwd) and
  * pipeline_parallel.py:103,153.  row_loss[r] = lse - logit[target]; dlogits (may alias logits) =
- * (softmax - onehot) * scale * (*inv_count if non-NULL).  targets int64, ignore_index rows -> 0. */
+ * (softmax - onehot) * scale * (*inv_count if non-NULL).  targets int64, ignore_index rows -> 0.
+ * dlogits == NULL: loss only (one read of the logits; the autograd forward). */
 int pt_cross_entropy_fwd_bwd(const void* logits, int64_t logits_stride, const int64_t* targets, void* dlogits,
                              int64_t dlogits_stride, float* row_loss, int64_t rows, int64_t vocab, float scale,
                              const float* inv_count, int64_t ignore_index, hipStream_t stream);
@@ -68,11 +69,13 @@ int pt_cross_entropy_fwd_bwd(const void* logits, int64_t logits_stride, const in
  * C[M,N] (op)= A[M,K] B[K,N].  a_kcontig: A stored [M,K] (else [K,M]); b_kcontig: B stored
  * [N,K] (weights; else [K,N]).  B may be split into nb pointer segments along N (b_seg_dim 0)
  * or K (1), C into nc segments along M; *_bounds hold n+1 boundaries (NULL = one segment).
- * epilogue 0: C bf16 = acc, 1: C bf16 += acc, 2: C f32 = acc, 3: C f32 += acc.  tile -1 = auto. */
+ * epilogue 0: C bf16 = acc, 1: C bf16 += acc, 2: C f32 = acc, 3: C f32 += acc,
+ * 4: C bf16 = residual + acc (residual [M, N] bf16, leading dim ldr; the residual add of
+ * model.py:207-208 fused into the producing projection).  tile -1 = auto. */
 int pt_gemm(const void* A, int64_t lda, int a_kcontig, const void* const* B, const int64_t* ldb,
             const int64_t* b_bounds, int nb, int b_kcontig, int b_seg_dim, void* const* C, const int64_t* ldc,
-            const int64_t* c_bounds, int nc, int64_t M, int64_t N, int64_t K, int epilogue, int tile,
-            hipStream_t stream);
+            const int64_t* c_bounds, int nc, int64_t M, int64_t N, int64_t K, int epilogue,
+            const void* residual, int64_t ldr, int tile, hipStream_t stream);
 int pt_gemm_pick_tile(int64_t M, int64_t N, const int64_t* mseg, int nmseg, const int64_t* nseg, int nnseg);
 
 /* ---- flash attention ----------------------------------------------------------------------

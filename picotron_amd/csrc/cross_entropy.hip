@@ -74,6 +74,7 @@ __global__ __launch_bounds__(kThreads) void ce_kernel(const uint16_t* __restrict
   const float lse = mx + __logf(se);
   const float g = valid ? scale * (inv_count ? *inv_count : 1.0f) : 0.f;
   if (threadIdx.x == 0) row_loss[row] = valid ? lse - xt : 0.f;
+  if (!dlogits) return;  // loss-only (forward) launch
   uint16_t* d = dlogits + row * ds;
 #pragma unroll
   for (int i = 0; i < NC; ++i) {
@@ -135,6 +136,7 @@ __global__ __launch_bounds__(kThreads) void ce_kernel_2pass(const uint16_t* __re
   const float g = valid ? scale * (inv_count ? *inv_count : 1.0f) : 0.f;
   if (threadIdx.x == 0) row_loss[row] = valid ? lse - bf2f(x[t]) : 0.f;
   __syncthreads();  // x[t] read before any in-place write
+  if (!dlogits) return;
   uint16_t* d = dlogits + row * ds;
   for (int c = threadIdx.x; c < nch; c += kThreads) {
     float f[8];
@@ -151,9 +153,9 @@ extern "C" int pt_cross_entropy_fwd_bwd(const void* logits, int64_t logits_strid
                                         void* dlogits, int64_t dlogits_stride, float* row_loss, int64_t rows,
                                         int64_t vocab, float scale, const float* inv_count, int64_t ignore_index,
                                         hipStream_t stream) {
-  if (!logits || !targets || !dlogits || !row_loss || rows <= 0 || vocab <= 0) return PT_EINVAL;
-  if ((vocab & 7) || (logits_stride & 7) || (dlogits_stride & 7)) return PT_EALIGN;
-  if (!pt_aligned16(logits) || !pt_aligned16(dlogits)) return PT_EALIGN;
+  if (!logits || !targets || !row_loss || rows <= 0 || vocab <= 0) return PT_EINVAL;
+  if ((vocab & 7) || (logits_stride & 7) || (dlogits && (dlogits_stride & 7))) return PT_EALIGN;
+  if (!pt_aligned16(logits) || (dlogits && !pt_aligned16(dlogits))) return PT_EALIGN;
   const auto* L = (const uint16_t*)logits;
   auto* D = (uint16_t*)dlogits;
   const int nc = (int)((vocab / 8 + kThreads - 1) / kThreads);

@@ -32,7 +32,9 @@ namespace {
 
 constexpr int BK = 64;
 
-enum Epilogue { EPI_BF16 = 0, EPI_BF16_ACC = 1, EPI_F32 = 2, EPI_F32_ACC = 3 };
+// EPI_BF16_RES: C = bf16(R + bf16(acc)) -- the residual add of model.py:207-208 fused into the
+// producing GEMM (R may alias C).
+enum Epilogue { EPI_BF16 = 0, EPI_BF16_ACC = 1, EPI_F32 = 2, EPI_F32_ACC = 3, EPI_BF16_RES = 4 };
 
 struct GemmArgs {
   const uint16_t* A;
@@ -46,6 +48,8 @@ struct GemmArgs {
   int64_t ldc[4];
   int64_t cseg[5];  // boundaries along M
   int ncseg;
+  const uint16_t* R;  // residual (EPI_BF16_RES), indexed like C segment 0
+  int64_t ldr;
   int M, N, K;
   int tiles_m, tiles_n;
 };
@@ -213,7 +217,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(GemmArgs a) {
   const int64_t ldc = a.ldc[cs];
   const int64_t mrow0 = m0 - a.cseg[cs] + wm * TM;
   const int ncol0 = n0 + wn * TN;
-  if (EPI == EPI_BF16 || EPI == EPI_BF16_ACC) {
+  if (EPI == EPI_BF16 || EPI == EPI_BF16_ACC || EPI == EPI_BF16_RES) {
     // stage this wave's TM x TN tile as bf16 rows in LDS, then write 16-B row segments
     constexpr int ROWB = TN * 2 + 16;  // +16 B pad: spreads the column-wise 2-B writes over banks
     lds_u8* st = smem + wave * (TM * ROWB);
@@ -238,10 +242,10 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(GemmArgs a) {
       bf16x8 v;
       v.w[0] = raw[0]; v.w[1] = raw[1]; v.w[2] = raw[2]; v.w[3] = raw[3];
       uint16_t* dst = C + (mrow0 + row) * ldc + ncol0 + ch * 8;
-      if (EPI == EPI_BF16_ACC) {
+      if (EPI == EPI_BF16_ACC || EPI == EPI_BF16_RES) {
         float o[8], f[8];
         unpack8(v, f);
-        unpack8(ld8(dst), o);
+        unpack8(ld8(EPI == EPI_BF16_ACC ? dst : a.R + (mrow0 + row) * a.ldr + ncol0 + ch * 8), o);
         // acc was rounded to bf16 once above; add in f32 and round again (== torch's bf16 add)
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] += f[e];
@@ -335,9 +339,10 @@ int pt_gemm_pick_tile(int64_t M, int64_t N, const int64_t* mseg, int nmseg, cons
 // 1 bf16 accumulate (C = bf16(C + bf16(acc))), 2 fp32 store, 3 fp32 accumulate.  tile: -1 = auto.
 int pt_gemm(const void* A, int64_t lda, int a_kcontig, const void* const* B, const int64_t* ldb,
             const int64_t* b_bounds, int nb, int b_kcontig, int b_seg_dim, void* const* C, const int64_t* ldc,
-            const int64_t* c_bounds, int nc, int64_t M, int64_t N, int64_t K, int epilogue, int tile,
-            hipStream_t stream) {
+            const int64_t* c_bounds, int nc, int64_t M, int64_t N, int64_t K, int epilogue,
+            const void* residual, int64_t ldr, int tile, hipStream_t stream) {
   if (!A || !B || !C || nb < 1 || nb > 4 || nc < 1 || nc > 4 || M <= 0 || N <= 0 || K <= 0) return PT_EINVAL;
+  if (epilogue == EPI_BF16_RES && (!residual || nc != 1 || !pt_aligned16(residual) || (ldr & 7))) return PT_EINVAL;
   if (K % BK) return PT_EUNSUPPORTED;
   if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX) return PT_EUNSUPPORTED;
   GemmArgs a{};
@@ -366,6 +371,8 @@ int pt_gemm(const void* A, int64_t lda, int a_kcontig, const void* const* B, con
   a.M = (int)M;
   a.N = (int)N;
   a.K = (int)K;
+  a.R = (const uint16_t*)residual;
+  a.ldr = ldr;
   // K-segment boundaries must be multiples of BK
   if (b_seg_dim == 1)
     for (int i = 0; i <= nb; ++i)
@@ -383,6 +390,9 @@ int pt_gemm(const void* A, int64_t lda, int a_kcontig, const void* const* B, con
     case EPI_BF16_ACC: return launch_epi<EPI_BF16_ACC>(a, a_kcontig, b_kcontig, tile, stream);
     case EPI_F32: return launch_epi<EPI_F32>(a, a_kcontig, b_kcontig, tile, stream);
     case EPI_F32_ACC: return launch_epi<EPI_F32_ACC>(a, a_kcontig, b_kcontig, tile, stream);
+    case EPI_BF16_RES:  // forward projections only (weights K-contiguous)
+      if (!a_kcontig || !b_kcontig) return PT_EUNSUPPORTED;
+      return launch_layout<true, true, EPI_BF16_RES>(a, tile, stream);
     default: return PT_EINVAL;
   }
 }

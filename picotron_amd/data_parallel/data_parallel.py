@@ -1,0 +1,113 @@
+"""Data parallelism: naive per-parameter and bucketed gradient all-reduce over cp_dp_group.
+
+Mirrors picotron/data_parallel/data_parallel.py (okoge-kaz/picotron @ 2025-03-02):
+DataParallelNaive (:10-60) and DataParallelBucket (:62-170) with the same interface
+(`require_backward_grad_sync`, `no_sync()`, `reset()`, `backward(...)` for the PP engine,
+`bucket_manager`), fp32 `main_grad` accumulation and the post-backward callback that waits for the
+buckets and sets `p.grad = main_grad.to(p.dtype)` (:153-165).
+
+Two gradient paths feed the buckets:
+  * parameters whose gradient comes from autograd (the embedding) use the reference's hook on the
+    gradient accumulator (:93-144): main_grad += grad; grad = None;
+  * parameters consumed by the fused kernels (every projection and norm weight) have their
+    gradient written into main_grad by the kernel epilogue itself; the kernels then call
+    `param._pt_grad_ready`, which does the reference hook's remaining work (queue the
+    post-backward callback, mark the parameter ready).
+"""
+import contextlib
+
+import torch
+import torch.distributed as dist
+from torch import nn
+from torch.autograd import Variable
+
+from .. import process_group_manager as pgm
+from .bucket import BucketManager
+
+
+class DataParallelNaive(nn.Module):
+    def __init__(self, module):
+        super().__init__()
+        self.module = module
+        self.require_backward_grad_sync = True
+        for p in self.module.parameters():
+            if p.requires_grad:
+                p.register_post_accumulate_grad_hook(self._allreduce_grads)
+
+    def forward(self, *inputs, **kwargs):
+        return self.module(*inputs, **kwargs)
+
+    def _allreduce_grads(self, param):
+        if self.require_backward_grad_sync and param.grad is not None:
+            m = pgm.current()
+            dist.all_reduce(param.grad, op=dist.ReduceOp.SUM, group=m.cp_dp_group)
+            param.grad /= m.cp_dp_world_size
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        self.require_backward_grad_sync = False
+        yield
+        self.require_backward_grad_sync = True
+
+
+class DataParallelBucket(nn.Module):
+    def __init__(self, module, bucket_cap_mb=25, grad_type=torch.float32):
+        super().__init__()
+        self.module = module
+        self.require_backward_grad_sync = True
+        grad_size = 2 if grad_type == torch.bfloat16 else 4
+        bucket_size = bucket_cap_mb * 1024 * 1024 // grad_size
+        self.bucket_manager = BucketManager(module.parameters(), pgm.current().cp_dp_group, bucket_size, grad_type)
+        self.register_backward_hook()
+        self._post_backward_callback_set = False
+
+    def forward(self, *inputs, **kwargs):
+        return self.module(*inputs, **kwargs)
+
+    def backward(self, input_tensor, output_tensor, output_tensor_grad):
+        return self.module.backward(input_tensor, output_tensor, output_tensor_grad)
+
+    def register_backward_hook(self):
+        self.grad_accs = []
+        for param in self.module.parameters():
+            if param.requires_grad:
+                param_tmp = param.expand_as(param)
+                grad_acc_fn = param_tmp.grad_fn.next_functions[0][0]
+                grad_acc_fn.register_hook(self._make_param_hook(param))
+                self.grad_accs.append(grad_acc_fn)
+                param._pt_grad_ready = self._fused_grad_ready
+
+    def _ready(self, param):
+        if self.require_backward_grad_sync:
+            if not self._post_backward_callback_set:
+                Variable._execution_engine.queue_callback(self._post_backward)
+                self._post_backward_callback_set = True
+            self.bucket_manager.mark_param_as_ready(param)
+
+    def _make_param_hook(self, param):
+        def param_hook(*unused):
+            if param.requires_grad:
+                assert param.grad is not None
+                param.main_grad.add_(param.grad.data)
+                param.grad = None
+                self._ready(param)
+        return param_hook
+
+    def _fused_grad_ready(self, param):
+        self._ready(param)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        self.require_backward_grad_sync = False
+        yield
+        self.require_backward_grad_sync = True
+
+    def _post_backward(self):
+        self.bucket_manager.wait()
+        self._post_backward_callback_set = False
+        for p in self.module.parameters():
+            if p.requires_grad:
+                p.grad = p.main_grad.to(p.dtype)
+
+    def reset(self):
+        self.bucket_manager.reset()

@@ -1,0 +1,405 @@
+"""Autograd functions of the decoder-layer hot path, composed from the gfx950 kernels.
+
+Each Function mirrors the saved-tensor contract of the reference op it replaces and launches only
+HIP kernels from csrc/ (through kernels.py); collectives go through torch.distributed (RCCL).
+There is no eager/CPU fallback: without the HIP library every forward raises.
+
+Reference (okoge-kaz/picotron @ 2025-03-02, paths relative to the checkout):
+  * DecoderLayer.forward             picotron/model.py:204-209
+  * Attention.forward                picotron/model.py:122-162
+  * MLP.forward                      picotron/model.py:184-186
+  * TritonRMSNorm / LlamaRMSNorm     picotron/model.py:39-86
+  * Column/Row TP linears            picotron/tensor_parallel/tensor_parallel.py:116-123,184-189
+  * f / g conjugate TP collectives   picotron/tensor_parallel/tp_communications.py:19-49,74-101
+  * F.cross_entropy / grad_acc       train.py:46-49
+
+Layout: activations are token-major 2-D [T = B*S, features] bf16 buffers.  The fused projection
+outputs ([T, q|k|v], [T, gate|up]) are consumed in place by strided kernels; nothing is transposed.
+
+Weight gradients are written straight into the gradient buffer by the wgrad GEMM epilogue
+(`_wgrad_target`): bf16 `param.grad` accumulation when there is no data parallelism (what autograd
+does for the reference at DP=1) or fp32 `param.main_grad` when DataParallelBucket owns the
+gradients (data_parallel.py:122-144).  The Functions therefore return None for weight inputs and
+notify the gradient owner through `param._pt_grad_ready`.
+"""
+import math
+import os
+
+import torch
+import torch.distributed as dist
+
+from . import kernels as K
+
+BF16 = torch.bfloat16
+
+
+# ------------------------------------------------------------------------ gradient sinks
+def _wgrad_target(p):
+    """(buffer, epilogue) the wgrad GEMM of parameter p writes into."""
+    mg = getattr(p, "main_grad", None)
+    if mg is not None:
+        return mg, K.EPI_F32_ACC
+    if p.grad is None:
+        p.grad = torch.empty_like(p)
+        return p.grad, K.EPI_BF16
+    return p.grad, K.EPI_BF16_ACC
+
+
+def _grad_ready(p):
+    """Tell the owner of p's gradient (DataParallelBucket) that this backward's grad is in place."""
+    hook = getattr(p, "_pt_grad_ready", None)
+    if hook is not None:
+        hook(p)
+
+
+def wgrad(dy2d, x2d, params):
+    """dW_i = dY_i^T X for the column segments of dY; one launch when the sinks agree."""
+    targets = [_wgrad_target(p) for p in params]
+    epis = {e for _, e in targets}
+    if len(epis) == 1:
+        K.linear_wgrad(dy2d, x2d, [t for t, _ in targets], epilogue=epis.pop())
+    else:  # mixed sinks (one grad already allocated, another not): one launch per parameter
+        lo = 0
+        for (t, e), p in zip(targets, params):
+            n = p.shape[0]
+            K.linear_wgrad(dy2d[:, lo:lo + n], x2d, [t], epilogue=e)
+            lo += n
+    for p in params:
+        _grad_ready(p)
+
+
+def add_vector_grad(p, g):
+    """Accumulate a small (norm-weight) gradient g into p's sink."""
+    mg = getattr(p, "main_grad", None)
+    if mg is not None:
+        mg.add_(g)
+    elif p.grad is None:
+        p.grad = g
+    else:
+        p.grad.add_(g)
+    _grad_ready(p)
+
+
+# ------------------------------------------------------------------------ TP collectives
+class TPContext:
+    """The tp group as a layer sees it (process_group_manager.py:18,35-37 of the reference)."""
+
+    def __init__(self, group=None, world_size=1, rank=0):
+        self.group, self.world_size, self.rank = group, world_size, rank
+
+    @staticmethod
+    def current():
+        from . import process_group_manager as pgm
+        m = pgm.process_group_manager
+        if m is None or m.tp_world_size == 1:
+            return TPContext()
+        return TPContext(m.tp_group, m.tp_world_size, m.tp_rank)
+
+    def all_reduce(self, t, async_op=False):
+        """Sum over the tp group (tp_communications.py:32,44).  Identity at tp=1."""
+        if self.world_size == 1:
+            return None
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+
+
+def _contig2d(x):
+    x2 = x.reshape(-1, x.shape[-1])
+    return x2 if x2.is_contiguous() else x2.contiguous()
+
+
+# ------------------------------------------------------------------------ RMSNorm
+class RMSNormFunction(torch.autograd.Function):
+    """TritonRMSNorm (mode 0, model.py:51-65) / LlamaRMSNorm (mode 1, model.py:81-86)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, eps, mode):
+        x2 = _contig2d(x)
+        y, rstd, _ = K.rmsnorm_fwd(x2, weight, eps, mode)
+        ctx.save_for_backward(x2, weight, rstd)
+        ctx.mode, ctx.shape = mode, x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight, rstd = ctx.saved_tensors
+        dx, dw = K.rmsnorm_bwd(_contig2d(dy), x2, weight, rstd, ctx.mode)
+        if ctx.needs_input_grad[1]:
+            add_vector_grad(weight, dw)
+        return dx.view(ctx.shape), None, None, None
+
+
+class AddRMSNormFunction(torch.autograd.Function):
+    """flash-attn layer_norm_fn(x, w, residual=r, prenorm=True, is_rms_norm=True) as reachable from
+    TritonRMSNorm.forward (model.py:51-65): z = bf16(x + r); y = norm(z); returns (y, z)."""
+
+    @staticmethod
+    def forward(ctx, x, residual, weight, eps, mode):
+        x2, r2 = _contig2d(x), _contig2d(residual)
+        y, rstd, z = K.rmsnorm_fwd(x2, weight, eps, mode, residual=r2)
+        ctx.save_for_backward(z, weight, rstd)
+        ctx.mode, ctx.shape = mode, x.shape
+        return y.view(x.shape), z.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy, dz):
+        z, weight, rstd = ctx.saved_tensors
+        if dy is None:
+            dy = torch.zeros(ctx.shape, dtype=z.dtype, device=z.device)
+        dres = _contig2d(dz) if dz is not None else None
+        dx, dw = K.rmsnorm_bwd(_contig2d(dy), z, weight, rstd, ctx.mode, dres=dres)
+        if ctx.needs_input_grad[2]:
+            add_vector_grad(weight, dw)
+        dx = dx.view(ctx.shape)
+        return dx, dx, None, None, None
+
+
+# ------------------------------------------------------------------------ linear
+class LinearFunction(torch.autograd.Function):
+    """Y = X W^T (F.linear, no bias).  tp_reduce_fwd: sum Y over tp (RowParallelLinear's
+    ReduceFromModelParallelRegion, tp_communications.py:44); tp_reduce_bwd: sum dX over tp
+    (ColumnParallelLinear's CopyToModelParallelRegion, tp_communications.py:32), overlapped with the
+    dW GEMM as LinearWithAsyncAllReduce does (tp_communications.py:83-101)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, tp_reduce_fwd, tp_reduce_bwd):
+        x2 = _contig2d(x)
+        y = K.linear_fwd(x2, [weight])
+        if tp_reduce_fwd:
+            TPContext.current().all_reduce(y)
+        ctx.save_for_backward(x2, weight)
+        ctx.tp_reduce_bwd, ctx.xshape = tp_reduce_bwd, x.shape
+        return y.view(*x.shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight = ctx.saved_tensors
+        dy2 = _contig2d(dy)
+        dx = handle = None
+        if ctx.needs_input_grad[0]:
+            dx = K.linear_dgrad(dy2, [weight])
+            if ctx.tp_reduce_bwd:
+                handle = TPContext.current().all_reduce(dx, async_op=True)
+        if ctx.needs_input_grad[1]:
+            wgrad(dy2, x2, [weight])
+        if handle is not None:
+            handle.wait()
+        return (dx.view(ctx.xshape) if dx is not None else None), None, None, None
+
+
+def linear(x, weight, tp_reduce_fwd=False, tp_reduce_bwd=False):
+    return LinearFunction.apply(x, weight, tp_reduce_fwd, tp_reduce_bwd)
+
+
+# ------------------------------------------------------------------------ attention block
+def ring_enabled():
+    """model.py:148: the CONTEXT_PARALLEL switch set by apply_context_parallel."""
+    return os.getenv("CONTEXT_PARALLEL", "0") == "1"
+
+
+class AttnShape:
+    """Views of the fused [T, q | k | v] projection as token-major [B, S, heads, d] tensors."""
+
+    def __init__(self, B, S, nh, nkv, d):
+        self.B, self.S, self.nh, self.nkv, self.d = B, S, nh, nkv, d
+        self.T = B * S
+        self.wq, self.wkv = nh * d, nkv * d
+
+    def q(self, t):
+        return t[:, :self.wq].view(self.B, self.S, self.nh, self.d)
+
+    def k(self, t):
+        return t[:, self.wq:self.wq + self.wkv].view(self.B, self.S, self.nkv, self.d)
+
+    def v(self, t):
+        return t[:, self.wq + self.wkv:].view(self.B, self.S, self.nkv, self.d)
+
+
+def attention_core_fwd(qkv, sh, cos, sin, scale):
+    """RoPE on q|k in place (model.py:136-137), then causal flash attention (model.py:154) or the
+    ring (model.py:148-151).  Returns (o [B,S,nh,d] bf16, lse f32 [B,nh,S])."""
+    K.rope_(qkv, sh.nh + sh.nkv, sh.d, cos, sin, sh.S)
+    if ring_enabled():
+        from .context_parallel.context_parallel import ring_attention_tokens
+        return ring_attention_tokens(qkv, sh, scale, True)
+    return K.attn_fwd(sh.q(qkv), sh.k(qkv), sh.v(qkv), scale, True)
+
+
+def attention_core_bwd(do, qkv, o, lse, sh, cos, sin, scale):
+    """dq|dk|dv written into one [T, q|k|v] buffer, then the inverse rotation of dq|dk."""
+    dqkv = torch.empty_like(qkv)
+    if ring_enabled():
+        from .context_parallel.context_parallel import ring_attention_tokens_bwd
+        ring_attention_tokens_bwd(do, qkv, o, lse, sh, scale, True, dqkv)
+    else:
+        K.attn_bwd(do, sh.q(qkv), sh.k(qkv), sh.v(qkv), o, lse, scale, True,
+                   dq=sh.q(dqkv), dk=sh.k(dqkv), dv=sh.v(dqkv))
+    K.rope_(dqkv, sh.nh + sh.nkv, sh.d, cos, sin, sh.S, inverse=True)
+    return dqkv
+
+
+def attn_block_fwd(h2, wq, wk, wv, wo, cos, sin, sh, tp):
+    """h2 [T,H] -> (a [T,H], saved).  Row-parallel out_proj: a = sum over tp of o W_o^T."""
+    qkv = K.linear_fwd(h2, [wq, wk, wv])
+    scale = 1.0 / math.sqrt(sh.d)
+    o, lse = attention_core_fwd(qkv, sh, cos, sin, scale)
+    a = K.linear_fwd(o.view(sh.T, sh.wq), [wo])
+    tp.all_reduce(a)
+    return a, (qkv, o, lse)
+
+
+def attn_block_bwd(da, h2, saved, wq, wk, wv, wo, cos, sin, sh, tp, need_dx=True):
+    qkv, o, lse = saved
+    scale = 1.0 / math.sqrt(sh.d)
+    do2 = K.linear_dgrad(da, [wo])
+    wgrad(da, o.view(sh.T, sh.wq), [wo])
+    dqkv = attention_core_bwd(do2.view(sh.B, sh.S, sh.nh, sh.d), qkv, o, lse, sh, cos, sin, scale)
+    dh = handle = None
+    if need_dx:
+        dh = K.linear_dgrad(dqkv, [wq, wk, wv])
+        handle = tp.all_reduce(dh, async_op=True)
+    wgrad(dqkv, h2, [wq, wk, wv])
+    if handle is not None:
+        handle.wait()
+    return dh
+
+
+class AttentionFunction(torch.autograd.Function):
+    """Attention.forward (model.py:122-162) as one node: fused q|k|v GEMM, in-place RoPE, flash
+    attention, out_proj, with the Column/Row TP reductions."""
+
+    @staticmethod
+    def forward(ctx, x, wq, wk, wv, wo, cos, sin, nh, nkv, d):
+        B, S, _ = x.shape
+        sh = AttnShape(B, S, nh, nkv, d)
+        h2 = _contig2d(x)
+        a, saved = attn_block_fwd(h2, wq, wk, wv, wo, cos, sin, sh, TPContext.current())
+        ctx.save_for_backward(h2, *saved, wq, wk, wv, wo, cos, sin)
+        ctx.sh = sh
+        return a.view(B, S, -1)
+
+    @staticmethod
+    def backward(ctx, da):
+        h2, qkv, o, lse, wq, wk, wv, wo, cos, sin = ctx.saved_tensors
+        sh = ctx.sh
+        dh = attn_block_bwd(_contig2d(da), h2, (qkv, o, lse), wq, wk, wv, wo, cos, sin, sh, TPContext.current(),
+                            need_dx=ctx.needs_input_grad[0])
+        return (dh.view(sh.B, sh.S, -1) if dh is not None else None,) + (None,) * 9
+
+
+# ------------------------------------------------------------------------ MLP block
+def mlp_block_fwd(h2, wg, wu, wd, tp, residual=None):
+    """h2 [T,H] -> down(silu(gate) * up) (+ residual, entering the tp sum once, from tp rank 0)."""
+    I = wg.shape[0]
+    gu = K.linear_fwd(h2, [wg, wu])
+    hh = K.swiglu_fwd(gu[:, :I], gu[:, I:])
+    res = residual if (residual is not None and tp.rank == 0) else None
+    m = K.linear_fwd(hh, [wd], residual=res)
+    tp.all_reduce(m)
+    return m, (gu, hh)
+
+
+def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True):
+    gu, hh = saved
+    I = wg.shape[0]
+    dhh = K.linear_dgrad(dm, [wd])
+    wgrad(dm, hh, [wd])
+    dgu = torch.empty_like(gu)
+    K.swiglu_bwd(dhh, gu[:, :I], gu[:, I:], dg=dgu[:, :I], du=dgu[:, I:])
+    dh = handle = None
+    if need_dx:
+        dh = K.linear_dgrad(dgu, [wg, wu])
+        handle = tp.all_reduce(dh, async_op=True)
+    wgrad(dgu, h2, [wg, wu])
+    if handle is not None:
+        handle.wait()
+    return dh
+
+
+class MLPFunction(torch.autograd.Function):
+    """MLP.forward (model.py:184-186): gate|up in one GEMM, SwiGLU, down_proj."""
+
+    @staticmethod
+    def forward(ctx, x, wg, wu, wd):
+        h2 = _contig2d(x)
+        m, saved = mlp_block_fwd(h2, wg, wu, wd, TPContext.current())
+        ctx.save_for_backward(h2, *saved, wg, wu, wd)
+        ctx.shape = x.shape
+        return m.view(*x.shape[:-1], -1)
+
+    @staticmethod
+    def backward(ctx, dm):
+        h2, gu, hh, wg, wu, wd = ctx.saved_tensors
+        dh = mlp_block_bwd(_contig2d(dm), h2, (gu, hh), wg, wu, wd, TPContext.current(),
+                           need_dx=ctx.needs_input_grad[0])
+        return (dh.view(ctx.shape) if dh is not None else None), None, None, None
+
+
+# ------------------------------------------------------------------------ decoder layer
+class DecoderLayerFunction(torch.autograd.Function):
+    """DecoderLayer.forward (model.py:204-209) as one autograd node:
+
+        h1 = norm1(x);  a = Attn(h1);  z = x + a  (fused into norm2);  h2 = norm2(z)
+        out = z + MLP(h2)                  (residual fused into the down_proj epilogue)
+
+    Backward runs the same kernels in reverse; the residual gradients are fused into the norm
+    backward kernels (dres) and the TP dX all-reduces overlap the dW GEMMs."""
+
+    @staticmethod
+    def forward(ctx, x, w1, w2, wq, wk, wv, wo, wg, wu, wd, cos, sin, eps, mode, nh, nkv, d):
+        B, S, H = x.shape
+        sh = AttnShape(B, S, nh, nkv, d)
+        tp = TPContext.current()
+        x2 = _contig2d(x)
+        h1, rstd1, _ = K.rmsnorm_fwd(x2, w1, eps, mode)
+        a, asaved = attn_block_fwd(h1, wq, wk, wv, wo, cos, sin, sh, tp)
+        h2, rstd2, z = K.rmsnorm_fwd(a, w2, eps, mode, residual=x2)
+        out, msaved = mlp_block_fwd(h2, wg, wu, wd, tp, residual=z)
+        ctx.save_for_backward(x2, h1, rstd1, *asaved, z, h2, rstd2, *msaved,
+                              w1, w2, wq, wk, wv, wo, wg, wu, wd, cos, sin)
+        ctx.sh, ctx.mode = sh, mode
+        return out.view(B, S, H)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (x2, h1, rstd1, qkv, o, lse, z, h2, rstd2, gu, hh,
+         w1, w2, wq, wk, wv, wo, wg, wu, wd, cos, sin) = ctx.saved_tensors
+        sh, mode = ctx.sh, ctx.mode
+        tp = TPContext.current()
+        dout2 = _contig2d(dout)
+        dh2 = mlp_block_bwd(dout2, h2, (gu, hh), wg, wu, wd, tp)
+        dz, dw2 = K.rmsnorm_bwd(dh2, z, w2, rstd2, mode, dres=dout2)
+        add_vector_grad(w2, dw2)
+        dh1 = attn_block_bwd(dz, h1, (qkv, o, lse), wq, wk, wv, wo, cos, sin, sh, tp)
+        dx, dw1 = K.rmsnorm_bwd(dh1, x2, w1, rstd1, mode, dres=dz)
+        add_vector_grad(w1, dw1)
+        return (dx.view(sh.B, sh.S, -1),) + (None,) * 16
+
+
+# ------------------------------------------------------------------------ cross entropy
+class CrossEntropyFunction(torch.autograd.Function):
+    """F.cross_entropy(logits [N, V], targets [N], reduction='mean') as called at train.py:49.
+    Forward reads the logits once for the per-row loss; backward writes
+    (softmax - onehot) * grad / #valid in one more read + write, with the incoming gradient (the
+    reference's `/ grad_acc_steps`) taken from device memory -- no host synchronisation."""
+
+    @staticmethod
+    def forward(ctx, logits, targets, ignore_index):
+        lg = _contig2d(logits)
+        tg = targets.reshape(-1)
+        loss, inv_count = K.cross_entropy_loss(lg, tg, ignore_index)
+        ctx.save_for_backward(lg, tg, inv_count)
+        ctx.ignore_index, ctx.shape = ignore_index, logits.shape
+        return loss.to(logits.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        lg, tg, inv_count = ctx.saved_tensors
+        dl = K.cross_entropy_grad(lg, tg, g.float().reshape(1) * inv_count, ctx.ignore_index)
+        return dl.view(ctx.shape), None, None
+
+
+def cross_entropy(input, target, reduction="mean", ignore_index=-100):
+    """Drop-in for F.cross_entropy(outputs [N, V], target_ids [N], reduction='mean') of train.py:49."""
+    if reduction != "mean":
+        raise ValueError("picotron_amd.cross_entropy implements reduction='mean' (train.py:49)")
+    return CrossEntropyFunction.apply(input, target, ignore_index)

@@ -124,18 +124,85 @@ def cross_entropy_fwd_bwd(logits, targets, scale=1.0, ignore_index=-100, inplace
     return loss, dlogits, inv_count
 
 
+def cross_entropy_loss(logits, targets, ignore_index=-100):
+    """Forward only: (mean loss f32 scalar tensor, inv_count [1] f32) -- one read of the logits."""
+    _bf16_rowmajor(logits, "logits")
+    rows, vocab = logits.shape
+    _req(targets.dtype == torch.int64 and targets.numel() == rows, "targets: int64 [rows]")
+    targets = targets.contiguous()
+    inv_count = (1.0 / (targets != ignore_index).sum().clamp_min(1).to(torch.float32)).reshape(1)
+    row_loss = torch.empty(rows, dtype=torch.float32, device=logits.device)
+    rc = _C.lib().pt_cross_entropy_fwd_bwd(_ptr(logits), logits.stride(0), _ptr(targets), None, 0, _ptr(row_loss),
+                                           rows, vocab, 1.0, None, int(ignore_index), _C.stream_ptr())
+    _C.check(rc, "pt_cross_entropy_fwd_bwd(loss)")
+    return row_loss.sum() * inv_count[0], inv_count
+
+
+def cross_entropy_grad(logits, targets, scale_dev, ignore_index=-100):
+    """dlogits = (softmax - onehot) * scale_dev[0] (a device scalar, e.g. grad_output / #valid)."""
+    _bf16_rowmajor(logits, "logits")
+    rows, vocab = logits.shape
+    targets = targets.contiguous()
+    _req(scale_dev.dtype == torch.float32 and scale_dev.numel() == 1, "scale: f32 device scalar")
+    scale_dev = scale_dev.contiguous()
+    dl = torch.empty(rows, vocab, dtype=BF16, device=logits.device)
+    row_loss = torch.empty(rows, dtype=torch.float32, device=logits.device)
+    rc = _C.lib().pt_cross_entropy_fwd_bwd(_ptr(logits), logits.stride(0), _ptr(targets), _ptr(dl), dl.stride(0),
+                                           _ptr(row_loss), rows, vocab, 1.0, _ptr(scale_dev), int(ignore_index),
+                                           _C.stream_ptr())
+    _C.check(rc, "pt_cross_entropy_fwd_bwd(grad)")
+    return dl
+
+
 # ------------------------------------------------------------------------------------ GEMM
-EPI_BF16, EPI_BF16_ACC, EPI_F32, EPI_F32_ACC = 0, 1, 2, 3
+EPI_BF16, EPI_BF16_ACC, EPI_F32, EPI_F32_ACC, EPI_BF16_RES = 0, 1, 2, 3, 4
+
+
+class GemmProbe:
+    """Live timing of every GEMM launch (bench.py's roofline): a pair of HIP events recorded on
+    the launch stream around each pt_gemm call, plus its algorithmic FLOPs (2*M*N*K)."""
+
+    def __init__(self):
+        self.records = []
+
+    def __enter__(self):
+        global _PROBE
+        _PROBE = self
+        return self
+
+    def __exit__(self, *exc):
+        global _PROBE
+        _PROBE = None
+
+    def summary(self):
+        torch.cuda.synchronize()
+        ms = [s.elapsed_time(e) for s, e, _ in self.records]
+        flops = [f for _, _, f in self.records]
+        n = len(ms)
+        return {"launches": n, "total_ms": sum(ms), "total_flop": sum(flops),
+                "avg_ms": sum(ms) / max(n, 1), "avg_flop": sum(flops) / max(n, 1)}
+
+
+_PROBE = None
 
 
 def _gemm(A, lda, a_kcontig, Bs, ldbs, b_bounds, b_kcontig, b_seg_dim, Cs, ldcs, c_bounds, M, N, K, epilogue,
-          tile=-1):
+          tile=-1, residual=None, ldr=0):
     lib = _C.lib()
     nb, nc = len(Bs), len(Cs)
+    probe = _PROBE
+    if probe is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
     rc = lib.pt_gemm(_ptr(A), lda, int(a_kcontig), _C.ptrarr([_ptr(b) for b in Bs]), _C.i64arr(ldbs),
                      _C.i64arr(b_bounds), nb, int(b_kcontig), int(b_seg_dim), _C.ptrarr([_ptr(c) for c in Cs]),
-                     _C.i64arr(ldcs), _C.i64arr(c_bounds), nc, M, N, K, int(epilogue), int(tile), _C.stream_ptr())
+                     _C.i64arr(ldcs), _C.i64arr(c_bounds), nc, M, N, K, int(epilogue), _ptr(residual), int(ldr),
+                     int(tile), _C.stream_ptr())
     _C.check(rc, f"pt_gemm(M={M}, N={N}, K={K}, a_k={a_kcontig}, b_k={b_kcontig}, epi={epilogue})")
+    if probe is not None:
+        ev1.record()
+        probe.records.append((ev0, ev1, 2.0 * M * N * K))
 
 
 def _bounds(sizes):
@@ -145,8 +212,9 @@ def _bounds(sizes):
     return out
 
 
-def linear_fwd(x2d, weights, out=None, tile=-1):
-    """Y = x . [W_0; W_1; ...]^T  -> [T, sum N_i] (one launch; F.linear of model.py:124-126,186)."""
+def linear_fwd(x2d, weights, out=None, tile=-1, residual=None):
+    """Y = x . [W_0; W_1; ...]^T  -> [T, sum N_i] (one launch; F.linear of model.py:124-126,186).
+    residual [T, N]: Y = residual + x W^T (the residual add of model.py:208 in the epilogue)."""
     _bf16_rowmajor(x2d, "x")
     T, K = x2d.shape
     for w in weights:
@@ -155,8 +223,13 @@ def linear_fwd(x2d, weights, out=None, tile=-1):
     N = sum(ns)
     y = out if out is not None else torch.empty(T, N, dtype=BF16, device=x2d.device)
     _req(y.stride(1) == 1 and y.shape == (T, N), "out shape")
+    epi, ldr = EPI_BF16, 0
+    if residual is not None:
+        _bf16_rowmajor(residual, "residual")
+        _req(tuple(residual.shape) == (T, N), "residual shape")
+        epi, ldr = EPI_BF16_RES, residual.stride(0)
     _gemm(x2d, x2d.stride(0), 1, weights, [K] * len(weights), _bounds(ns), 1, 0, [y], [y.stride(0)], [0, T],
-          T, N, K, EPI_BF16, tile)
+          T, N, K, epi, tile, residual=residual, ldr=ldr)
     return y
 
 
@@ -209,15 +282,22 @@ def attn_fwd(q, k, v, scale, causal, out=None, lse=None, merge=False):
     return out, lse
 
 
+def attn_delta(dout, out):
+    """delta[b, h, q] = sum_d dO * O  (f32 [B, H, Sq]) for the backward (FA2 'D')."""
+    B, Sq, H, D = out.shape
+    delta = torch.empty(B, H, Sq, dtype=torch.float32, device=out.device)
+    rc = _C.lib().pt_attn_bwd_delta(_ptr(dout), _str3(dout), _ptr(out), _str3(out), _ptr(delta), B, H, Sq, D,
+                                    _C.stream_ptr())
+    _C.check(rc, "pt_attn_bwd_delta")
+    return delta
+
+
 def attn_bwd(dout, q, k, v, out, lse, scale, causal, dq=None, dk=None, dv=None, grad_f32=False, delta=None):
     B, Sq, H, D = q.shape
     Sk, HKV = k.shape[1], k.shape[2]
     lib = _C.lib()
     if delta is None:
-        delta = torch.empty(B, H, Sq, dtype=torch.float32, device=q.device)
-        rc = lib.pt_attn_bwd_delta(_ptr(dout), _str3(dout), _ptr(out), _str3(out), _ptr(delta), B, H, Sq, D,
-                                   _C.stream_ptr())
-        _C.check(rc, "pt_attn_bwd_delta")
+        delta = attn_delta(dout, out)
     gdt = torch.float32 if grad_f32 else BF16
     if dq is None:
         dq = (torch.zeros if grad_f32 else torch.empty)(B, Sq, H, D, dtype=gdt, device=q.device)
