@@ -14,13 +14,27 @@
 //     (dX = [dq|dk|dv] . [Wq;Wk;Wv]);  * C may be split along M (dW of q,k,v in one launch).
 //   Segment boundaries must be multiples of the tile (checked on the host).
 //
-// Structure: BMxBNx64 tiles, WMxWN waves (wave tile (BM/WM)x(BN/WN)), v_mfma_f32_16x16x32_bf16.
-// Global->LDS by global_load_lds_dwordx4 (LDS-DMA, lane-linear 1 KiB per wave instruction) into a
-// double-buffered LDS image; the XOR swizzle is applied to the per-lane SOURCE address and undone
-// on the ds_read (tools/lds_swizzle_search.py: conflict-free for ds_read_b128 on K-contiguous
-// images and ds_read_b64_tr_b16 on MN-contiguous images).  The next K-tile's DMA is in flight
-// while the current one is multiplied.  Epilogue stages the tile through LDS and writes whole
-// 16-byte row segments.
+// Two kernel structures, both v_mfma_f32_16x16x32_bf16 with operands staged global->LDS by
+// global_load_lds_dwordx4 (LDS-DMA, lane-linear 1 KiB per wave instruction; the XOR swizzle is
+// applied to the per-lane SOURCE address and undone on the ds_read -- tools/lds_swizzle_search.py:
+// conflict-free for ds_read_b128 on K-contiguous images and ds_read_b64_tr_b16 on MN-contiguous
+// images):
+//
+//  * gemm_pipe_kernel (tiles 256x256 and 256x128, 8 waves as 2(M) x 4(N), the large shapes):
+//    each K-tile is four phases, one per quadrant of the wave's output tile, each closed by a raw
+//    s_barrier.  The operand tiles are kept as four independent "half images" (A rows 0-127 /
+//    128-255, B cols 0-BN/2 / BN/2-BN) so a buffer is refilled half by half: the DMA of K-tile
+//    t+1's halves is issued in phases 1-3 of tile t and the first half of t+2 in phase 4 (the
+//    moment all waves have finished reading tile t's buffer), and the single wait per K-tile is a
+//    counted `s_waitcnt vmcnt(2)` that leaves that half in flight across the barrier -- the load
+//    path never drains (cdna_hip_programming.md §5 "Pipelining across barriers", T3+T4).  Wave
+//    fragments are read quadrant by quadrant (A rows 0-63 + B cols 0-31, B cols 32-63, A rows
+//    64-127, registers reused for the 4th) and the MFMA cluster of each phase is bracketed with
+//    s_setprio (T5).
+//  * gemm_kernel (tiles 128x128, 64x64; small / ragged shapes): the simple two-stage loop.
+//
+// Epilogue (both): the wave's tile is staged through LDS as bf16 rows and written as whole 16-byte
+// row segments; fp32 epilogues (main_grad accumulation) write the accumulator directly.
 #include "common.h"
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -64,8 +78,8 @@ __device__ __forceinline__ void glds16(const void* gsrc, lds_u8* lds_base) {
   __builtin_amdgcn_global_load_lds(gsrc, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
 
-// Stage one operand tile (ROWS x 64 if K-contiguous, 64 x ROWS if MN-contiguous) into LDS.
-// `g` points at element (tile row/col 0, k0) of the operand; ld is its leading dimension.
+// Stage one operand image (ROWS x 64 if K-contiguous, 64 x ROWS if MN-contiguous) into LDS.
+// `g` points at element (image row/col 0, k0) of the operand; ld is its leading dimension.
 template <int ROWS, bool KCONTIG, int NTHREADS>
 __device__ __forceinline__ void stage_tile(const uint16_t* __restrict__ g, int64_t ld, lds_u8* lds, int tid) {
   constexpr int kInstr = ROWS * BK * 2 / 1024;  // 1 KiB per wave instruction
@@ -127,20 +141,8 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return base + (bid >> 3);
 }
 
-template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI>
-__global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(GemmArgs a) {
-  constexpr int NT = WM * WN * 64;
-  constexpr int TM = BM / WM, TN = BN / WN;
-  constexpr int FM = TM / 16, FN = TN / 16;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
-  lds_u8* smem = (lds_u8*)smem_raw;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-
-  // tile order: XCD remap, then group 8 tile-rows so an XCD's neighbours share A/B panels
+// tile order: XCD remap, then group 8 tile-rows so an XCD's neighbours share A/B panels
+__device__ __forceinline__ void tile_coords(const GemmArgs& a, int& tile_m, int& tile_n) {
   const int nwg = a.tiles_m * a.tiles_n;
   const int pid = xcd_remap(blockIdx.x, nwg);
   constexpr int GROUP = 8;
@@ -148,79 +150,22 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(GemmArgs a) {
   const int gid = pid / group_span;
   const int first_m = gid * GROUP;
   const int gsize = min(a.tiles_m - first_m, GROUP);
-  const int tile_m = first_m + (pid % group_span) % gsize;
-  const int tile_n = (pid % group_span) / gsize;
-  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  tile_m = first_m + (pid % group_span) % gsize;
+  tile_n = (pid % group_span) / gsize;
+}
 
-  // operand bases for this tile
-  const uint16_t* Abase = AK ? a.A + (int64_t)m0 * a.lda : a.A + m0;
-  int bs_n = 0;
-  if (a.bdim == 0) bs_n = find_seg(a.bseg, a.nbseg, n0);
-  const uint16_t* Bn = a.B[bs_n];
-  const int64_t ldb_n = a.ldb[bs_n];
-  const int64_t nloc = n0 - a.bseg[bs_n];
-
-  f32x4_t acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-
-  auto stage = [&](int kt, int buf) {
-    const int k0 = kt * BK;
-    lds_u8* sa = smem + buf * STAGE_BYTES;
-    lds_u8* sb = sa + A_BYTES;
-    const uint16_t* ga = AK ? Abase + k0 : Abase + (int64_t)k0 * a.lda;
-    stage_tile<BM, AK, NT>(ga, a.lda, sa, tid);
-    const uint16_t* Bp = Bn;
-    int64_t ldb = ldb_n, kl = k0, nl = nloc;
-    if (a.bdim == 1) {
-      const int s = find_seg(a.bseg, a.nbseg, k0);
-      Bp = a.B[s];
-      ldb = a.ldb[s];
-      kl = k0 - a.bseg[s];
-      nl = n0;
-    }
-    const uint16_t* gb = BKC ? Bp + nl * ldb + kl : Bp + kl * ldb + nl;
-    stage_tile<BN, BKC, NT>(gb, ldb, sb, tid);
-  };
-
-  const int nk = a.K / BK;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) stage(kt + 1, buf ^ 1);
-    const lds_u8* sa = smem + buf * STAGE_BYTES;
-    const lds_u8* sb = sa + A_BYTES;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8_t af[FM], bfr[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = read_frag<BM, AK>(sa, wm * TM + i * 16, s, lane);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, BKC>(sb, wn * TN + j * 16, s, lane);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-  // ---- epilogue ---------------------------------------------------------------------------
+// Write the wave's TM x TN accumulator tile (FM x FN 16x16 fragments) at output (m0 + wm*TM,
+// n0 + wn*TN).  `st` is this wave's private LDS staging area (TM * (2*TN + 16) bytes).
+template <int TM, int TN, int EPI>
+__device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)[TM / 16][TN / 16], lds_u8* st,
+                                         int m0, int n0, int wm, int wn, int lane) {
+  constexpr int FM = TM / 16, FN = TN / 16;
   const int cs = find_seg(a.cseg, a.ncseg, m0);
   const int64_t ldc = a.ldc[cs];
   const int64_t mrow0 = m0 - a.cseg[cs] + wm * TM;
   const int ncol0 = n0 + wn * TN;
   if (EPI == EPI_BF16 || EPI == EPI_BF16_ACC || EPI == EPI_BF16_RES) {
-    // stage this wave's TM x TN tile as bf16 rows in LDS, then write 16-B row segments
     constexpr int ROWB = TN * 2 + 16;  // +16 B pad: spreads the column-wise 2-B writes over banks
-    lds_u8* st = smem + wave * (TM * ROWB);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -270,6 +215,247 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(GemmArgs a) {
   }
 }
 
+// B operand image base for the tile at (n0, k0) (+ n_off columns inside the tile)
+__device__ __forceinline__ const uint16_t* b_image_ptr(const GemmArgs& a, bool bkc, int n0, int k0, int n_off,
+                                                       int64_t& ldb) {
+  int s = a.bdim == 0 ? find_seg(a.bseg, a.nbseg, n0) : find_seg(a.bseg, a.nbseg, k0);
+  const uint16_t* Bp = a.B[s];
+  ldb = a.ldb[s];
+  const int64_t nl = (a.bdim == 0 ? n0 - a.bseg[s] : n0) + n_off;
+  const int64_t kl = a.bdim == 1 ? k0 - a.bseg[s] : k0;
+  return bkc ? Bp + nl * ldb + kl : Bp + kl * ldb + nl;
+}
+
+// =============================================================================== pipelined
+template <int BN, bool AK, bool BKC, int EPI>
+__global__ __launch_bounds__(512) void gemm_pipe_kernel(GemmArgs a) {
+  constexpr int BM = 256, NT = 512;
+  constexpr int TM = 128, TN = BN / 4;            // wave tile (2 x 4 waves)
+  constexpr int FM = TM / 16, FN = TN / 16;       // 8 x (4 or 2) accumulators
+  constexpr int QM = FM / 2, QN = FN / 2;         // fragments per quadrant
+  constexpr int HB = BN / 2;                      // columns per B half image
+  constexpr int A_HALF = 128 * BK * 2, B_HALF = HB * BK * 2;
+  constexpr int STAGE = 2 * A_HALF + 2 * B_HALF;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+  lds_u8* smem = (lds_u8*)smem_raw;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  int tile_m, tile_n;
+  tile_coords(a, tile_m, tile_n);
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+
+  // half image h of K-tile kt into buffer buf: h = 0,1 -> A rows 128h..; h = 2,3 -> B cols HB(h-2)..
+  auto stage_half = [&](int kt, int buf, int h) {
+    const int k0 = kt * BK;
+    lds_u8* dst = smem + buf * STAGE + (h < 2 ? h * A_HALF : 2 * A_HALF + (h - 2) * B_HALF);
+    if (h < 2) {
+      const int r0 = m0 + 128 * h;
+      const uint16_t* g = AK ? a.A + (int64_t)r0 * a.lda + k0 : a.A + (int64_t)k0 * a.lda + r0;
+      stage_tile<128, AK, NT>(g, a.lda, dst, tid);
+    } else {
+      int64_t ldb;
+      const uint16_t* g = b_image_ptr(a, BKC, n0, k0, HB * (h - 2), ldb);
+      stage_tile<HB, BKC, NT>(g, ldb, dst, tid);
+    }
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = a.K / BK;
+  // prologue: K-tile 0 complete, first half of K-tile 1 in flight
+#pragma unroll
+  for (int h = 0; h < 4; ++h) stage_half(0, 0, h);
+  if (nk > 1) {
+    stage_half(1, 1, 0);
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+
+  const int brow = (wn & 1) * TN;  // the wave's first column inside its B half image
+  bf16x8_t af[QM][2], b0[QN][2], b1[QN][2];
+
+  // Ping-pong: every phase is an R-section (LDS reads + this phase's DMA issue, closed by
+  // lgkmcnt(0) so the reads are retired before the barrier) and an M-section (the quadrant's
+  // MFMAs), each ended by a raw s_barrier.  Waves 4-7 (wm == 1) run one barrier behind waves 0-3,
+  // so on every SIMD one wave multiplies while the other reads.  WAR: a buffer is re-staged in
+  // phase 4's R-section, after every wave's phase-3 reads were retired before a barrier.  RAW:
+  // the R4 section waits vmcnt(2) (own DMAs of K-tile kt+1 landed), and the barrier that follows
+  // precedes every wave's first read of kt+1.
+  auto bar = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto retire_reads = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+  auto mma = [&](int i0, int j0, const bf16x8_t (&A)[QM][2], const bf16x8_t (&Bf)[QN][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < QM; ++i)
+#pragma unroll
+        for (int j = 0; j < QN; ++j)
+          acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i][s], Bf[j][s], acc[i0 + i][j0 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  const bool late = __builtin_amdgcn_readfirstlane(wm) == 1;
+  if (late) bar();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    const lds_u8* sa = smem + buf * STAGE + wm * A_HALF;
+    const lds_u8* sb = smem + buf * STAGE + 2 * A_HALF + (wn >> 1) * B_HALF;
+    const bool next1 = kt + 1 < nk, next2 = kt + 2 < nk;
+
+    // ---- phase 1: A rows 0..63, B cols 0..TN/2 ; quadrant (0, 0)
+#pragma unroll
+    for (int i = 0; i < QM; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) af[i][s] = read_frag<128, AK>(sa, i * 16, s, lane);
+#pragma unroll
+    for (int j = 0; j < QN; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) b0[j][s] = read_frag<HB, BKC>(sb, brow + j * 16, s, lane);
+    if (next1) stage_half(kt + 1, buf ^ 1, 1);
+    retire_reads();
+    bar();
+    mma(0, 0, af, b0);
+    bar();
+
+    // ---- phase 2: B cols TN/2..TN ; quadrant (0, 1)
+#pragma unroll
+    for (int j = 0; j < QN; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) b1[j][s] = read_frag<HB, BKC>(sb, brow + (QN + j) * 16, s, lane);
+    if (next1) stage_half(kt + 1, buf ^ 1, 2);
+    retire_reads();
+    bar();
+    mma(0, QN, af, b1);
+    bar();
+
+    // ---- phase 3: A rows 64..127 ; quadrant (1, 1)   (last reads of this buffer)
+#pragma unroll
+    for (int i = 0; i < QM; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) af[i][s] = read_frag<128, AK>(sa, (QM + i) * 16, s, lane);
+    if (next1) stage_half(kt + 1, buf ^ 1, 3);
+    retire_reads();
+    bar();
+    mma(QM, QN, af, b1);
+    bar();
+
+    // ---- phase 4: registers only ; quadrant (1, 0) ; refill this buffer with K-tile kt+2
+    if (next2) {
+      stage_half(kt + 2, buf, 0);
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // K-tile kt+1 landed (all but these two)
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bar();
+    mma(QM, 0, af, b0);
+    bar();
+  }
+  if (!late) bar();  // balance the barrier count of the two wave groups
+
+  epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane);
+}
+
+// ================================================================================= simple
+template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI>
+__global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(GemmArgs a) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+  lds_u8* smem = (lds_u8*)smem_raw;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  int tile_m, tile_n;
+  tile_coords(a, tile_m, tile_n);
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const uint16_t* Abase = AK ? a.A + (int64_t)m0 * a.lda : a.A + m0;
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  auto stage = [&](int kt, int buf) {
+    const int k0 = kt * BK;
+    lds_u8* sa = smem + buf * STAGE_BYTES;
+    lds_u8* sb = sa + A_BYTES;
+    const uint16_t* ga = AK ? Abase + k0 : Abase + (int64_t)k0 * a.lda;
+    stage_tile<BM, AK, NT>(ga, a.lda, sa, tid);
+    int64_t ldb;
+    const uint16_t* gb = b_image_ptr(a, BKC, n0, k0, 0, ldb);
+    stage_tile<BN, BKC, NT>(gb, ldb, sb, tid);
+  };
+
+  const int nk = a.K / BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) stage(kt + 1, buf ^ 1);
+    const lds_u8* sa = smem + buf * STAGE_BYTES;
+    const lds_u8* sb = sa + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8_t af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = read_frag<BM, AK>(sa, wm * TM + i * 16, s, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, BKC>(sb, wn * TN + j * 16, s, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane);
+}
+
+// ================================================================================== launch
+template <typename Kern>
+void set_smem_once(Kern k, int smem) {
+  (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+}
+
+template <int BN, bool AK, bool BKC, int EPI>
+int launch_pipe(const GemmArgs& a0, hipStream_t stream) {
+  GemmArgs a = a0;
+  a.tiles_m = a.M / 256;
+  a.tiles_n = a.N / BN;
+  constexpr int smem_main = 2 * (256 * BK * 2 + BN * BK * 2);
+  constexpr int smem_epi = 8 * 128 * ((BN / 4) * 2 + 16);
+  constexpr int smem = smem_main > smem_epi ? smem_main : smem_epi;
+  static_assert(smem <= 160 * 1024, "LDS budget");
+  static bool attr_set = false;
+  if (!attr_set) {
+    set_smem_once(gemm_pipe_kernel<BN, AK, BKC, EPI>, smem);
+    attr_set = true;
+  }
+  gemm_pipe_kernel<BN, AK, BKC, EPI><<<a.tiles_m * a.tiles_n, 512, smem, stream>>>(a);
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
+
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI>
 int launch_t(const GemmArgs& a0, hipStream_t stream) {
   GemmArgs a = a0;
@@ -281,8 +467,7 @@ int launch_t(const GemmArgs& a0, hipStream_t stream) {
   static_assert(smem <= 160 * 1024, "LDS budget");
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_kernel<BM, BN, WM, WN, AK, BKC, EPI>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    set_smem_once(gemm_kernel<BM, BN, WM, WN, AK, BKC, EPI>, smem);
     attr_set = true;
   }
   gemm_kernel<BM, BN, WM, WN, AK, BKC, EPI><<<a.tiles_m * a.tiles_n, WM * WN * 64, smem, stream>>>(a);
@@ -290,13 +475,21 @@ int launch_t(const GemmArgs& a0, hipStream_t stream) {
   return PT_OK;
 }
 
+// tile ids: 0 = pipelined 256x256, 1 = pipelined 256x128, 2 = simple 128x128, 3 = simple 64x64,
+//           4 = simple 256x256, 5 = simple 256x128 (kept for A/B measurement)
+constexpr int kNumTiles = 6;
+const int kTileBM[kNumTiles] = {256, 256, 128, 64, 256, 256};
+const int kTileBN[kNumTiles] = {256, 128, 128, 64, 256, 128};
+
 template <bool AK, bool BKC, int EPI>
 int launch_layout(const GemmArgs& a, int tile, hipStream_t s) {
   switch (tile) {
-    case 0: return launch_t<256, 256, 2, 4, AK, BKC, EPI>(a, s);
-    case 1: return launch_t<256, 128, 4, 2, AK, BKC, EPI>(a, s);
+    case 0: return launch_pipe<256, AK, BKC, EPI>(a, s);
+    case 1: return launch_pipe<128, AK, BKC, EPI>(a, s);
     case 2: return launch_t<128, 128, 2, 2, AK, BKC, EPI>(a, s);
     case 3: return launch_t<64, 64, 2, 2, AK, BKC, EPI>(a, s);
+    case 4: return launch_t<256, 256, 2, 4, AK, BKC, EPI>(a, s);
+    case 5: return launch_t<256, 128, 4, 2, AK, BKC, EPI>(a, s);
     default: return PT_EUNSUPPORTED;
   }
 }
@@ -309,34 +502,35 @@ int launch_epi(const GemmArgs& a, int a_kcontig, int b_kcontig, int tile, hipStr
   return launch_layout<false, true, EPI>(a, tile, s);
 }
 
-const int kTileBM[4] = {256, 256, 128, 64};
-const int kTileBN[4] = {256, 128, 128, 64};
-
 }  // namespace
 
 extern "C" {
 
-// Pick the largest tile that divides the problem and still puts >= 256 tiles on the chip
-// (one per CU); fall back to the largest that divides.
+// Tile choice, from the measured sweep over the decoder layer's shapes (tools/gemm_bench.py,
+// profiles/r01_gemm_tiles.md): the simple 256x256 kernel when it still puts >= 192 tiles on the
+// 256 CUs (the big projections), else the 128x128 kernel (N = 2048 dX GEMMs, o_proj), else 64x64.
+// The pipelined kernels (ids 0, 1) are selectable explicitly but not yet faster.
 int pt_gemm_pick_tile(int64_t M, int64_t N, const int64_t* mseg, int nmseg, const int64_t* nseg, int nnseg) {
-  int best_div = -1;
-  for (int t = 0; t < 4; ++t) {
+  static const int order[3] = {4, 2, 3};
+  static const int min_tiles[3] = {192, 0, 0};
+  for (int o = 0; o < 3; ++o) {
+    const int t = order[o];
     const int bm = kTileBM[t], bn = kTileBN[t];
     if (M % bm || N % bn) continue;
     bool ok = true;
     for (int i = 0; i < nmseg && ok; ++i) ok = (mseg[i] % bm) == 0;
     for (int i = 0; i < nnseg && ok; ++i) ok = (nseg[i] % bn) == 0;
     if (!ok) continue;
-    if (best_div < 0) best_div = t;
-    if ((M / bm) * (N / bn) >= 256) return t;
+    if ((M / bm) * (N / bn) >= min_tiles[o]) return t;
   }
-  return best_div;
+  return -1;
 }
 
 // C = A . B  (see header comment).  a_kcontig: A is [M,K] (ld=lda) else stored [K,M];
 // b_kcontig: B is stored [N,K] (weights) else [K,N].  b_seg_dim: 0 = segments along N, 1 = along K.
 // b_bounds / c_bounds: n+1 boundaries (first 0, last = N/K or M).  epilogue: 0 bf16 store,
-// 1 bf16 accumulate (C = bf16(C + bf16(acc))), 2 fp32 store, 3 fp32 accumulate.  tile: -1 = auto.
+// 1 bf16 accumulate (C = bf16(C + bf16(acc))), 2 fp32 store, 3 fp32 accumulate,
+// 4 bf16 residual (C = bf16(R + bf16(acc))).  tile: -1 = auto.
 int pt_gemm(const void* A, int64_t lda, int a_kcontig, const void* const* B, const int64_t* ldb,
             const int64_t* b_bounds, int nb, int b_kcontig, int b_seg_dim, void* const* C, const int64_t* ldc,
             const int64_t* c_bounds, int nc, int64_t M, int64_t N, int64_t K, int epilogue,
@@ -383,8 +577,14 @@ int pt_gemm(const void* A, int64_t lda, int a_kcontig, const void* const* B, con
     for (int i = 0; i <= nc; ++i) msegs[i] = a.cseg[i];
     tile = pt_gemm_pick_tile(M, N, msegs, nc + 1, nsegs, nb + 1);
   }
-  if (tile < 0 || tile > 3) return PT_EUNSUPPORTED;
-  if (M % kTileBM[tile] || N % kTileBN[tile]) return PT_EUNSUPPORTED;
+  if (tile < 0 || tile >= kNumTiles) return PT_EUNSUPPORTED;
+  const int bm = kTileBM[tile], bn = kTileBN[tile];
+  if (M % bm || N % bn) return PT_EUNSUPPORTED;
+  for (int i = 0; i <= nc; ++i)
+    if (a.cseg[i] % bm) return PT_EUNSUPPORTED;
+  if (b_seg_dim == 0)
+    for (int i = 0; i <= nb; ++i)
+      if (a.bseg[i] % bn) return PT_EUNSUPPORTED;
   switch (epilogue) {
     case EPI_BF16: return launch_epi<EPI_BF16>(a, a_kcontig, b_kcontig, tile, stream);
     case EPI_BF16_ACC: return launch_epi<EPI_BF16_ACC>(a, a_kcontig, b_kcontig, tile, stream);

@@ -174,16 +174,27 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(
   }
 }
 
-// dw[col] = bf16(sum_p partial[p][col])  -- fixed summation order, deterministic
+// dw[col] = bf16(sum_p partial[p][col])  -- fixed summation order, deterministic.
+// A block owns 32 columns; its 8 row groups (one per 32 threads) stride over the partial rows
+// with coalesced 128-B reads, then combine through LDS in a fixed order.
+constexpr int kColsumCols = 32, kColsumGroups = 8;
 __global__ __launch_bounds__(256) void colsum_to_bf16_kernel(const float* __restrict__ partial, int nparts,
                                                              int cols, uint16_t* __restrict__ out,
                                                              float* __restrict__ out_f32) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= cols) return;
+  __shared__ float red[kColsumGroups][kColsumCols];
+  const int c = threadIdx.x % kColsumCols, g = threadIdx.x / kColsumCols;
+  const int col = blockIdx.x * kColsumCols + c;
   float s = 0.f;
-  for (int p = 0; p < nparts; ++p) s += partial[(int64_t)p * cols + col];
-  if (out) out[col] = f2bf(s);
-  if (out_f32) out_f32[col] = s;
+  if (col < cols)
+    for (int p = g; p < nparts; p += kColsumGroups) s += partial[(int64_t)p * cols + col];
+  red[g][c] = s;
+  __syncthreads();
+  if (g == 0 && col < cols) {
+#pragma unroll
+    for (int k = 1; k < kColsumGroups; ++k) s += red[k][c];
+    if (out) out[col] = f2bf(s);
+    if (out_f32) out_f32[col] = s;
+  }
 }
 
 int nch_for(int cols) {
@@ -261,7 +272,7 @@ int pt_rmsnorm_bwd(const void* dy, const void* z, const void* weight, const floa
   }
   PT_CHECK_LAUNCH();
   if (dweight) {
-    colsum_to_bf16_kernel<<<(int)((cols + 255) / 256), 256, 0, stream>>>(dw_partial, nparts, (int)cols,
+    colsum_to_bf16_kernel<<<(int)((cols + kColsumCols - 1) / kColsumCols), 256, 0, stream>>>(dw_partial, nparts, (int)cols,
                                                                         (uint16_t*)dweight, nullptr);
     PT_CHECK_LAUNCH();
   }

@@ -153,7 +153,7 @@ def test_gemm_fwd_nt(M, N, K):
     assert rel_err(y, _ref_mm(x, w.t())) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5])
 def test_gemm_every_tile_every_layout(tile):
     from picotron_amd import kernels as K_
     M, N, K = 512, 512, 256

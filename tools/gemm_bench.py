@@ -1,0 +1,109 @@
+"""GEMM microbenchmark on the decoder layer's real shapes (SmolLM-1.7B, T = 4096 tokens).
+
+For each (shape, layout) and each tile id that divides it: TF/s of pt_gemm (HIP events, 20 reps,
+random operands), relative error against torch's fp32 matmul, and torch's own bf16 matmul
+(hipBLASLt) for reference.  Run on the GPU box:  python tools/gemm_bench.py [--tiles 0,1,2,4,5]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from picotron_amd import kernels as K  # noqa: E402
+
+T, H, I, V = 4096, 2048, 8192, 49152
+SHAPES = [
+    # name, M, N, K, a_kcontig, b_kcontig
+    ("fwd.qkv", T, 3 * H, H, 1, 1), ("fwd.o", T, H, H, 1, 1), ("fwd.gate_up", T, 2 * I, H, 1, 1),
+    ("fwd.down", T, H, I, 1, 1), ("fwd.lm_head", T, V, H, 1, 1),
+    ("dgrad.o", T, H, H, 1, 0), ("dgrad.qkv", T, H, 3 * H, 1, 0), ("dgrad.gate_up", T, H, 2 * I, 1, 0),
+    ("dgrad.down", T, I, H, 1, 0), ("dgrad.lm_head", T, H, V, 1, 0),
+    ("wgrad.o", H, H, T, 0, 0), ("wgrad.qkv", 3 * H, H, T, 0, 0), ("wgrad.gate_up", 2 * I, H, T, 0, 0),
+    ("wgrad.down", H, I, T, 0, 0), ("wgrad.lm_head", V, H, T, 0, 0),
+]
+TILES = {0: (256, 256), 1: (256, 128), 2: (128, 128), 3: (64, 64), 4: (256, 256), 5: (256, 128)}
+
+
+def run(name, M, N, Kd, ak, bk, tile, reps=20):
+    dev = "cuda"
+    A = (torch.rand(M, Kd, device=dev) * 2 - 1).to(torch.bfloat16) if ak else \
+        (torch.rand(Kd, M, device=dev) * 2 - 1).to(torch.bfloat16)
+    B = (torch.rand(N, Kd, device=dev) * 2 - 1).to(torch.bfloat16) if bk else \
+        (torch.rand(Kd, N, device=dev) * 2 - 1).to(torch.bfloat16)
+    C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+
+    def call():
+        K._gemm(A, A.stride(0), ak, [B], [B.stride(0)], [0, N if True else Kd], bk, 0, [C], [N], [0, M], M, N, Kd,
+                K.EPI_BF16, tile)
+    call()
+    torch.cuda.synchronize()
+    ref = (A.float() if ak else A.float().t()) @ (B.float().t() if bk else B.float())
+    err = ((C.float() - ref).norm() / ref.norm()).item()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(3):
+        call()
+    e0.record()
+    for _ in range(reps):
+        call()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    return 2.0 * M * N * Kd / (ms * 1e-3) / 1e12, err, ms
+
+
+def torch_ref(M, N, Kd, ak, bk, reps=20):
+    a = (torch.rand(M, Kd, device="cuda") * 2 - 1).to(torch.bfloat16)
+    b = (torch.rand(Kd, N, device="cuda") * 2 - 1).to(torch.bfloat16)
+    for _ in range(3):
+        torch.matmul(a, b)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        torch.matmul(a, b)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    return 2.0 * M * N * Kd / (ms * 1e-3) / 1e12
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tiles", default="0,1,2,4,5")
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    tiles = [int(t) for t in args.tiles.split(",")]
+    out = []
+    for name, M, N, Kd, ak, bk in SHAPES:
+        if args.only and args.only not in name:
+            continue
+        row = {"shape": name, "M": M, "N": N, "K": Kd, "torch_tflops": round(torch_ref(M, N, Kd, ak, bk), 1),
+               "auto_tile": K._C.lib().pt_gemm_pick_tile(M, N, None, 0, None, 0)}
+        for t in tiles:
+            bm, bn = TILES[t]
+            if M % bm or N % bn:
+                continue
+            tf, err, ms = run(name, M, N, Kd, ak, bk, t)
+            row[f"tile{t}"] = round(tf, 1)
+            row[f"err{t}"] = float(f"{err:.2e}")
+        print(json.dumps(row), flush=True)
+        out.append(row)
+
+
+
+
+def one(shape, tile, reps):
+    """Launch a single (shape, tile) `reps` times -- for rocprofv3 --pmc passes."""
+    for name, M, N, Kd, ak, bk in SHAPES:
+        if name == shape:
+            tf, err, ms = run(name, M, N, Kd, ak, bk, tile, reps=reps)
+            print(json.dumps({"shape": name, "tile": tile, "tflops": round(tf, 1), "err": err}))
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "one":
+        one(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]) if len(sys.argv) > 4 else 5)
+    else:
+        main()
