@@ -86,8 +86,9 @@ class DataParallelBucket(nn.Module):
 
     def _make_param_hook(self, param):
         def param_hook(*unused):
-            if param.requires_grad:
-                assert param.grad is not None
+            # A fused kernel returns no gradient for its weights (it has written main_grad
+            # itself and called _fused_grad_ready); the accumulator node still runs, with grad None.
+            if param.requires_grad and param.grad is not None:
                 param.main_grad.add_(param.grad.data)
                 param.grad = None
                 self._ready(param)

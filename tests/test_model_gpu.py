@@ -194,3 +194,47 @@ def test_flash_attention_api_and_ring_pure_functions():
         ob, lb = CP.ring_attention_forward(q.cuda(), k.cuda(), v.cuda(), sc, causal)
         orf, lrf = O.attention_lse(q.float(), k.float(), v.float(), sc, causal)
         assert rel(ob, orf) < TOL and rel(lb, lrf) < 1e-3
+
+
+def test_data_parallel_bucket_fused_sinks_world1(monkeypatch):
+    """DataParallelBucket over the fused model (fp32 main_grad written by the wgrad epilogue,
+    grad_acc 2, world 1 on gloo): p.grad equals the plain bf16-accumulated gradients."""
+    import socket
+    import torch.distributed as dist
+    monkeypatch.setenv("FLASH_ATTEN", "1")
+    from picotron_amd import functional as FN
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.data_parallel.data_parallel import DataParallelBucket
+    from picotron_amd.model import Llama
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        pgm.setup_process_group_manager(1, 1, 1, 1)
+        cfg = cfg_tiny(layers=1)
+        torch.manual_seed(3)
+        with torch.device("cuda"):
+            model = Llama(cfg)
+        model.to(BF)
+        ref_state = {k: v.clone() for k, v in model.state_dict().items()}
+        g = torch.Generator().manual_seed(5)
+        ids = [torch.randint(0, cfg.vocab_size, (2, 129), generator=g) for _ in range(2)]
+        # reference: bf16 autograd accumulation (DP = 1 semantics)
+        for t in ids:
+            lo = model(t[:, :-1].cuda())
+            (FN.cross_entropy(lo.view(-1, cfg.vocab_size), t[:, 1:].reshape(-1).cuda()) / 2).backward()
+        want = {n: p.grad.float().clone() for n, p in model.named_parameters()}
+        model.zero_grad(set_to_none=True)
+        model.load_state_dict(ref_state)
+        dp = DataParallelBucket(model)
+        for i, t in enumerate(ids):
+            dp.require_backward_grad_sync = (i == 1)
+            lo = dp(t[:, :-1].cuda())
+            (FN.cross_entropy(lo.view(-1, cfg.vocab_size), t[:, 1:].reshape(-1).cuda()) / 2).backward()
+        for n, p in model.named_parameters():
+            assert p.grad is not None and p.grad.dtype == BF, n
+            assert rel(p.grad, want[n]) < 1e-2, n
+    finally:
+        dist.destroy_process_group()
+        pgm.setup_process_group_manager(1, 1, 1, 1)

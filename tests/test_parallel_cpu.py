@@ -1,0 +1,231 @@
+"""CPU (gloo, world_size 2-4) tests of the parallel host logic: the process grid, the TP f/g
+collectives, the DP gradient buckets (both the autograd-hook path and the fused-kernel sink path)
+and the ring-attention schedule (forward merge, backward dK/dV ring).
+
+The ring schedule runs with an oracle-backed block implementation injected by the test (the
+package's only implementation is the HIP kernel): the schedule, the p2p pattern and the merge
+algebra are what is under test, against full causal attention over the concatenated sequence."""
+import math
+
+import pytest
+import torch
+import torch.distributed as dist
+
+from tests import _dist
+
+
+# ----------------------------------------------------------------------------- process grid
+def _grid(rank, world):
+    from picotron_amd import process_group_manager as pgm
+    m = pgm.setup_process_group_manager(tp_size=2, cp_size=1, pp_size=1, dp_size=2)
+    # grid = arange(4).view(dp=2, pp=1, cp=1, tp=2): TP innermost (process_group_manager.py:13)
+    assert (m.dp_rank, m.tp_rank) == (rank // 2, rank % 2)
+    assert m.tp_group_ids == [rank - rank % 2, rank - rank % 2 + 1]
+    assert m.dp_group_ids == [rank % 2, rank % 2 + 2]
+    assert m.cp_dp_world_size == 2 and m.tp_world_size == 2
+    t = torch.tensor([float(rank)])
+    dist.all_reduce(t, group=m.tp_group)
+    assert t.item() == sum(m.tp_group_ids)
+    t = torch.tensor([float(rank)])
+    dist.all_reduce(t, group=m.cp_dp_group)
+    assert t.item() == sum(m.dp_group_ids)
+
+
+def test_process_grid_dp2_tp2():
+    _dist.run(_grid, 4)
+
+
+# ----------------------------------------------------------------------------- TP f / g
+def _tp_comms(rank, world):
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.tensor_parallel.tp_communications import (CopyToModelParallelRegion,
+                                                                GatherFromModelParallelRegion,
+                                                                ReduceFromModelParallelRegion)
+    pgm.setup_process_group_manager(tp_size=world, cp_size=1, pp_size=1, dp_size=1)
+    x = torch.full((2, 3), float(rank + 1), requires_grad=True)
+    y = CopyToModelParallelRegion.apply(x)            # identity fwd, all-reduce bwd
+    assert torch.equal(y, x)
+    y.backward(torch.ones(2, 3))
+    assert torch.equal(x.grad, torch.full((2, 3), float(world)))
+    x2 = torch.full((2, 3), float(rank + 1), requires_grad=True)
+    z = ReduceFromModelParallelRegion.apply(x2 * 1)   # all-reduce fwd, identity bwd
+    assert torch.equal(z, torch.full((2, 3), float(sum(range(1, world + 1)))))
+    z.backward(torch.ones(2, 3))
+    assert torch.equal(x2.grad, torch.ones(2, 3))
+    x3 = torch.full((2, 2), float(rank), requires_grad=True)
+    g = GatherFromModelParallelRegion.apply(x3 * 1)   # all-gather along the last dim, split bwd
+    assert g.shape == (2, 2 * world) and torch.equal(g[:, 2 * rank:2 * rank + 2], x3.detach())
+    g.backward(torch.arange(2 * 2 * world, dtype=torch.float32).view(2, 2 * world))
+    assert torch.equal(x3.grad, torch.arange(2 * 2 * world, dtype=torch.float32).view(2, 2 * world)[:, 2 * rank:2 * rank + 2])
+
+
+def test_tp_collectives_world2():
+    _dist.run(_tp_comms, 2)
+
+
+# ----------------------------------------------------------------------------- DP buckets
+class _FusedSinkLinear(torch.autograd.Function):
+    """A stand-in for the fused kernels' gradient path: writes dW straight into the parameter's
+    sink (main_grad when DataParallelBucket owns it) and returns None, like functional.wgrad."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return x @ w.t()
+
+    @staticmethod
+    def backward(ctx, dy):
+        from picotron_amd import functional as FN
+        x, w = ctx.saved_tensors
+        g = dy.t() @ x
+        if getattr(w, "main_grad", None) is not None:
+            w.main_grad.add_(g)
+        elif w.grad is None:
+            w.grad = g
+        else:
+            w.grad.add_(g)
+        FN._grad_ready(w)
+        return dy @ w, None
+
+
+class _Net(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        g = torch.Generator().manual_seed(0)
+        self.emb = torch.nn.Parameter(torch.randn(16, 8, generator=g))       # autograd-hook path
+        self.w1 = torch.nn.Parameter(torch.randn(8, 8, generator=g) / 3)     # fused-sink path
+        self.w2 = torch.nn.Parameter(torch.randn(4, 8, generator=g) / 3)
+
+    def forward(self, ids):
+        h = torch.nn.functional.embedding(ids, self.emb)
+        return _FusedSinkLinear.apply(torch.tanh(_FusedSinkLinear.apply(h, self.w1)), self.w2)
+
+
+def _dp_bucket(rank, world, bucket_mb):
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.data_parallel.data_parallel import DataParallelBucket
+    pgm.setup_process_group_manager(tp_size=1, cp_size=1, pp_size=1, dp_size=world)
+    model = DataParallelBucket(_Net(), bucket_cap_mb=bucket_mb)
+    ref = _Net()
+    ga = 3
+    grads = {n: torch.zeros_like(p) for n, p in ref.named_parameters()}
+    for i in range(ga):
+        g = torch.Generator().manual_seed(100 * i + rank)
+        ids = torch.randint(0, 16, (5,), generator=g)
+        model.require_backward_grad_sync = (i == ga - 1)
+        (model(ids).square().mean() / ga).backward()
+        ref.zero_grad()
+        (ref(ids).square().mean() / ga).backward()
+        for n, p in ref.named_parameters():
+            grads[n] += p.grad
+    for n, p in model.module.named_parameters():
+        want = grads[n].clone()
+        dist.all_reduce(want)
+        want /= world
+        torch.testing.assert_close(p.grad, want, rtol=1e-5, atol=1e-6)
+    model.reset()
+    for p in model.module.parameters():
+        assert p.main_grad.abs().sum().item() == 0.0
+
+
+@pytest.mark.parametrize("bucket_mb", [25, 0.0002])   # one bucket / one bucket per parameter
+def test_dp_bucket_grad_average(bucket_mb):
+    _dist.run(_dp_bucket, 2, bucket_mb)
+
+
+def test_bucket_assignment_matches_reference_rule():
+    """bucket.py:84-129: greedy in parameters() order; a parameter that does not fit opens a new
+    bucket; an oversized parameter gets a bucket of its own."""
+    import os
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    from picotron_amd.data_parallel import bucket as B
+
+    class PG:  # world-size-1 stand-in: only dist.get_world_size(group) is consulted
+        pass
+    orig = dist.get_world_size
+    dist.get_world_size = lambda group=None: 1
+    try:
+        ps = [torch.nn.Parameter(torch.zeros(n)) for n in (3, 4, 10, 2, 2, 1)]
+        bm = B.BucketManager(ps, PG(), bucket_size=8)
+        locs = [bm.params_to_bucket_location[p] for p in ps]
+        assert locs == [(0, 3, 0), (3, 7, 0), (0, 10, 1), (0, 2, 2), (2, 4, 2), (4, 5, 2)]
+        assert bm.bucket_sizes == [7, 10, 5]
+        assert ps[1].main_grad.data_ptr() == bm.grad_data_list[0][3:].data_ptr()
+    finally:
+        dist.get_world_size = orig
+
+
+# ----------------------------------------------------------------------------- ring attention
+class OracleBlocks:
+    """Per-block attention restated from the oracle (fp32), with the same accumulation contract as
+    the HIP kernels: fwd merges into (acc f32 [B,S,nh,d], lse f32 [B,nh,S]); bwd accumulates."""
+
+    @staticmethod
+    def _expand(t, nh):
+        tt = t.float().transpose(1, 2)
+        return tt.repeat_interleave(nh // tt.shape[1], dim=1)
+
+    @staticmethod
+    def fwd(q, k, v, scale, causal, acc, lse):
+        from oracle import picotron_oracle as O
+        nh = q.shape[2]
+        o, l = O.attention_lse(q.float().transpose(1, 2), OracleBlocks._expand(k, nh), OracleBlocks._expand(v, nh),
+                               scale, causal)
+        new = torch.logaddexp(lse, l)
+        w_old = torch.exp(lse - new).nan_to_num(0.0)
+        w_blk = torch.exp(l - new)
+        acc.mul_(w_old.transpose(1, 2).unsqueeze(-1)).add_(o.transpose(1, 2) * w_blk.transpose(1, 2).unsqueeze(-1))
+        lse.copy_(new)
+
+    @staticmethod
+    def delta(do, o):
+        return (do.float() * o.float()).sum(-1).transpose(1, 2).contiguous()
+
+    @staticmethod
+    def bwd(do, q, k, v, o, lse, delta, scale, causal, dq, dk, dv):
+        from oracle import picotron_oracle as O
+        nh, nkv = q.shape[2], k.shape[2]
+        dq_, dk_, dv_ = O.ring_attention_backward(do.float().transpose(1, 2), q.float().transpose(1, 2),
+                                                  OracleBlocks._expand(k, nh), OracleBlocks._expand(v, nh),
+                                                  o.float().transpose(1, 2), lse, scale, causal)
+        B, S, _, d = q.shape
+        dq += dq_.transpose(1, 2)
+        dk += dk_.view(B, nkv, nh // nkv, S, d).sum(2).transpose(1, 2)
+        dv += dv_.view(B, nkv, nh // nkv, S, d).sum(2).transpose(1, 2)
+
+
+def _ring(rank, world, nh, nkv):
+    from oracle import picotron_oracle as O
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.context_parallel import context_parallel as CP
+    pgm.setup_process_group_manager(tp_size=1, cp_size=world, pp_size=1, dp_size=1)
+    B, S, d = 2, 8, 16
+    g = torch.Generator().manual_seed(7)
+    q = torch.randn(B, world * S, nh, d, generator=g)
+    k = torch.randn(B, world * S, nkv, d, generator=g)
+    v = torch.randn(B, world * S, nkv, d, generator=g)
+    do = torch.randn(B, world * S, nh, d, generator=g)
+    sl = slice(rank * S, (rank + 1) * S)
+    scale = 1 / math.sqrt(d)
+    kv = torch.cat([k[:, sl].reshape(B * S, -1), v[:, sl].reshape(B * S, -1)], dim=1).contiguous()
+    acc, lse = CP.ring_forward(q[:, sl], kv, nkv, scale, True, blocks=OracleBlocks)
+    # reference: full causal attention over the whole sequence
+    qr = q.transpose(1, 2).requires_grad_(True)
+    kr = k.transpose(1, 2).repeat_interleave(nh // nkv, 1).detach().requires_grad_(True)
+    vr = v.transpose(1, 2).repeat_interleave(nh // nkv, 1).detach().requires_grad_(True)
+    o_ref, lse_ref = O.attention_lse(qr, kr, vr, scale, True)
+    torch.testing.assert_close(acc, o_ref.transpose(1, 2)[:, sl].detach(), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(lse, lse_ref[:, :, sl].detach(), rtol=1e-5, atol=1e-5)
+    (o_ref * do.transpose(1, 2)).sum().backward()
+    dq, dkv = CP.ring_backward(do[:, sl], q[:, sl], kv, acc, lse, nkv, scale, True, blocks=OracleBlocks)
+    torch.testing.assert_close(dq, qr.grad.transpose(1, 2)[:, sl], rtol=1e-4, atol=1e-5)
+    dk_ref = kr.grad.view(B, nkv, nh // nkv, world * S, d).sum(2).transpose(1, 2)[:, sl]
+    dv_ref = vr.grad.view(B, nkv, nh // nkv, world * S, d).sum(2).transpose(1, 2)[:, sl]
+    w = nkv * d
+    torch.testing.assert_close(dkv[:, :w].view(B, S, nkv, d), dk_ref, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(dkv[:, w:].view(B, S, nkv, d), dv_ref, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("world,nh,nkv", [(2, 2, 2), (4, 4, 2)])
+def test_ring_attention_schedule_matches_full_attention(world, nh, nkv):
+    _dist.run(_ring, world, nh, nkv)
