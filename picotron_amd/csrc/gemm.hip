@@ -216,18 +216,40 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
 }
 
 // B operand image base for the tile at (n0, k0) (+ n_off columns inside the tile)
+// Segment selection by a compare chain on constant indices: every kernarg load is loop-invariant
+// (hoisted into SGPRs) -- an indexed a.B[s] load would put a dependent scalar-memory round trip
+// in front of every DMA issue.
 __device__ __forceinline__ const uint16_t* b_image_ptr(const GemmArgs& a, bool bkc, int n0, int k0, int n_off,
                                                        int64_t& ldb) {
-  int s = a.bdim == 0 ? find_seg(a.bseg, a.nbseg, n0) : find_seg(a.bseg, a.nbseg, k0);
-  const uint16_t* Bp = a.B[s];
-  ldb = a.ldb[s];
-  const int64_t nl = (a.bdim == 0 ? n0 - a.bseg[s] : n0) + n_off;
-  const int64_t kl = a.bdim == 1 ? k0 - a.bseg[s] : k0;
-  return bkc ? Bp + nl * ldb + kl : Bp + kl * ldb + nl;
+  const int64_t x = a.bdim == 0 ? n0 : k0;
+  const uint16_t* Bp = a.B[0];
+  int64_t ld = a.ldb[0], base = 0;
+#pragma unroll
+  for (int i = 1; i < 4; ++i) {
+    const bool in = i < a.nbseg && x >= a.bseg[i];
+    Bp = in ? a.B[i] : Bp;
+    ld = in ? a.ldb[i] : ld;
+    base = in ? a.bseg[i] : base;
+  }
+  ldb = ld;
+  const int64_t nl = (a.bdim == 0 ? n0 - base : n0) + n_off;
+  const int64_t kl = a.bdim == 1 ? k0 - base : k0;
+  return bkc ? Bp + nl * ld + kl : Bp + kl * ld + nl;
 }
 
 // =============================================================================== pipelined
-template <int BN, bool AK, bool BKC, int EPI>
+// LDS holds two rings of half images: A halves (128 rows x 64 k, 16 KiB) in 5 slots and B halves
+// (BN/2 cols x 64 k) in 5 slots -- 2.5 K-tiles, 160 KiB at BN = 256.  Half images of K-tile u are
+// issued during the four phases of K-tile u-2, in the order A0, B0, B1, A1, each into the slot of
+// a half image whose last read retired at least one barrier earlier:
+//   A slot (2u + a) % 5 last held A1 of u-3 (a = 0) or A0 of u-2 (a = 1: read until phase 3 of
+//   u-2, re-staged in phase 4);  B slot (2u + b) % 5 last held B1 of u-3 or B0 of u-2 (read until
+//   phase 2, re-staged in phase 3).
+// DMAs are issued at the start of M-sections and LDS reads are retired inside the following
+// M-section (not before the barrier), so a slot is re-staged >= 2 barriers after its last read even
+// across the staggered wave groups.  The wait for K-tile u+1 (end of phase 3's M-section of u)
+// leaves K-tile u+2's first three halves in flight: vmcnt(6) (BN 256) / vmcnt(4) (BN 128).
+template <int BN, bool AK, bool BKC, int EPI, bool STAG>
 __global__ __launch_bounds__(512) void gemm_pipe_kernel(GemmArgs a) {
   constexpr int BM = 256, NT = 512;
   constexpr int TM = 128, TN = BN / 4;            // wave tile (2 x 4 waves)
@@ -235,7 +257,10 @@ __global__ __launch_bounds__(512) void gemm_pipe_kernel(GemmArgs a) {
   constexpr int QM = FM / 2, QN = FN / 2;         // fragments per quadrant
   constexpr int HB = BN / 2;                      // columns per B half image
   constexpr int A_HALF = 128 * BK * 2, B_HALF = HB * BK * 2;
-  constexpr int STAGE = 2 * A_HALF + 2 * B_HALF;
+  constexpr int NSLOT = 5;
+  constexpr int B_RING = NSLOT * A_HALF;          // byte offset of the B ring
+  constexpr int B_INSTR = B_HALF / 1024 / 8;      // DMA instructions per wave per B half (2 or 1)
+  constexpr int AHEAD = 2 * 2 + 2 * B_INSTR;      // a K-tile's DMA instructions per wave
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
   lds_u8* smem = (lds_u8*)smem_raw;
 
@@ -245,19 +270,17 @@ __global__ __launch_bounds__(512) void gemm_pipe_kernel(GemmArgs a) {
   tile_coords(a, tile_m, tile_n);
   const int m0 = tile_m * BM, n0 = tile_n * BN;
 
-  // half image h of K-tile kt into buffer buf: h = 0,1 -> A rows 128h..; h = 2,3 -> B cols HB(h-2)..
-  auto stage_half = [&](int kt, int buf, int h) {
-    const int k0 = kt * BK;
-    lds_u8* dst = smem + buf * STAGE + (h < 2 ? h * A_HALF : 2 * A_HALF + (h - 2) * B_HALF);
-    if (h < 2) {
-      const int r0 = m0 + 128 * h;
-      const uint16_t* g = AK ? a.A + (int64_t)r0 * a.lda + k0 : a.A + (int64_t)k0 * a.lda + r0;
-      stage_tile<128, AK, NT>(g, a.lda, dst, tid);
-    } else {
-      int64_t ldb;
-      const uint16_t* g = b_image_ptr(a, BKC, n0, k0, HB * (h - 2), ldb);
-      stage_tile<HB, BKC, NT>(g, ldb, dst, tid);
-    }
+  auto a_slot = [&](int u, int h) { return smem + ((2 * u + h) % NSLOT) * A_HALF; };
+  auto b_slot = [&](int u, int h) { return smem + B_RING + ((2 * u + h) % NSLOT) * B_HALF; };
+  auto stage_a = [&](int u, int h) {
+    const int k0 = u * BK, r0 = m0 + 128 * h;
+    const uint16_t* g = AK ? a.A + (int64_t)r0 * a.lda + k0 : a.A + (int64_t)k0 * a.lda + r0;
+    stage_tile<128, AK, NT>(g, a.lda, a_slot(u, h), tid);
+  };
+  auto stage_b = [&](int u, int h) {
+    int64_t ldb;
+    const uint16_t* g = b_image_ptr(a, BKC, n0, u * BK, HB * h, ldb);
+    stage_tile<HB, BKC, NT>(g, ldb, b_slot(u, h), tid);
   };
 
   f32x4_t acc[FM][FN];
@@ -267,12 +290,12 @@ __global__ __launch_bounds__(512) void gemm_pipe_kernel(GemmArgs a) {
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
   const int nk = a.K / BK;
-  // prologue: K-tile 0 complete, first half of K-tile 1 in flight
-#pragma unroll
-  for (int h = 0; h < 4; ++h) stage_half(0, 0, h);
+  // prologue: K-tiles 0 and 1 issued, K-tile 0 waited for
+  stage_a(0, 0); stage_b(0, 0); stage_b(0, 1); stage_a(0, 1);
   if (nk > 1) {
-    stage_half(1, 1, 0);
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    stage_a(1, 0); stage_b(1, 0); stage_b(1, 1); stage_a(1, 1);
+    if (B_INSTR == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -281,19 +304,15 @@ __global__ __launch_bounds__(512) void gemm_pipe_kernel(GemmArgs a) {
   const int brow = (wn & 1) * TN;  // the wave's first column inside its B half image
   bf16x8_t af[QM][2], b0[QN][2], b1[QN][2];
 
-  // Ping-pong: every phase is an R-section (LDS reads + this phase's DMA issue, closed by
-  // lgkmcnt(0) so the reads are retired before the barrier) and an M-section (the quadrant's
-  // MFMAs), each ended by a raw s_barrier.  Waves 4-7 (wm == 1) run one barrier behind waves 0-3,
-  // so on every SIMD one wave multiplies while the other reads.  WAR: a buffer is re-staged in
-  // phase 4's R-section, after every wave's phase-3 reads were retired before a barrier.  RAW:
-  // the R4 section waits vmcnt(2) (own DMAs of K-tile kt+1 landed), and the barrier that follows
-  // precedes every wave's first read of kt+1.
+  // Every phase = R-section (LDS reads, left in flight across the barrier) + M-section (one half
+  // image DMA + the quadrant's 16 / 8 MFMAs), each closed by a raw s_barrier.
+  // STAG: waves 4-7 run one barrier behind waves 0-3, so on each SIMD one wave multiplies while
+  // the other reads (ping-pong).
   auto bar = [] {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
-  auto retire_reads = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
   auto mma = [&](int i0, int j0, const bf16x8_t (&A)[QM][2], const bf16x8_t (&Bf)[QN][2]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -305,16 +324,15 @@ __global__ __launch_bounds__(512) void gemm_pipe_kernel(GemmArgs a) {
           acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i][s], Bf[j][s], acc[i0 + i][j0 + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
-  const bool late = __builtin_amdgcn_readfirstlane(wm) == 1;
+  const bool late = STAG && __builtin_amdgcn_readfirstlane(wm) == 1;
   if (late) bar();
 
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    const lds_u8* sa = smem + buf * STAGE + wm * A_HALF;
-    const lds_u8* sb = smem + buf * STAGE + 2 * A_HALF + (wn >> 1) * B_HALF;
-    const bool next1 = kt + 1 < nk, next2 = kt + 2 < nk;
+    const lds_u8* sa = a_slot(kt, wm);
+    const lds_u8* sb = b_slot(kt, wn >> 1);
+    const bool pre = kt + 2 < nk;
 
-    // ---- phase 1: A rows 0..63, B cols 0..TN/2 ; quadrant (0, 0)
+    // ---- phase 1: R: A rows 0..63, B cols 0..TN/2 | M: DMA A0 of kt+2, quadrant (0, 0)
 #pragma unroll
     for (int i = 0; i < QM; ++i)
 #pragma unroll
@@ -323,52 +341,52 @@ __global__ __launch_bounds__(512) void gemm_pipe_kernel(GemmArgs a) {
     for (int j = 0; j < QN; ++j)
 #pragma unroll
       for (int s = 0; s < 2; ++s) b0[j][s] = read_frag<HB, BKC>(sb, brow + j * 16, s, lane);
-    if (next1) stage_half(kt + 1, buf ^ 1, 1);
-    retire_reads();
     bar();
+    if (pre) stage_a(kt + 2, 0);
     mma(0, 0, af, b0);
     bar();
 
-    // ---- phase 2: B cols TN/2..TN ; quadrant (0, 1)
+    // ---- phase 2: R: B cols TN/2..TN (last B reads) | M: DMA B0 of kt+2, quadrant (0, 1)
 #pragma unroll
     for (int j = 0; j < QN; ++j)
 #pragma unroll
       for (int s = 0; s < 2; ++s) b1[j][s] = read_frag<HB, BKC>(sb, brow + (QN + j) * 16, s, lane);
-    if (next1) stage_half(kt + 1, buf ^ 1, 2);
-    retire_reads();
     bar();
+    if (pre) stage_b(kt + 2, 0);
     mma(0, QN, af, b1);
     bar();
 
-    // ---- phase 3: A rows 64..127 ; quadrant (1, 1)   (last reads of this buffer)
+    // ---- phase 3: R: A rows 64..127 (last A reads) | M: DMA B1 of kt+2 (into B0 of kt),
+    //      quadrant (1, 1), then wait for K-tile kt+1 (all but kt+2's three halves in flight)
 #pragma unroll
     for (int i = 0; i < QM; ++i)
 #pragma unroll
       for (int s = 0; s < 2; ++s) af[i][s] = read_frag<128, AK>(sa, (QM + i) * 16, s, lane);
-    if (next1) stage_half(kt + 1, buf ^ 1, 3);
-    retire_reads();
     bar();
+    if (pre) stage_b(kt + 2, 1);
     mma(QM, QN, af, b1);
-    bar();
-
-    // ---- phase 4: registers only ; quadrant (1, 0) ; refill this buffer with K-tile kt+2
-    if (next2) {
-      stage_half(kt + 2, buf, 0);
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // K-tile kt+1 landed (all but these two)
+    if (pre) {
+      if (B_INSTR == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     bar();
+
+    // ---- phase 4: R: nothing | M: DMA A1 of kt+2 (into A0 of kt), quadrant (1, 0)
+    bar();
+    if (pre) stage_a(kt + 2, 1);
     mma(QM, 0, af, b0);
     bar();
   }
-  if (!late) bar();  // balance the barrier count of the two wave groups
+  if (STAG && !late) bar();  // balance the barrier count of the two wave groups
+  (void)AHEAD;
 
   epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane);
 }
 
 // ================================================================================= simple
-template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI>
+template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, int SCHED>
 __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(GemmArgs a) {
   constexpr int NT = WM * WN * 64;
   constexpr int TM = BM / WM, TN = BN / WN;
@@ -412,23 +430,164 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(GemmArgs a) {
     if (kt + 1 < nk) stage(kt + 1, buf ^ 1);
     const lds_u8* sa = smem + buf * STAGE_BYTES;
     const lds_u8* sb = sa + A_BYTES;
+    if (SCHED == 0) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8_t af[FM], bfr[FN];
+      for (int s = 0; s < 2; ++s) {
+        bf16x8_t af[FM], bfr[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = read_frag<BM, AK>(sa, wm * TM + i * 16, s, lane);
+        for (int i = 0; i < FM; ++i) af[i] = read_frag<BM, AK>(sa, wm * TM + i * 16, s, lane);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, BKC>(sb, wn * TN + j * 16, s, lane);
+        for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, BKC>(sb, wn * TN + j * 16, s, lane);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    } else {
+      // both k-substeps' fragments in flight at once (two register sets, B first so the first
+      // MFMA row can start after FN + 1 reads), MFMAs in one prioritised cluster, raw barrier
+      bf16x8_t a0[FM], b0[FN], a1[FM], b1[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) b0[j] = read_frag<BN, BKC>(sb, wn * TN + j * 16, 0, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a0[i] = read_frag<BM, AK>(sa, wm * TM + i * 16, 0, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) b1[j] = read_frag<BN, BKC>(sb, wn * TN + j * 16, 1, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a1[i] = read_frag<BM, AK>(sa, wm * TM + i * 16, 1, lane);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], b0[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
   epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane);
+}
+
+// ============================================================================ 4-wave 256x256
+// One workgroup of 4 waves (2 x 2) per CU, each wave owning a 128 x 128 output tile: 256 fp32
+// accumulators per lane held across the unified 512-entry register file (one wave per SIMD,
+// amdgpu_waves_per_eu(1, 1)).  Per K-tile a wave reads its A and B panels once (32 KiB; 128 KiB
+// per CU instead of the 192 KiB an 8-wave 128 x 64 decomposition reads) for 128 MFMAs.
+// Latency is hidden inside the wave: the K-tile is two MFMA blocks of 64 (k-substeps 0 and 1)
+// and each block carries the LDS reads of the NEXT block's fragments (second register set):
+//   block A(kt): MFMA(kt, s0)  ||  ds_read(kt, s1)
+//   s_waitcnt vmcnt(0); s_barrier    <- K-tile kt+1 landed; every wave done reading K-tile kt
+//   block B(kt): MFMA(kt, s1)  ||  ds_read(kt+1, s0), DMA(kt+2 -> the buffer kt just freed)
+// so there is one barrier per K-tile and no read or DMA sits on the critical path.
+template <bool AK, bool BKC, int EPI, int ABL = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void gemm_w4_kernel(GemmArgs a) {
+  constexpr int BM = 256, BN = 256, NT = 256;
+  constexpr int TM = 128, TN = 128, FM = 8, FN = 8;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+  lds_u8* smem = (lds_u8*)smem_raw;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  int tile_m, tile_n;
+  tile_coords(a, tile_m, tile_n);
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const uint16_t* Abase = AK ? a.A + (int64_t)m0 * a.lda : a.A + m0;
+
+  auto stage = [&](int kt, int buf) {
+    const int k0 = kt * BK;
+    lds_u8* sa = smem + buf * STAGE;
+    const uint16_t* ga = AK ? Abase + k0 : Abase + (int64_t)k0 * a.lda;
+    stage_tile<BM, AK, NT>(ga, a.lda, sa, tid);
+    int64_t ldb;
+    const uint16_t* gb = b_image_ptr(a, BKC, n0, k0, 0, ldb);
+    stage_tile<BN, BKC, NT>(gb, ldb, sa + A_BYTES, tid);
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  bf16x8_t a0[FM], b0[FN], a1[FM], b1[FN];
+  auto read_set = [&](int buf, int s, bf16x8_t (&A)[FM], bf16x8_t (&Bf)[FN]) {
+    const lds_u8* sa = smem + buf * STAGE;
+    const lds_u8* sb = sa + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) A[i] = read_frag<BM, AK>(sa, wm * TM + i * 16, s, lane);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) Bf[j] = read_frag<BN, BKC>(sb, wn * TN + j * 16, s, lane);
+  };
+  auto mma = [&](const bf16x8_t (&A)[FM], const bf16x8_t (&Bf)[FN]) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], Bf[j], acc[i][j], 0, 0, 0);
+  };
+
+  const int nk = a.K / BK;
+  stage(0, 0);
+  if (nk > 1) stage(1, 1);
+  if (nk > 1) {
+    // K-tile 0's DMA instructions are the older half: wait for them only
+    constexpr int PER_TILE = (A_BYTES + B_BYTES) / 1024 / (NT / 64);
+    static_assert(PER_TILE == 16, "DMA instructions per wave per K-tile");
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  read_set(0, 0, a0, b0);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    // block A: MFMA(kt, s0) with the reads of (kt, s1)
+    read_set(buf, 1, a1, b1);
+    mma(a0, b0);
+    // K-tile kt+1 landed (its DMA is the only one outstanding); all reads of buffer `buf` retired
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // block B: MFMA(kt, s1) with the reads of (kt+1, s0) and the DMA of kt+2 into `buf`
+    if (kt + 1 < nk) read_set(buf ^ 1, 0, a0, b0);
+    if (ABL == 0 && kt + 2 < nk) stage(kt + 2, buf);   // ABL = 1: timing ablation without the DMA
+    mma(a1, b1);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane);
+}
+
+template <bool AK, bool BKC, int EPI, int ABL = 0>
+int launch_w4(const GemmArgs& a0, hipStream_t stream) {
+  GemmArgs a = a0;
+  a.tiles_m = a.M / 256;
+  a.tiles_n = a.N / 256;
+  constexpr int smem_main = 2 * (256 + 256) * BK * 2;
+  constexpr int smem_epi = 4 * 128 * (128 * 2 + 16);
+  constexpr int smem = smem_main > smem_epi ? smem_main : smem_epi;
+  static_assert(smem <= 160 * 1024, "LDS budget");
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm_w4_kernel<AK, BKC, EPI, ABL>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  gemm_w4_kernel<AK, BKC, EPI, ABL><<<a.tiles_m * a.tiles_n, 256, smem, stream>>>(a);
+  PT_CHECK_LAUNCH();
+  return PT_OK;
 }
 
 // ================================================================================== launch
@@ -437,26 +596,26 @@ void set_smem_once(Kern k, int smem) {
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
 }
 
-template <int BN, bool AK, bool BKC, int EPI>
+template <int BN, bool AK, bool BKC, int EPI, bool STAG>
 int launch_pipe(const GemmArgs& a0, hipStream_t stream) {
   GemmArgs a = a0;
   a.tiles_m = a.M / 256;
   a.tiles_n = a.N / BN;
-  constexpr int smem_main = 2 * (256 * BK * 2 + BN * BK * 2);
+  constexpr int smem_main = 5 * (128 * BK * 2 + (BN / 2) * BK * 2);
   constexpr int smem_epi = 8 * 128 * ((BN / 4) * 2 + 16);
   constexpr int smem = smem_main > smem_epi ? smem_main : smem_epi;
   static_assert(smem <= 160 * 1024, "LDS budget");
   static bool attr_set = false;
   if (!attr_set) {
-    set_smem_once(gemm_pipe_kernel<BN, AK, BKC, EPI>, smem);
+    set_smem_once(gemm_pipe_kernel<BN, AK, BKC, EPI, STAG>, smem);
     attr_set = true;
   }
-  gemm_pipe_kernel<BN, AK, BKC, EPI><<<a.tiles_m * a.tiles_n, 512, smem, stream>>>(a);
+  gemm_pipe_kernel<BN, AK, BKC, EPI, STAG><<<a.tiles_m * a.tiles_n, 512, smem, stream>>>(a);
   PT_CHECK_LAUNCH();
   return PT_OK;
 }
 
-template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI>
+template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, int SCHED = 0>
 int launch_t(const GemmArgs& a0, hipStream_t stream) {
   GemmArgs a = a0;
   a.tiles_m = a.M / BM;
@@ -467,25 +626,32 @@ int launch_t(const GemmArgs& a0, hipStream_t stream) {
   static_assert(smem <= 160 * 1024, "LDS budget");
   static bool attr_set = false;
   if (!attr_set) {
-    set_smem_once(gemm_kernel<BM, BN, WM, WN, AK, BKC, EPI>, smem);
+    set_smem_once(gemm_kernel<BM, BN, WM, WN, AK, BKC, EPI, SCHED>, smem);
     attr_set = true;
   }
-  gemm_kernel<BM, BN, WM, WN, AK, BKC, EPI><<<a.tiles_m * a.tiles_n, WM * WN * 64, smem, stream>>>(a);
+  gemm_kernel<BM, BN, WM, WN, AK, BKC, EPI, SCHED><<<a.tiles_m * a.tiles_n, WM * WN * 64, smem, stream>>>(a);
   PT_CHECK_LAUNCH();
   return PT_OK;
 }
 
-// tile ids: 0 = pipelined 256x256, 1 = pipelined 256x128, 2 = simple 128x128, 3 = simple 64x64,
-//           4 = simple 256x256, 5 = simple 256x128 (kept for A/B measurement)
-constexpr int kNumTiles = 6;
-const int kTileBM[kNumTiles] = {256, 256, 128, 64, 256, 256};
-const int kTileBN[kNumTiles] = {256, 128, 128, 64, 256, 128};
+// tile ids: 0 = pipelined 256x256, 1 = pipelined 256x128 (ping-pong wave groups), 2 = simple
+//           128x128, 3 = simple 64x64, 4 = simple 256x256, 5 = simple 256x128, 6 / 7 = pipelined
+//           256x256 / 256x128 without the ping-pong stagger (kept for A/B measurement)
+constexpr int kNumTiles = 12;
+const int kTileBM[kNumTiles] = {256, 256, 128, 64, 256, 256, 256, 256, 256, 128, 256, 256};
+const int kTileBN[kNumTiles] = {256, 128, 128, 64, 256, 128, 256, 128, 256, 128, 256, 256};
 
 template <bool AK, bool BKC, int EPI>
 int launch_layout(const GemmArgs& a, int tile, hipStream_t s) {
   switch (tile) {
-    case 0: return launch_pipe<256, AK, BKC, EPI>(a, s);
-    case 1: return launch_pipe<128, AK, BKC, EPI>(a, s);
+    case 0: return launch_pipe<256, AK, BKC, EPI, true>(a, s);
+    case 1: return launch_pipe<128, AK, BKC, EPI, true>(a, s);
+    case 6: return launch_pipe<256, AK, BKC, EPI, false>(a, s);
+    case 7: return launch_pipe<128, AK, BKC, EPI, false>(a, s);
+    case 8: return launch_t<256, 256, 2, 4, AK, BKC, EPI, 1>(a, s);
+    case 9: return launch_t<128, 128, 2, 2, AK, BKC, EPI, 1>(a, s);
+    case 10: return launch_w4<AK, BKC, EPI>(a, s);
+    case 11: return launch_w4<AK, BKC, EPI, 1>(a, s);
     case 2: return launch_t<128, 128, 2, 2, AK, BKC, EPI>(a, s);
     case 3: return launch_t<64, 64, 2, 2, AK, BKC, EPI>(a, s);
     case 4: return launch_t<256, 256, 2, 4, AK, BKC, EPI>(a, s);
