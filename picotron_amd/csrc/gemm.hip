@@ -37,6 +37,8 @@
 // row segments; fp32 epilogues (main_grad accumulation) write the accumulator directly.
 #include "common.h"
 
+#include <type_traits>
+
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
@@ -385,6 +387,349 @@ __global__ __launch_bounds__(512) void gemm_pipe_kernel(GemmArgs a) {
   epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane);
 }
 
+// ============================================================================ 8-phase 256x256
+// 256x256 tile, BK = 64, 8 waves as 2(M) x 4(N), each wave a 128 x 64 output (8 x 4 accumulators
+// of 16x16).  Each operand tile is held as two "half images" of 128 rows (A) / columns (B) x 64 k,
+// split so that one half holds exactly the fragments every wave reads in one phase:
+//   At = tile rows {0-63, 128-191}   (rows 0-63 of each M-wave's 128)   read in phase 1
+//   Ab = tile rows {64-127, 192-255}                                    read in phase 3
+//   Bl = tile cols {0-31, 64-95, 128-159, 192-223} (cols 0-31 of each N-wave's 64)   phase 1
+//   Br = the other 128 columns                                          read in phase 2
+// K-tile t = 4 phases (one 64x32 quadrant of the wave's output each: (0,0) (0,1) (1,1) (1,0)),
+// each { LDS reads; one half-image LDS-DMA; lgkmcnt(0); barrier; 16 MFMAs; barrier }.  A half
+// image is re-staged the phase after its last read (the reads were retired before that phase's
+// first barrier): At, Bl, Br of K-tile t+2 in phases 2-4 of t (into t's buffer), Ab of t+1 in
+// phase 1 of t.  The single wait per K-tile (phase 4, before its first barrier) is vmcnt(6): it
+// retires K-tile t+1 and leaves t+2's three halves in flight.  Wave group 1 (waves 4-7) runs one
+// barrier behind group 0, so on each SIMD one wave multiplies while the other reads and stages
+// (cdna_hip_programming.md §5 "The 256² 8-phase template"; RAW: data is read >= 2 barriers after
+// the wait that retired it).  LDS: 2 buffers x 4 halves x 16 KiB = 128 KiB (+ epilogue staging).
+template <bool KC, int SPAN>
+__device__ __forceinline__ uint32_t himg_voff(int i, int lane, int64_t ld, int off) {
+  // element offset (from the operand's (tile row/col 0, k0) element) of lane's 16-B chunk of
+  // 1-KiB DMA instruction i of a half image whose image row/col r maps to tile row/col
+  // (r / SPAN) * 2 SPAN + r % SPAN + off
+  if (KC) {
+    const int r = i * 8 + (lane >> 3), c = lane & 7;
+    const int row = (r / SPAN) * 2 * SPAN + r % SPAN + off;
+    return (uint32_t)(row * ld + 8 * (c ^ swz_k(r)));
+  } else {
+    const int r = i * 4 + (lane >> 4), c = lane & 15;
+    const int col = 8 * (c ^ swz_mn(r, 256));
+    const int tc = (col / SPAN) * 2 * SPAN + col % SPAN + off;
+    return (uint32_t)(r * ld + tc);
+  }
+}
+
+// LDS-DMA issued from inline asm (saddr form: uniform base + per-lane byte offset).  The compiler
+// does not see these as LDS writes, so it does not put an `s_waitcnt vmcnt(0)` in front of every
+// ds_read_b64_tr_b16 (it cannot prove the transposed reads disjoint from an in-flight LDS-DMA and
+// drained the whole prefetch pipeline before each MN-contiguous fragment read); ordering is ours:
+// the counted vmcnt + barrier of the K-loop.  M0 is written here and used by nothing else in the
+// kernel.
+__device__ __forceinline__ void glds16_asm(const uint16_t* base, uint32_t voff_elems, lds_u8* dst) {
+  const uint64_t p = (uint64_t)(uintptr_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+  const uint64_t sb = (uint64_t)lo | ((uint64_t)hi << 32);
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst);
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(m0), "v"(voff_elems * 2u), "s"(sb)
+               : "memory");
+}
+
+template <bool AK, bool BKC, int EPI>
+__global__ __launch_bounds__(512) void gemm_8ph_kernel(GemmArgs a) {
+  constexpr int NT = 512, TM = 128, TN = 64, FM = 8, FN = 4;
+  constexpr int HALF = 128 * BK * 2;          // 16 KiB
+  constexpr int BUF = 4 * HALF;               // At, Bl, Br, Ab
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+  lds_u8* smem = (lds_u8*)smem_raw;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  int tile_m, tile_n;
+  tile_coords(a, tile_m, tile_n);
+  const int m0 = tile_m * 256, n0 = tile_n * 256;
+
+  // B segment for this tile (N-segments) or the first K-segment; ld is per tile (host checks
+  // that K-segments share one ld)
+  int64_t ldb;
+  const uint16_t* Bt0 = b_image_ptr(a, BKC, n0, 0, 0, ldb);
+  const int64_t lda = a.lda;
+  // loop-invariant per-lane element offsets of this wave's 2 DMA instructions per half image
+  uint32_t vA[2][2], vB[2][2];  // [half][it]
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int i = it * 8 + wave;
+    vA[0][it] = himg_voff<AK, 64>(i, lane, lda, 0);
+    vA[1][it] = himg_voff<AK, 64>(i, lane, lda, 64);
+    vB[0][it] = himg_voff<BKC, 32>(i, lane, ldb, 0);
+    vB[1][it] = himg_voff<BKC, 32>(i, lane, ldb, 32);
+  }
+  const uint16_t* Ab0 = AK ? a.A + (int64_t)m0 * lda : a.A + m0;
+  auto a_ptr = [&](int t) { return AK ? Ab0 + t * BK : Ab0 + (int64_t)t * BK * lda; };
+  auto b_ptr = [&](int t) {
+    if (a.bdim == 0) return BKC ? Bt0 + t * BK : Bt0 + (int64_t)t * BK * ldb;
+    int64_t ld;
+    return b_image_ptr(a, BKC, n0, t * BK, 0, ld);
+  };
+  // half image h (0 At, 1 Bl, 2 Br, 3 Ab) of K-tile t into buffer buf
+  auto stage = [&](int t, int buf, int h) {
+    lds_u8* dst = smem + buf * BUF + h * HALF;
+    const bool isA = h == 0 || h == 3;
+    const uint16_t* base = isA ? a_ptr(t) : b_ptr(t);
+    const int sel = (h == 0 || h == 1) ? 0 : 1;
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const uint32_t vo = isA ? vA[sel][it] : vB[sel][it];
+      glds16_asm(base, vo, dst + (it * 8 + wave) * 1024);
+    }
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = a.K / BK;
+  stage(0, 0, 0); stage(0, 0, 1); stage(0, 0, 2); stage(0, 0, 3);
+  if (nk > 1) {
+    stage(1, 1, 0); stage(1, 1, 1); stage(1, 1, 2);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+
+  auto bar = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  bf16x8_t af[4][2], b0[2][2], b1[2][2];
+  auto mma = [&](int i0, int j0, const bf16x8_t (&A)[4][2], const bf16x8_t (&Bf)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i][s], Bf[j][s], acc[i0 + i][j0 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  const bool late = __builtin_amdgcn_readfirstlane(wm) == 1;
+  if (late) bar();
+
+  auto ktile = [&](int t, auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
+    const lds_u8* sAt = smem + buf * BUF;
+    const lds_u8* sBl = sAt + HALF;
+    const lds_u8* sBr = sAt + 2 * HALF;
+    const lds_u8* sAb = sAt + 3 * HALF;
+    const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
+    // phase 1: At rows + Bl cols; stage Ab(t+1); quadrant (0, 0)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) af[i][s] = read_frag<128, AK>(sAt, wm * 64 + i * 16, s, lane);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) b0[j][s] = read_frag<128, BKC>(sBl, wn * 32 + j * 16, s, lane);
+    if (n1) stage(t + 1, buf ^ 1, 3);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    mma(0, 0, af, b0);
+    bar();
+    // phase 2: Br cols; stage At(t+2); quadrant (0, 1)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) b1[j][s] = read_frag<128, BKC>(sBr, wn * 32 + j * 16, s, lane);
+    if (n2) stage(t + 2, buf, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    mma(0, 2, af, b1);
+    bar();
+    // phase 3: Ab rows; stage Bl(t+2); quadrant (1, 1)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) af[i][s] = read_frag<128, AK>(sAb, wm * 64 + i * 16, s, lane);
+    if (n2) stage(t + 2, buf, 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    mma(4, 2, af, b1);
+    bar();
+    // phase 4: no reads; stage Br(t+2); retire K-tile t+1; quadrant (1, 0)
+    if (n2) {
+      stage(t + 2, buf, 2);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else if (n1) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bar();
+    mma(4, 0, af, b0);
+    bar();
+  };
+
+  int t = 0;
+  for (; t + 1 < nk; t += 2) {
+    ktile(t, std::integral_constant<int, 0>{});
+    ktile(t + 1, std::integral_constant<int, 1>{});
+  }
+  if (t < nk) ktile(t, std::integral_constant<int, 0>{});
+  if (!late) bar();  // balance the barrier count of the two wave groups
+  __syncthreads();
+  epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane);
+}
+
+// ============================================================================ 4-phase 256x128
+// For the N = 2048 shapes (o_proj, down_proj forward, every dX GEMM of the layer, the lm_head dX),
+// where 256x256 tiles put only 128 workgroups on the 256 CUs.  256x128 tile, BK = 64, 8 waves as
+// 4(M) x 2(N), each wave a 64 x 64 output (4 x 4 accumulators): the same A + B fragment bytes per
+// MFMA as the 8-wave 256x256 kernel's 128 x 64 wave tiles.  Three images per K-tile:
+//   At = tile rows {0-31, 64-95, 128-159, 192-223} (rows 0-31 of each M-wave's 64)  read in phase 1
+//   Ab = the other 128 rows                                                           read in phase 2
+//   B  = all 128 columns                                                              read in phase 1
+// K-tile t = 2 phases (upper / lower 32 x 64 half of the wave's output, 16 MFMAs each), same
+// phase anatomy and wave-group stagger as the 8-phase kernel.  With 48 KiB per K-tile the LDS holds
+// THREE K-tiles (144 KiB): K-tile t+2 is staged during K-tile t into the buffer K-tile t-1 freed
+// (At in phase 1, B and Ab in phase 2), and the one wait per K-tile (phase 2, vmcnt(6)) retires
+// K-tile t+1 with t+2 in flight -- every DMA has >= 1.5 K-tiles to land.
+template <bool AK, bool BKC, int EPI>
+__global__ __launch_bounds__(512) void gemm_4ph_kernel(GemmArgs a) {
+  constexpr int TM = 64, TN = 64, FM = 4, FN = 4;
+  constexpr int IMG = 128 * BK * 2;           // 16 KiB
+  constexpr int BUF = 3 * IMG;                // At, B, Ab
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+  lds_u8* smem = (lds_u8*)smem_raw;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  int tile_m, tile_n;
+  tile_coords(a, tile_m, tile_n);
+  const int m0 = tile_m * 256, n0 = tile_n * 128;
+
+  int64_t ldb;
+  const uint16_t* Bt0 = b_image_ptr(a, BKC, n0, 0, 0, ldb);
+  const int64_t lda = a.lda;
+  uint32_t vA[2][2], vB[2];
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int i = it * 8 + wave;
+    vA[0][it] = himg_voff<AK, 32>(i, lane, lda, 0);
+    vA[1][it] = himg_voff<AK, 32>(i, lane, lda, 32);
+    vB[it] = himg_voff<BKC, 128>(i, lane, ldb, 0);
+  }
+  const uint16_t* Ab0 = AK ? a.A + (int64_t)m0 * lda : a.A + m0;
+  auto a_ptr = [&](int t) { return AK ? Ab0 + t * BK : Ab0 + (int64_t)t * BK * lda; };
+  auto b_ptr = [&](int t) {
+    if (a.bdim == 0) return BKC ? Bt0 + t * BK : Bt0 + (int64_t)t * BK * ldb;
+    int64_t ld;
+    return b_image_ptr(a, BKC, n0, t * BK, 0, ld);
+  };
+  // image h (0 At, 1 B, 2 Ab) of K-tile t into buffer buf
+  auto stage = [&](int t, int buf, int h) {
+    lds_u8* dst = smem + buf * BUF + h * IMG;
+    const uint16_t* base = h == 1 ? b_ptr(t) : a_ptr(t);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const uint32_t vo = h == 1 ? vB[it] : vA[h == 2 ? 1 : 0][it];
+      glds16_asm(base, vo, dst + (it * 8 + wave) * 1024);
+    }
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = a.K / BK;
+  stage(0, 0, 0); stage(0, 0, 1); stage(0, 0, 2);
+  if (nk > 1) {
+    stage(1, 1, 0); stage(1, 1, 1); stage(1, 1, 2);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+
+  auto bar = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  bf16x8_t af[2][2], bf[4][2];
+  auto mma = [&](int i0) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i0 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bf[j][s], acc[i0 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  const bool late = __builtin_amdgcn_readfirstlane(wm) >= 2;
+  if (late) bar();
+
+  auto ktile = [&](int t, auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
+    constexpr int nbuf = (buf + 2) % 3;  // K-tile t+2's buffer (freed by K-tile t-1)
+    const lds_u8* sAt = smem + buf * BUF;
+    const lds_u8* sB = sAt + IMG;
+    const lds_u8* sAb = sAt + 2 * IMG;
+    const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
+    // phase 1: At rows + all B cols; stage At(t+2); upper half
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) af[i][s] = read_frag<128, AK>(sAt, wm * 32 + i * 16, s, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) bf[j][s] = read_frag<128, BKC>(sB, wn * 64 + j * 16, s, lane);
+    if (n2) stage(t + 2, nbuf, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    mma(0);
+    bar();
+    // phase 2: Ab rows; stage B, Ab of t+2; retire K-tile t+1; lower half
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) af[i][s] = read_frag<128, AK>(sAb, wm * 32 + i * 16, s, lane);
+    if (n2) {
+      stage(t + 2, nbuf, 1);
+      stage(t + 2, nbuf, 2);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else if (n1) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    mma(2);
+    bar();
+  };
+
+  int t = 0;
+  for (; t + 2 < nk; t += 3) {
+    ktile(t, std::integral_constant<int, 0>{});
+    ktile(t + 1, std::integral_constant<int, 1>{});
+    ktile(t + 2, std::integral_constant<int, 2>{});
+  }
+  if (t < nk) ktile(t, std::integral_constant<int, 0>{});
+  if (t + 1 < nk) ktile(t + 1, std::integral_constant<int, 1>{});
+  if (!late) bar();
+  __syncthreads();
+  epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane);
+}
+
 // ================================================================================= simple
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, int SCHED>
 __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(GemmArgs a) {
@@ -637,9 +982,49 @@ int launch_t(const GemmArgs& a0, hipStream_t stream) {
 // tile ids: 0 = pipelined 256x256, 1 = pipelined 256x128 (ping-pong wave groups), 2 = simple
 //           128x128, 3 = simple 64x64, 4 = simple 256x256, 5 = simple 256x128, 6 / 7 = pipelined
 //           256x256 / 256x128 without the ping-pong stagger (kept for A/B measurement)
-constexpr int kNumTiles = 12;
-const int kTileBM[kNumTiles] = {256, 256, 128, 64, 256, 256, 256, 256, 256, 128, 256, 256};
-const int kTileBN[kNumTiles] = {256, 128, 128, 64, 256, 128, 256, 128, 256, 128, 256, 256};
+//           12 = 8-phase 256x256 (two half-image wave groups, one wait per K-tile)
+//           13 = 4-phase 256x128 (three K-tiles resident)
+constexpr int kNumTiles = 14;
+const int kTileBM[kNumTiles] = {256, 256, 128, 64, 256, 256, 256, 256, 256, 128, 256, 256, 256, 256};
+const int kTileBN[kNumTiles] = {256, 128, 128, 64, 256, 128, 256, 128, 256, 128, 256, 256, 256, 128};
+
+template <bool AK, bool BKC, int EPI>
+int launch_8ph(const GemmArgs& a0, hipStream_t stream) {
+  GemmArgs a = a0;
+  a.tiles_m = a.M / 256;
+  a.tiles_n = a.N / 256;
+  constexpr int smem_main = 8 * 128 * BK * 2;
+  constexpr int smem_epi = 8 * 128 * (64 * 2 + 16);
+  constexpr int smem = smem_main > smem_epi ? smem_main : smem_epi;
+  static_assert(smem <= 160 * 1024, "LDS budget");
+  static bool attr_set = false;
+  if (!attr_set) {
+    set_smem_once(gemm_8ph_kernel<AK, BKC, EPI>, smem);
+    attr_set = true;
+  }
+  gemm_8ph_kernel<AK, BKC, EPI><<<a.tiles_m * a.tiles_n, 512, smem, stream>>>(a);
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
+
+template <bool AK, bool BKC, int EPI>
+int launch_4ph(const GemmArgs& a0, hipStream_t stream) {
+  GemmArgs a = a0;
+  a.tiles_m = a.M / 256;
+  a.tiles_n = a.N / 128;
+  constexpr int smem_main = 9 * 128 * BK * 2;
+  constexpr int smem_epi = 8 * 64 * (64 * 2 + 16);
+  constexpr int smem = smem_main > smem_epi ? smem_main : smem_epi;
+  static_assert(smem <= 160 * 1024, "LDS budget");
+  static bool attr_set = false;
+  if (!attr_set) {
+    set_smem_once(gemm_4ph_kernel<AK, BKC, EPI>, smem);
+    attr_set = true;
+  }
+  gemm_4ph_kernel<AK, BKC, EPI><<<a.tiles_m * a.tiles_n, 512, smem, stream>>>(a);
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
 
 template <bool AK, bool BKC, int EPI>
 int launch_layout(const GemmArgs& a, int tile, hipStream_t s) {
@@ -652,6 +1037,8 @@ int launch_layout(const GemmArgs& a, int tile, hipStream_t s) {
     case 9: return launch_t<128, 128, 2, 2, AK, BKC, EPI, 1>(a, s);
     case 10: return launch_w4<AK, BKC, EPI>(a, s);
     case 11: return launch_w4<AK, BKC, EPI, 1>(a, s);
+    case 12: return launch_8ph<AK, BKC, EPI>(a, s);
+    case 13: return launch_4ph<AK, BKC, EPI>(a, s);
     case 2: return launch_t<128, 128, 2, 2, AK, BKC, EPI>(a, s);
     case 3: return launch_t<64, 64, 2, 2, AK, BKC, EPI>(a, s);
     case 4: return launch_t<256, 256, 2, 4, AK, BKC, EPI>(a, s);
@@ -673,12 +1060,14 @@ int launch_epi(const GemmArgs& a, int a_kcontig, int b_kcontig, int tile, hipStr
 extern "C" {
 
 // Tile choice, from the measured sweep over the decoder layer's shapes (tools/gemm_bench.py,
-// profiles/r01_gemm_tiles.md): the simple 256x256 kernel when it still puts >= 192 tiles on the
-// 256 CUs (the big projections), else the 128x128 kernel (N = 2048 dX GEMMs, o_proj), else 64x64.
-// The pipelined kernels (ids 0, 1) are selectable explicitly but not yet faster.
-int pt_gemm_pick_tile(int64_t M, int64_t N, const int64_t* mseg, int nmseg, const int64_t* nseg, int nnseg) {
-  static const int order[3] = {4, 2, 3};
-  static const int min_tiles[3] = {192, 0, 0};
+// profiles/r01_gemm_tiles_8ph.md): the 8-phase 256x256 kernel whenever it puts >= 192 tiles on
+// the 256 CUs (1.04-1.38 PF/s on the big projections, every layout), and at 128 tiles when B is
+// N-contiguous (the dX GEMMs); else the 128x128 two-stage kernel (K-contiguous N = 2048 shapes,
+// o_proj), else 64x64.
+static int pick_tile(int64_t M, int64_t N, const int64_t* mseg, int nmseg, const int64_t* nseg, int nnseg,
+                     int b_kcontig) {
+  static const int order[3] = {12, 2, 3};
+  const int min_tiles[3] = {b_kcontig ? 192 : 128, 0, 0};
   for (int o = 0; o < 3; ++o) {
     const int t = order[o];
     const int bm = kTileBM[t], bn = kTileBN[t];
@@ -690,6 +1079,10 @@ int pt_gemm_pick_tile(int64_t M, int64_t N, const int64_t* mseg, int nmseg, cons
     if ((M / bm) * (N / bn) >= min_tiles[o]) return t;
   }
   return -1;
+}
+
+int pt_gemm_pick_tile(int64_t M, int64_t N, const int64_t* mseg, int nmseg, const int64_t* nseg, int nnseg) {
+  return pick_tile(M, N, mseg, nmseg, nseg, nnseg, 1);
 }
 
 // C = A . B  (see header comment).  a_kcontig: A is [M,K] (ld=lda) else stored [K,M];
@@ -741,7 +1134,10 @@ int pt_gemm(const void* A, int64_t lda, int a_kcontig, const void* const* B, con
     int64_t nsegs[5], msegs[5];
     for (int i = 0; i <= nb; ++i) nsegs[i] = b_seg_dim == 0 ? a.bseg[i] : 0;
     for (int i = 0; i <= nc; ++i) msegs[i] = a.cseg[i];
-    tile = pt_gemm_pick_tile(M, N, msegs, nc + 1, nsegs, nb + 1);
+    tile = pick_tile(M, N, msegs, nc + 1, nsegs, nb + 1, b_kcontig);
+    if ((tile == 12 || tile == 13) && b_seg_dim == 1)
+      for (int i = 1; i < nb; ++i)
+        if (a.ldb[i] != a.ldb[0]) tile = 2;
   }
   if (tile < 0 || tile >= kNumTiles) return PT_EUNSUPPORTED;
   const int bm = kTileBM[tile], bn = kTileBN[tile];
@@ -751,6 +1147,9 @@ int pt_gemm(const void* A, int64_t lda, int a_kcontig, const void* const* B, con
   if (b_seg_dim == 0)
     for (int i = 0; i <= nb; ++i)
       if (a.bseg[i] % bn) return PT_EUNSUPPORTED;
+  if ((tile == 12 || tile == 13) && b_seg_dim == 1)  // one B leading dimension per tile
+    for (int i = 1; i < nb; ++i)
+      if (a.ldb[i] != a.ldb[0]) return PT_EUNSUPPORTED;
   switch (epilogue) {
     case EPI_BF16: return launch_epi<EPI_BF16>(a, a_kcontig, b_kcontig, tile, stream);
     case EPI_BF16_ACC: return launch_epi<EPI_BF16_ACC>(a, a_kcontig, b_kcontig, tile, stream);

@@ -153,7 +153,7 @@ def test_gemm_fwd_nt(M, N, K):
     assert rel_err(y, _ref_mm(x, w.t())) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 12, 13])
 def test_gemm_every_tile_every_layout(tile):
     from picotron_amd import kernels as K_
     M, N, K = 512, 512, 256
@@ -170,6 +170,34 @@ def test_gemm_every_tile_every_layout(tile):
     K_.linear_wgrad(dy.to(DEV), a.to(DEV), [dw], tile=tile)
     torch.cuda.synchronize()
     assert rel_err(dw, _ref_mm(dy.t(), a)) < 1e-2
+
+
+@pytest.mark.parametrize("tile", [12, 13])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 192), (768, 512, 512), (256, 512, 2048),
+                                   (512, 256, 320), (256, 256, 128)])
+def test_gemm_8phase_shapes(M, N, K, tile):
+    """the phased kernels (tile 12: 256x256, 13: 256x128): 1-5 K-tiles (every remainder of the
+    2- and 3-buffer loops), every layout"""
+    from picotron_amd import kernels as K_
+    a = torch.randn(M, K).to(BF)
+    b = (torch.randn(N, K) / 16).to(BF)
+    bn = 256 if tile == 12 else 128
+    y = K_.linear_fwd(a.to(DEV), [b.to(DEV)], tile=tile)
+    assert rel_err(y, _ref_mm(a, b.t())) < 1e-2
+    dy = torch.randn(M, N).to(BF)
+    if K % bn == 0:
+        dx = K_.linear_dgrad(dy.to(DEV), [b.to(DEV)], tile=tile)
+        assert rel_err(dx, _ref_mm(dy, b)) < 1e-2
+    dw = torch.empty(N, K, dtype=BF, device=DEV)
+    if N % 256 == 0 and K % bn == 0:
+        K_.linear_wgrad(dy.to(DEV), a.to(DEV), [dw], tile=tile)
+        torch.cuda.synchronize()
+        assert rel_err(dw, _ref_mm(dy.t(), a)) < 1e-2
+    # exactness: A = I picks rows of B^T
+    eye = torch.eye(M, K).to(BF)
+    y = K_.linear_fwd(eye.to(DEV), [b.to(DEV)], tile=tile)
+    torch.cuda.synchronize()
+    assert torch.equal(y.cpu()[:min(M, K)], b.t()[:min(M, K)])
 
 
 def test_gemm_segmented_qkv():
