@@ -1060,24 +1060,34 @@ int launch_epi(const GemmArgs& a, int a_kcontig, int b_kcontig, int tile, hipStr
 extern "C" {
 
 // Tile choice, from the measured sweep over the decoder layer's shapes (tools/gemm_bench.py,
-// profiles/r01_gemm_tiles_8ph.md): the 8-phase 256x256 kernel whenever it puts >= 192 tiles on
-// the 256 CUs (1.04-1.38 PF/s on the big projections, every layout), and at 128 tiles when B is
-// N-contiguous (the dX GEMMs); else the 128x128 two-stage kernel (K-contiguous N = 2048 shapes,
-// o_proj), else 64x64.
+// profiles/r01_gemm_tiles_8ph.md): the phased kernels whenever the shape divides -- 256x256 (tile
+// 12) or 256x128 (tile 13), whichever fills the 256 CUs' last round better (ties -> 256x256: fewer
+// operand bytes per MFMA); 1.0-1.38 PF/s on every projection of the layer.  Else the 128x128
+// two-stage kernel, else 64x64.
+static bool tile_fits(int t, int64_t M, int64_t N, const int64_t* mseg, int nmseg, const int64_t* nseg, int nnseg) {
+  const int bm = kTileBM[t], bn = kTileBN[t];
+  if (M % bm || N % bn) return false;
+  for (int i = 0; i < nmseg; ++i)
+    if (mseg[i] % bm) return false;
+  for (int i = 0; i < nnseg; ++i)
+    if (nseg[i] % bn) return false;
+  return true;
+}
+
 static int pick_tile(int64_t M, int64_t N, const int64_t* mseg, int nmseg, const int64_t* nseg, int nnseg,
                      int b_kcontig) {
-  static const int order[3] = {12, 2, 3};
-  const int min_tiles[3] = {b_kcontig ? 192 : 128, 0, 0};
-  for (int o = 0; o < 3; ++o) {
-    const int t = order[o];
-    const int bm = kTileBM[t], bn = kTileBN[t];
-    if (M % bm || N % bn) continue;
-    bool ok = true;
-    for (int i = 0; i < nmseg && ok; ++i) ok = (mseg[i] % bm) == 0;
-    for (int i = 0; i < nnseg && ok; ++i) ok = (nseg[i] % bn) == 0;
-    if (!ok) continue;
-    if ((M / bm) * (N / bn) >= min_tiles[o]) return t;
-  }
+  (void)b_kcontig;
+  auto fill = [&](int t) {  // fraction of the CU-rounds this tile grid keeps busy
+    const int64_t tiles = (M / kTileBM[t]) * (N / kTileBN[t]);
+    const int64_t rounds = (tiles + 255) / 256;
+    return (double)tiles / (double)(rounds * 256);
+  };
+  const bool f12 = tile_fits(12, M, N, mseg, nmseg, nseg, nnseg);
+  const bool f13 = tile_fits(13, M, N, mseg, nmseg, nseg, nnseg);
+  if (f12 && (!f13 || fill(12) >= fill(13))) return 12;
+  if (f13) return 13;
+  if (tile_fits(2, M, N, mseg, nmseg, nseg, nnseg)) return 2;
+  if (tile_fits(3, M, N, mseg, nmseg, nseg, nnseg)) return 3;
   return -1;
 }
 
@@ -1137,7 +1147,7 @@ int pt_gemm(const void* A, int64_t lda, int a_kcontig, const void* const* B, con
     tile = pick_tile(M, N, msegs, nc + 1, nsegs, nb + 1, b_kcontig);
     if ((tile == 12 || tile == 13) && b_seg_dim == 1)
       for (int i = 1; i < nb; ++i)
-        if (a.ldb[i] != a.ldb[0]) tile = 2;
+        if (a.ldb[i] != a.ldb[0]) tile = tile_fits(2, M, N, msegs, nc + 1, nsegs, nb + 1) ? 2 : 3;
   }
   if (tile < 0 || tile >= kNumTiles) return PT_EUNSUPPORTED;
   const int bm = kTileBM[tile], bn = kTileBN[tile];
