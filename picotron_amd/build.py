@@ -34,9 +34,15 @@ def sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
 
 
+# per-source code-generation flags.  attention: MFMA results in VGPRs (gfx950's unified register
+# file) instead of AGPRs -- the softmax reads every S / dP accumulator, and the AGPR form cost a
+# v_accvgpr_read per element plus registers (fwd 156 -> 124 VGPRs: 3 -> 4 waves per SIMD).
+FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+
+
 def _compile(src, obj, extra):
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-c", src, "-o", obj,
-           "-Wno-unused-result"] + extra
+           "-Wno-unused-result"] + FILE_FLAGS.get(os.path.basename(src), []) + extra
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed on {os.path.basename(src)}:\n{r.stderr}")

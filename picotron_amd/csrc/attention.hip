@@ -33,6 +33,7 @@ namespace {
 
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
+constexpr float kRescaleLog2 = 8.0f;
 constexpr int KT = 64;  // rows per staged K/V (or Q/dO) tile
 constexpr int NW = 4;   // waves per workgroup, 32 rows each
 
@@ -60,10 +61,6 @@ __device__ __forceinline__ int aswz(int r) {
   return ((r & 1) << 2) | (((r >> 1) & 1) << 3) | ((r >> 3) & 1) | (((r >> 4) & 1) << 1);
 }
 
-__device__ __forceinline__ void glds16(const void* gsrc, lds_u8* lds_base) {
-  __builtin_amdgcn_global_load_lds(gsrc, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
-}
-
 // stage a [KT][D] bf16 tile (rows `row_stride` elements apart) into a swizzled LDS image
 template <int D>
 __device__ __forceinline__ void stage_rows(const uint16_t* __restrict__ g, int64_t row_stride, lds_u8* dst,
@@ -74,7 +71,8 @@ __device__ __forceinline__ void stage_rows(const uint16_t* __restrict__ g, int64
   for (int it = 0; it < NI / NW; ++it) {
     const int i = it * NW + wave;
     const int r = i * RPI + lane / RC, c = lane % RC;
-    glds16(g + (int64_t)r * row_stride + 8 * (c ^ aswz<D>(r)), dst + i * 1024);
+    pt_glds16(g, (uint32_t)((r * row_stride + 8 * (c ^ aswz<D>(r))) * 2),
+              (__attribute__((address_space(3))) void*)(dst + i * 1024));
   }
 }
 
@@ -116,6 +114,21 @@ __device__ __forceinline__ bf16x8_t ld_row_frag(const uint16_t* row_ptr, int ks,
 
 // C layout row index of register r for this lane
 __device__ __forceinline__ int crow(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+// XCD-aware block order.  The dispatcher deals workgroups round-robin over the 8 XCDs (linear id
+// mod 8), which would spread the 8-16 blocks of one (batch, head) -- all re-reading that head's
+// K/V (or Q/dO) tiles -- over 8 different L2s.  Remap so each XCD gets a contiguous range of
+// (block, head, batch) ids, blocks of one head adjacent: a head's tiles are fetched into one L2
+// and re-read from there (a head's K+V at S 1024, d 64 is 256 KiB; an XCD's L2 is 4 MiB).
+__device__ __forceinline__ void attn_coords(int& x, int& y, int& z) {
+  const int nx = gridDim.x, ny = gridDim.y, nwg = nx * ny * gridDim.z;
+  const int id = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+  const int xcd = id & 7, q = nwg >> 3, r = nwg & 7;
+  const int pid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
+  x = pid % nx;
+  y = (pid / nx) % ny;
+  z = pid / (nx * ny);
+}
 
 __device__ __forceinline__ f32x16_t zero16() {
   f32x16_t z;
@@ -160,8 +173,9 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
   lds_u8* smem = (lds_u8*)smem_raw;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nqb = a.Sq / (NW * 32);
-  const int qb = a.causal ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;  // heavy blocks first
-  const int h = blockIdx.y, b = blockIdx.z;
+  int bx, h, b;
+  attn_coords(bx, h, b);
+  const int qb = a.causal ? nqb - 1 - bx : bx;  // heavy blocks first
   const int hk = h / (a.H / a.HKV);
   const int q0 = qb * NW * 32 + wave * 32;
   const int myq = q0 + (lane & 31);
@@ -188,7 +202,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
     stage_rows<D>(vbase + (int64_t)kt * KT * a.v_ss, a.v_ss, sk + TILE_B, wave, lane);
   };
   stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler: its own fragment loads are done
   __syncthreads();
 
   for (int kt = 0; kt < nkt; ++kt) {
@@ -205,35 +219,42 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) s[kh] = mfma(rd_row<D>(sk, 32 * kh, ks, lane), qf[ks], s[kh]);
       }
-      const bool diag = a.causal && (kv0 + KT - 1 > q0);
+      // causal mask, diagonal tiles only: key row 32 kh + crow(r) visible iff <= thr
+      if (a.causal && (kv0 + KT - 1 > q0)) {
+        const int thr = myq - kv0 - 4 * (lane >> 5);
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (32 * kh + (r & 3) + 8 * (r >> 2) > thr) s[kh][r] = -INFINITY;
+      }
       float mt = -INFINITY;
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float x = s[kh][r] * c2;
-          if (diag && kv0 + 32 * kh + crow(r, lane) > myq) x = -INFINITY;
-          s[kh][r] = x;
-          mt = fmaxf(mt, x);
-        }
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      const float mn = fmaxf(m, mt);
-      const float alpha = exp2f(m - mn);
-      m = mn;
-      float ls = 0.f;
+        for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[kh][r]);
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * c2;  // log2 units (c2 > 0)
+      // lazy rescale (FA-style deferred max): only when some query's max grew by > 2^8; P may then
+      // exceed 1 by at most 2^8, harmless in f32 accumulation and in bf16 (relative precision)
+      if (__any(mt > m + kRescaleLog2)) {
+        const float mn = fmaxf(m, mt);
+        const float alpha = __builtin_amdgcn_exp2f(m - mn);
+        m = mn;
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+      }
+      const float nm = -m;
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = exp2f(s[kh][r] - mn);
+          const float p = __builtin_amdgcn_exp2f(fmaf(s[kh][r], c2, nm));
           s[kh][r] = p;
-          ls += p;
+          l += p;
         }
-      l = l * alpha + ls;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
         const bf16x8_t pb = acc_as_b(s[st >> 1], st & 1);
@@ -309,7 +330,8 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
   lds_u8* smem = (lds_u8*)smem_raw;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int kb = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  int kb, hk, b;
+  attn_coords(kb, hk, b);
   const int k0 = kb * NW * 32 + wave * 32;
   const int mykey = k0 + (lane & 31);
   const int group = a.H / a.HKV;
@@ -342,12 +364,12 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv_kernel(AttnArgs a) {
     stage_rows<D>(a.dout + b * a.do_sb + (int64_t)qt * KT * a.do_ss + hq * a.do_sh, a.do_ss, sq + TILE_B, wave, lane);
     if (wave == 0) {  // 64 lse + 64 delta floats = 2 x 256 B: one 4-byte DMA per lane each
       const int64_t ro = ((int64_t)b * a.H + hq) * a.Sq + qt * KT;
-      __builtin_amdgcn_global_load_lds(a.lse + ro + lane, (__attribute__((address_space(3))) void*)(sq + 2 * TILE_B), 4, 0, 0);
-      __builtin_amdgcn_global_load_lds(a.delta + ro + lane, (__attribute__((address_space(3))) void*)(sq + 2 * TILE_B + KT * 4), 4, 0, 0);
+      pt_glds4(a.lse + ro, lane * 4u, (__attribute__((address_space(3))) void*)(sq + 2 * TILE_B));
+      pt_glds4(a.delta + ro, lane * 4u, (__attribute__((address_space(3))) void*)(sq + 2 * TILE_B + KT * 4));
     }
   };
   if (n_iter > 0) stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler: its own fragment loads are done
   __syncthreads();
 
   for (int it = 0; it < n_iter; ++it) {
@@ -369,12 +391,16 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv_kernel(AttnArgs a) {
         s = mfma(rd_row<D>(sq, 32 * qh, ks, lane), kf[ks], s);
         dp = mfma(rd_row<D>(sdo, 32 * qh, ks, lane), vf[ks], dp);
       }
-      const bool diag = a.causal && (qs < k0 + 31);
+      if (a.causal && (qs < k0 + 31)) {  // diagonal: query row crow(r) sees my key iff >= thr
+        const int thr = mykey - qs - 4 * (lane >> 5);
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if ((r & 3) + 8 * (r >> 2) < thr) s[r] = -INFINITY;
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qi = 32 * qh + crow(r, lane);
-        float p = exp2f(s[r] * c2 - slse[qi] * kLog2e);
-        if (diag && mykey > qt * KT + qi) p = 0.f;
+        const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -slse[qi] * kLog2e));
         s[r] = p;                             // P
         dp[r] = p * (dp[r] - sdel[qi]);       // dS
       }
@@ -420,8 +446,9 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnArgs a) {
   lds_u8* smem = (lds_u8*)smem_raw;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nqb = a.Sq / (NW * 32);
-  const int qb = a.causal ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;
-  const int h = blockIdx.y, b = blockIdx.z;
+  int bx, h, b;
+  attn_coords(bx, h, b);
+  const int qb = a.causal ? nqb - 1 - bx : bx;
   const int hk = h / (a.H / a.HKV);
   const int q0 = qb * NW * 32 + wave * 32;
   const int myq = q0 + (lane & 31);
@@ -435,7 +462,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnArgs a) {
     dof[ks] = ld_row_frag(dorow, ks, lane);
   }
   const int64_t ri = ((int64_t)b * a.H + h) * a.Sq + myq;
-  const float lse2 = a.lse[ri] * kLog2e;
+  const float nlse2 = -a.lse[ri] * kLog2e;
   const float del = a.delta[ri];
   const float c2 = a.scale * kLog2e;
 
@@ -453,7 +480,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnArgs a) {
     stage_rows<D>(vbase + (int64_t)kt * KT * a.v_ss, a.v_ss, sk + TILE_B, wave, lane);
   };
   stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler: its own fragment loads are done
   __syncthreads();
 
   for (int kt = 0; kt < nkt; ++kt) {
@@ -473,10 +500,15 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnArgs a) {
           s = mfma(rd_row<D>(sk, 32 * kh, ks, lane), qf[ks], s);
           dp = mfma(rd_row<D>(sv, 32 * kh, ks, lane), dof[ks], dp);
         }
+        if (diag) {  // key row 32 kh + crow(r) visible iff <= thr
+          const int thr = myq - kv0 - 32 * kh - 4 * (lane >> 5);
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if ((r & 3) + 8 * (r >> 2) > thr) s[r] = -INFINITY;
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float p = exp2f(s[r] * c2 - lse2);
-          if (diag && kv0 + 32 * kh + crow(r, lane) > myq) p = 0.f;
+          const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, nlse2));
           s[r] = p * (dp[r] - del);
         }
         ds[kh] = s;

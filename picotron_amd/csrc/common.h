@@ -64,6 +64,31 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// ---- LDS-DMA from inline asm ----------------------------------------------------
+// global -> LDS copies (saddr form: wave-uniform base + per-lane byte offset; M0 = the LDS
+// destination of lane 0).  Issued from asm so the compiler does not treat them as pending LDS
+// writes: it otherwise cannot prove ds_read_b64_tr_b16 reads disjoint from an in-flight LDS-DMA
+// and puts an `s_waitcnt vmcnt(0)` in front of them, draining every prefetch.  The kernels order
+// the copies themselves (counted `s_waitcnt vmcnt(N)` + barrier before the first read).  M0 is
+// written here and read by nothing else in those kernels.
+__device__ __forceinline__ uint64_t pt_uniform_u64(uint64_t p) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+__device__ __forceinline__ void pt_glds16(const void* base, uint32_t voff_bytes,
+                                          __attribute__((address_space(3))) void* dst) {
+  const uint64_t sb = pt_uniform_u64((uint64_t)(uintptr_t)base);
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst);
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(m0), "v"(voff_bytes), "s"(sb) : "memory");
+}
+__device__ __forceinline__ void pt_glds4(const void* base, uint32_t voff_bytes,
+                                         __attribute__((address_space(3))) void* dst) {
+  const uint64_t sb = pt_uniform_u64((uint64_t)(uintptr_t)base);
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst);
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, %2" ::"s"(m0), "v"(voff_bytes), "s"(sb) : "memory");
+}
+
 static inline bool pt_aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 // Grid cap for streaming (HBM-bound) kernels: 256 CUs x 8 blocks.

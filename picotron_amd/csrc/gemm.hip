@@ -421,20 +421,8 @@ __device__ __forceinline__ uint32_t himg_voff(int i, int lane, int64_t ld, int o
   }
 }
 
-// LDS-DMA issued from inline asm (saddr form: uniform base + per-lane byte offset).  The compiler
-// does not see these as LDS writes, so it does not put an `s_waitcnt vmcnt(0)` in front of every
-// ds_read_b64_tr_b16 (it cannot prove the transposed reads disjoint from an in-flight LDS-DMA and
-// drained the whole prefetch pipeline before each MN-contiguous fragment read); ordering is ours:
-// the counted vmcnt + barrier of the K-loop.  M0 is written here and used by nothing else in the
-// kernel.
 __device__ __forceinline__ void glds16_asm(const uint16_t* base, uint32_t voff_elems, lds_u8* dst) {
-  const uint64_t p = (uint64_t)(uintptr_t)base;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
-  const uint64_t sb = (uint64_t)lo | ((uint64_t)hi << 32);
-  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst);
-  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(m0), "v"(voff_elems * 2u), "s"(sb)
-               : "memory");
+  pt_glds16(base, voff_elems * 2u, (__attribute__((address_space(3))) void*)dst);  // common.h
 }
 
 template <bool AK, bool BKC, int EPI>
