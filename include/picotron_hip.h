@@ -33,7 +33,12 @@ int pt_rmsnorm_fwd(const void* x, const void* residual, const void* weight, void
                    int64_t rows, int64_t cols, float eps, int mode, hipStream_t stream);
 /* number of f32 rows of `cols` the bwd needs in dw_partial */
 int pt_rmsnorm_bwd_partials(int64_t rows, int cols);
-/* autograd backward of the above: dx = d/dz (+ dres), dweight [cols] bf16 (may be NULL) */
+/* autograd backward of the above: dx = d/dz (+ dres), dweight [cols] (may be NULL).
+ * mode = norm mode (0 / 1) | dweight sink: 0 store bf16; PT_DW_ACC_BF16 dweight = bf16(dweight +
+ * bf16(dw)) (autograd's accumulation into a bf16 .grad); PT_DW_ACC_F32 dweight is f32, += dw
+ * (DataParallelBucket main_grad).  The weight sum is in a fixed order (deterministic). */
+#define PT_DW_ACC_BF16 4
+#define PT_DW_ACC_F32 8
 int pt_rmsnorm_bwd(const void* dy, const void* z, const void* weight, const float* rstd, const void* dres,
                    void* dx, void* dweight, float* dw_partial, int64_t rows, int64_t cols, int mode,
                    hipStream_t stream);
@@ -62,6 +67,15 @@ int pt_swiglu_bwd(const void* dh, int64_t dh_stride, const void* g, int64_t g_st
 int pt_cross_entropy_fwd_bwd(const void* logits, int64_t logits_stride, const int64_t* targets, void* dlogits,
                              int64_t dlogits_stride, float* row_loss, int64_t rows, int64_t vocab, float scale,
                              const float* inv_count, int64_t ignore_index, hipStream_t stream);
+
+/* ---- fused AdamW step ---------------------------------------------------------------------
+ * replaces train.py:209 torch.optim.AdamW(...).step() for one tensor: the eight foreach passes of
+ * torch's multi-tensor Adam (decoupled weight decay) in one, same per-op rounding to the storage
+ * dtype (dtype 0 bf16, 1 f32).  Scalars as torch casts them: decay = 1 - lr*wd, w1 = 1 - beta1,
+ * c2 = 1 - beta2, bc2_sqrt = sqrt(1 - beta2^t), step_size = -lr / (1 - beta1^t). */
+int pt_adamw_step(void* param, const void* grad, void* exp_avg, void* exp_avg_sq, int64_t n, int dtype,
+                  float decay, float w1, float beta2, float c2, float bc2_sqrt, float eps, float step_size,
+                  hipStream_t stream);
 
 /* ---- bf16 GEMM, f32 accumulate -------------------------------------------------------------
  * replaces every F.linear / matmul of the layer: model.py:124-126,161,186,270,

@@ -1,0 +1,125 @@
+// Fused AdamW step for gfx950: one pass over (param, grad, exp_avg, exp_avg_sq) per tensor.
+//
+// Replaces (reference, /root/reference): picotron/train.py:205-209 -- `torch.optim.AdamW(
+// model.parameters(), lr=learning_rate)` (the reference's own fused switch at :205-207 is dead
+// code), i.e. torch's multi-tensor Adam with decoupled weight decay, which on bf16 tensors runs
+// eight foreach passes, each computing in f32 and rounding its result to the tensor dtype:
+//   p  = r(p * decay)                       _foreach_mul_      decay = 1 - lr * wd
+//   m  = r(m + w1 * (g - m))                _foreach_lerp_     w1 = 1 - beta1 (|w| < .5 form)
+//   v  = r(v * beta2)                       _foreach_mul_
+//   v  = r(v + c2 * (g * g))                _foreach_addcmul_  c2 = 1 - beta2
+//   s  = r(sqrt(v)); s = r(s / bc2s); s = r(s + eps)   _foreach_sqrt / div_ / add_
+//   p  = r(p + step * (m / s))              _foreach_addcdiv_  step = -lr / (1 - beta1^t)
+// r() = round to the storage dtype.  This kernel performs exactly that sequence per element, with
+// the roundings, so its result matches torch's bit for bit up to f32 contraction differences --
+// but reads each of the four tensors once and writes three (14 bytes per bf16 parameter instead
+// of ~44 over the eight passes).  Scalars arrive as f32, as torch's foreach kernels cast them.
+#include "common.h"
+
+namespace {
+
+struct AdamScalars {
+  float decay, w1, beta2, c2, bc2s, eps, step;
+};
+
+template <typename T>
+__device__ __forceinline__ float ld_as_f(const T* p, int64_t i);
+template <>
+__device__ __forceinline__ float ld_as_f<uint16_t>(const uint16_t* p, int64_t i) { return bf2f(p[i]); }
+template <>
+__device__ __forceinline__ float ld_as_f<float>(const float* p, int64_t i) { return p[i]; }
+
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamScalars& s, bool bf) {
+  auto r = [bf](float x) { return bf ? round_bf(x) : x; };
+  p = r(p * s.decay);
+  m = r(m + s.w1 * (g - m));
+  v = r(v * s.beta2);
+  v = r(v + s.c2 * (g * g));
+  float d = r(sqrtf(v));
+  d = r(d / s.bc2s);
+  d = r(d + s.eps);
+  p = r(p + s.step * (m / d));
+}
+
+// bf16 tensors: 8 elements per thread (16-byte loads / stores on all four streams)
+__global__ __launch_bounds__(256) void adamw_bf16_kernel(uint16_t* __restrict__ param, const uint16_t* __restrict__ grad,
+                                                         uint16_t* __restrict__ m, uint16_t* __restrict__ v,
+                                                         int64_t n8, AdamScalars s) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    float p[8], g[8], a[8], b[8];
+    unpack8(ld8(param + i * 8), p);
+    unpack8(ld8(grad + i * 8), g);
+    unpack8(ld8(m + i * 8), a);
+    unpack8(ld8(v + i * 8), b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) adam_elem(p[j], g[j], a[j], b[j], s, true);
+    st8(param + i * 8, pack8(p));
+    st8(m + i * 8, pack8(a));
+    st8(v + i * 8, pack8(b));
+  }
+}
+
+// scalar tail (n % 8) of a bf16 tensor, and f32 tensors
+template <typename T>
+__global__ __launch_bounds__(256) void adamw_scalar_kernel(T* __restrict__ param, const T* __restrict__ grad,
+                                                           T* __restrict__ m, T* __restrict__ v, int64_t n,
+                                                           AdamScalars s) {
+  constexpr bool bf = sizeof(T) == 2;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float p = ld_as_f(param, i), g = ld_as_f(grad, i), a = ld_as_f(m, i), b = ld_as_f(v, i);
+    adam_elem(p, g, a, b, s, bf);
+    if (bf) {
+      ((uint16_t*)param)[i] = f2bf(p);
+      ((uint16_t*)m)[i] = f2bf(a);
+      ((uint16_t*)v)[i] = f2bf(b);
+    } else {
+      ((float*)param)[i] = p;
+      ((float*)m)[i] = a;
+      ((float*)v)[i] = b;
+    }
+  }
+}
+
+int grid_for(int64_t work) {
+  int64_t g = (work + 255) / 256;
+  return (int)(g < PT_STREAM_GRID_CAP ? (g < 1 ? 1 : g) : PT_STREAM_GRID_CAP);
+}
+
+}  // namespace
+
+extern "C" {
+
+int pt_adamw_step(void* param, const void* grad, void* exp_avg, void* exp_avg_sq, int64_t n, int dtype,
+                  float decay, float w1, float beta2, float c2, float bc2_sqrt, float eps, float step_size,
+                  hipStream_t stream) {
+  if (!param || !grad || !exp_avg || !exp_avg_sq || n < 0) return PT_EINVAL;
+  if (n == 0) return PT_OK;
+  const AdamScalars s{decay, w1, beta2, c2, bc2_sqrt, eps, step_size};
+  if (dtype == 0) {  // bf16
+    auto* P = (uint16_t*)param;
+    auto* G = (const uint16_t*)grad;
+    auto* M = (uint16_t*)exp_avg;
+    auto* V = (uint16_t*)exp_avg_sq;
+    const bool vec = pt_aligned16(P) && pt_aligned16(G) && pt_aligned16(M) && pt_aligned16(V);
+    const int64_t n8 = vec ? n / 8 : 0;
+    if (n8) {
+      adamw_bf16_kernel<<<grid_for(n8), 256, 0, stream>>>(P, G, M, V, n8, s);
+      PT_CHECK_LAUNCH();
+    }
+    const int64_t done = n8 * 8;
+    if (done < n) {
+      adamw_scalar_kernel<uint16_t><<<grid_for(n - done), 256, 0, stream>>>(P + done, G + done, M + done, V + done,
+                                                                             n - done, s);
+      PT_CHECK_LAUNCH();
+    }
+  } else if (dtype == 1) {  // f32
+    adamw_scalar_kernel<float><<<grid_for(n), 256, 0, stream>>>((float*)param, (const float*)grad, (float*)exp_avg,
+                                                                (float*)exp_avg_sq, n, s);
+    PT_CHECK_LAUNCH();
+  } else {
+    return PT_EINVAL;
+  }
+  return PT_OK;
+}
+
+}  // extern "C"

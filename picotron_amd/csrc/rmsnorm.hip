@@ -82,6 +82,10 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_fwd_kernel(
 // dz = rstd * (dxh - xh * mean(dxh * xh)),  dxh = dy * w,  xh = z * rstd
 // dx = dz (+ dres when the residual branch gradient is fused in)
 // dw partial per block: sum over this block's rows of dy * xh (mode 1: dy * bf16(xh))
+// A wave owns RB rows (row, row + nwaves, ...) and issues all of their z / dy loads before it
+// reduces the first: RB x 2 x NCH x 16 B in flight per lane instead of one row's worth -- the
+// single-row loop was a chain of load -> wave reduction -> store per row at one wave per SIMD.
+constexpr int kBwdRows = 4;
 template <int NCH>
 __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ z, const uint16_t* __restrict__ w,
@@ -104,41 +108,63 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(
     if (c < nchunk) unpack8(ld8(w + c * 8), wf[i]);
   }
 
-  for (int64_t row = wave; row < rows; row += nwaves) {
-    const float rstd = rstd_in[row];
-    float xh[NCH][8], g[NCH][8];
-    float dot = 0.f;
+  for (int64_t row0 = wave; row0 < rows; row0 += nwaves * kBwdRows) {
+    bf16x8 zr[kBwdRows][NCH], dr[kBwdRows][NCH];
+    float rs[kBwdRows];
 #pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int c = lane + i * PT_WAVE;
-      if (c < nchunk) {
-        float zz[8], d[8];
-        unpack8(ld8(z + row * cols + c * 8), zz);
-        unpack8(ld8(dy + row * cols + c * 8), d);
+    for (int k = 0; k < kBwdRows; ++k) {
+      const int64_t row = row0 + k * nwaves;
+      if (row < rows) {
+        rs[k] = rstd_in[row];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          xh[i][j] = zz[j] * rstd;
-          g[i][j] = d[j] * wf[i][j];
-          dot += g[i][j] * xh[i][j];
-          dwacc[i][j] += d[j] * (mode == 0 ? xh[i][j] : round_bf(xh[i][j]));
+        for (int i = 0; i < NCH; ++i) {
+          const int c = lane + i * PT_WAVE;
+          if (c < nchunk) {
+            zr[k][i] = ld8(z + row * cols + c * 8);
+            dr[k][i] = ld8(dy + row * cols + c * 8);
+          }
         }
       }
     }
-    dot = wave_sum(dot) * inv_cols;
 #pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int c = lane + i * PT_WAVE;
-      if (c < nchunk) {
-        float o[8];
+    for (int k = 0; k < kBwdRows; ++k) {
+      const int64_t row = row0 + k * nwaves;
+      if (row >= rows) break;
+      const float rstd = rs[k];
+      float xh[NCH][8], g[NCH][8];
+      float dot = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = rstd * (g[i][j] - xh[i][j] * dot);
-        if (dres) {
-          float r[8];
-          unpack8(ld8(dres + row * cols + c * 8), r);
+      for (int i = 0; i < NCH; ++i) {
+        const int c = lane + i * PT_WAVE;
+        if (c < nchunk) {
+          float zz[8], d[8];
+          unpack8(zr[k][i], zz);
+          unpack8(dr[k][i], d);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] += r[j];
+          for (int j = 0; j < 8; ++j) {
+            xh[i][j] = zz[j] * rstd;
+            g[i][j] = d[j] * wf[i][j];
+            dot += g[i][j] * xh[i][j];
+            dwacc[i][j] += d[j] * (mode == 0 ? xh[i][j] : round_bf(xh[i][j]));
+          }
         }
-        st8(dx + row * cols + c * 8, pack8(o));
+      }
+      dot = wave_sum(dot) * inv_cols;
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        const int c = lane + i * PT_WAVE;
+        if (c < nchunk) {
+          float o[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = rstd * (g[i][j] - xh[i][j] * dot);
+          if (dres) {
+            float r[8];
+            unpack8(ld8(dres + row * cols + c * 8), r);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] += r[j];
+          }
+          st8(dx + row * cols + c * 8, pack8(o));
+        }
       }
     }
   }
@@ -174,26 +200,49 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(
   }
 }
 
-// dw[col] = bf16(sum_p partial[p][col])  -- fixed summation order, deterministic.
-// A block owns 32 columns; its 8 row groups (one per 32 threads) stride over the partial rows
-// with coalesced 128-B reads, then combine through LDS in a fixed order.
-constexpr int kColsumCols = 32, kColsumGroups = 8;
-__global__ __launch_bounds__(256) void colsum_to_bf16_kernel(const float* __restrict__ partial, int nparts,
-                                                             int cols, uint16_t* __restrict__ out,
-                                                             float* __restrict__ out_f32) {
-  __shared__ float red[kColsumGroups][kColsumCols];
-  const int c = threadIdx.x % kColsumCols, g = threadIdx.x / kColsumCols;
-  const int col = blockIdx.x * kColsumCols + c;
-  float s = 0.f;
-  if (col < cols)
-    for (int p = g; p < nparts; p += kColsumGroups) s += partial[(int64_t)p * cols + col];
-  red[g][c] = s;
-  __syncthreads();
-  if (g == 0 && col < cols) {
+// dw[col] = sum_p partial[p][col]  -- fixed summation order, deterministic.  One block per 8
+// columns (256 blocks for cols 2048: every CU): thread t sums partial rows t, t + 256, ... of its
+// block's 8 columns (two 16-B loads per row), then a fixed-shape LDS tree over the 256 threads.
+// Sink (flags): 0 store bf16, DW_ACC_BF16 bf16 accumulate (= autograd's grad + bf16(new)),
+// DW_ACC_F32 f32 accumulate (DataParallelBucket main_grad).
+constexpr int kColsumThreads = 256;
+__global__ __launch_bounds__(kColsumThreads) void colsum_kernel(const float* __restrict__ partial, int nparts,
+                                                                int cols, void* __restrict__ out, int sink) {
+  __shared__ float red[kColsumThreads][9];  // +1 pad
+  const int t = threadIdx.x;
+  const int col0 = blockIdx.x * 8;
+  float s[8];
 #pragma unroll
-    for (int k = 1; k < kColsumGroups; ++k) s += red[k][c];
-    if (out) out[col] = f2bf(s);
-    if (out_f32) out_f32[col] = s;
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+  for (int p = t; p < nparts; p += kColsumThreads) {
+    const float4 a = *(const float4*)(partial + (int64_t)p * cols + col0);
+    const float4 b = *(const float4*)(partial + (int64_t)p * cols + col0 + 4);
+    s[0] += a.x; s[1] += a.y; s[2] += a.z; s[3] += a.w;
+    s[4] += b.x; s[5] += b.y; s[6] += b.z; s[7] += b.w;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[t][j] = s[j];
+  __syncthreads();
+  for (int w = kColsumThreads / 2; w >= 8; w >>= 1) {
+    if (t < w) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[t][j] += red[t + w][j];
+    }
+    __syncthreads();
+  }
+  if (t < 8) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v += red[k][t];
+    const int col = col0 + t;
+    if (sink == PT_DW_ACC_F32) {
+      ((float*)out)[col] += v;
+    } else if (sink == PT_DW_ACC_BF16) {
+      uint16_t* o = (uint16_t*)out;
+      o[col] = f2bf(bf2f(o[col]) + round_bf(v));
+    } else {
+      ((uint16_t*)out)[col] = f2bf(v);
+    }
   }
 }
 
@@ -256,6 +305,8 @@ int pt_rmsnorm_bwd(const void* dy, const void* z, const void* weight, const floa
     return PT_EALIGN;
   const int nch = nch_for((int)cols);
   if (nch < 0) return PT_EUNSUPPORTED;
+  const int nmode = mode & 3;
+  if (nmode > 1 || (mode & PT_DW_ACC_BF16 && mode & PT_DW_ACC_F32)) return PT_EINVAL;
   const int grid = (int)(rows < 256 * kWavesPerBlock ? (rows + kWavesPerBlock - 1) / kWavesPerBlock : 256);
   const int nparts = pt_rmsnorm_bwd_partials(rows, (int)cols);
   const auto* DY = (const uint16_t*)dy;
@@ -264,16 +315,17 @@ int pt_rmsnorm_bwd(const void* dy, const void* z, const void* weight, const floa
   const auto* DR = (const uint16_t*)dres;
   auto* DX = (uint16_t*)dx;
   switch (nch) {
-    case 1: rmsnorm_bwd_kernel<1><<<grid, kThreads, 0, stream>>>(DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, mode); break;
-    case 2: rmsnorm_bwd_kernel<2><<<grid, kThreads, 0, stream>>>(DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, mode); break;
-    case 4: rmsnorm_bwd_kernel<4><<<grid, kThreads, 0, stream>>>(DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, mode); break;
-    case 8: rmsnorm_bwd_kernel<8><<<grid, kThreads, 0, stream>>>(DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, mode); break;
+    case 1: rmsnorm_bwd_kernel<1><<<grid, kThreads, 0, stream>>>(DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
+    case 2: rmsnorm_bwd_kernel<2><<<grid, kThreads, 0, stream>>>(DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
+    case 4: rmsnorm_bwd_kernel<4><<<grid, kThreads, 0, stream>>>(DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
+    case 8: rmsnorm_bwd_kernel<8><<<grid, kThreads, 0, stream>>>(DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
     default: return PT_EUNSUPPORTED;
   }
   PT_CHECK_LAUNCH();
   if (dweight) {
-    colsum_to_bf16_kernel<<<(int)((cols + kColsumCols - 1) / kColsumCols), 256, 0, stream>>>(dw_partial, nparts, (int)cols,
-                                                                        (uint16_t*)dweight, nullptr);
+    if (cols % 8) return PT_EUNSUPPORTED;
+    colsum_kernel<<<(int)(cols / 8), kColsumThreads, 0, stream>>>(dw_partial, nparts, (int)cols, dweight,
+                                                                  mode & (PT_DW_ACC_BF16 | PT_DW_ACC_F32));
     PT_CHECK_LAUNCH();
   }
   return PT_OK;

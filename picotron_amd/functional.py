@@ -68,16 +68,23 @@ def wgrad(dy2d, x2d, params):
         _grad_ready(p)
 
 
-def add_vector_grad(p, g):
-    """Accumulate a small (norm-weight) gradient g into p's sink."""
-    mg = getattr(p, "main_grad", None)
+def norm_bwd(dy2, z, weight, rstd, mode, dres=None, need_dw=True):
+    """RMSNorm backward with the weight gradient summed straight into p's sink (bf16 .grad store or
+    accumulate -- autograd's AccumulateGrad -- or the f32 main_grad of DataParallelBucket)."""
+    if not need_dw:
+        dx, _ = K.rmsnorm_bwd(dy2, z, weight, rstd, mode, dres=dres)
+        return dx
+    mg = getattr(weight, "main_grad", None)
     if mg is not None:
-        mg.add_(g)
-    elif p.grad is None:
-        p.grad = g
+        buf, sink = mg, K.DW_ACC_F32
+    elif weight.grad is None:
+        weight.grad = torch.empty_like(weight)
+        buf, sink = weight.grad, 0
     else:
-        p.grad.add_(g)
-    _grad_ready(p)
+        buf, sink = weight.grad, K.DW_ACC_BF16
+    dx, _ = K.rmsnorm_bwd(dy2, z, weight, rstd, mode, dres=dres, dw_out=buf, dw_sink=sink)
+    _grad_ready(weight)
+    return dx
 
 
 # ------------------------------------------------------------------------ TP collectives
@@ -122,9 +129,7 @@ class RMSNormFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x2, weight, rstd = ctx.saved_tensors
-        dx, dw = K.rmsnorm_bwd(_contig2d(dy), x2, weight, rstd, ctx.mode)
-        if ctx.needs_input_grad[1]:
-            add_vector_grad(weight, dw)
+        dx = norm_bwd(_contig2d(dy), x2, weight, rstd, ctx.mode, need_dw=ctx.needs_input_grad[1])
         return dx.view(ctx.shape), None, None, None
 
 
@@ -146,9 +151,7 @@ class AddRMSNormFunction(torch.autograd.Function):
         if dy is None:
             dy = torch.zeros(ctx.shape, dtype=z.dtype, device=z.device)
         dres = _contig2d(dz) if dz is not None else None
-        dx, dw = K.rmsnorm_bwd(_contig2d(dy), z, weight, rstd, ctx.mode, dres=dres)
-        if ctx.needs_input_grad[2]:
-            add_vector_grad(weight, dw)
+        dx = norm_bwd(_contig2d(dy), z, weight, rstd, ctx.mode, dres=dres, need_dw=ctx.needs_input_grad[2])
         dx = dx.view(ctx.shape)
         return dx, dx, None, None, None
 
@@ -367,11 +370,9 @@ class DecoderLayerFunction(torch.autograd.Function):
         tp = TPContext.current()
         dout2 = _contig2d(dout)
         dh2 = mlp_block_bwd(dout2, h2, (gu, hh), wg, wu, wd, tp)
-        dz, dw2 = K.rmsnorm_bwd(dh2, z, w2, rstd2, mode, dres=dout2)
-        add_vector_grad(w2, dw2)
+        dz = norm_bwd(dh2, z, w2, rstd2, mode, dres=dout2)
         dh1 = attn_block_bwd(dz, h1, (qkv, o, lse), wq, wk, wv, wo, cos, sin, sh, tp)
-        dx, dw1 = K.rmsnorm_bwd(dh1, x2, w1, rstd1, mode, dres=dz)
-        add_vector_grad(w1, dw1)
+        dx = norm_bwd(dh1, x2, w1, rstd1, mode, dres=dz)
         return (dx.view(sh.B, sh.S, -1),) + (None,) * 16
 
 

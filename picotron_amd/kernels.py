@@ -53,8 +53,13 @@ def rmsnorm_fwd(x, weight, eps, mode=MODE_TRITON, residual=None):
     return y, rstd, z
 
 
-def rmsnorm_bwd(dy, z, weight, rstd, mode=MODE_TRITON, dres=None):
-    """Returns (dx, dweight).  dres (same shape as dy) is added into dx when given."""
+DW_ACC_BF16, DW_ACC_F32 = 4, 8   # pt_rmsnorm_bwd dweight sinks (include/picotron_hip.h)
+
+
+def rmsnorm_bwd(dy, z, weight, rstd, mode=MODE_TRITON, dres=None, dw_out=None, dw_sink=0):
+    """Returns (dx, dweight).  dres (same shape as dy) is added into dx when given.
+    dw_out/dw_sink: write the weight gradient into an existing buffer -- 0 store (bf16),
+    DW_ACC_BF16 accumulate into a bf16 .grad, DW_ACC_F32 accumulate into an f32 main_grad."""
     dy = dy.contiguous()
     rows, cols = z.shape
     lib = _C.lib()
@@ -62,13 +67,36 @@ def rmsnorm_bwd(dy, z, weight, rstd, mode=MODE_TRITON, dres=None):
     _C.check(0 if nparts > 0 else nparts, "pt_rmsnorm_bwd_partials")
     partial = torch.empty(nparts, cols, dtype=torch.float32, device=z.device)
     dx = torch.empty_like(z)
-    dw = torch.empty(cols, dtype=BF16, device=z.device)
+    if dw_out is None:
+        dw_out, dw_sink = torch.empty(cols, dtype=BF16, device=z.device), 0
+    _req(dw_out.is_contiguous() and dw_out.numel() == cols, "dweight buffer must be contiguous [cols]")
+    _req(dw_out.dtype == (torch.float32 if dw_sink == DW_ACC_F32 else BF16), "dweight buffer dtype")
     if dres is not None:
         dres = dres.contiguous()
-    rc = lib.pt_rmsnorm_bwd(_ptr(dy), _ptr(z), _ptr(weight), _ptr(rstd), _ptr(dres), _ptr(dx), _ptr(dw),
-                            _ptr(partial), rows, cols, int(mode), _C.stream_ptr())
+    rc = lib.pt_rmsnorm_bwd(_ptr(dy), _ptr(z), _ptr(weight), _ptr(rstd), _ptr(dres), _ptr(dx), _ptr(dw_out),
+                            _ptr(partial), rows, cols, int(mode) | int(dw_sink), _C.stream_ptr())
     _C.check(rc, "pt_rmsnorm_bwd")
-    return dx, dw
+    return dx, dw_out
+
+
+# ----------------------------------------------------------------------------------- AdamW
+def adamw_step(p, grad, exp_avg, exp_avg_sq, decay, w1, beta2, c2, bc2_sqrt, eps, step_size):
+    """One fused AdamW update of tensor p in place (csrc/adamw.hip; torch foreach semantics)."""
+    for t, nm in ((grad, "grad"), (exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq")):
+        _req(t.dtype == p.dtype and t.numel() == p.numel() and t.device == p.device, f"adamw: {nm} must match param")
+        _req(t.is_contiguous() or t.stride() == p.stride(), f"adamw: {nm} layout must match param")
+    _req(p.is_contiguous(), "adamw: param must be contiguous")
+    _req(grad.is_contiguous() and exp_avg.is_contiguous() and exp_avg_sq.is_contiguous(), "adamw: dense tensors")
+    if p.dtype == BF16:
+        dt = 0
+    elif p.dtype == torch.float32:
+        dt = 1
+    else:
+        raise _C.HipKernelError(f"adamw: unsupported dtype {p.dtype}")
+    rc = _C.lib().pt_adamw_step(_ptr(p), _ptr(grad), _ptr(exp_avg), _ptr(exp_avg_sq), p.numel(), dt, float(decay),
+                                float(w1), float(beta2), float(c2), float(bc2_sqrt), float(eps), float(step_size),
+                                _C.stream_ptr())
+    _C.check(rc, "pt_adamw_step")
 
 
 # ------------------------------------------------------------------------------------ RoPE

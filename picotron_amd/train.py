@@ -68,11 +68,14 @@ class SyntheticMicroBatchDataLoader:
                 "hidden_states": None}
 
 
-def train_step(model, data_loader, device):
-    """train.py:29-55 with the fused HIP cross-entropy; returns the accumulated loss (float)."""
+def train_step(model, data_loader, device, on_microbatch=None):
+    """train.py:29-55 with the fused HIP cross-entropy; returns the accumulated loss (float).
+    on_microbatch(i): optional hook called before micro-batch i (bench.py samples its GEMM timing)."""
     acc_loss = torch.zeros((), dtype=torch.float32, device=device)
     requires_grad_sync = pgm.current().cp_dp_world_size > 1
     for i in range(data_loader.grad_acc_steps):
+        if on_microbatch is not None:
+            on_microbatch(i)
         batch = next(data_loader)
         input_ids = batch["input_ids"].to(device)
         target_ids = batch["target_ids"].to(device)

@@ -65,6 +65,32 @@ def test_rmsnorm_fused_residual():
     assert rel_err(dx, zf.grad + dres.float()) < 1e-2
 
 
+@pytest.mark.parametrize("rows", [4096, 1000, 5000])
+def test_rmsnorm_dweight_sinks(rows):
+    """dweight written into an existing sink: bf16 store, bf16 accumulate (= autograd's grad +
+    bf16(new)), f32 accumulate (main_grad); the partial-row sum is deterministic (bitwise repeat)."""
+    from picotron_amd import kernels as K
+    cols = 2048
+    x, dy = torch.randn(rows, cols).to(BF).to(DEV), torch.randn(rows, cols).to(BF).to(DEV)
+    w = (1 + 0.1 * torch.randn(cols)).to(BF).to(DEV)
+    _, rstd, _ = K.rmsnorm_fwd(x, w, 1e-5, 0)
+    _, dw = K.rmsnorm_bwd(dy, x, w, rstd, 0)
+    _, dw2 = K.rmsnorm_bwd(dy, x, w, rstd, 0)
+    assert torch.equal(dw, dw2)
+    xr = x.float().cpu().requires_grad_(True)
+    wr = w.float().cpu().requires_grad_(True)
+    O.rmsnorm_flash_semantics(xr, wr, 1e-5).backward(dy.float().cpu())
+    assert rel_err(dw, wr.grad) < 1e-2
+    old = torch.randn(cols).to(BF).to(DEV)
+    acc = old.clone()
+    K.rmsnorm_bwd(dy, x, w, rstd, 0, dw_out=acc, dw_sink=K.DW_ACC_BF16)
+    assert torch.equal(acc, old + dw)
+    oldf = torch.randn(cols, device=DEV)
+    accf = oldf.clone()
+    _, _ = K.rmsnorm_bwd(dy, x, w, rstd, 0, dw_out=accf, dw_sink=K.DW_ACC_F32)
+    assert rel_err(accf - oldf, dw.float()) < 1e-2
+
+
 # ------------------------------------------------------------------------------ RoPE
 @pytest.mark.parametrize("d", [64, 128])
 def test_rope_fused_qk_rows(d):
