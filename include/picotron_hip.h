@@ -91,6 +91,27 @@ int pt_gemm(const void* A, int64_t lda, int a_kcontig, const void* const* B, con
             const int64_t* c_bounds, int nc, int64_t M, int64_t N, int64_t K, int epilogue,
             const void* residual, int64_t ldr, int tile, hipStream_t stream);
 int pt_gemm_pick_tile(int64_t M, int64_t N, const int64_t* mseg, int nmseg, const int64_t* nseg, int nnseg);
+/* Grouped GEMM: nprob (<= 4) independent problems in ONE launch, each described like pt_gemm's
+ * arguments, sharing layouts (a_kcontig, b_kcontig), epilogue and tile (-1 = auto over the
+ * group).  Used where one problem alone would leave CUs idle (dW of q|k|v + dW of o_proj). */
+typedef struct {
+  const void* A;
+  int64_t lda;
+  const void* B[4];
+  int64_t ldb[4];
+  int64_t b_bounds[5];
+  int nb;
+  int b_seg_dim;
+  void* C[4];
+  int64_t ldc[4];
+  int64_t c_bounds[5];
+  int nc;
+  int64_t M, N, K;
+  const void* residual;
+  int64_t ldr;
+} pt_gemm_problem;
+int pt_gemm_grouped(const pt_gemm_problem* probs, int nprob, int a_kcontig, int b_kcontig, int epilogue, int tile,
+                    hipStream_t stream);
 
 /* ---- flash attention ----------------------------------------------------------------------
  * replaces model.py:33-37,154 flash_attn_func(causal=True) / model.py:157 SDPA, and the ring

@@ -14,27 +14,20 @@
 //     (dX = [dq|dk|dv] . [Wq;Wk;Wv]);  * C may be split along M (dW of q,k,v in one launch).
 //   Segment boundaries must be multiples of the tile (checked on the host).
 //
-// Two kernel structures, both v_mfma_f32_16x16x32_bf16 with operands staged global->LDS by
-// global_load_lds_dwordx4 (LDS-DMA, lane-linear 1 KiB per wave instruction; the XOR swizzle is
+// Kernels (all v_mfma_f32_16x16x32_bf16, fp32 accumulators, operands staged global->LDS by
+// global_load_lds_dwordx4: LDS-DMA, lane-linear 1 KiB per wave instruction; the XOR swizzle is
 // applied to the per-lane SOURCE address and undone on the ds_read -- tools/lds_swizzle_search.py:
 // conflict-free for ds_read_b128 on K-contiguous images and ds_read_b64_tr_b16 on MN-contiguous
 // images):
+//  * gemm_8ph_kernel (tile 12, 256x256) and gemm_4ph_kernel (tile 13, 256x128): phased,
+//    wave-group ping-pong schedules with one counted vmcnt per K-tile (see each kernel) -- every
+//    projection of the layer, 1.0-1.38 PF/s (profiles/r01_gemm_tiles_8ph.md).
+//  * gemm_kernel (tiles 2 / 3 / 4 / 5 / 8 / 9): the simple two-stage loop, for shapes the phased
+//    kernels do not divide.
+// One launch may carry up to 4 independent problems (pt_gemm_grouped) to fill the CUs.
 //
-//  * gemm_pipe_kernel (tiles 256x256 and 256x128, 8 waves as 2(M) x 4(N), the large shapes):
-//    each K-tile is four phases, one per quadrant of the wave's output tile, each closed by a raw
-//    s_barrier.  The operand tiles are kept as four independent "half images" (A rows 0-127 /
-//    128-255, B cols 0-BN/2 / BN/2-BN) so a buffer is refilled half by half: the DMA of K-tile
-//    t+1's halves is issued in phases 1-3 of tile t and the first half of t+2 in phase 4 (the
-//    moment all waves have finished reading tile t's buffer), and the single wait per K-tile is a
-//    counted `s_waitcnt vmcnt(2)` that leaves that half in flight across the barrier -- the load
-//    path never drains (cdna_hip_programming.md §5 "Pipelining across barriers", T3+T4).  Wave
-//    fragments are read quadrant by quadrant (A rows 0-63 + B cols 0-31, B cols 32-63, A rows
-//    64-127, registers reused for the 4th) and the MFMA cluster of each phase is bracketed with
-//    s_setprio (T5).
-//  * gemm_kernel (tiles 128x128, 64x64; small / ragged shapes): the simple two-stage loop.
-//
-// Epilogue (both): the wave's tile is staged through LDS as bf16 rows and written as whole 16-byte
-// row segments; fp32 epilogues (main_grad accumulation) write the accumulator directly.
+// Epilogue: the wave's tile is staged through LDS as bf16 rows and written as whole 16-byte row
+// segments; fp32 epilogues (main_grad accumulation) write the accumulator directly.
 #include "common.h"
 
 #include <type_traits>
@@ -143,10 +136,27 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return base + (bid >> 3);
 }
 
-// tile order: XCD remap, then group 8 tile-rows so an XCD's neighbours share A/B panels
-__device__ __forceinline__ void tile_coords(const GemmArgs& a, int& tile_m, int& tile_n) {
-  const int nwg = a.tiles_m * a.tiles_n;
-  const int pid = xcd_remap(blockIdx.x, nwg);
+// A launch runs up to kMaxProb independent problems ("grouped GEMM": e.g. dW of q|k|v and dW of
+// o_proj, 192 + 64 tiles, fill the 256 CUs together where each alone leaves CUs idle).  Problems
+// share the kernel instantiation (layouts, epilogue, tile); their tiles are numbered
+// consecutively (start[i] = first tile id of problem i).
+constexpr int kMaxProb = 4;
+struct GemmGroup {
+  GemmArgs p[kMaxProb];
+  int start[kMaxProb + 1];
+  int nprob;
+};
+
+// tile order: XCD remap over the whole grid (consecutive ids share an XCD), then the problem,
+// then group 8 tile-rows so an XCD's neighbours share A/B panels
+__device__ __forceinline__ const GemmArgs& select_problem(const GemmGroup& g, int& tile_m, int& tile_n) {
+  const int pid_all = xcd_remap(blockIdx.x, gridDim.x);
+  int pi = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxProb; ++i)
+    if (i < g.nprob && pid_all >= g.start[i]) pi = i;
+  const GemmArgs& a = g.p[pi];
+  const int pid = pid_all - g.start[pi];
   constexpr int GROUP = 8;
   const int group_span = GROUP * a.tiles_n;
   const int gid = pid / group_span;
@@ -154,6 +164,7 @@ __device__ __forceinline__ void tile_coords(const GemmArgs& a, int& tile_m, int&
   const int gsize = min(a.tiles_m - first_m, GROUP);
   tile_m = first_m + (pid % group_span) % gsize;
   tile_n = (pid % group_span) / gsize;
+  return a;
 }
 
 // Write the wave's TM x TN accumulator tile (FM x FN 16x16 fragments) at output (m0 + wm*TM,
@@ -239,154 +250,6 @@ __device__ __forceinline__ const uint16_t* b_image_ptr(const GemmArgs& a, bool b
   return bkc ? Bp + nl * ld + kl : Bp + kl * ld + nl;
 }
 
-// =============================================================================== pipelined
-// LDS holds two rings of half images: A halves (128 rows x 64 k, 16 KiB) in 5 slots and B halves
-// (BN/2 cols x 64 k) in 5 slots -- 2.5 K-tiles, 160 KiB at BN = 256.  Half images of K-tile u are
-// issued during the four phases of K-tile u-2, in the order A0, B0, B1, A1, each into the slot of
-// a half image whose last read retired at least one barrier earlier:
-//   A slot (2u + a) % 5 last held A1 of u-3 (a = 0) or A0 of u-2 (a = 1: read until phase 3 of
-//   u-2, re-staged in phase 4);  B slot (2u + b) % 5 last held B1 of u-3 or B0 of u-2 (read until
-//   phase 2, re-staged in phase 3).
-// DMAs are issued at the start of M-sections and LDS reads are retired inside the following
-// M-section (not before the barrier), so a slot is re-staged >= 2 barriers after its last read even
-// across the staggered wave groups.  The wait for K-tile u+1 (end of phase 3's M-section of u)
-// leaves K-tile u+2's first three halves in flight: vmcnt(6) (BN 256) / vmcnt(4) (BN 128).
-template <int BN, bool AK, bool BKC, int EPI, bool STAG>
-__global__ __launch_bounds__(512) void gemm_pipe_kernel(GemmArgs a) {
-  constexpr int BM = 256, NT = 512;
-  constexpr int TM = 128, TN = BN / 4;            // wave tile (2 x 4 waves)
-  constexpr int FM = TM / 16, FN = TN / 16;       // 8 x (4 or 2) accumulators
-  constexpr int QM = FM / 2, QN = FN / 2;         // fragments per quadrant
-  constexpr int HB = BN / 2;                      // columns per B half image
-  constexpr int A_HALF = 128 * BK * 2, B_HALF = HB * BK * 2;
-  constexpr int NSLOT = 5;
-  constexpr int B_RING = NSLOT * A_HALF;          // byte offset of the B ring
-  constexpr int B_INSTR = B_HALF / 1024 / 8;      // DMA instructions per wave per B half (2 or 1)
-  constexpr int AHEAD = 2 * 2 + 2 * B_INSTR;      // a K-tile's DMA instructions per wave
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
-  lds_u8* smem = (lds_u8*)smem_raw;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-  int tile_m, tile_n;
-  tile_coords(a, tile_m, tile_n);
-  const int m0 = tile_m * BM, n0 = tile_n * BN;
-
-  auto a_slot = [&](int u, int h) { return smem + ((2 * u + h) % NSLOT) * A_HALF; };
-  auto b_slot = [&](int u, int h) { return smem + B_RING + ((2 * u + h) % NSLOT) * B_HALF; };
-  auto stage_a = [&](int u, int h) {
-    const int k0 = u * BK, r0 = m0 + 128 * h;
-    const uint16_t* g = AK ? a.A + (int64_t)r0 * a.lda + k0 : a.A + (int64_t)k0 * a.lda + r0;
-    stage_tile<128, AK, NT>(g, a.lda, a_slot(u, h), tid);
-  };
-  auto stage_b = [&](int u, int h) {
-    int64_t ldb;
-    const uint16_t* g = b_image_ptr(a, BKC, n0, u * BK, HB * h, ldb);
-    stage_tile<HB, BKC, NT>(g, ldb, b_slot(u, h), tid);
-  };
-
-  f32x4_t acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-
-  const int nk = a.K / BK;
-  // prologue: K-tiles 0 and 1 issued, K-tile 0 waited for
-  stage_a(0, 0); stage_b(0, 0); stage_b(0, 1); stage_a(0, 1);
-  if (nk > 1) {
-    stage_a(1, 0); stage_b(1, 0); stage_b(1, 1); stage_a(1, 1);
-    if (B_INSTR == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-
-  const int brow = (wn & 1) * TN;  // the wave's first column inside its B half image
-  bf16x8_t af[QM][2], b0[QN][2], b1[QN][2];
-
-  // Every phase = R-section (LDS reads, left in flight across the barrier) + M-section (one half
-  // image DMA + the quadrant's 16 / 8 MFMAs), each closed by a raw s_barrier.
-  // STAG: waves 4-7 run one barrier behind waves 0-3, so on each SIMD one wave multiplies while
-  // the other reads (ping-pong).
-  auto bar = [] {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  auto mma = [&](int i0, int j0, const bf16x8_t (&A)[QM][2], const bf16x8_t (&Bf)[QN][2]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < QM; ++i)
-#pragma unroll
-        for (int j = 0; j < QN; ++j)
-          acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i][s], Bf[j][s], acc[i0 + i][j0 + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  const bool late = STAG && __builtin_amdgcn_readfirstlane(wm) == 1;
-  if (late) bar();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const lds_u8* sa = a_slot(kt, wm);
-    const lds_u8* sb = b_slot(kt, wn >> 1);
-    const bool pre = kt + 2 < nk;
-
-    // ---- phase 1: R: A rows 0..63, B cols 0..TN/2 | M: DMA A0 of kt+2, quadrant (0, 0)
-#pragma unroll
-    for (int i = 0; i < QM; ++i)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) af[i][s] = read_frag<128, AK>(sa, i * 16, s, lane);
-#pragma unroll
-    for (int j = 0; j < QN; ++j)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) b0[j][s] = read_frag<HB, BKC>(sb, brow + j * 16, s, lane);
-    bar();
-    if (pre) stage_a(kt + 2, 0);
-    mma(0, 0, af, b0);
-    bar();
-
-    // ---- phase 2: R: B cols TN/2..TN (last B reads) | M: DMA B0 of kt+2, quadrant (0, 1)
-#pragma unroll
-    for (int j = 0; j < QN; ++j)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) b1[j][s] = read_frag<HB, BKC>(sb, brow + (QN + j) * 16, s, lane);
-    bar();
-    if (pre) stage_b(kt + 2, 0);
-    mma(0, QN, af, b1);
-    bar();
-
-    // ---- phase 3: R: A rows 64..127 (last A reads) | M: DMA B1 of kt+2 (into B0 of kt),
-    //      quadrant (1, 1), then wait for K-tile kt+1 (all but kt+2's three halves in flight)
-#pragma unroll
-    for (int i = 0; i < QM; ++i)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) af[i][s] = read_frag<128, AK>(sa, (QM + i) * 16, s, lane);
-    bar();
-    if (pre) stage_b(kt + 2, 1);
-    mma(QM, QN, af, b1);
-    if (pre) {
-      if (B_INSTR == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    bar();
-
-    // ---- phase 4: R: nothing | M: DMA A1 of kt+2 (into A0 of kt), quadrant (1, 0)
-    bar();
-    if (pre) stage_a(kt + 2, 1);
-    mma(QM, 0, af, b0);
-    bar();
-  }
-  if (STAG && !late) bar();  // balance the barrier count of the two wave groups
-  (void)AHEAD;
-
-  epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane);
-}
-
 // ============================================================================ 8-phase 256x256
 // 256x256 tile, BK = 64, 8 waves as 2(M) x 4(N), each wave a 128 x 64 output (8 x 4 accumulators
 // of 16x16).  Each operand tile is held as two "half images" of 128 rows (A) / columns (B) x 64 k,
@@ -426,7 +289,7 @@ __device__ __forceinline__ void glds16_asm(const uint16_t* base, uint32_t voff_e
 }
 
 template <bool AK, bool BKC, int EPI>
-__global__ __launch_bounds__(512) void gemm_8ph_kernel(GemmArgs a) {
+__global__ __launch_bounds__(512) void gemm_8ph_kernel(const GemmGroup g) {
   constexpr int NT = 512, TM = 128, TN = 64, FM = 8, FN = 4;
   constexpr int HALF = 128 * BK * 2;          // 16 KiB
   constexpr int BUF = 4 * HALF;               // At, Bl, Br, Ab
@@ -436,7 +299,7 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(GemmArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   int tile_m, tile_n;
-  tile_coords(a, tile_m, tile_n);
+  const GemmArgs& a = select_problem(g, tile_m, tile_n);
   const int m0 = tile_m * 256, n0 = tile_n * 256;
 
   // B segment for this tile (N-segments) or the first K-segment; ld is per tile (host checks
@@ -588,7 +451,7 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(GemmArgs a) {
 // (At in phase 1, B and Ab in phase 2), and the one wait per K-tile (phase 2, vmcnt(6)) retires
 // K-tile t+1 with t+2 in flight -- every DMA has >= 1.5 K-tiles to land.
 template <bool AK, bool BKC, int EPI>
-__global__ __launch_bounds__(512) void gemm_4ph_kernel(GemmArgs a) {
+__global__ __launch_bounds__(512) void gemm_4ph_kernel(const GemmGroup g) {
   constexpr int TM = 64, TN = 64, FM = 4, FN = 4;
   constexpr int IMG = 128 * BK * 2;           // 16 KiB
   constexpr int BUF = 3 * IMG;                // At, B, Ab
@@ -598,7 +461,7 @@ __global__ __launch_bounds__(512) void gemm_4ph_kernel(GemmArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   int tile_m, tile_n;
-  tile_coords(a, tile_m, tile_n);
+  const GemmArgs& a = select_problem(g, tile_m, tile_n);
   const int m0 = tile_m * 256, n0 = tile_n * 128;
 
   int64_t ldb;
@@ -720,7 +583,7 @@ __global__ __launch_bounds__(512) void gemm_4ph_kernel(GemmArgs a) {
 
 // ================================================================================= simple
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, int SCHED>
-__global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(GemmArgs a) {
+__global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const GemmGroup g) {
   constexpr int NT = WM * WN * 64;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
@@ -732,7 +595,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(GemmArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   int tile_m, tile_n;
-  tile_coords(a, tile_m, tile_n);
+  const GemmArgs& a = select_problem(g, tile_m, tile_n);
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const uint16_t* Abase = AK ? a.A + (int64_t)m0 * a.lda : a.A + m0;
 
@@ -810,149 +673,28 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(GemmArgs a) {
   epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane);
 }
 
-// ============================================================================ 4-wave 256x256
-// One workgroup of 4 waves (2 x 2) per CU, each wave owning a 128 x 128 output tile: 256 fp32
-// accumulators per lane held across the unified 512-entry register file (one wave per SIMD,
-// amdgpu_waves_per_eu(1, 1)).  Per K-tile a wave reads its A and B panels once (32 KiB; 128 KiB
-// per CU instead of the 192 KiB an 8-wave 128 x 64 decomposition reads) for 128 MFMAs.
-// Latency is hidden inside the wave: the K-tile is two MFMA blocks of 64 (k-substeps 0 and 1)
-// and each block carries the LDS reads of the NEXT block's fragments (second register set):
-//   block A(kt): MFMA(kt, s0)  ||  ds_read(kt, s1)
-//   s_waitcnt vmcnt(0); s_barrier    <- K-tile kt+1 landed; every wave done reading K-tile kt
-//   block B(kt): MFMA(kt, s1)  ||  ds_read(kt+1, s0), DMA(kt+2 -> the buffer kt just freed)
-// so there is one barrier per K-tile and no read or DMA sits on the critical path.
-template <bool AK, bool BKC, int EPI, int ABL = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
-void gemm_w4_kernel(GemmArgs a) {
-  constexpr int BM = 256, BN = 256, NT = 256;
-  constexpr int TM = 128, TN = 128, FM = 8, FN = 8;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  constexpr int STAGE = A_BYTES + B_BYTES;
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
-  lds_u8* smem = (lds_u8*)smem_raw;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  int tile_m, tile_n;
-  tile_coords(a, tile_m, tile_n);
-  const int m0 = tile_m * BM, n0 = tile_n * BN;
-  const uint16_t* Abase = AK ? a.A + (int64_t)m0 * a.lda : a.A + m0;
-
-  auto stage = [&](int kt, int buf) {
-    const int k0 = kt * BK;
-    lds_u8* sa = smem + buf * STAGE;
-    const uint16_t* ga = AK ? Abase + k0 : Abase + (int64_t)k0 * a.lda;
-    stage_tile<BM, AK, NT>(ga, a.lda, sa, tid);
-    int64_t ldb;
-    const uint16_t* gb = b_image_ptr(a, BKC, n0, k0, 0, ldb);
-    stage_tile<BN, BKC, NT>(gb, ldb, sa + A_BYTES, tid);
-  };
-
-  f32x4_t acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-
-  bf16x8_t a0[FM], b0[FN], a1[FM], b1[FN];
-  auto read_set = [&](int buf, int s, bf16x8_t (&A)[FM], bf16x8_t (&Bf)[FN]) {
-    const lds_u8* sa = smem + buf * STAGE;
-    const lds_u8* sb = sa + A_BYTES;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) A[i] = read_frag<BM, AK>(sa, wm * TM + i * 16, s, lane);
-#pragma unroll
-    for (int j = 0; j < FN; ++j) Bf[j] = read_frag<BN, BKC>(sb, wn * TN + j * 16, s, lane);
-  };
-  auto mma = [&](const bf16x8_t (&A)[FM], const bf16x8_t (&Bf)[FN]) {
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], Bf[j], acc[i][j], 0, 0, 0);
-  };
-
-  const int nk = a.K / BK;
-  stage(0, 0);
-  if (nk > 1) stage(1, 1);
-  if (nk > 1) {
-    // K-tile 0's DMA instructions are the older half: wait for them only
-    constexpr int PER_TILE = (A_BYTES + B_BYTES) / 1024 / (NT / 64);
-    static_assert(PER_TILE == 16, "DMA instructions per wave per K-tile");
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-  read_set(0, 0, a0, b0);
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    // block A: MFMA(kt, s0) with the reads of (kt, s1)
-    read_set(buf, 1, a1, b1);
-    mma(a0, b0);
-    // K-tile kt+1 landed (its DMA is the only one outstanding); all reads of buffer `buf` retired
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    // block B: MFMA(kt, s1) with the reads of (kt+1, s0) and the DMA of kt+2 into `buf`
-    if (kt + 1 < nk) read_set(buf ^ 1, 0, a0, b0);
-    if (ABL == 0 && kt + 2 < nk) stage(kt + 2, buf);   // ABL = 1: timing ablation without the DMA
-    mma(a1, b1);
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane);
-}
-
-template <bool AK, bool BKC, int EPI, int ABL = 0>
-int launch_w4(const GemmArgs& a0, hipStream_t stream) {
-  GemmArgs a = a0;
-  a.tiles_m = a.M / 256;
-  a.tiles_n = a.N / 256;
-  constexpr int smem_main = 2 * (256 + 256) * BK * 2;
-  constexpr int smem_epi = 4 * 128 * (128 * 2 + 16);
-  constexpr int smem = smem_main > smem_epi ? smem_main : smem_epi;
-  static_assert(smem <= 160 * 1024, "LDS budget");
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_w4_kernel<AK, BKC, EPI, ABL>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr_set = true;
-  }
-  gemm_w4_kernel<AK, BKC, EPI, ABL><<<a.tiles_m * a.tiles_n, 256, smem, stream>>>(a);
-  PT_CHECK_LAUNCH();
-  return PT_OK;
-}
-
 // ================================================================================== launch
 template <typename Kern>
 void set_smem_once(Kern k, int smem) {
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
 }
 
-template <int BN, bool AK, bool BKC, int EPI, bool STAG>
-int launch_pipe(const GemmArgs& a0, hipStream_t stream) {
-  GemmArgs a = a0;
-  a.tiles_m = a.M / 256;
-  a.tiles_n = a.N / BN;
-  constexpr int smem_main = 5 * (128 * BK * 2 + (BN / 2) * BK * 2);
-  constexpr int smem_epi = 8 * 128 * ((BN / 4) * 2 + 16);
-  constexpr int smem = smem_main > smem_epi ? smem_main : smem_epi;
-  static_assert(smem <= 160 * 1024, "LDS budget");
-  static bool attr_set = false;
-  if (!attr_set) {
-    set_smem_once(gemm_pipe_kernel<BN, AK, BKC, EPI, STAG>, smem);
-    attr_set = true;
+// per-problem tile grid + consecutive tile ids; returns the total tile count
+inline int group_tiles(GemmGroup& g, int bm, int bn) {
+  int n = 0;
+  for (int i = 0; i < g.nprob; ++i) {
+    g.p[i].tiles_m = g.p[i].M / bm;
+    g.p[i].tiles_n = g.p[i].N / bn;
+    g.start[i] = n;
+    n += g.p[i].tiles_m * g.p[i].tiles_n;
   }
-  gemm_pipe_kernel<BN, AK, BKC, EPI, STAG><<<a.tiles_m * a.tiles_n, 512, smem, stream>>>(a);
-  PT_CHECK_LAUNCH();
-  return PT_OK;
+  for (int i = g.nprob; i <= kMaxProb; ++i) g.start[i] = n;
+  return n;
 }
 
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, int SCHED = 0>
-int launch_t(const GemmArgs& a0, hipStream_t stream) {
-  GemmArgs a = a0;
-  a.tiles_m = a.M / BM;
-  a.tiles_n = a.N / BN;
+int launch_t(GemmGroup g, hipStream_t stream) {
+  const int tiles = group_tiles(g, BM, BN);
   constexpr int smem_main = 2 * (BM + BN) * BK * 2;
   constexpr int smem_epi = WM * WN * (BM / WM) * ((BN / WN) * 2 + 16);
   constexpr int smem = smem_main > smem_epi ? smem_main : smem_epi;
@@ -962,25 +704,14 @@ int launch_t(const GemmArgs& a0, hipStream_t stream) {
     set_smem_once(gemm_kernel<BM, BN, WM, WN, AK, BKC, EPI, SCHED>, smem);
     attr_set = true;
   }
-  gemm_kernel<BM, BN, WM, WN, AK, BKC, EPI, SCHED><<<a.tiles_m * a.tiles_n, WM * WN * 64, smem, stream>>>(a);
+  gemm_kernel<BM, BN, WM, WN, AK, BKC, EPI, SCHED><<<tiles, WM * WN * 64, smem, stream>>>(g);
   PT_CHECK_LAUNCH();
   return PT_OK;
 }
 
-// tile ids: 0 = pipelined 256x256, 1 = pipelined 256x128 (ping-pong wave groups), 2 = simple
-//           128x128, 3 = simple 64x64, 4 = simple 256x256, 5 = simple 256x128, 6 / 7 = pipelined
-//           256x256 / 256x128 without the ping-pong stagger (kept for A/B measurement)
-//           12 = 8-phase 256x256 (two half-image wave groups, one wait per K-tile)
-//           13 = 4-phase 256x128 (three K-tiles resident)
-constexpr int kNumTiles = 14;
-const int kTileBM[kNumTiles] = {256, 256, 128, 64, 256, 256, 256, 256, 256, 128, 256, 256, 256, 256};
-const int kTileBN[kNumTiles] = {256, 128, 128, 64, 256, 128, 256, 128, 256, 128, 256, 256, 256, 128};
-
 template <bool AK, bool BKC, int EPI>
-int launch_8ph(const GemmArgs& a0, hipStream_t stream) {
-  GemmArgs a = a0;
-  a.tiles_m = a.M / 256;
-  a.tiles_n = a.N / 256;
+int launch_8ph(GemmGroup g, hipStream_t stream) {
+  const int tiles = group_tiles(g, 256, 256);
   constexpr int smem_main = 8 * 128 * BK * 2;
   constexpr int smem_epi = 8 * 128 * (64 * 2 + 16);
   constexpr int smem = smem_main > smem_epi ? smem_main : smem_epi;
@@ -990,16 +721,14 @@ int launch_8ph(const GemmArgs& a0, hipStream_t stream) {
     set_smem_once(gemm_8ph_kernel<AK, BKC, EPI>, smem);
     attr_set = true;
   }
-  gemm_8ph_kernel<AK, BKC, EPI><<<a.tiles_m * a.tiles_n, 512, smem, stream>>>(a);
+  gemm_8ph_kernel<AK, BKC, EPI><<<tiles, 512, smem, stream>>>(g);
   PT_CHECK_LAUNCH();
   return PT_OK;
 }
 
 template <bool AK, bool BKC, int EPI>
-int launch_4ph(const GemmArgs& a0, hipStream_t stream) {
-  GemmArgs a = a0;
-  a.tiles_m = a.M / 256;
-  a.tiles_n = a.N / 128;
+int launch_4ph(GemmGroup g, hipStream_t stream) {
+  const int tiles = group_tiles(g, 256, 128);
   constexpr int smem_main = 9 * 128 * BK * 2;
   constexpr int smem_epi = 8 * 64 * (64 * 2 + 16);
   constexpr int smem = smem_main > smem_epi ? smem_main : smem_epi;
@@ -1009,22 +738,25 @@ int launch_4ph(const GemmArgs& a0, hipStream_t stream) {
     set_smem_once(gemm_4ph_kernel<AK, BKC, EPI>, smem);
     attr_set = true;
   }
-  gemm_4ph_kernel<AK, BKC, EPI><<<a.tiles_m * a.tiles_n, 512, smem, stream>>>(a);
+  gemm_4ph_kernel<AK, BKC, EPI><<<tiles, 512, smem, stream>>>(g);
   PT_CHECK_LAUNCH();
   return PT_OK;
 }
 
+// tile ids: 2 = simple 128x128, 3 = simple 64x64, 4 = simple 256x256, 5 = simple 256x128,
+//           8 / 9 = simple 256x256 / 128x128 with both k-substeps' fragments in flight,
+//           12 = 8-phase 256x256 (two half-image wave groups, one wait per K-tile)
+//           13 = 4-phase 256x128 (three K-tiles resident)
+//           (ids 0, 1, 6, 7, 10, 11 were pipelining experiments, measured slower and retired)
+constexpr int kNumTiles = 14;
+const int kTileBM[kNumTiles] = {0, 0, 128, 64, 256, 256, 0, 0, 256, 128, 0, 0, 256, 256};
+const int kTileBN[kNumTiles] = {0, 0, 128, 64, 256, 128, 0, 0, 256, 128, 0, 0, 256, 128};
+
 template <bool AK, bool BKC, int EPI>
-int launch_layout(const GemmArgs& a, int tile, hipStream_t s) {
+int launch_layout(const GemmGroup& a, int tile, hipStream_t s) {
   switch (tile) {
-    case 0: return launch_pipe<256, AK, BKC, EPI, true>(a, s);
-    case 1: return launch_pipe<128, AK, BKC, EPI, true>(a, s);
-    case 6: return launch_pipe<256, AK, BKC, EPI, false>(a, s);
-    case 7: return launch_pipe<128, AK, BKC, EPI, false>(a, s);
     case 8: return launch_t<256, 256, 2, 4, AK, BKC, EPI, 1>(a, s);
     case 9: return launch_t<128, 128, 2, 2, AK, BKC, EPI, 1>(a, s);
-    case 10: return launch_w4<AK, BKC, EPI>(a, s);
-    case 11: return launch_w4<AK, BKC, EPI, 1>(a, s);
     case 12: return launch_8ph<AK, BKC, EPI>(a, s);
     case 13: return launch_4ph<AK, BKC, EPI>(a, s);
     case 2: return launch_t<128, 128, 2, 2, AK, BKC, EPI>(a, s);
@@ -1036,7 +768,7 @@ int launch_layout(const GemmArgs& a, int tile, hipStream_t s) {
 }
 
 template <int EPI>
-int launch_epi(const GemmArgs& a, int a_kcontig, int b_kcontig, int tile, hipStream_t s) {
+int launch_epi(const GemmGroup& a, int a_kcontig, int b_kcontig, int tile, hipStream_t s) {
   if (a_kcontig && b_kcontig) return launch_layout<true, true, EPI>(a, tile, s);
   if (a_kcontig && !b_kcontig) return launch_layout<true, false, EPI>(a, tile, s);
   if (!a_kcontig && !b_kcontig) return launch_layout<false, false, EPI>(a, tile, s);
@@ -1045,58 +777,18 @@ int launch_epi(const GemmArgs& a, int a_kcontig, int b_kcontig, int tile, hipStr
 
 }  // namespace
 
-extern "C" {
+namespace {
 
-// Tile choice, from the measured sweep over the decoder layer's shapes (tools/gemm_bench.py,
-// profiles/r01_gemm_tiles_8ph.md): the phased kernels whenever the shape divides -- 256x256 (tile
-// 12) or 256x128 (tile 13), whichever fills the 256 CUs' last round better (ties -> 256x256: fewer
-// operand bytes per MFMA); 1.0-1.38 PF/s on every projection of the layer.  Else the 128x128
-// two-stage kernel, else 64x64.
-static bool tile_fits(int t, int64_t M, int64_t N, const int64_t* mseg, int nmseg, const int64_t* nseg, int nnseg) {
-  const int bm = kTileBM[t], bn = kTileBN[t];
-  if (M % bm || N % bn) return false;
-  for (int i = 0; i < nmseg; ++i)
-    if (mseg[i] % bm) return false;
-  for (int i = 0; i < nnseg; ++i)
-    if (nseg[i] % bn) return false;
-  return true;
-}
-
-static int pick_tile(int64_t M, int64_t N, const int64_t* mseg, int nmseg, const int64_t* nseg, int nnseg,
-                     int b_kcontig) {
-  (void)b_kcontig;
-  auto fill = [&](int t) {  // fraction of the CU-rounds this tile grid keeps busy
-    const int64_t tiles = (M / kTileBM[t]) * (N / kTileBN[t]);
-    const int64_t rounds = (tiles + 255) / 256;
-    return (double)tiles / (double)(rounds * 256);
-  };
-  const bool f12 = tile_fits(12, M, N, mseg, nmseg, nseg, nnseg);
-  const bool f13 = tile_fits(13, M, N, mseg, nmseg, nseg, nnseg);
-  if (f12 && (!f13 || fill(12) >= fill(13))) return 12;
-  if (f13) return 13;
-  if (tile_fits(2, M, N, mseg, nmseg, nseg, nnseg)) return 2;
-  if (tile_fits(3, M, N, mseg, nmseg, nseg, nnseg)) return 3;
-  return -1;
-}
-
-int pt_gemm_pick_tile(int64_t M, int64_t N, const int64_t* mseg, int nmseg, const int64_t* nseg, int nnseg) {
-  return pick_tile(M, N, mseg, nmseg, nseg, nnseg, 1);
-}
-
-// C = A . B  (see header comment).  a_kcontig: A is [M,K] (ld=lda) else stored [K,M];
-// b_kcontig: B is stored [N,K] (weights) else [K,N].  b_seg_dim: 0 = segments along N, 1 = along K.
-// b_bounds / c_bounds: n+1 boundaries (first 0, last = N/K or M).  epilogue: 0 bf16 store,
-// 1 bf16 accumulate (C = bf16(C + bf16(acc))), 2 fp32 store, 3 fp32 accumulate,
-// 4 bf16 residual (C = bf16(R + bf16(acc))).  tile: -1 = auto.
-int pt_gemm(const void* A, int64_t lda, int a_kcontig, const void* const* B, const int64_t* ldb,
-            const int64_t* b_bounds, int nb, int b_kcontig, int b_seg_dim, void* const* C, const int64_t* ldc,
-            const int64_t* c_bounds, int nc, int64_t M, int64_t N, int64_t K, int epilogue,
-            const void* residual, int64_t ldr, int tile, hipStream_t stream) {
+// Validate one problem and fill its kernel arguments.  Returns PT_OK or a PT_E* code.
+int fill_args(GemmArgs& a, const void* A, int64_t lda, const void* const* B, const int64_t* ldb,
+              const int64_t* b_bounds, int nb, int b_seg_dim, void* const* C, const int64_t* ldc,
+              const int64_t* c_bounds, int nc, int64_t M, int64_t N, int64_t K, int epilogue, const void* residual,
+              int64_t ldr) {
   if (!A || !B || !C || nb < 1 || nb > 4 || nc < 1 || nc > 4 || M <= 0 || N <= 0 || K <= 0) return PT_EINVAL;
   if (epilogue == EPI_BF16_RES && (!residual || nc != 1 || !pt_aligned16(residual) || (ldr & 7))) return PT_EINVAL;
   if (K % BK) return PT_EUNSUPPORTED;
   if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX) return PT_EUNSUPPORTED;
-  GemmArgs a{};
+  a = GemmArgs{};
   a.A = (const uint16_t*)A;
   a.lda = lda;
   a.nbseg = nb;
@@ -1124,40 +816,119 @@ int pt_gemm(const void* A, int64_t lda, int a_kcontig, const void* const* B, con
   a.K = (int)K;
   a.R = (const uint16_t*)residual;
   a.ldr = ldr;
-  // K-segment boundaries must be multiples of BK
-  if (b_seg_dim == 1)
+  if (b_seg_dim == 1)  // K-segment boundaries must be multiples of BK
     for (int i = 0; i <= nb; ++i)
       if (a.bseg[i] % BK) return PT_EUNSUPPORTED;
-  if (tile < 0) {
-    int64_t nsegs[5], msegs[5];
-    for (int i = 0; i <= nb; ++i) nsegs[i] = b_seg_dim == 0 ? a.bseg[i] : 0;
-    for (int i = 0; i <= nc; ++i) msegs[i] = a.cseg[i];
-    tile = pick_tile(M, N, msegs, nc + 1, nsegs, nb + 1, b_kcontig);
-    if ((tile == 12 || tile == 13) && b_seg_dim == 1)
-      for (int i = 1; i < nb; ++i)
-        if (a.ldb[i] != a.ldb[0]) tile = tile_fits(2, M, N, msegs, nc + 1, nsegs, nb + 1) ? 2 : 3;
-  }
-  if (tile < 0 || tile >= kNumTiles) return PT_EUNSUPPORTED;
+  return PT_OK;
+}
+
+bool args_fit(const GemmArgs& a, int tile) {
+  if (tile < 0 || tile >= kNumTiles || kTileBM[tile] == 0) return false;
   const int bm = kTileBM[tile], bn = kTileBN[tile];
-  if (M % bm || N % bn) return PT_EUNSUPPORTED;
-  for (int i = 0; i <= nc; ++i)
-    if (a.cseg[i] % bm) return PT_EUNSUPPORTED;
-  if (b_seg_dim == 0)
-    for (int i = 0; i <= nb; ++i)
-      if (a.bseg[i] % bn) return PT_EUNSUPPORTED;
-  if ((tile == 12 || tile == 13) && b_seg_dim == 1)  // one B leading dimension per tile
-    for (int i = 1; i < nb; ++i)
-      if (a.ldb[i] != a.ldb[0]) return PT_EUNSUPPORTED;
+  if (a.M % bm || a.N % bn) return false;
+  for (int i = 0; i <= a.ncseg; ++i)
+    if (a.cseg[i] % bm) return false;
+  if (a.bdim == 0)
+    for (int i = 0; i <= a.nbseg; ++i)
+      if (a.bseg[i] % bn) return false;
+  if ((tile == 12 || tile == 13) && a.bdim == 1)  // the phased kernels keep one B ld per tile
+    for (int i = 1; i < a.nbseg; ++i)
+      if (a.ldb[i] != a.ldb[0]) return false;
+  return true;
+}
+
+// auto tile for a group: the phased kernels when every problem divides -- 256x256 or 256x128,
+// whichever fills the CUs' last round better over the whole group (ties -> 256x256) -- else the
+// 128x128 two-stage kernel, else 64x64
+int pick_group_tile(const GemmGroup& g) {
+  auto fits = [&](int t) {
+    for (int i = 0; i < g.nprob; ++i)
+      if (!args_fit(g.p[i], t)) return false;
+    return true;
+  };
+  auto fill = [&](int t) {
+    int64_t tiles = 0;
+    for (int i = 0; i < g.nprob; ++i) tiles += (int64_t)(g.p[i].M / kTileBM[t]) * (g.p[i].N / kTileBN[t]);
+    const int64_t rounds = (tiles + 255) / 256;
+    return (double)tiles / (double)(rounds * 256);
+  };
+  const bool f12 = fits(12), f13 = fits(13);
+  if (f12 && (!f13 || fill(12) >= fill(13))) return 12;
+  if (f13) return 13;
+  if (fits(2)) return 2;
+  if (fits(3)) return 3;
+  return -1;
+}
+
+int launch_group(GemmGroup& g, int a_kcontig, int b_kcontig, int epilogue, int tile, hipStream_t stream) {
+  if (tile < 0) tile = pick_group_tile(g);
+  for (int i = 0; i < g.nprob; ++i)
+    if (!args_fit(g.p[i], tile)) return PT_EUNSUPPORTED;
   switch (epilogue) {
-    case EPI_BF16: return launch_epi<EPI_BF16>(a, a_kcontig, b_kcontig, tile, stream);
-    case EPI_BF16_ACC: return launch_epi<EPI_BF16_ACC>(a, a_kcontig, b_kcontig, tile, stream);
-    case EPI_F32: return launch_epi<EPI_F32>(a, a_kcontig, b_kcontig, tile, stream);
-    case EPI_F32_ACC: return launch_epi<EPI_F32_ACC>(a, a_kcontig, b_kcontig, tile, stream);
+    case EPI_BF16: return launch_epi<EPI_BF16>(g, a_kcontig, b_kcontig, tile, stream);
+    case EPI_BF16_ACC: return launch_epi<EPI_BF16_ACC>(g, a_kcontig, b_kcontig, tile, stream);
+    case EPI_F32: return launch_epi<EPI_F32>(g, a_kcontig, b_kcontig, tile, stream);
+    case EPI_F32_ACC: return launch_epi<EPI_F32_ACC>(g, a_kcontig, b_kcontig, tile, stream);
     case EPI_BF16_RES:  // forward projections only (weights K-contiguous)
       if (!a_kcontig || !b_kcontig) return PT_EUNSUPPORTED;
-      return launch_layout<true, true, EPI_BF16_RES>(a, tile, stream);
+      return launch_layout<true, true, EPI_BF16_RES>(g, tile, stream);
     default: return PT_EINVAL;
   }
+}
+
+}  // namespace
+
+extern "C" {
+
+// C = A . B  (see header comment).  a_kcontig: A is [M,K] (ld=lda) else stored [K,M];
+// b_kcontig: B is stored [N,K] (weights) else [K,N].  b_seg_dim: 0 = segments along N, 1 = along K.
+// b_bounds / c_bounds: n+1 boundaries (first 0, last = N/K or M).  epilogue: 0 bf16 store,
+// 1 bf16 accumulate (C = bf16(C + bf16(acc))), 2 fp32 store, 3 fp32 accumulate,
+// 4 bf16 residual (C = bf16(R + bf16(acc))).  tile: -1 = auto.
+int pt_gemm(const void* A, int64_t lda, int a_kcontig, const void* const* B, const int64_t* ldb,
+            const int64_t* b_bounds, int nb, int b_kcontig, int b_seg_dim, void* const* C, const int64_t* ldc,
+            const int64_t* c_bounds, int nc, int64_t M, int64_t N, int64_t K, int epilogue,
+            const void* residual, int64_t ldr, int tile, hipStream_t stream) {
+  GemmGroup g{};
+  g.nprob = 1;
+  const int rc = fill_args(g.p[0], A, lda, B, ldb, b_bounds, nb, b_seg_dim, C, ldc, c_bounds, nc, M, N, K, epilogue,
+                           residual, ldr);
+  if (rc) return rc;
+  return launch_group(g, a_kcontig, b_kcontig, epilogue, tile, stream);
+}
+
+// Several independent problems in one launch (same layouts / epilogue; see include/picotron_hip.h).
+int pt_gemm_grouped(const pt_gemm_problem* probs, int nprob, int a_kcontig, int b_kcontig, int epilogue, int tile,
+                    hipStream_t stream) {
+  if (!probs || nprob < 1 || nprob > kMaxProb) return PT_EINVAL;
+  GemmGroup g{};
+  g.nprob = nprob;
+  for (int i = 0; i < nprob; ++i) {
+    const pt_gemm_problem& q = probs[i];
+    const int rc = fill_args(g.p[i], q.A, q.lda, q.B, q.ldb, q.b_bounds, q.nb, q.b_seg_dim, q.C, q.ldc, q.c_bounds,
+                             q.nc, q.M, q.N, q.K, epilogue, q.residual, q.ldr);
+    if (rc) return rc;
+  }
+  return launch_group(g, a_kcontig, b_kcontig, epilogue, tile, stream);
+}
+
+// Tile the auto-pick chooses for one [M, N] problem with the given segment boundaries (see
+// pick_group_tile: the phased 256x256 / 256x128 kernels by last-round fill, then 128x128, 64x64).
+int pt_gemm_pick_tile(int64_t M, int64_t N, const int64_t* mseg, int nmseg, const int64_t* nseg, int nnseg) {
+  GemmGroup g{};
+  g.nprob = 1;
+  GemmArgs& a = g.p[0];
+  a.M = (int)M;
+  a.N = (int)N;
+  a.ncseg = nmseg > 1 ? nmseg - 1 : 1;
+  a.cseg[0] = 0;
+  a.cseg[a.ncseg] = M;
+  for (int i = 0; i < nmseg && i < 5; ++i) a.cseg[i] = mseg[i];
+  a.nbseg = nnseg > 1 ? nnseg - 1 : 1;
+  a.bseg[0] = 0;
+  a.bseg[a.nbseg] = N;
+  for (int i = 0; i < nnseg && i < 5; ++i) a.bseg[i] = nseg[i];
+  return pick_group_tile(g);
 }
 
 }  // extern "C"

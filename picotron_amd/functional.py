@@ -68,6 +68,22 @@ def wgrad(dy2d, x2d, params):
         _grad_ready(p)
 
 
+def wgrad_group(jobs):
+    """Several wgrads [(dy2d, x2d, params), ...] in one grouped launch when every sink takes the
+    same epilogue (else one wgrad() per job)."""
+    targets = [[_wgrad_target(p) for p in params] for _, _, params in jobs]
+    epis = {e for tg in targets for _, e in tg}
+    if len(epis) != 1:
+        for dy2d, x2d, params in jobs:
+            wgrad(dy2d, x2d, params)
+        return
+    K.linear_wgrad_grouped([(dy2d, x2d, [t for t, _ in tg]) for (dy2d, x2d, _), tg in zip(jobs, targets)],
+                           epilogue=epis.pop())
+    for _, _, params in jobs:
+        for p in params:
+            _grad_ready(p)
+
+
 def norm_bwd(dy2, z, weight, rstd, mode, dres=None, need_dw=True):
     """RMSNorm backward with the weight gradient summed straight into p's sink (bf16 .grad store or
     accumulate -- autograd's AccumulateGrad -- or the f32 main_grad of DataParallelBucket)."""
@@ -254,13 +270,15 @@ def attn_block_bwd(da, h2, saved, wq, wk, wv, wo, cos, sin, sh, tp, need_dx=True
     qkv, o, lse = saved
     scale = 1.0 / math.sqrt(sh.d)
     do2 = K.linear_dgrad(da, [wo])
-    wgrad(da, o.view(sh.T, sh.wq), [wo])
     dqkv = attention_core_bwd(do2.view(sh.B, sh.S, sh.nh, sh.d), qkv, o, lse, sh, cos, sin, scale)
     dh = handle = None
     if need_dx:
         dh = K.linear_dgrad(dqkv, [wq, wk, wv])
         handle = tp.all_reduce(dh, async_op=True)
-    wgrad(dqkv, h2, [wq, wk, wv])
+    # dW of q|k|v and of o_proj in one launch: 192 + 64 tiles of 256x256 at SmolLM-1.7B dims,
+    # where either alone leaves CUs idle (o_proj's wgrad was deferred from above; its inputs
+    # da and o stay alive until here anyway)
+    wgrad_group([(dqkv, h2, [wq, wk, wv]), (da, o.view(sh.T, sh.wq), [wo])])
     if handle is not None:
         handle.wait()
     return dh

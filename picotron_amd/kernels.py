@@ -240,6 +240,49 @@ def _bounds(sizes):
     return out
 
 
+def _problem(A, lda, Bs, ldbs, b_bounds, b_seg_dim, Cs, ldcs, c_bounds, M, N, K):
+    pr = _C.GemmProblem()
+    pr.A, pr.lda = _ptr(A), int(lda)
+    for i, (b, ld) in enumerate(zip(Bs, ldbs)):
+        pr.B[i], pr.ldb[i] = _ptr(b), int(ld)
+    for i, v in enumerate(b_bounds):
+        pr.b_bounds[i] = int(v)
+    pr.nb, pr.b_seg_dim = len(Bs), int(b_seg_dim)
+    for i, (c, ld) in enumerate(zip(Cs, ldcs)):
+        pr.C[i], pr.ldc[i] = _ptr(c), int(ld)
+    for i, v in enumerate(c_bounds):
+        pr.c_bounds[i] = int(v)
+    pr.nc = len(Cs)
+    pr.M, pr.N, pr.K = int(M), int(N), int(K)
+    return pr
+
+
+def linear_wgrad_grouped(jobs, epilogue=EPI_BF16, tile=-1):
+    """Several wgrad GEMMs (dW_i = dY_i^T X for each job (dy2d, x2d, outs)) in ONE launch
+    (pt_gemm_grouped): e.g. dW of q|k|v (192 tiles) + dW of o_proj (64 tiles) fill 256 CUs."""
+    probs = (_C.GemmProblem * len(jobs))()
+    flops = 0.0
+    for j, (dy2d, x2d, outs) in enumerate(jobs):
+        _bf16_rowmajor(dy2d, "dy")
+        _bf16_rowmajor(x2d, "x")
+        T, N = dy2d.shape
+        Kin = x2d.shape[1]
+        ns = [o.shape[0] for o in outs]
+        _req(sum(ns) == N and x2d.shape[0] == T, "wgrad: output rows must cover dY's width")
+        probs[j] = _problem(dy2d, dy2d.stride(0), [x2d], [x2d.stride(0)], [0, Kin], 0, outs,
+                            [o.stride(0) for o in outs], _bounds(ns), N, Kin, T)
+        flops += 2.0 * N * Kin * T
+    probe = _PROBE
+    if probe is not None:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    rc = _C.lib().pt_gemm_grouped(probs, len(jobs), 0, 0, int(epilogue), int(tile), _C.stream_ptr())
+    _C.check(rc, f"pt_gemm_grouped({len(jobs)} problems, epi={epilogue})")
+    if probe is not None:
+        ev1.record()
+        probe.records.append((ev0, ev1, flops))
+
+
 def linear_fwd(x2d, weights, out=None, tile=-1, residual=None):
     """Y = x . [W_0; W_1; ...]^T  -> [T, sum N_i] (one launch; F.linear of model.py:124-126,186).
     residual [T, N]: Y = residual + x W^T (the residual add of model.py:208 in the epilogue)."""
