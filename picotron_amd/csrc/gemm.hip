@@ -43,7 +43,18 @@ constexpr int BK = 64;
 
 // EPI_BF16_RES: C = bf16(R + bf16(acc)) -- the residual add of model.py:207-208 fused into the
 // producing GEMM (R may alias C).
-enum Epilogue { EPI_BF16 = 0, EPI_BF16_ACC = 1, EPI_F32 = 2, EPI_F32_ACC = 3, EPI_BF16_RES = 4 };
+// EPI_SWIGLU_FWD: the gate|up projection with SwiGLU (model.py:186) in its epilogue: B = {W_gate,
+//   W_up} consumed in PAIRED tiles (output tile n = gate rows and up rows 128n..128n+127), writes
+//   C[0] = h = bf16(bf16(silu(g)) * u) [M, N] and C[1] = the [M, 2N] g|u buffer the backward reads.
+// EPI_SWIGLU_BWD: dh = dY . W_down with the SwiGLU backward in its epilogue: R = g|u [M, 2N];
+//   C[0] = dg|du [M, 2N] (dh itself is never written).
+enum Epilogue {
+  EPI_BF16 = 0, EPI_BF16_ACC = 1, EPI_F32 = 2, EPI_F32_ACC = 3, EPI_BF16_RES = 4,
+  EPI_SWIGLU_FWD = 5, EPI_SWIGLU_BWD = 6
+};
+
+// SwiGLU element math, the same expressions as csrc/swiglu.hip (torch's bf16 roundings)
+__device__ __forceinline__ float silu_sig(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
 struct GemmArgs {
   const uint16_t* A;
@@ -177,7 +188,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
   const int64_t ldc = a.ldc[cs];
   const int64_t mrow0 = m0 - a.cseg[cs] + wm * TM;
   const int ncol0 = n0 + wn * TN;
-  if (EPI == EPI_BF16 || EPI == EPI_BF16_ACC || EPI == EPI_BF16_RES) {
+  if (EPI == EPI_BF16 || EPI == EPI_BF16_ACC || EPI == EPI_BF16_RES || EPI == EPI_SWIGLU_BWD) {
     constexpr int ROWB = TN * 2 + 16;  // +16 B pad: spreads the column-wise 2-B writes over banks
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -200,6 +211,22 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
       bf16x8 v;
       v.w[0] = raw[0]; v.w[1] = raw[1]; v.w[2] = raw[2]; v.w[3] = raw[3];
       uint16_t* dst = C + (mrow0 + row) * ldc + ncol0 + ch * 8;
+      if (EPI == EPI_SWIGLU_BWD) {  // v = dh; g|u from R; dg|du to C (swiglu.hip's bwd)
+        const uint16_t* gp = a.R + (mrow0 + row) * a.ldr + ncol0 + ch * 8;
+        float d[8], gg[8], uu[8], og[8], ou[8];
+        unpack8(v, d);
+        unpack8(ld8(gp), gg);
+        unpack8(ld8(gp + a.N), uu);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float sg = silu_sig(gg[e]);
+          ou[e] = d[e] * round_bf(gg[e] * sg);
+          og[e] = round_bf(d[e] * uu[e]) * (sg * (1.0f + gg[e] * (1.0f - sg)));
+        }
+        st8(dst, pack8(og));
+        st8(dst + a.N, pack8(ou));
+        continue;
+      }
       if (EPI == EPI_BF16_ACC || EPI == EPI_BF16_RES) {
         float o[8], f[8];
         unpack8(v, f);
@@ -226,6 +253,55 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
           else *d = acc[i][j][r];
         }
   }
+}
+
+// Stage a 128 x 32 bf16 tile (values f(i, j, r) at wave row 16 i + 4 (lane >> 4) + r, column
+// 16 j + (lane & 15)) through this wave's LDS area and write it at dst (+ row * ld) as 16-B row
+// segments.
+template <typename F>
+__device__ __forceinline__ void write_128x32(lds_u8* st, int lane, uint16_t* dst, int64_t ld, F f) {
+  constexpr int ROWB = 32 * 2 + 16;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = i * 16 + (lane >> 4) * 4 + r, col = j * 16 + (lane & 15);
+        *(__attribute__((address_space(3))) uint16_t*)(st + row * ROWB + col * 2) = f2bf(f(i, j, r));
+      }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+#pragma unroll
+  for (int it = 0; it < 128 / 16; ++it) {
+    const int row = it * 16 + lane / 4, ch = lane % 4;
+    typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+    const u32x4_t raw = *(const __attribute__((address_space(3))) u32x4_t*)(st + row * ROWB + ch * 16);
+    bf16x8 v;
+    v.w[0] = raw[0]; v.w[1] = raw[1]; v.w[2] = raw[2]; v.w[3] = raw[3];
+    st8(dst + row * ld + ch * 8, v);
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // the staging area is reused by the next call
+}
+
+// EPI_SWIGLU_FWD: the wave's 128 x 64 accumulators are 32 gate columns (acc[.][0..1]) and the
+// SAME 32 up columns (acc[.][2..3]) of output columns hc0 .. hc0+31.
+__device__ __forceinline__ void epilogue_swiglu_fwd(const GemmArgs& a, f32x4_t (&acc)[8][4], lds_u8* st, int64_t row0,
+                                                    int hc0, int lane) {
+  uint16_t* H = (uint16_t*)a.C[0];
+  uint16_t* GU = (uint16_t*)a.C[1];
+  const int64_t ldh = a.ldc[0], ldgu = a.ldc[1];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = round_bf(acc[i][j][r]);  // g, u are bf16 tensors
+  write_128x32(st, lane, GU + row0 * ldgu + hc0, ldgu, [&](int i, int j, int r) { return acc[i][j][r]; });
+  write_128x32(st, lane, GU + row0 * ldgu + a.N + hc0, ldgu, [&](int i, int j, int r) { return acc[i][j + 2][r]; });
+  write_128x32(st, lane, H + row0 * ldh + hc0, ldh, [&](int i, int j, int r) {
+    const float g = acc[i][j][r];
+    return round_bf(g * silu_sig(g)) * acc[i][j + 2][r];
+  });
 }
 
 // B operand image base for the tile at (n0, k0) (+ n_off columns inside the tile)
@@ -304,8 +380,10 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const GemmGroup g) {
 
   // B segment for this tile (N-segments) or the first K-segment; ld is per tile (host checks
   // that K-segments share one ld)
+  constexpr bool PAIR = EPI == EPI_SWIGLU_FWD;  // Bl = W_gate rows, Br = W_up rows of tile n
   int64_t ldb;
-  const uint16_t* Bt0 = b_image_ptr(a, BKC, n0, 0, 0, ldb);
+  const uint16_t* Bt0 = PAIR ? a.B[0] : b_image_ptr(a, BKC, n0, 0, 0, ldb);
+  if (PAIR) ldb = a.ldb[0];
   const int64_t lda = a.lda;
   // loop-invariant per-lane element offsets of this wave's 2 DMA instructions per half image
   uint32_t vA[2][2], vB[2][2];  // [half][it]
@@ -314,8 +392,12 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const GemmGroup g) {
     const int i = it * 8 + wave;
     vA[0][it] = himg_voff<AK, 64>(i, lane, lda, 0);
     vA[1][it] = himg_voff<AK, 64>(i, lane, lda, 64);
-    vB[0][it] = himg_voff<BKC, 32>(i, lane, ldb, 0);
-    vB[1][it] = himg_voff<BKC, 32>(i, lane, ldb, 32);
+    if (PAIR) {
+      vB[0][it] = vB[1][it] = himg_voff<BKC, 128>(i, lane, ldb, 0);
+    } else {
+      vB[0][it] = himg_voff<BKC, 32>(i, lane, ldb, 0);
+      vB[1][it] = himg_voff<BKC, 32>(i, lane, ldb, 32);
+    }
   }
   const uint16_t* Ab0 = AK ? a.A + (int64_t)m0 * lda : a.A + m0;
   auto a_ptr = [&](int t) { return AK ? Ab0 + t * BK : Ab0 + (int64_t)t * BK * lda; };
@@ -324,11 +406,15 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const GemmGroup g) {
     int64_t ld;
     return b_image_ptr(a, BKC, n0, t * BK, 0, ld);
   };
+  // paired: rows tile_n * 128 .. +127 of W_gate (Bl) and W_up (Br), K-contiguous
+  auto pair_ptr = [&](int t, int which) {
+    return (which ? a.B[1] : a.B[0]) + (int64_t)tile_n * 128 * ldb + t * BK;
+  };
   // half image h (0 At, 1 Bl, 2 Br, 3 Ab) of K-tile t into buffer buf
   auto stage = [&](int t, int buf, int h) {
     lds_u8* dst = smem + buf * BUF + h * HALF;
     const bool isA = h == 0 || h == 3;
-    const uint16_t* base = isA ? a_ptr(t) : b_ptr(t);
+    const uint16_t* base = isA ? a_ptr(t) : (PAIR ? pair_ptr(t, h == 2) : b_ptr(t));
     const int sel = (h == 0 || h == 1) ? 0 : 1;
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
@@ -434,7 +520,11 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const GemmGroup g) {
   if (t < nk) ktile(t, std::integral_constant<int, 0>{});
   if (!late) bar();  // balance the barrier count of the two wave groups
   __syncthreads();
-  epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane);
+  if constexpr (PAIR) {
+    epilogue_swiglu_fwd(a, acc, smem + wave * (TM * (32 * 2 + 16)), m0 + wm * TM, tile_n * 128 + wn * 32, lane);
+  } else {
+    epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane);
+  }
 }
 
 // ============================================================================ 4-phase 256x128
@@ -711,7 +801,7 @@ int launch_t(GemmGroup g, hipStream_t stream) {
 
 template <bool AK, bool BKC, int EPI>
 int launch_8ph(GemmGroup g, hipStream_t stream) {
-  const int tiles = group_tiles(g, 256, 256);
+  const int tiles = group_tiles(g, 256, EPI == EPI_SWIGLU_FWD ? 128 : 256);
   constexpr int smem_main = 8 * 128 * BK * 2;
   constexpr int smem_epi = 8 * 128 * (64 * 2 + 16);
   constexpr int smem = smem_main > smem_epi ? smem_main : smem_epi;
@@ -786,6 +876,34 @@ int fill_args(GemmArgs& a, const void* A, int64_t lda, const void* const* B, con
               int64_t ldr) {
   if (!A || !B || !C || nb < 1 || nb > 4 || nc < 1 || nc > 4 || M <= 0 || N <= 0 || K <= 0) return PT_EINVAL;
   if (epilogue == EPI_BF16_RES && (!residual || nc != 1 || !pt_aligned16(residual) || (ldr & 7))) return PT_EINVAL;
+  if (epilogue == EPI_SWIGLU_FWD) {
+    // B = {W_gate, W_up} ([N/2, K] each, same ld), C = {h [M, N/2], g|u [M, N]}; N = 2 I
+    if (nb != 2 || b_seg_dim != 0 || nc != 2 || (N & 1) || ldb[0] != ldb[1]) return PT_EINVAL;
+    if (b_bounds && (b_bounds[0] != 0 || b_bounds[1] != N / 2 || b_bounds[2] != N)) return PT_EINVAL;
+    a = GemmArgs{};
+    a.A = (const uint16_t*)A;
+    a.lda = lda;
+    a.nbseg = 2;
+    for (int i = 0; i < 2; ++i) {
+      if (!B[i] || !pt_aligned16(B[i]) || (ldb[i] & 7) || !C[i] || !pt_aligned16(C[i]) || (ldc[i] & 7))
+        return PT_EALIGN;
+      a.B[i] = (const uint16_t*)B[i];
+      a.ldb[i] = ldb[i];
+      a.C[i] = C[i];
+      a.ldc[i] = ldc[i];
+    }
+    a.bseg[1] = N / 2;
+    for (int i = 2; i < 5; ++i) a.bseg[i] = N;
+    a.ncseg = 1;
+    for (int i = 1; i < 5; ++i) a.cseg[i] = M;
+    if (!pt_aligned16(A) || (lda & 7) || K % BK) return PT_EALIGN;
+    a.M = (int)M;
+    a.N = (int)(N / 2);  // h columns; the tile grid is 256 x 128 of h
+    a.K = (int)K;
+    return PT_OK;
+  }
+  if (epilogue == EPI_SWIGLU_BWD && (!residual || nc != 1 || !pt_aligned16(residual) || (ldr & 7) || (ldc[0] & 7)))
+    return PT_EINVAL;
   if (K % BK) return PT_EUNSUPPORTED;
   if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX) return PT_EUNSUPPORTED;
   a = GemmArgs{};
@@ -860,7 +978,11 @@ int pick_group_tile(const GemmGroup& g) {
   return -1;
 }
 
+int launch_swiglu(GemmGroup& g, int a_kcontig, int b_kcontig, int epilogue, int tile, hipStream_t stream);
+
 int launch_group(GemmGroup& g, int a_kcontig, int b_kcontig, int epilogue, int tile, hipStream_t stream) {
+  if (epilogue == EPI_SWIGLU_FWD || epilogue == EPI_SWIGLU_BWD)
+    return launch_swiglu(g, a_kcontig, b_kcontig, epilogue, tile, stream);
   if (tile < 0) tile = pick_group_tile(g);
   for (int i = 0; i < g.nprob; ++i)
     if (!args_fit(g.p[i], tile)) return PT_EUNSUPPORTED;
@@ -874,6 +996,22 @@ int launch_group(GemmGroup& g, int a_kcontig, int b_kcontig, int epilogue, int t
       return launch_layout<true, true, EPI_BF16_RES>(g, tile, stream);
     default: return PT_EINVAL;
   }
+}
+
+// the SwiGLU-fused projections: 8-phase kernel only (tile 12)
+int launch_swiglu(GemmGroup& g, int a_kcontig, int b_kcontig, int epilogue, int tile, hipStream_t stream) {
+  if (tile != -1 && tile != 12) return PT_EUNSUPPORTED;
+  for (int i = 0; i < g.nprob; ++i) {
+    const GemmArgs& a = g.p[i];
+    if (a.M % 256 || a.N % (epilogue == EPI_SWIGLU_FWD ? 128 : 256)) return PT_EUNSUPPORTED;
+    if (epilogue == EPI_SWIGLU_BWD && (a.ncseg != 1 || a.bdim != 0 || a.nbseg != 1)) return PT_EUNSUPPORTED;
+  }
+  if (epilogue == EPI_SWIGLU_FWD) {
+    if (!a_kcontig || !b_kcontig) return PT_EUNSUPPORTED;
+    return launch_8ph<true, true, EPI_SWIGLU_FWD>(g, stream);
+  }
+  if (!a_kcontig || b_kcontig) return PT_EUNSUPPORTED;
+  return launch_8ph<true, false, EPI_SWIGLU_BWD>(g, stream);
 }
 
 }  // namespace

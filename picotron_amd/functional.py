@@ -311,8 +311,11 @@ class AttentionFunction(torch.autograd.Function):
 def mlp_block_fwd(h2, wg, wu, wd, tp, residual=None):
     """h2 [T,H] -> down(silu(gate) * up) (+ residual, entering the tp sum once, from tp rank 0)."""
     I = wg.shape[0]
-    gu = K.linear_fwd(h2, [wg, wu])
-    hh = K.swiglu_fwd(gu[:, :I], gu[:, I:])
+    if K.swiglu_fusable(h2.shape[0], I):   # SwiGLU in the gate|up GEMM's epilogue
+        gu, hh = K.linear_swiglu_fwd(h2, wg, wu)
+    else:
+        gu = K.linear_fwd(h2, [wg, wu])
+        hh = K.swiglu_fwd(gu[:, :I], gu[:, I:])
     res = residual if (residual is not None and tp.rank == 0) else None
     m = K.linear_fwd(hh, [wd], residual=res)
     tp.all_reduce(m)
@@ -322,10 +325,13 @@ def mlp_block_fwd(h2, wg, wu, wd, tp, residual=None):
 def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True):
     gu, hh = saved
     I = wg.shape[0]
-    dhh = K.linear_dgrad(dm, [wd])
+    if K.swiglu_fusable(dm.shape[0], I, backward=True):   # SwiGLU bwd in the down dX epilogue
+        dgu = K.linear_dgrad_swiglu(dm, wd, gu)
+    else:
+        dhh = K.linear_dgrad(dm, [wd])
+        dgu = torch.empty_like(gu)
+        K.swiglu_bwd(dhh, gu[:, :I], gu[:, I:], dg=dgu[:, :I], du=dgu[:, I:])
     wgrad(dm, hh, [wd])
-    dgu = torch.empty_like(gu)
-    K.swiglu_bwd(dhh, gu[:, :I], gu[:, I:], dg=dgu[:, :I], du=dgu[:, I:])
     dh = handle = None
     if need_dx:
         dh = K.linear_dgrad(dgu, [wg, wu])

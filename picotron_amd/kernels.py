@@ -304,6 +304,46 @@ def linear_fwd(x2d, weights, out=None, tile=-1, residual=None):
     return y
 
 
+EPI_SWIGLU_FWD, EPI_SWIGLU_BWD = 5, 6
+
+
+def swiglu_fusable(T, I, backward=False):
+    """Shapes the SwiGLU-fused projections tile (8-phase kernel: T % 256, I % 128 (fwd) / 256 (bwd))."""
+    return T % 256 == 0 and I % (256 if backward else 128) == 0
+
+
+def linear_swiglu_fwd(x2d, wg, wu):
+    """gate|up projection with SwiGLU in the GEMM epilogue (model.py:186): returns (gu [T, 2I] =
+    [x Wg^T | x Wu^T], h = bf16(bf16(silu(g)) * u) [T, I]) in one launch."""
+    _bf16_rowmajor(x2d, "x")
+    T, K = x2d.shape
+    I = wg.shape[0]
+    for w in (wg, wu):
+        _req(w.dtype == BF16 and w.is_contiguous() and tuple(w.shape) == (I, K), "gate/up weights [I, K] bf16")
+    _req(swiglu_fusable(T, I), "linear_swiglu_fwd: T % 256 and I % 128 required")
+    gu = torch.empty(T, 2 * I, dtype=BF16, device=x2d.device)
+    h = torch.empty(T, I, dtype=BF16, device=x2d.device)
+    _gemm(x2d, x2d.stride(0), 1, [wg, wu], [K, K], [0, I, 2 * I], 1, 0, [h, gu], [I, 2 * I], [0, T], T, 2 * I, K,
+          EPI_SWIGLU_FWD)
+    return gu, h
+
+
+def linear_dgrad_swiglu(dy2d, wd, gu):
+    """dh = dY W_down (model.py:186 backward) with the SwiGLU backward in the epilogue: returns
+    dgu = [dg | du] [T, 2I] (dh is never materialised)."""
+    _bf16_rowmajor(dy2d, "dy")
+    _bf16_rowmajor(gu, "gu")
+    T, H = dy2d.shape
+    I = wd.shape[1]
+    _req(wd.dtype == BF16 and wd.is_contiguous() and wd.shape[0] == H, "down weight [H, I] bf16")
+    _req(tuple(gu.shape) == (T, 2 * I), "gu must be [T, 2I]")
+    _req(swiglu_fusable(T, I, backward=True), "linear_dgrad_swiglu: T % 256 and I % 256 required")
+    dgu = torch.empty(T, 2 * I, dtype=BF16, device=dy2d.device)
+    _gemm(dy2d, dy2d.stride(0), 1, [wd], [I], [0, I], 0, 0, [dgu], [dgu.stride(0)], [0, T], T, I, H, EPI_SWIGLU_BWD,
+          residual=gu, ldr=gu.stride(0))
+    return dgu
+
+
 def linear_dgrad(dy2d, weights, out=None, accumulate=False, tile=-1):
     """dX = dY . [W_0; W_1; ...]  where dY = [dY_0 | dY_1 | ...] is [T, sum N_i]."""
     _bf16_rowmajor(dy2d, "dy")

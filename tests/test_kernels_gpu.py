@@ -248,6 +248,31 @@ def test_gemm_grouped_wgrad(epi):
     assert rel_err(outs[0], full[:H] + base) < 1e-2
 
 
+@pytest.mark.parametrize("T,H,I", [(256, 256, 128), (512, 512, 1024), (1024, 256, 384)])
+def test_gemm_swiglu_fused(T, H, I):
+    """gate|up GEMM with SwiGLU in the epilogue == GEMM + swiglu kernel, bit for bit; and the down
+    dX GEMM with the SwiGLU backward in the epilogue == dgrad GEMM + swiglu bwd kernel"""
+    from picotron_amd import kernels as K_
+    x = torch.randn(T, H).to(BF).to(DEV)
+    wg, wu = [(torch.randn(I, H) / math.sqrt(H)).to(BF).to(DEV) for _ in range(2)]
+    gu, h = K_.linear_swiglu_fwd(x, wg, wu)
+    gu_ref = K_.linear_fwd(x, [wg, wu], tile=12 if I % 256 == 0 else 2)
+    h_ref = K_.swiglu_fwd(gu_ref[:, :I], gu_ref[:, I:])
+    torch.cuda.synchronize()
+    assert torch.equal(gu, gu_ref)
+    assert torch.equal(h, h_ref)
+    if I % 256:
+        return
+    wd = (torch.randn(H, I) / math.sqrt(I)).to(BF).to(DEV)
+    dm = torch.randn(T, H).to(BF).to(DEV)
+    dgu = K_.linear_dgrad_swiglu(dm, wd, gu)
+    dh = K_.linear_dgrad(dm, [wd], tile=12)
+    dg, du = K_.swiglu_bwd(dh, gu[:, :I], gu[:, I:])
+    torch.cuda.synchronize()
+    assert torch.equal(dgu[:, :I], dg)
+    assert torch.equal(dgu[:, I:], du)
+
+
 def test_gemm_segmented_qkv():
     """fused q|k|v forward, dX over stacked weights, dW into three outputs: one launch each."""
     from picotron_amd import kernels as K_
