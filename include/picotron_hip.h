@@ -91,6 +91,13 @@ int pt_gemm(const void* A, int64_t lda, int a_kcontig, const void* const* B, con
             const int64_t* c_bounds, int nc, int64_t M, int64_t N, int64_t K, int epilogue,
             const void* residual, int64_t ldr, int tile, hipStream_t stream);
 int pt_gemm_pick_tile(int64_t M, int64_t N, const int64_t* mseg, int nmseg, const int64_t* nseg, int nnseg);
+/* The q|k|v projection with RoPE fused into its epilogue (model.py:124-126 + 136-137): columns
+ * [0, rot_cols) of C = A . [B_0; ...]^T (B K-contiguous, segments along N) are rotated like
+ * pt_rope (position = row % seq_len in the [seq, table_stride] bf16 cos/sin tables); head_dim 64. */
+int pt_gemm_rope(const void* A, int64_t lda, const void* const* B, const int64_t* ldb, const int64_t* b_bounds, int nb,
+                 void* C, int64_t ldc, int64_t M, int64_t N, int64_t K, const void* cos_table, const void* sin_table,
+                 int64_t table_stride, int64_t seq_len, int64_t rot_cols, int64_t head_dim, int tile,
+                 hipStream_t stream);
 /* Grouped GEMM: nprob (<= 4) independent problems in ONE launch, each described like pt_gemm's
  * arguments, sharing layouts (a_kcontig, b_kcontig), epilogue and tile (-1 = auto over the
  * group).  Used where one problem alone would leave CUs idle (dW of q|k|v + dW of o_proj). */
@@ -118,7 +125,9 @@ int pt_gemm_grouped(const pt_gemm_problem* probs, int nprob, int a_kcontig, int 
  * blocks context_parallel.py:112-155 with update_out_and_lse (:157-187) fused (merge = 1).
  * q/k/v/o/dout/dq/dk/dv: token-major [B, S, H, D] views given as base + 3 strides
  * {batch, seq, head} (elements; d contiguous).  lse, delta: f32 [B, H, Sq].  D in {64, 128},
- * Sq % 128 == 0, Sk % 64 == 0 (bwd: Sk % 128 == 0).  causal: key j visible to query i iff j <= i. */
+ * Sq % 128 == 0, Sk % 64 == 0 (bwd: Sk % 128 == 0).  causal: key j visible to query i iff j <= i.
+ * bwd rope_cos/rope_sin (may be NULL): [S, rope_stride] bf16 tables; dq and dk are then stored
+ * rotated back by -theta (pt_rope inverse fused; positions = query / key index, Sq == Sk, bf16). */
 int pt_attn_fwd(const void* q, const int64_t* q_str, const void* k, const int64_t* k_str, const void* v,
                 const int64_t* v_str, void* o, const int64_t* o_str, float* lse, int64_t B, int64_t H, int64_t HKV,
                 int64_t Sq, int64_t Sk, int64_t D, float scale, int causal, int merge, hipStream_t stream);
@@ -128,7 +137,7 @@ int pt_attn_bwd(const void* q, const int64_t* q_str, const void* k, const int64_
                 const int64_t* v_str, const void* dout, const int64_t* do_str, const float* lse, const float* delta,
                 void* dq, const int64_t* dq_str, void* dk, const int64_t* dk_str, void* dv, const int64_t* dv_str,
                 int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int64_t D, float scale, int causal,
-                int grad_f32, hipStream_t stream);
+                int grad_f32, const void* rope_cos, const void* rope_sin, int64_t rope_stride, hipStream_t stream);
 
 #ifdef __cplusplus
 }

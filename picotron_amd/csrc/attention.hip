@@ -53,6 +53,11 @@ struct AttnArgs {
   int causal;
   int merge;      // fwd: merge into (o f32, lse) accumulators
   int grad_f32;   // bwd: dq/dk/dv are f32 accumulators (+=) instead of bf16 stores
+  // bwd: when set, dq and dk are rotated back by -theta (the RoPE backward, model.py:136-137)
+  // before their bf16 store, position = the query / key index; tables [Sq, rope_ld] bf16
+  const uint16_t* rope_cos;
+  const uint16_t* rope_sin;
+  int64_t rope_ld;
 };
 
 template <int D>
@@ -153,6 +158,36 @@ __device__ __forceinline__ void store_T_bf16(uint16_t* row_ptr, int dt, const f3
     *(uint2*)(row_ptr + d) = w;
   }
 }
+// store_T_bf16 of all DT tiles of one row with the inverse RoPE rotation applied to the bf16
+// values, exactly as csrc/rope.hip's backward (sj = -s; o1 = fma(g1, c, -(g2 sj)), o2 = fma(g2, c, g1 sj))
+template <int DT>
+__device__ __forceinline__ void store_T_bf16_unrope(uint16_t* row_ptr, const f32x16_t (&x)[DT], float mul,
+                                                    const uint16_t* cos_row, const uint16_t* sin_row, int lane) {
+  constexpr int HD = DT / 2;  // (d, d + 32 HD) pairs sit in tiles dt and dt + HD
+#pragma unroll
+  for (int dt = 0; dt < HD; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = 32 * dt + 8 * g4 + 4 * (lane >> 5);
+      const uint2 cw = *(const uint2*)(cos_row + d), sw = *(const uint2*)(sin_row + d);
+      const float c[4] = {lo_bf(cw.x), hi_bf(cw.x), lo_bf(cw.y), hi_bf(cw.y)};
+      const float sn[4] = {lo_bf(sw.x), hi_bf(sw.x), lo_bf(sw.y), hi_bf(sw.y)};
+      float o1[4], o2[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float g1 = round_bf(x[dt][4 * g4 + e] * mul), g2 = round_bf(x[dt + HD][4 * g4 + e] * mul);
+        const float sj = -sn[e];
+        o1[e] = fmaf(g1, c[e], -(g2 * sj));
+        o2[e] = fmaf(g2, c[e], g1 * sj);
+      }
+      uint2 w1, w2;
+      w1.x = pack_bf2(o1[0], o1[1]); w1.y = pack_bf2(o1[2], o1[3]);
+      w2.x = pack_bf2(o2[0], o2[1]); w2.y = pack_bf2(o2[2], o2[3]);
+      *(uint2*)(row_ptr + d) = w1;
+      *(uint2*)(row_ptr + d + 32 * HD) = w2;
+    }
+}
+
 __device__ __forceinline__ void accum_T_f32(float* row_ptr, int dt, const f32x16_t& x, float mul, int lane) {
 #pragma unroll
   for (int g4 = 0; g4 < 4; ++g4) {
@@ -421,11 +456,15 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv_kernel(AttnArgs a) {
   if (!a.grad_f32) {
     uint16_t* dkr = (uint16_t*)a.dk + b * a.dk_sb + (int64_t)mykey * a.dk_ss + hk * a.dk_sh;
     uint16_t* dvr = (uint16_t*)a.dv + b * a.dv_sb + (int64_t)mykey * a.dv_ss + hk * a.dv_sh;
+    if (a.rope_cos) {
+      store_T_bf16_unrope<DT>(dkr, dk, a.scale, a.rope_cos + (int64_t)mykey * a.rope_ld,
+                              a.rope_sin + (int64_t)mykey * a.rope_ld, lane);
+    } else {
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      store_T_bf16(dkr, dt, dk[dt], a.scale, lane);
-      store_T_bf16(dvr, dt, dv[dt], 1.0f, lane);
+      for (int dt = 0; dt < DT; ++dt) store_T_bf16(dkr, dt, dk[dt], a.scale, lane);
     }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) store_T_bf16(dvr, dt, dv[dt], 1.0f, lane);
   } else {
     float* dkr = (float*)a.dk + b * a.dk_sb + (int64_t)mykey * a.dk_ss + hk * a.dk_sh;
     float* dvr = (float*)a.dv + b * a.dv_sb + (int64_t)mykey * a.dv_ss + hk * a.dv_sh;
@@ -526,8 +565,13 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnArgs a) {
 
   if (!a.grad_f32) {
     uint16_t* dqr = (uint16_t*)a.dq + b * a.dq_sb + (int64_t)myq * a.dq_ss + h * a.dq_sh;
+    if (a.rope_cos) {
+      store_T_bf16_unrope<DT>(dqr, dq, a.scale, a.rope_cos + (int64_t)myq * a.rope_ld,
+                              a.rope_sin + (int64_t)myq * a.rope_ld, lane);
+    } else {
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt) store_T_bf16(dqr, dt, dq[dt], a.scale, lane);
+      for (int dt = 0; dt < DT; ++dt) store_T_bf16(dqr, dt, dq[dt], a.scale, lane);
+    }
   } else {
     float* dqr = (float*)a.dq + b * a.dq_sb + (int64_t)myq * a.dq_ss + h * a.dq_sh;
 #pragma unroll
@@ -601,8 +645,11 @@ int pt_attn_bwd(const void* q, const int64_t* q_str, const void* k, const int64_
                 const int64_t* v_str, const void* dout, const int64_t* do_str, const float* lse, const float* delta,
                 void* dq, const int64_t* dq_str, void* dk, const int64_t* dk_str, void* dv, const int64_t* dv_str,
                 int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int64_t D, float scale, int causal,
-                int grad_f32, hipStream_t stream) {
+                int grad_f32, const void* rope_cos, const void* rope_sin, int64_t rope_stride, hipStream_t stream) {
   if (!q || !k || !v || !dout || !lse || !delta || !dq || !dk || !dv) return PT_EINVAL;
+  if (rope_cos && (!rope_sin || grad_f32 || Sq != Sk || (rope_stride & 3) || !pt_aligned16(rope_cos) ||
+                   !pt_aligned16(rope_sin)))
+    return PT_EINVAL;
   AttnArgs a{};
   a.q = (const uint16_t*)q; a.q_sb = q_str[0]; a.q_ss = q_str[1]; a.q_sh = q_str[2];
   a.k = (const uint16_t*)k; a.k_sb = k_str[0]; a.k_ss = k_str[1]; a.k_sh = k_str[2];
@@ -614,6 +661,7 @@ int pt_attn_bwd(const void* q, const int64_t* q_str, const void* k, const int64_
   a.dv = dv; a.dv_sb = dv_str[0]; a.dv_ss = dv_str[1]; a.dv_sh = dv_str[2];
   a.B = (int)B; a.H = (int)H; a.HKV = (int)HKV; a.Sq = (int)Sq; a.Sk = (int)Sk;
   a.scale = scale; a.causal = causal; a.grad_f32 = grad_f32;
+  a.rope_cos = (const uint16_t*)rope_cos; a.rope_sin = (const uint16_t*)rope_sin; a.rope_ld = rope_stride;
   int rc = check_common(a, (int)D);
   if (rc) return rc;
   if (Sk % (NW * 32)) return PT_EUNSUPPORTED;

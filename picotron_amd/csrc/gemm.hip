@@ -50,7 +50,10 @@ constexpr int BK = 64;
 //   C[0] = dg|du [M, 2N] (dh itself is never written).
 enum Epilogue {
   EPI_BF16 = 0, EPI_BF16_ACC = 1, EPI_F32 = 2, EPI_F32_ACC = 3, EPI_BF16_RES = 4,
-  EPI_SWIGLU_FWD = 5, EPI_SWIGLU_BWD = 6
+  EPI_SWIGLU_FWD = 5, EPI_SWIGLU_BWD = 6,
+  // EPI_ROPE: the q|k|v projection with RoPE (model.py:136-137) on its q|k columns in the
+  // epilogue; head_dim 64 = the wave tile's width, so (d, d + 32) pairs sit in one lane
+  EPI_ROPE = 7
 };
 
 // SwiGLU element math, the same expressions as csrc/swiglu.hip (torch's bf16 roundings)
@@ -70,6 +73,10 @@ struct GemmArgs {
   int ncseg;
   const uint16_t* R;  // residual (EPI_BF16_RES), indexed like C segment 0
   int64_t ldr;
+  const uint16_t* rope_cos;  // EPI_ROPE: [seq, rope_ld] bf16 tables (get_cos_sin, model.py:21-31)
+  const uint16_t* rope_sin;
+  int64_t rope_ld;
+  int rope_seq, rope_cols;   // position = row % rope_seq; columns [0, rope_cols) are rotated
   int M, N, K;
   int tiles_m, tiles_n;
 };
@@ -188,7 +195,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
   const int64_t ldc = a.ldc[cs];
   const int64_t mrow0 = m0 - a.cseg[cs] + wm * TM;
   const int ncol0 = n0 + wn * TN;
-  if (EPI == EPI_BF16 || EPI == EPI_BF16_ACC || EPI == EPI_BF16_RES || EPI == EPI_SWIGLU_BWD) {
+  if (EPI == EPI_BF16 || EPI == EPI_BF16_ACC || EPI == EPI_BF16_RES || EPI == EPI_SWIGLU_BWD || EPI == EPI_ROPE) {
     constexpr int ROWB = TN * 2 + 16;  // +16 B pad: spreads the column-wise 2-B writes over banks
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -201,6 +208,37 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
         }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-private staging, no barrier needed
     uint16_t* C = (uint16_t*)a.C[cs];
+    if constexpr (EPI == EPI_ROPE && TN == 64) {
+      if (ncol0 < a.rope_cols) {
+        // the wave's 64 columns are one head: lane = (row, chunk ch < 4) rotates chunk ch with
+        // its partner ch + 4 (d, d + 32) from the bf16 staging, as csrc/rope.hip does
+        typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int it = 0; it < TM / 16; ++it) {
+          const int row = it * 16 + lane / 4, ch = lane % 4;
+          const u32x4_t r1 = *(const __attribute__((address_space(3))) u32x4_t*)(st + row * ROWB + ch * 16);
+          const u32x4_t r2 = *(const __attribute__((address_space(3))) u32x4_t*)(st + row * ROWB + (ch + 4) * 16);
+          const int64_t pos = (mrow0 + row) % a.rope_seq;
+          float x1[8], x2[8], c[8], sn[8], o1[8], o2[8];
+          bf16x8 v1, v2;
+          v1.w[0] = r1[0]; v1.w[1] = r1[1]; v1.w[2] = r1[2]; v1.w[3] = r1[3];
+          v2.w[0] = r2[0]; v2.w[1] = r2[1]; v2.w[2] = r2[2]; v2.w[3] = r2[3];
+          unpack8(v1, x1);
+          unpack8(v2, x2);
+          unpack8(ld8(a.rope_cos + pos * a.rope_ld + ch * 8), c);
+          unpack8(ld8(a.rope_sin + pos * a.rope_ld + ch * 8), sn);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            o1[e] = fmaf(x1[e], c[e], -(x2[e] * sn[e]));
+            o2[e] = fmaf(x2[e], c[e], x1[e] * sn[e]);
+          }
+          uint16_t* dst = C + (mrow0 + row) * ldc + ncol0 + ch * 8;
+          st8(dst, pack8(o1));
+          st8(dst + 32, pack8(o2));
+        }
+        return;
+      }
+    }
     constexpr int CPR = TN / 8;          // 16-B chunks per row
     constexpr int RPI = 64 / CPR;        // rows per wave instruction
 #pragma unroll
@@ -984,6 +1022,14 @@ int launch_group(GemmGroup& g, int a_kcontig, int b_kcontig, int epilogue, int t
   if (epilogue == EPI_SWIGLU_FWD || epilogue == EPI_SWIGLU_BWD)
     return launch_swiglu(g, a_kcontig, b_kcontig, epilogue, tile, stream);
   if (tile < 0) tile = pick_group_tile(g);
+  if (epilogue == EPI_ROPE) {  // wave tiles 64 columns wide: the phased kernels only
+    if (!a_kcontig || !b_kcontig) return PT_EUNSUPPORTED;
+    for (int i = 0; i < g.nprob; ++i)
+      if (!args_fit(g.p[i], tile)) return PT_EUNSUPPORTED;
+    if (tile == 12) return launch_8ph<true, true, EPI_ROPE>(g, stream);
+    if (tile == 13) return launch_4ph<true, true, EPI_ROPE>(g, stream);
+    return PT_EUNSUPPORTED;
+  }
   for (int i = 0; i < g.nprob; ++i)
     if (!args_fit(g.p[i], tile)) return PT_EUNSUPPORTED;
   switch (epilogue) {
@@ -1048,6 +1094,29 @@ int pt_gemm_grouped(const pt_gemm_problem* probs, int nprob, int a_kcontig, int 
     if (rc) return rc;
   }
   return launch_group(g, a_kcontig, b_kcontig, epilogue, tile, stream);
+}
+
+// q|k|v projection with RoPE fused (EPI_ROPE): C[M,N] = A[M,K] . [B_0; ...]^T with columns
+// [0, rot_cols) rotated by the [seq, table_stride] cos/sin tables at position row % seq_len.
+int pt_gemm_rope(const void* A, int64_t lda, const void* const* B, const int64_t* ldb, const int64_t* b_bounds, int nb,
+                 void* C, int64_t ldc, int64_t M, int64_t N, int64_t K, const void* cos_table, const void* sin_table,
+                 int64_t table_stride, int64_t seq_len, int64_t rot_cols, int64_t head_dim, int tile,
+                 hipStream_t stream) {
+  if (!cos_table || !sin_table || seq_len <= 0 || rot_cols < 0 || rot_cols > N) return PT_EINVAL;
+  if (head_dim != 64 || rot_cols % 64) return PT_EUNSUPPORTED;
+  GemmGroup g{};
+  g.nprob = 1;
+  void* const Cs[1] = {C};
+  const int64_t ldcs[1] = {ldc};
+  const int rc = fill_args(g.p[0], A, lda, B, ldb, b_bounds, nb, 0, Cs, ldcs, nullptr, 1, M, N, K, EPI_ROPE, nullptr, 0);
+  if (rc) return rc;
+  GemmArgs& a = g.p[0];
+  a.rope_cos = (const uint16_t*)cos_table;
+  a.rope_sin = (const uint16_t*)sin_table;
+  a.rope_ld = table_stride;
+  a.rope_seq = (int)seq_len;
+  a.rope_cols = (int)rot_cols;
+  return launch_group(g, 1, 1, EPI_ROPE, tile, stream);
 }
 
 // Tile the auto-pick chooses for one [M, N] problem with the given segment boundaries (see

@@ -42,8 +42,8 @@ __global__ __launch_bounds__(256) void rope_kernel(uint16_t* __restrict__ x, int
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float sj = sign * s[j];
-      o1[j] = a[j] * c[j] - b[j] * sj;
-      o2[j] = b[j] * c[j] + a[j] * sj;
+      o1[j] = fmaf(a[j], c[j], -(b[j] * sj));  // explicit contraction: the GEMM / attention
+      o2[j] = fmaf(b[j], c[j], a[j] * sj);     // epilogues that fuse RoPE round identically
     }
     st8(p1, pack8(o1));
     st8(p2, pack8(o2));

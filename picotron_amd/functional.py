@@ -33,6 +33,13 @@ from . import kernels as K
 BF16 = torch.bfloat16
 
 
+def _fuse():
+    """PICOTRON_FUSE=0 turns the epilogue fusions (RoPE in the q|k|v GEMM and the attention
+    backward, SwiGLU in the gate|up / down GEMMs) off -- for A/B measurement only; both paths are
+    HIP kernels with identical results."""
+    return os.environ.get("PICOTRON_FUSE", "1") != "0"
+
+
 # ------------------------------------------------------------------------ gradient sinks
 def _wgrad_target(p):
     """(buffer, epilogue) the wgrad GEMM of parameter p writes into."""
@@ -233,10 +240,12 @@ class AttnShape:
         return t[:, self.wq + self.wkv:].view(self.B, self.S, self.nkv, self.d)
 
 
-def attention_core_fwd(qkv, sh, cos, sin, scale):
-    """RoPE on q|k in place (model.py:136-137), then causal flash attention (model.py:154) or the
-    ring (model.py:148-151).  Returns (o [B,S,nh,d] bf16, lse f32 [B,nh,S])."""
-    K.rope_(qkv, sh.nh + sh.nkv, sh.d, cos, sin, sh.S)
+def attention_core_fwd(qkv, sh, cos, sin, scale, roped=False):
+    """RoPE on q|k in place (model.py:136-137; skipped when the projection epilogue already
+    rotated them: roped), then causal flash attention (model.py:154) or the ring
+    (model.py:148-151).  Returns (o [B,S,nh,d] bf16, lse f32 [B,nh,S])."""
+    if not roped:
+        K.rope_(qkv, sh.nh + sh.nkv, sh.d, cos, sin, sh.S)
     if ring_enabled():
         from .context_parallel.context_parallel import ring_attention_tokens
         return ring_attention_tokens(qkv, sh, scale, True)
@@ -249,18 +258,26 @@ def attention_core_bwd(do, qkv, o, lse, sh, cos, sin, scale):
     if ring_enabled():
         from .context_parallel.context_parallel import ring_attention_tokens_bwd
         ring_attention_tokens_bwd(do, qkv, o, lse, sh, scale, True, dqkv)
+        K.rope_(dqkv, sh.nh + sh.nkv, sh.d, cos, sin, sh.S, inverse=True)
+    elif _fuse():  # the RoPE backward is fused into the dq / dk stores
+        K.attn_bwd(do, sh.q(qkv), sh.k(qkv), sh.v(qkv), o, lse, scale, True,
+                   dq=sh.q(dqkv), dk=sh.k(dqkv), dv=sh.v(dqkv), rope=(cos, sin))
     else:
         K.attn_bwd(do, sh.q(qkv), sh.k(qkv), sh.v(qkv), o, lse, scale, True,
                    dq=sh.q(dqkv), dk=sh.k(dqkv), dv=sh.v(dqkv))
-    K.rope_(dqkv, sh.nh + sh.nkv, sh.d, cos, sin, sh.S, inverse=True)
+        K.rope_(dqkv, sh.nh + sh.nkv, sh.d, cos, sin, sh.S, inverse=True)
     return dqkv
 
 
 def attn_block_fwd(h2, wq, wk, wv, wo, cos, sin, sh, tp):
     """h2 [T,H] -> (a [T,H], saved).  Row-parallel out_proj: a = sum over tp of o W_o^T."""
-    qkv = K.linear_fwd(h2, [wq, wk, wv])
     scale = 1.0 / math.sqrt(sh.d)
-    o, lse = attention_core_fwd(qkv, sh, cos, sin, scale)
+    if _fuse() and K.rope_fusable(h2.shape[0], sh.d, sh.S):   # RoPE of q|k in the projection's epilogue
+        qkv = K.linear_fwd_rope(h2, [wq, wk, wv], cos, sin, sh.S, sh.nh + sh.nkv, sh.d)
+        o, lse = attention_core_fwd(qkv, sh, cos, sin, scale, roped=True)
+    else:
+        qkv = K.linear_fwd(h2, [wq, wk, wv])
+        o, lse = attention_core_fwd(qkv, sh, cos, sin, scale)
     a = K.linear_fwd(o.view(sh.T, sh.wq), [wo])
     tp.all_reduce(a)
     return a, (qkv, o, lse)
@@ -311,7 +328,7 @@ class AttentionFunction(torch.autograd.Function):
 def mlp_block_fwd(h2, wg, wu, wd, tp, residual=None):
     """h2 [T,H] -> down(silu(gate) * up) (+ residual, entering the tp sum once, from tp rank 0)."""
     I = wg.shape[0]
-    if K.swiglu_fusable(h2.shape[0], I):   # SwiGLU in the gate|up GEMM's epilogue
+    if _fuse() and K.swiglu_fusable(h2.shape[0], I):   # SwiGLU in the gate|up GEMM's epilogue
         gu, hh = K.linear_swiglu_fwd(h2, wg, wu)
     else:
         gu = K.linear_fwd(h2, [wg, wu])
@@ -325,7 +342,7 @@ def mlp_block_fwd(h2, wg, wu, wd, tp, residual=None):
 def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True):
     gu, hh = saved
     I = wg.shape[0]
-    if K.swiglu_fusable(dm.shape[0], I, backward=True):   # SwiGLU bwd in the down dX epilogue
+    if _fuse() and K.swiglu_fusable(dm.shape[0], I, backward=True):   # SwiGLU bwd in the down dX epilogue
         dgu = K.linear_dgrad_swiglu(dm, wd, gu)
     else:
         dhh = K.linear_dgrad(dm, [wd])

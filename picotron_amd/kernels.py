@@ -307,6 +307,38 @@ def linear_fwd(x2d, weights, out=None, tile=-1, residual=None):
 EPI_SWIGLU_FWD, EPI_SWIGLU_BWD = 5, 6
 
 
+def rope_fusable(T, head_dim, seq_len):
+    """The RoPE-fused q|k|v projection tiles head_dim 64 (the wave tile width) with T % 256."""
+    return head_dim == 64 and T % 256 == 0 and T % seq_len == 0
+
+
+def linear_fwd_rope(x2d, weights, cos, sin, seq_len, rot_heads, head_dim):
+    """Y = x . [W_0; ...]^T with the first rot_heads heads of every row rotated by RoPE in the GEMM
+    epilogue (model.py:124-126 + 136-137: the q|k|v projection, then apply_rotary_emb on q and k)."""
+    _bf16_rowmajor(x2d, "x")
+    T, K = x2d.shape
+    for w in weights:
+        _req(w.dtype == BF16 and w.is_contiguous() and w.shape[1] == K, "weight must be contiguous [N, K] bf16")
+    _req(cos.dtype == BF16 and sin.dtype == BF16 and cos.stride(-1) == 1 and sin.stride(0) == cos.stride(0),
+         "rope tables: bf16 [S, d]")
+    _req(cos.shape[0] >= seq_len and rope_fusable(T, head_dim, seq_len), "linear_fwd_rope: shape")
+    ns = [w.shape[0] for w in weights]
+    N = sum(ns)
+    y = torch.empty(T, N, dtype=BF16, device=x2d.device)
+    probe = _PROBE
+    if probe is not None:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    rc = _C.lib().pt_gemm_rope(_ptr(x2d), x2d.stride(0), _C.ptrarr([_ptr(w) for w in weights]), _C.i64arr([K] * len(weights)),
+                               _C.i64arr(_bounds(ns)), len(weights), _ptr(y), y.stride(0), T, N, K, _ptr(cos), _ptr(sin),
+                               cos.stride(0), seq_len, rot_heads * head_dim, head_dim, -1, _C.stream_ptr())
+    _C.check(rc, "pt_gemm_rope")
+    if probe is not None:
+        ev1.record()
+        probe.records.append((ev0, ev1, 2.0 * T * N * K))
+    return y
+
+
 def swiglu_fusable(T, I, backward=False):
     """Shapes the SwiGLU-fused projections tile (8-phase kernel: T % 256, I % 128 (fwd) / 256 (bwd))."""
     return T % 256 == 0 and I % (256 if backward else 128) == 0
@@ -403,7 +435,10 @@ def attn_delta(dout, out):
     return delta
 
 
-def attn_bwd(dout, q, k, v, out, lse, scale, causal, dq=None, dk=None, dv=None, grad_f32=False, delta=None):
+def attn_bwd(dout, q, k, v, out, lse, scale, causal, dq=None, dk=None, dv=None, grad_f32=False, delta=None,
+             rope=None):
+    """rope = (cos, sin) [S, d] bf16 tables: dq / dk are stored rotated back by -theta (the RoPE
+    backward fused into the attention backward; positions = sequence index)."""
     B, Sq, H, D = q.shape
     Sk, HKV = k.shape[1], k.shape[2]
     lib = _C.lib()
@@ -416,9 +451,17 @@ def attn_bwd(dout, q, k, v, out, lse, scale, causal, dq=None, dk=None, dv=None, 
         dk = (torch.zeros if grad_f32 else torch.empty)(B, Sk, HKV, D, dtype=gdt, device=q.device)
     if dv is None:
         dv = (torch.zeros if grad_f32 else torch.empty)(B, Sk, HKV, D, dtype=gdt, device=q.device)
+    rc_cos = rc_sin = None
+    rstride = 0
+    if rope is not None:
+        rc_cos, rc_sin = rope
+        _req(rc_cos.dtype == BF16 and rc_sin.dtype == BF16 and rc_cos.stride(-1) == 1 and rc_cos.shape[0] >= Sq,
+             "attn_bwd rope tables: bf16 [S, d]")
+        _req(rc_sin.stride(0) == rc_cos.stride(0), "attn_bwd rope tables share a stride")
+        rstride = rc_cos.stride(0)
     rc = lib.pt_attn_bwd(_ptr(q), _str3(q), _ptr(k), _str3(k), _ptr(v), _str3(v), _ptr(dout), _str3(dout),
                          _ptr(lse), _ptr(delta), _ptr(dq), _str3(dq), _ptr(dk), _str3(dk), _ptr(dv), _str3(dv),
                          B, H, HKV, Sq, Sk, D, float(scale), int(bool(causal)), int(bool(grad_f32)),
-                         _C.stream_ptr())
+                         _ptr(rc_cos), _ptr(rc_sin), rstride, _C.stream_ptr())
     _C.check(rc, "pt_attn_bwd")
     return dq, dk, dv, delta

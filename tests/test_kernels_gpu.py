@@ -273,6 +273,46 @@ def test_gemm_swiglu_fused(T, H, I):
     assert torch.equal(dgu[:, I:], du)
 
 
+@pytest.mark.parametrize("nh,nkv,S", [(4, 2, 256), (8, 8, 128), (32, 32, 1024)])
+def test_gemm_rope_fused(nh, nkv, S):
+    """q|k|v projection with RoPE in the epilogue == projection + rope kernel, bit for bit"""
+    from picotron_amd import kernels as K_
+    d, B = 64, 2
+    T, H = B * S, 256
+    x = torch.randn(T, H).to(BF).to(DEV)
+    ws = [(torch.randn(n * d, H) / math.sqrt(H)).to(BF).to(DEV) for n in (nh, nkv, nkv)]
+    cos, sin = [t.to(DEV) for t in O.get_cos_sin(S, d, base=10000.0)]
+    y = K_.linear_fwd_rope(x, ws, cos, sin, S, nh + nkv, d)
+    ref = K_.linear_fwd(x, ws)
+    K_.rope_(ref, nh + nkv, d, cos, sin, S)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_attention_bwd_rope_fused(D):
+    """attention backward with the RoPE backward fused into the dq / dk stores == attention
+    backward + inverse rope kernel, bit for bit"""
+    from picotron_amd import kernels as K_
+    B, S, H, HKV = 2, 256, 4, 2
+    T = B * S
+    qkv = torch.randn(T, (H + 2 * HKV) * D).to(BF).to(DEV)
+    sh = lambda t, lo, n: t.view(B, S, -1)[:, :, lo * D:(lo + n) * D].view(B, S, n, D)
+    q, k, v = sh(qkv, 0, H), sh(qkv, H, HKV), sh(qkv, H + HKV, HKV)
+    do = torch.randn(B, S, H, D).to(BF).to(DEV)
+    cos, sin = [t.to(DEV) for t in O.get_cos_sin(S, D, base=10000.0)]
+    scale = D ** -0.5
+    o, lse = K_.attn_fwd(q, k, v, scale, True)
+    d1 = torch.empty_like(qkv)
+    K_.attn_bwd(do, q, k, v, o, lse, scale, True, dq=sh(d1, 0, H), dk=sh(d1, H, HKV), dv=sh(d1, H + HKV, HKV),
+                rope=(cos, sin))
+    d2 = torch.empty_like(qkv)
+    K_.attn_bwd(do, q, k, v, o, lse, scale, True, dq=sh(d2, 0, H), dk=sh(d2, H, HKV), dv=sh(d2, H + HKV, HKV))
+    K_.rope_(d2, H + HKV, D, cos, sin, S, inverse=True)
+    torch.cuda.synchronize()
+    assert torch.equal(d1, d2)
+
+
 def test_gemm_segmented_qkv():
     """fused q|k|v forward, dX over stacked weights, dW into three outputs: one launch each."""
     from picotron_amd import kernels as K_
