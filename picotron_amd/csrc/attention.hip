@@ -24,6 +24,8 @@
 // K/V (fwd, dq) and Q/dO (dkdv) tiles arrive by global_load_lds_dwordx4 into a 2-deep ring.
 #include "common.h"
 
+#include <stdlib.h>
+
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
@@ -58,6 +60,9 @@ struct AttnArgs {
   const uint16_t* rope_cos;
   const uint16_t* rope_sin;
   int64_t rope_ld;
+  // causal load balance: each workgroup runs block x and block (n - 1 - x) one after the other,
+  // so every workgroup gets the same number of tiles whatever CU slot it lands in
+  int pair;
 };
 
 template <int D>
@@ -135,6 +140,8 @@ __device__ __forceinline__ void attn_coords(int& x, int& y, int& z) {
   z = pid / (nx * ny);
 }
 
+__device__ __forceinline__ int nqb_of(const AttnArgs& a) { return a.Sq / (NW * 32); }
+
 __device__ __forceinline__ f32x16_t zero16() {
   f32x16_t z;
 #pragma unroll
@@ -201,15 +208,14 @@ __device__ __forceinline__ void accum_T_f32(float* row_ptr, int dt, const f32x16
 
 // ============================================================================ forward
 template <int D>
-__global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
+__device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_or_hk, int b) {
   constexpr int DT = D / 32, KS = D / 16;
   constexpr int TILE_B = KT * D * 2;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
   lds_u8* smem = (lds_u8*)smem_raw;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nqb = a.Sq / (NW * 32);
-  int bx, h, b;
-  attn_coords(bx, h, b);
+  const int h = h_or_hk;
   const int qb = a.causal ? nqb - 1 - bx : bx;  // heavy blocks first
   const int hk = h / (a.H / a.HKV);
   const int q0 = qb * NW * 32 + wave * 32;
@@ -334,6 +340,16 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
   }
 }
 
+template <int D>
+__global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
+  int bx, hh, b;
+  attn_coords(bx, hh, b);
+  for (int pass = 0; pass <= a.pair; ++pass) {  // one inlined body: no register growth
+    if (pass) __syncthreads();
+    attn_fwd_block<D>(a, pass ? nqb_of(a) - 1 - bx : bx, hh, b);
+  }
+}
+
 // ======================================================================= delta = rowsum(dO * O)
 // one thread per (b, h, q) row; d in 16-byte chunks.  D is passed in a.dq_sh.
 __global__ __launch_bounds__(256) void attn_delta_kernel(AttnArgs a, const uint16_t* __restrict__ o) {
@@ -359,14 +375,13 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AttnArgs a, const uint1
 
 // ============================================================================ dK / dV
 template <int D>
-__global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv_kernel(AttnArgs a) {
+__device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, int h_or_hk, int b) {
   constexpr int DT = D / 32, KS = D / 16;
   constexpr int TILE_B = KT * D * 2;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
   lds_u8* smem = (lds_u8*)smem_raw;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int kb, hk, b;
-  attn_coords(kb, hk, b);
+  const int kb = bx, hk = h_or_hk;
   const int k0 = kb * NW * 32 + wave * 32;
   const int mykey = k0 + (lane & 31);
   const int group = a.H / a.HKV;
@@ -476,17 +491,26 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv_kernel(AttnArgs a) {
   }
 }
 
+template <int D>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv_kernel(AttnArgs a) {
+  int bx, hh, b;
+  attn_coords(bx, hh, b);
+  for (int pass = 0; pass <= a.pair; ++pass) {  // one inlined body: no register growth
+    if (pass) __syncthreads();
+    attn_bwd_dkdv_block<D>(a, pass ? a.Sk / (NW * 32) - 1 - bx : bx, hh, b);
+  }
+}
+
 // ============================================================================ dQ
 template <int D>
-__global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnArgs a) {
+__device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int h_or_hk, int b) {
   constexpr int DT = D / 32, KS = D / 16;
   constexpr int TILE_B = KT * D * 2;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
   lds_u8* smem = (lds_u8*)smem_raw;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nqb = a.Sq / (NW * 32);
-  int bx, h, b;
-  attn_coords(bx, h, b);
+  const int h = h_or_hk;
   const int qb = a.causal ? nqb - 1 - bx : bx;
   const int hk = h / (a.H / a.HKV);
   const int q0 = qb * NW * 32 + wave * 32;
@@ -579,9 +603,29 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnArgs a) {
   }
 }
 
+template <int D>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnArgs a) {
+  int bx, hh, b;
+  attn_coords(bx, hh, b);
+  for (int pass = 0; pass <= a.pair; ++pass) {  // one inlined body: no register growth
+    if (pass) __syncthreads();
+    attn_bwd_dq_block<D>(a, pass ? nqb_of(a) - 1 - bx : bx, hh, b);
+  }
+}
+
 template <typename K>
 void set_smem(K kern, int bytes) {
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
+// PICOTRON_ATTN_PAIR=0 turns the causal block pairing off (A/B measurement only)
+bool pair_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PICOTRON_ATTN_PAIR");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
 }
 
 int check_common(const AttnArgs& a, int D) {
@@ -613,7 +657,9 @@ int pt_attn_fwd(const void* q, const int64_t* q_str, const void* k, const int64_
   a.scale = scale; a.causal = causal; a.merge = merge;
   int rc = check_common(a, (int)D);
   if (rc) return rc;
-  const dim3 grid((unsigned)(Sq / (NW * 32)), (unsigned)H, (unsigned)B);
+  const int nqb = (int)(Sq / (NW * 32));
+  a.pair = causal && nqb % 2 == 0 && pair_enabled();
+  const dim3 grid((unsigned)(a.pair ? nqb / 2 : nqb), (unsigned)H, (unsigned)B);
   const int smem = 2 * 2 * KT * (int)D * 2;
   if (D == 64) { set_smem(attn_fwd_kernel<64>, smem); attn_fwd_kernel<64><<<grid, NW * 64, smem, stream>>>(a); }
   else { set_smem(attn_fwd_kernel<128>, smem); attn_fwd_kernel<128><<<grid, NW * 64, smem, stream>>>(a); }
@@ -667,8 +713,10 @@ int pt_attn_bwd(const void* q, const int64_t* q_str, const void* k, const int64_
   if (Sk % (NW * 32)) return PT_EUNSUPPORTED;
   const int smem_kv = 2 * 2 * KT * (int)D * 2;
   const int smem_q = 2 * (2 * KT * (int)D * 2 + 2 * KT * 4);
-  const dim3 gq((unsigned)(Sq / (NW * 32)), (unsigned)H, (unsigned)B);
-  const dim3 gk((unsigned)(Sk / (NW * 32)), (unsigned)HKV, (unsigned)B);
+  const int nqb = (int)(Sq / (NW * 32)), nkb = (int)(Sk / (NW * 32));
+  a.pair = causal && nqb % 2 == 0 && nkb % 2 == 0 && pair_enabled();
+  const dim3 gq((unsigned)(a.pair ? nqb / 2 : nqb), (unsigned)H, (unsigned)B);
+  const dim3 gk((unsigned)(a.pair ? nkb / 2 : nkb), (unsigned)HKV, (unsigned)B);
   if (D == 64) {
     set_smem(attn_bwd_dkdv_kernel<64>, smem_q);
     set_smem(attn_bwd_dq_kernel<64>, smem_kv);
