@@ -82,122 +82,111 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_fwd_kernel(
 // dz = rstd * (dxh - xh * mean(dxh * xh)),  dxh = dy * w,  xh = z * rstd
 // dx = dz (+ dres when the residual branch gradient is fused in)
 // dw partial per block: sum over this block's rows of dy * xh (mode 1: dy * bf16(xh))
-// A wave owns RB rows (row, row + nwaves, ...) and issues all of their z / dy loads before it
-// reduces the first: RB x 2 x NCH x 16 B in flight per lane instead of one row's worth -- the
-// single-row loop was a chain of load -> wave reduction -> store per row at one wave per SIMD.
-constexpr int kBwdRows = 4;
+// One row per wave at a time, kBwdWaves(NCH) waves per block (rows grid-strided): every load of a
+// row (z, dy, dres) is issued before the row's reduction, and many waves per SIMD keep HBM busy
+// (the kernel is HBM-bound: 8 bytes per element with the fused residual gradient).
 template <int NCH>
-__global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(
+constexpr int bwd_waves() { return NCH <= 4 ? 8 : 4; }
+constexpr int kBwdGridCap = 1024;
+
+template <int NCH>
+__global__ __launch_bounds__(bwd_waves<NCH>() * 64) void rmsnorm_bwd_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ z, const uint16_t* __restrict__ w,
     const float* __restrict__ rstd_in, const uint16_t* __restrict__ dres, uint16_t* __restrict__ dx,
     float* __restrict__ dw_partial, int64_t rows, int cols, int mode) {
-  __shared__ float red[kWavesPerBlock][NCH * PT_WAVE * 8 > 4096 ? 1 : NCH * PT_WAVE * 8];
+  constexpr int WPB = bwd_waves<NCH>();
+  __shared__ float red[WPB][NCH * PT_WAVE * 8];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + wid;
-  const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
   const int nchunk = cols >> 3;
   const float inv_cols = 1.0f / (float)cols;
 
-  float wf[NCH][8], dwacc[NCH][8];
+  bf16x8 wv[NCH];
+  float dwacc[NCH][8];
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
     const int c = lane + i * PT_WAVE;
 #pragma unroll
     for (int j = 0; j < 8; ++j) dwacc[i][j] = 0.f;
-    if (c < nchunk) unpack8(ld8(w + c * 8), wf[i]);
+    if (c < nchunk) wv[i] = ld8(w + c * 8);
   }
 
-  for (int64_t row0 = wave; row0 < rows; row0 += nwaves * kBwdRows) {
-    bf16x8 zr[kBwdRows][NCH], dr[kBwdRows][NCH];
-    float rs[kBwdRows];
-#pragma unroll
-    for (int k = 0; k < kBwdRows; ++k) {
-      const int64_t row = row0 + k * nwaves;
-      if (row < rows) {
-        rs[k] = rstd_in[row];
-#pragma unroll
-        for (int i = 0; i < NCH; ++i) {
-          const int c = lane + i * PT_WAVE;
-          if (c < nchunk) {
-            zr[k][i] = ld8(z + row * cols + c * 8);
-            dr[k][i] = ld8(dy + row * cols + c * 8);
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < kBwdRows; ++k) {
-      const int64_t row = row0 + k * nwaves;
-      if (row >= rows) break;
-      const float rstd = rs[k];
-      float xh[NCH][8], g[NCH][8];
-      float dot = 0.f;
-#pragma unroll
-      for (int i = 0; i < NCH; ++i) {
-        const int c = lane + i * PT_WAVE;
-        if (c < nchunk) {
-          float zz[8], d[8];
-          unpack8(zr[k][i], zz);
-          unpack8(dr[k][i], d);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            xh[i][j] = zz[j] * rstd;
-            g[i][j] = d[j] * wf[i][j];
-            dot += g[i][j] * xh[i][j];
-            dwacc[i][j] += d[j] * (mode == 0 ? xh[i][j] : round_bf(xh[i][j]));
-          }
-        }
-      }
-      dot = wave_sum(dot) * inv_cols;
-#pragma unroll
-      for (int i = 0; i < NCH; ++i) {
-        const int c = lane + i * PT_WAVE;
-        if (c < nchunk) {
-          float o[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = rstd * (g[i][j] - xh[i][j] * dot);
-          if (dres) {
-            float r[8];
-            unpack8(ld8(dres + row * cols + c * 8), r);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) o[j] += r[j];
-          }
-          st8(dx + row * cols + c * 8, pack8(o));
-        }
-      }
-    }
-  }
-
-  // combine the block's waves, then one partial row per block
-  if (NCH * PT_WAVE * 8 <= 4096) {
+  for (int64_t row = (int64_t)blockIdx.x * WPB + wid; row < rows; row += (int64_t)gridDim.x * WPB) {
+    bf16x8 zr[NCH], dr[NCH], rr[NCH];
+    const float rstd = rstd_in[row];
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int c = lane + i * PT_WAVE;
       if (c < nchunk) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) red[wid][c * 8 + j] = dwacc[i][j];
+        zr[i] = ld8(z + row * cols + c * 8);
+        dr[i] = ld8(dy + row * cols + c * 8);
+        if (dres) rr[i] = ld8(dres + row * cols + c * 8);
       }
     }
-    __syncthreads();
-    for (int col = threadIdx.x; col < cols; col += kThreads) {
-      float s = 0.f;
-#pragma unroll
-      for (int k = 0; k < kWavesPerBlock; ++k) s += red[k][col];
-      dw_partial[(int64_t)blockIdx.x * cols + col] = s;
-    }
-  } else {
-    // wide rows: one partial row per wave instead
+    float dot = 0.f;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int c = lane + i * PT_WAVE;
       if (c < nchunk) {
-        float* dst = dw_partial + ((int64_t)blockIdx.x * kWavesPerBlock + wid) * cols + c * 8;
+        float zz[8], d[8], wf[8];
+        unpack8(zr[i], zz);
+        unpack8(dr[i], d);
+        unpack8(wv[i], wf);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) dst[j] = dwacc[i][j];
+        for (int j = 0; j < 8; ++j) {
+          const float xh = zz[j] * rstd;
+          dot += d[j] * wf[j] * xh;
+          dwacc[i][j] += d[j] * (mode == 0 ? xh : round_bf(xh));
+        }
+      }
+    }
+    dot = wave_sum(dot) * inv_cols;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int c = lane + i * PT_WAVE;
+      if (c < nchunk) {
+        float zz[8], d[8], wf[8], o[8];
+        unpack8(zr[i], zz);
+        unpack8(dr[i], d);
+        unpack8(wv[i], wf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = zz[j] * rstd;
+          o[j] = rstd * (d[j] * wf[j] - xh * dot);
+        }
+        if (dres) {
+          float r[8];
+          unpack8(rr[i], r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += r[j];
+        }
+        st8(dx + row * cols + c * 8, pack8(o));
       }
     }
   }
+
+  // combine the block's waves (fixed order), one partial row per block
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int c = lane + i * PT_WAVE;
+    if (c < nchunk) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[wid][c * 8 + j] = dwacc[i][j];
+    }
+  }
+  __syncthreads();
+  for (int col = threadIdx.x; col < cols; col += WPB * 64) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < WPB; ++k) s += red[k][col];
+    dw_partial[(int64_t)blockIdx.x * cols + col] = s;
+  }
+}
+
+template <int NCH>
+int bwd_grid(int64_t rows) {
+  const int64_t g = (rows + bwd_waves<NCH>() - 1) / bwd_waves<NCH>();
+  return (int)(g < kBwdGridCap ? g : kBwdGridCap);
 }
 
 // dw[col] = sum_p partial[p][col]  -- fixed summation order, deterministic.  One block per 8
@@ -265,11 +254,13 @@ int fwd_grid(int64_t rows) {
 extern "C" {
 
 int pt_rmsnorm_bwd_partials(int64_t rows, int cols) {
-  const int nch = nch_for(cols);
-  if (nch < 0) return PT_EUNSUPPORTED;
-  // bwd grid is fixed at 256 blocks (one per CU); wide rows keep one partial per wave
-  const int grid = (int)(rows < 256 * kWavesPerBlock ? (rows + kWavesPerBlock - 1) / kWavesPerBlock : 256);
-  return (nch * PT_WAVE * 8 <= 4096) ? grid : grid * kWavesPerBlock;
+  switch (nch_for(cols)) {  // one partial row per bwd block
+    case 1: return bwd_grid<1>(rows);
+    case 2: return bwd_grid<2>(rows);
+    case 4: return bwd_grid<4>(rows);
+    case 8: return bwd_grid<8>(rows);
+    default: return PT_EUNSUPPORTED;
+  }
 }
 
 int pt_rmsnorm_fwd(const void* x, const void* residual, const void* weight, void* y, void* z_out,
@@ -307,7 +298,6 @@ int pt_rmsnorm_bwd(const void* dy, const void* z, const void* weight, const floa
   if (nch < 0) return PT_EUNSUPPORTED;
   const int nmode = mode & 3;
   if (nmode > 1 || (mode & PT_DW_ACC_BF16 && mode & PT_DW_ACC_F32)) return PT_EINVAL;
-  const int grid = (int)(rows < 256 * kWavesPerBlock ? (rows + kWavesPerBlock - 1) / kWavesPerBlock : 256);
   const int nparts = pt_rmsnorm_bwd_partials(rows, (int)cols);
   const auto* DY = (const uint16_t*)dy;
   const auto* Z = (const uint16_t*)z;
@@ -315,10 +305,10 @@ int pt_rmsnorm_bwd(const void* dy, const void* z, const void* weight, const floa
   const auto* DR = (const uint16_t*)dres;
   auto* DX = (uint16_t*)dx;
   switch (nch) {
-    case 1: rmsnorm_bwd_kernel<1><<<grid, kThreads, 0, stream>>>(DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
-    case 2: rmsnorm_bwd_kernel<2><<<grid, kThreads, 0, stream>>>(DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
-    case 4: rmsnorm_bwd_kernel<4><<<grid, kThreads, 0, stream>>>(DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
-    case 8: rmsnorm_bwd_kernel<8><<<grid, kThreads, 0, stream>>>(DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
+    case 1: rmsnorm_bwd_kernel<1><<<bwd_grid<1>(rows), bwd_waves<1>() * 64, 0, stream>>>(DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
+    case 2: rmsnorm_bwd_kernel<2><<<bwd_grid<2>(rows), bwd_waves<2>() * 64, 0, stream>>>(DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
+    case 4: rmsnorm_bwd_kernel<4><<<bwd_grid<4>(rows), bwd_waves<4>() * 64, 0, stream>>>(DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
+    case 8: rmsnorm_bwd_kernel<8><<<bwd_grid<8>(rows), bwd_waves<8>() * 64, 0, stream>>>(DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
     default: return PT_EUNSUPPORTED;
   }
   PT_CHECK_LAUNCH();
