@@ -32,6 +32,11 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+# HBM bytes per GEMM launch from rocprofv3 PMC passes (tools/gpu_round.sh <tag> pmc, then
+# tools/traffic_summary.py); read for the roofline's `traffic`
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_gemm_traffic.json")
+
+
 def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
@@ -156,10 +161,17 @@ def main():
     if probe:
         s = probe.summary()
         achieved = s["avg_flop"] / (s["avg_ms"] * 1e-3) / 1e12
+        traffic, tsrc = None, None
+        if os.path.exists(TRAFFIC_FILE):   # PMC-measured HBM bytes per GEMM launch (offline passes)
+            with open(TRAFFIC_FILE) as f:
+                tj = json.load(f)
+            traffic, tsrc = tj["gemm_avg_bytes_per_launch"], os.path.relpath(TRAFFIC_FILE, ROOT)
         roofline = {"bound": "mfma", "kernel": "gemm (all bf16 MFMA GEMM launches of micro-batch "
                     f"{probe_mb} of every timed step)", "achieved": achieved,
                     "peak": MI355X_BF16_DENSE_PEAK / 1e12, "unit": "TFLOP/s",
-                    "frac": achieved / (MI355X_BF16_DENSE_PEAK / 1e12), "traffic": None,
+                    "frac": achieved / (MI355X_BF16_DENSE_PEAK / 1e12), "traffic": traffic,
+                    "traffic_unit": "bytes per launch", "traffic_source": tsrc,
+                    "algorithmic_bytes_per_launch": s["avg_alg_bytes"],
                     "launches": s["launches"], "avg_launch_ms": s["avg_ms"], "avg_launch_gflop": s["avg_flop"] / 1e9,
                     "gemm_share_of_step": s["total_ms"] * 1e-3 * args.grad_acc / elapsed}
 

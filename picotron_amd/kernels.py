@@ -204,11 +204,26 @@ class GemmProbe:
 
     def summary(self):
         torch.cuda.synchronize()
-        ms = [s.elapsed_time(e) for s, e, _ in self.records]
-        flops = [f for _, _, f in self.records]
+        ms = [r[0].elapsed_time(r[1]) for r in self.records]
+        flops = [r[2] for r in self.records]
+        byts = [r[3] for r in self.records]
         n = len(ms)
         return {"launches": n, "total_ms": sum(ms), "total_flop": sum(flops),
-                "avg_ms": sum(ms) / max(n, 1), "avg_flop": sum(flops) / max(n, 1)}
+                "avg_ms": sum(ms) / max(n, 1), "avg_flop": sum(flops) / max(n, 1),
+                "avg_alg_bytes": sum(byts) / max(n, 1)}
+
+
+def _alg_bytes(M, N, K, epilogue):
+    """Algorithmic HBM bytes of one GEMM launch: A and B read once, C written once (read too when
+    accumulating / adding a residual; f32 for the main_grad epilogues; the SwiGLU epilogues move
+    two [M, N] bf16 tensors more)."""
+    elem = 4 if epilogue in (EPI_F32, EPI_F32_ACC) else 2
+    c = M * N * elem * (2 if epilogue in (EPI_BF16_ACC, EPI_F32_ACC, EPI_BF16_RES) else 1)
+    if epilogue == 5:      # gate|up: reads x, Wg, Wu; writes g|u and h
+        c = M * N * 2 + M * (N // 2) * 2
+    elif epilogue == 6:    # down dX: reads g|u, writes dg|du
+        c = 4 * M * N * 2
+    return 2 * (M * K + N * K) + c
 
 
 _PROBE = None
@@ -230,7 +245,7 @@ def _gemm(A, lda, a_kcontig, Bs, ldbs, b_bounds, b_kcontig, b_seg_dim, Cs, ldcs,
     _C.check(rc, f"pt_gemm(M={M}, N={N}, K={K}, a_k={a_kcontig}, b_k={b_kcontig}, epi={epilogue})")
     if probe is not None:
         ev1.record()
-        probe.records.append((ev0, ev1, 2.0 * M * N * K))
+        probe.records.append((ev0, ev1, 2.0 * M * N * K, _alg_bytes(M, N, K, epilogue)))
 
 
 def _bounds(sizes):
@@ -261,7 +276,7 @@ def linear_wgrad_grouped(jobs, epilogue=EPI_BF16, tile=-1):
     """Several wgrad GEMMs (dW_i = dY_i^T X for each job (dy2d, x2d, outs)) in ONE launch
     (pt_gemm_grouped): e.g. dW of q|k|v (192 tiles) + dW of o_proj (64 tiles) fill 256 CUs."""
     probs = (_C.GemmProblem * len(jobs))()
-    flops = 0.0
+    flops = nbytes = 0.0
     for j, (dy2d, x2d, outs) in enumerate(jobs):
         _bf16_rowmajor(dy2d, "dy")
         _bf16_rowmajor(x2d, "x")
@@ -272,6 +287,7 @@ def linear_wgrad_grouped(jobs, epilogue=EPI_BF16, tile=-1):
         probs[j] = _problem(dy2d, dy2d.stride(0), [x2d], [x2d.stride(0)], [0, Kin], 0, outs,
                             [o.stride(0) for o in outs], _bounds(ns), N, Kin, T)
         flops += 2.0 * N * Kin * T
+        nbytes += _alg_bytes(N, Kin, T, epilogue)
     probe = _PROBE
     if probe is not None:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -280,7 +296,7 @@ def linear_wgrad_grouped(jobs, epilogue=EPI_BF16, tile=-1):
     _C.check(rc, f"pt_gemm_grouped({len(jobs)} problems, epi={epilogue})")
     if probe is not None:
         ev1.record()
-        probe.records.append((ev0, ev1, flops))
+        probe.records.append((ev0, ev1, flops, nbytes))
 
 
 def linear_fwd(x2d, weights, out=None, tile=-1, residual=None):
@@ -335,7 +351,7 @@ def linear_fwd_rope(x2d, weights, cos, sin, seq_len, rot_heads, head_dim):
     _C.check(rc, "pt_gemm_rope")
     if probe is not None:
         ev1.record()
-        probe.records.append((ev0, ev1, 2.0 * T * N * K))
+        probe.records.append((ev0, ev1, 2.0 * T * N * K, _alg_bytes(T, N, K, EPI_BF16)))
     return y
 
 
