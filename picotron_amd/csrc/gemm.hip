@@ -30,6 +30,7 @@
 // segments; fp32 epilogues (main_grad accumulation) write the accumulator directly.
 #include "common.h"
 
+#include <stdlib.h>
 #include <type_traits>
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -79,6 +80,7 @@ struct GemmArgs {
   int rope_seq, rope_cols;   // position = row % rope_seq; columns [0, rope_cols) are rotated
   int M, N, K;
   int tiles_m, tiles_n;
+  int group_m;
 };
 
 // swizzles (chunk = 16 bytes); see tools/lds_swizzle_search.py
@@ -166,7 +168,9 @@ struct GemmGroup {
 };
 
 // tile order: XCD remap over the whole grid (consecutive ids share an XCD), then the problem,
-// then group 8 tile-rows so an XCD's neighbours share A/B panels
+// then group `group_m` tile-rows so an XCD's 32 consecutive tiles form a compact block of the
+// output (A and B panels shared through that XCD's L2): 8 for 256x256 tiles, 4 for 256x128
+// (32 tiles = 1024 x 1024 elements either way)
 __device__ __forceinline__ const GemmArgs& select_problem(const GemmGroup& g, int& tile_m, int& tile_n) {
   const int pid_all = xcd_remap(blockIdx.x, gridDim.x);
   int pi = 0;
@@ -175,7 +179,7 @@ __device__ __forceinline__ const GemmArgs& select_problem(const GemmGroup& g, in
     if (i < g.nprob && pid_all >= g.start[i]) pi = i;
   const GemmArgs& a = g.p[pi];
   const int pid = pid_all - g.start[pi];
-  constexpr int GROUP = 8;
+  const int GROUP = a.group_m;
   const int group_span = GROUP * a.tiles_n;
   const int gid = pid / group_span;
   const int first_m = gid * GROUP;
@@ -611,14 +615,16 @@ __global__ __launch_bounds__(512) void gemm_4ph_kernel(const GemmGroup g) {
     return b_image_ptr(a, BKC, n0, t * BK, 0, ld);
   };
   // image h (0 At, 1 B, 2 Ab) of K-tile t into buffer buf
-  auto stage = [&](int t, int buf, int h) {
+  // DMA instruction `it` (of 2 per wave) of image h (0 At, 1 B, 2 Ab) of K-tile t into buffer buf
+  auto stage1 = [&](int t, int buf, int h, int it) {
     lds_u8* dst = smem + buf * BUF + h * IMG;
     const uint16_t* base = h == 1 ? b_ptr(t) : a_ptr(t);
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const uint32_t vo = h == 1 ? vB[it] : vA[h == 2 ? 1 : 0][it];
-      glds16_asm(base, vo, dst + (it * 8 + wave) * 1024);
-    }
+    const uint32_t vo = h == 1 ? vB[it] : vA[h == 2 ? 1 : 0][it];
+    glds16_asm(base, vo, dst + (it * 8 + wave) * 1024);
+  };
+  auto stage = [&](int t, int buf, int h) {
+    stage1(t, buf, h, 0);
+    stage1(t, buf, h, 1);
   };
 
   f32x4_t acc[FM][FN];
@@ -673,7 +679,7 @@ __global__ __launch_bounds__(512) void gemm_4ph_kernel(const GemmGroup g) {
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int s = 0; s < 2; ++s) bf[j][s] = read_frag<128, BKC>(sB, wn * 64 + j * 16, s, lane);
-    if (n2) stage(t + 2, nbuf, 0);
+    if (n2) stage(t + 2, nbuf, 0);  // (measured: moving DMA between the phases only loses)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     bar();
     mma(0);
@@ -808,11 +814,23 @@ void set_smem_once(Kern k, int smem) {
 }
 
 // per-problem tile grid + consecutive tile ids; returns the total tile count
+int group_m_for(int bm, int bn) {
+  static int env = -2;
+  if (env == -2) {  // PICOTRON_GEMM_GROUP_M overrides (A/B measurement)
+    const char* e = getenv("PICOTRON_GEMM_GROUP_M");
+    env = e ? atoi(e) : -1;
+  }
+  if (env > 0) return env;
+  return bm == 2 * bn ? 4 : 8;
+}
+
 inline int group_tiles(GemmGroup& g, int bm, int bn) {
   int n = 0;
+  const int gm = group_m_for(bm, bn);
   for (int i = 0; i < g.nprob; ++i) {
     g.p[i].tiles_m = g.p[i].M / bm;
     g.p[i].tiles_n = g.p[i].N / bn;
+    g.p[i].group_m = gm;
     g.start[i] = n;
     n += g.p[i].tiles_m * g.p[i].tiles_n;
   }

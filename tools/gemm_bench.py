@@ -73,7 +73,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tiles", default="0,1,2,4,5")
     ap.add_argument("--only", default="")
+    ap.add_argument("--lib", default="", help="load this libpicotron_hip.so instead (A/B runs)")
+    ap.add_argument("--brief", action="store_true", help="one short line per shape")
     args = ap.parse_args()
+    if args.lib:
+        K._C.load_library(os.path.abspath(args.lib))
     tiles = [int(t) for t in args.tiles.split(",")]
     out = []
     for name, M, N, Kd, ak, bk in SHAPES:
@@ -88,7 +92,10 @@ def main():
             tf, err, ms = run(name, M, N, Kd, ak, bk, t)
             row[f"tile{t}"] = round(tf, 1)
             row[f"err{t}"] = float(f"{err:.2e}")
-        print(json.dumps(row), flush=True)
+        if args.brief:
+            print(name, " ".join(f"t{t}={row.get(f'tile{t}')}" for t in tiles), flush=True)
+        else:
+            print(json.dumps(row), flush=True)
         out.append(row)
 
 
