@@ -68,6 +68,18 @@ int pt_cross_entropy_fwd_bwd(const void* logits, int64_t logits_stride, const in
                              int64_t dlogits_stride, float* row_loss, int64_t rows, int64_t vocab, float scale,
                              const float* inv_count, int64_t ignore_index, hipStream_t stream);
 
+/* ---- token embedding ----------------------------------------------------------------------
+ * replaces model.py:224-225 (F.embedding + autograd's dense backward) and the masked lookup of
+ * VocabParallelEmbedding (tensor_parallel.py:246-270): rows of ids outside [vocab_lo, vocab_hi)
+ * are zero.  ids int64 [T]; weight [vocab_hi - vocab_lo, H] bf16 (leading dim ldw).
+ * bwd: ids sorted ascending with their token positions perm (stable; -1 = token to skip);
+ * dweight[id - vocab_lo] (sink: 0 store bf16, PT_DW_ACC_BF16, PT_DW_ACC_F32) gets the f32 sum of
+ * the dY rows of each id rounded to bf16 once; untouched rows are not accessed. */
+int pt_embedding_fwd(const int64_t* ids, int64_t T, const void* weight, int64_t ldw, int64_t vocab_lo, int64_t vocab_hi,
+                     void* out, int64_t ldo, int64_t H, hipStream_t stream);
+int pt_embedding_bwd(const int64_t* sorted_ids, const int64_t* perm, int64_t T, const void* dy, int64_t ldy,
+                     int64_t vocab_lo, void* dweight, int64_t lddw, int64_t H, int sink, hipStream_t stream);
+
 /* ---- fused AdamW step ---------------------------------------------------------------------
  * replaces train.py:209 torch.optim.AdamW(...).step() for one tensor: the eight foreach passes of
  * torch's multi-tensor Adam (decoupled weight decay) in one, same per-op rounding to the storage

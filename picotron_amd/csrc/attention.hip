@@ -352,24 +352,30 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
 
 // ======================================================================= delta = rowsum(dO * O)
 // one thread per (b, h, q) row; d in 16-byte chunks.  D is passed in a.dq_sh.
+// rows in memory order (b, s, h: one row = D contiguous bf16 of the token-major layout), D/8 lanes
+// per row each loading one 16-B chunk of dO and O, the row's partial dots reduced over those lanes
+// by shuffles -- every wave instruction reads whole contiguous rows (coalesced), no serial chain
 __global__ __launch_bounds__(256) void attn_delta_kernel(AttnArgs a, const uint16_t* __restrict__ o) {
-  const int64_t total = (int64_t)a.B * a.H * a.Sq;
   const int Dh = (int)a.dq_sh;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int qq = (int)(i % a.Sq);
-    const int h = (int)((i / a.Sq) % a.H);
-    const int b = (int)(i / ((int64_t)a.Sq * a.H));
-    const uint16_t* dr = a.dout + b * a.do_sb + (int64_t)qq * a.do_ss + h * a.do_sh;
-    const uint16_t* orow = o + b * a.o_sb + (int64_t)qq * a.o_ss + h * a.o_sh;
+  const int lpr = Dh / 8;  // lanes per row (8 or 16)
+  const int64_t rows = (int64_t)a.B * a.Sq * a.H;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = tid; t < rows * lpr; t += nthreads) {
+    const int64_t row = t / lpr;
+    const int c = (int)(t - row * lpr);
+    const int h = (int)(row % a.H);
+    const int64_t bs = row / a.H;
+    const int qq = (int)(bs % a.Sq);
+    const int b = (int)(bs / a.Sq);
+    float x[8], y[8];
+    unpack8(ld8(a.dout + b * a.do_sb + (int64_t)qq * a.do_ss + h * a.do_sh + c * 8), x);
+    unpack8(ld8(o + b * a.o_sb + (int64_t)qq * a.o_ss + h * a.o_sh + c * 8), y);
     float acc = 0.f;
-    for (int d = 0; d < Dh; d += 8) {
-      float x[8], y[8];
-      unpack8(ld8(dr + d), x);
-      unpack8(ld8(orow + d), y);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc += x[j] * y[j];
-    }
-    a.lse[i] = acc;  // the delta buffer travels in the lse slot
+    for (int j = 0; j < 8; ++j) acc += x[j] * y[j];
+    for (int off = lpr >> 1; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (c == 0) a.lse[((int64_t)b * a.H + h) * a.Sq + qq] = acc;  // the delta buffer travels in the lse slot
   }
 }
 
@@ -677,9 +683,10 @@ int pt_attn_bwd_delta(const void* dout, const int64_t* do_str, const void* o, co
   a.lse = delta;
   a.dq_sh = D;
   a.B = (int)B; a.H = (int)H; a.Sq = (int)Sq;
-  const int64_t total = B * H * Sq;
+  if (D != 64 && D != 128) return PT_EUNSUPPORTED;
+  const int64_t total = B * H * Sq * (D / 8);  // one thread per 16-B chunk
   int64_t g = (total + 255) / 256;
-  if (g > PT_STREAM_GRID_CAP) g = PT_STREAM_GRID_CAP;
+  if (g > 4 * PT_STREAM_GRID_CAP) g = 4 * PT_STREAM_GRID_CAP;
   attn_delta_kernel<<<(int)g, 256, 0, stream>>>(a, (const uint16_t*)o);
   PT_CHECK_LAUNCH();
   return PT_OK;

@@ -418,6 +418,38 @@ class DecoderLayerFunction(torch.autograd.Function):
 
 
 # ------------------------------------------------------------------------ cross entropy
+class EmbeddingFunction(torch.autograd.Function):
+    """F.embedding (model.py:224-225) / VocabParallelEmbedding's masked lookup
+    (tensor_parallel.py:246-270) with the backward written straight into the table's gradient sink:
+    only the rows the micro-batch touches are read / written (csrc/embedding.hip)."""
+
+    @staticmethod
+    def forward(ctx, ids, weight, vocab_lo, vocab_hi, padding_idx):
+        ctx.save_for_backward(ids)
+        ctx.weight, ctx.lo, ctx.hi, ctx.pad = weight, vocab_lo, vocab_hi, padding_idx
+        return K.embedding_fwd(ids, weight, vocab_lo, vocab_hi)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (ids,) = ctx.saved_tensors
+        weight = ctx.weight
+        mg = getattr(weight, "main_grad", None)
+        if mg is not None:
+            buf, sink = mg, K.DW_ACC_F32
+        else:
+            if weight.grad is None:   # untouched rows of a fresh gradient are zero, as autograd's
+                weight.grad = torch.zeros_like(weight)
+            buf, sink = weight.grad, K.DW_ACC_BF16
+        K.embedding_bwd(ids, _contig2d(dy), buf, sink, ctx.lo, ctx.hi, ctx.pad)
+        _grad_ready(weight)
+        return None, None, None, None, None
+
+
+def embedding(ids, weight, vocab_lo=0, vocab_hi=None, padding_idx=None):
+    hi = vocab_lo + weight.shape[0] if vocab_hi is None else vocab_hi
+    return EmbeddingFunction.apply(ids, weight, vocab_lo, hi, padding_idx)
+
+
 class CrossEntropyFunction(torch.autograd.Function):
     """F.cross_entropy(logits [N, V], targets [N], reduction='mean') as called at train.py:49.
     Forward reads the logits once for the per-row loss; backward writes

@@ -79,6 +79,37 @@ def rmsnorm_bwd(dy, z, weight, rstd, mode=MODE_TRITON, dres=None, dw_out=None, d
     return dx, dw_out
 
 
+# ------------------------------------------------------------------------------- embedding
+def embedding_fwd(ids, weight, vocab_lo=0, vocab_hi=None):
+    """out[t] = weight[ids[t] - vocab_lo] (zero rows for ids outside [vocab_lo, vocab_hi))."""
+    _req(weight.dtype == BF16 and weight.stride(1) == 1, "embedding table: bf16 rows")
+    vocab_hi = vocab_lo + weight.shape[0] if vocab_hi is None else vocab_hi
+    flat = ids.reshape(-1).contiguous().to(torch.int64)
+    H = weight.shape[1]
+    out = torch.empty(flat.numel(), H, dtype=BF16, device=weight.device)
+    rc = _C.lib().pt_embedding_fwd(_ptr(flat), flat.numel(), _ptr(weight), weight.stride(0), int(vocab_lo),
+                                   int(vocab_hi), _ptr(out), out.stride(0), H, _C.stream_ptr())
+    _C.check(rc, "pt_embedding_fwd")
+    return out.view(*ids.shape, H)
+
+
+def embedding_bwd(ids, dy2d, dweight, sink, vocab_lo=0, vocab_hi=None, padding_idx=None):
+    """Sum the dY rows of every id into dweight (sink: 0 / DW_ACC_BF16 / DW_ACC_F32); ids outside
+    [vocab_lo, vocab_hi) and padding_idx contribute nothing (F.embedding's backward)."""
+    _bf16_rowmajor(dy2d, "dy")
+    flat = ids.reshape(-1).to(torch.int64)
+    vocab_hi = vocab_lo + dweight.shape[0] if vocab_hi is None else vocab_hi
+    skip = (flat < vocab_lo) | (flat >= vocab_hi)
+    if padding_idx is not None:
+        skip = skip | (flat == padding_idx)
+    keyed = torch.where(skip, torch.full_like(flat, -1), flat)
+    sorted_ids, perm = torch.sort(keyed, stable=True)
+    rc = _C.lib().pt_embedding_bwd(_ptr(sorted_ids), _ptr(perm), flat.numel(), _ptr(dy2d), dy2d.stride(0),
+                                   int(vocab_lo), _ptr(dweight), dweight.stride(0), dy2d.shape[1], int(sink),
+                                   _C.stream_ptr())
+    _C.check(rc, "pt_embedding_bwd")
+
+
 # ----------------------------------------------------------------------------------- AdamW
 def adamw_step(p, grad, exp_avg, exp_avg_sq, decay, w1, beta2, c2, bc2_sqrt, eps, step_size):
     """One fused AdamW update of tensor p in place (csrc/adamw.hip; torch foreach semantics)."""

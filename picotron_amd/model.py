@@ -277,7 +277,7 @@ class Embedding(nn.Module):
         torch.nn.init.normal_(self.weight, mean=0.0, std=1.0)
 
     def forward(self, x):
-        return F.embedding(x, self.weight, self.padding_idx)
+        return FN.embedding(x, self.weight, padding_idx=self.padding_idx)
 
 
 class Llama(nn.Module):

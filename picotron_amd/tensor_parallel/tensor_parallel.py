@@ -152,10 +152,10 @@ class VocabParallelEmbedding(nn.Module):
         self.weight.data = weight_list[self.tp_rank].contiguous()
 
     def forward(self, x):
-        input_mask = (x < self.vocab_start_index) | (x >= self.vocab_end_index)
-        masked_input = x.clone() - self.vocab_start_index
-        masked_input[input_mask] = 0
-        output_parallel = F.embedding(masked_input, self.weight, self.padding_idx, self.max_norm, self.norm_type,
-                                      self.scale_grad_by_freq, self.sparse)
-        output_parallel[input_mask, :] = 0.0
+        if self.max_norm is not None or self.scale_grad_by_freq or self.sparse:
+            raise NotImplementedError("VocabParallelEmbedding: max_norm / scale_grad_by_freq / sparse are not used "
+                                      "by picotron")
+        # the masked lookup (ids outside this rank's slice -> zero rows, no gradient) in one kernel
+        output_parallel = FN.embedding(x, self.weight, self.vocab_start_index, self.vocab_end_index,
+                                       self.padding_idx)
         return ReduceFromModelParallelRegion.apply(output_parallel)

@@ -421,3 +421,50 @@ def test_attention_ring_merge_matches_full():
     o_ref, lse_ref = O.attention_lse(qq, kk, vv, scale, True)
     assert rel_err(acc, o_ref[:, :, S:].transpose(1, 2)) < 1e-2
     assert maxabs(lse, lse_ref[:, :, S:]) < 1e-2
+
+
+# ------------------------------------------------------------------------------ embedding
+@pytest.mark.parametrize("lo,hi,pad", [(0, 512, None), (128, 384, None), (0, 512, 7)])
+def test_embedding_fwd_bwd_matches_torch(lo, hi, pad):
+    """masked lookup + backward into the grad sink == F.embedding (+ VocabParallel masking) and
+    autograd's dense backward / AccumulateGrad, over two micro-batches with repeated ids"""
+    import torch.nn.functional as F
+    from picotron_amd import functional as FN
+    V, H, T = 512, 256, 1024
+    g = torch.Generator().manual_seed(0)
+    w0 = torch.randn(hi - lo, H, generator=g).to(BF).to(DEV)
+    ids = [torch.randint(0, 64, (T,), generator=g).to(DEV), torch.randint(0, V, (T,), generator=g).to(DEV)]
+    dys = [torch.randn(T, H, generator=g).to(BF).to(DEV) for _ in range(2)]
+    w = torch.nn.Parameter(w0.clone())
+    wr = torch.nn.Parameter(w0.clone())
+    for t, dy in zip(ids, dys):
+        y = FN.embedding(t, w, lo, hi, pad)
+        mask = (t < lo) | (t >= hi)
+        yr = F.embedding(torch.where(mask, torch.zeros_like(t), t - lo), wr,
+                         None if pad is None else pad - lo).masked_fill(mask[:, None], 0.0)
+        assert torch.equal(y, yr)
+        y.backward(dy)
+        yr.backward(dy)
+    torch.cuda.synchronize()
+    assert rel_err(w.grad, wr.grad.float().cpu()) < 1e-2
+    a, b = w.grad.float(), wr.grad.float()
+    # f32 sums in a different order, then three bf16 roundings on each side (sum of micro-batch 1,
+    # sum of micro-batch 2, their sum): each error <= 2^-9 x the absolute mass of the dY rows summed
+    # (cancellation can make the result itself tiny, so the bound is on the mass, not the result)
+    mass = torch.zeros(hi - lo, H, device=DEV)
+    for t, dy in zip(ids, dys):
+        keep = (t >= lo) & (t < hi) & (t != (-1 if pad is None else pad))
+        mass.index_add_(0, (t - lo)[keep], dy.float().abs()[keep])
+    assert ((a - b).abs() <= 2.0 ** -6 * mass + 1e-6).all()
+    # bit-exact against the kernel's documented order: f32 sum over the tokens of an id in ascending
+    # position, rounded to bf16 once, added to the bf16 gradient with one more rounding
+    gref = torch.zeros(hi - lo, H, dtype=BF)
+    for t, dy in zip(ids, dys):
+        acc = torch.zeros(hi - lo, H)
+        tc, dc = t.cpu(), dy.float().cpu()
+        for i in range(T):
+            r = int(tc[i])
+            if lo <= r < hi and r != pad:
+                acc[r - lo] += dc[i]
+        gref = (gref.float() + acc.to(BF).float()).to(BF)
+    assert torch.equal(w.grad.cpu(), gref)
