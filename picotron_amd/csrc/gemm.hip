@@ -30,6 +30,7 @@
 // segments; fp32 epilogues (main_grad accumulation) write the accumulator directly.
 #include "common.h"
 
+#include <limits.h>
 #include <stdlib.h>
 #include <type_traits>
 
@@ -368,6 +369,54 @@ __device__ __forceinline__ const uint16_t* b_image_ptr(const GemmArgs& a, bool b
   return bkc ? Bp + nl * ld + kl : Bp + kl * ld + nl;
 }
 
+// B image base of K-tile k0 for the tile at n0, with the B segments (N- or K-split) read from the
+// kernarg ONCE, before the K loop, into registers.  (Calling b_image_ptr per K-tile re-issued its
+// kernarg loads after every inline-asm wait -- the "memory" clobber -- behind an s_waitcnt
+// lgkmcnt(0) that also drained the phase's in-flight LDS reads: every K-segmented launch, i.e.
+// every dX GEMM, ran 20-30 % slow.)
+struct BImg {
+  // element (k = 0, n = n0) of the first segment; a K-segment i >= 1 adds d_i elements to the
+  // base from k = s_i on (INT_MAX: no such segment) -- independent selects against 0 on plain
+  // integers: pointer selects over an array / nested chain were materialised in scratch memory
+  // (a scratch load per K-tile).  K-segments share one ld (checked on the host).
+  const uint16_t* b0;
+  int64_t d1, d2, d3;
+  int s1, s2, s3;
+  int64_t ld;
+};
+
+__device__ __forceinline__ int64_t bimg_seg_base(const GemmArgs& a, bool bkc, int n0, int i, int& start) {
+  const bool kseg = a.bdim == 1 && i < a.nbseg;
+  const int64_t k0 = kseg ? a.bseg[i] : 0;
+  // element (k, n0) of segment i = B_i + (k - k0) ld + n0  (N-contig) / B_i + n0 ld + (k - k0)
+  const int64_t off = bkc ? (int64_t)n0 * a.ldb[i] - k0 : (int64_t)n0 - k0 * a.ldb[i];
+  start = kseg ? (int)k0 : INT_MAX;
+  return kseg ? (int64_t)((intptr_t)a.B[i] + off * 2) : 0;
+}
+
+__device__ __forceinline__ BImg bimg_make(const GemmArgs& a, bool bkc, int n0) {
+  BImg r;
+  int64_t ld;
+  r.b0 = b_image_ptr(a, bkc, n0, 0, 0, ld);
+  r.ld = ld;
+  const int64_t p0 = (int64_t)(intptr_t)r.b0;
+  const int64_t p1 = bimg_seg_base(a, bkc, n0, 1, r.s1);
+  const int64_t p2 = bimg_seg_base(a, bkc, n0, 2, r.s2);
+  const int64_t p3 = bimg_seg_base(a, bkc, n0, 3, r.s3);
+  r.d1 = r.s1 == INT_MAX ? 0 : p1 - p0;
+  r.d2 = r.s2 == INT_MAX ? 0 : p2 - p1;
+  r.d3 = r.s3 == INT_MAX ? 0 : p3 - p2;
+  return r;
+}
+
+__device__ __forceinline__ const uint16_t* bimg_ptr(const BImg& b, bool bkc, int k0) {
+  const int64_t e1 = k0 >= b.s1 ? b.d1 : 0;
+  const int64_t e2 = k0 >= b.s2 ? b.d2 : 0;
+  const int64_t e3 = k0 >= b.s3 ? b.d3 : 0;
+  const int64_t k_off = bkc ? (int64_t)k0 : (int64_t)k0 * b.ld;
+  return (const uint16_t*)((intptr_t)b.b0 + e1 + e2 + e3 + k_off * 2);
+}
+
 // ============================================================================ 8-phase 256x256
 // 256x256 tile, BK = 64, 8 waves as 2(M) x 4(N), each wave a 128 x 64 output (8 x 4 accumulators
 // of 16x16).  Each operand tile is held as two "half images" of 128 rows (A) / columns (B) x 64 k,
@@ -423,9 +472,10 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const GemmGroup g) {
   // B segment for this tile (N-segments) or the first K-segment; ld is per tile (host checks
   // that K-segments share one ld)
   constexpr bool PAIR = EPI == EPI_SWIGLU_FWD;  // Bl = W_gate rows, Br = W_up rows of tile n
-  int64_t ldb;
-  const uint16_t* Bt0 = PAIR ? a.B[0] : b_image_ptr(a, BKC, n0, 0, 0, ldb);
-  if (PAIR) ldb = a.ldb[0];
+  const BImg bi = bimg_make(a, BKC, PAIR ? 0 : n0);
+  const int64_t ldb = PAIR ? a.ldb[0] : bi.ld;
+  const uint16_t* const pairB0 = a.B[0];
+  const uint16_t* const pairB1 = a.B[1];
   const int64_t lda = a.lda;
   // loop-invariant per-lane element offsets of this wave's 2 DMA instructions per half image
   uint32_t vA[2][2], vB[2][2];  // [half][it]
@@ -443,14 +493,10 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const GemmGroup g) {
   }
   const uint16_t* Ab0 = AK ? a.A + (int64_t)m0 * lda : a.A + m0;
   auto a_ptr = [&](int t) { return AK ? Ab0 + t * BK : Ab0 + (int64_t)t * BK * lda; };
-  auto b_ptr = [&](int t) {
-    if (a.bdim == 0) return BKC ? Bt0 + t * BK : Bt0 + (int64_t)t * BK * ldb;
-    int64_t ld;
-    return b_image_ptr(a, BKC, n0, t * BK, 0, ld);
-  };
+  auto b_ptr = [&](int t) { return bimg_ptr(bi, BKC, t * BK); };
   // paired: rows tile_n * 128 .. +127 of W_gate (Bl) and W_up (Br), K-contiguous
   auto pair_ptr = [&](int t, int which) {
-    return (which ? a.B[1] : a.B[0]) + (int64_t)tile_n * 128 * ldb + t * BK;
+    return (which ? pairB1 : pairB0) + (int64_t)tile_n * 128 * ldb + t * BK;
   };
   // half image h (0 At, 1 Bl, 2 Br, 3 Ab) of K-tile t into buffer buf
   auto stage = [&](int t, int buf, int h) {
@@ -596,8 +642,8 @@ __global__ __launch_bounds__(512) void gemm_4ph_kernel(const GemmGroup g) {
   const GemmArgs& a = select_problem(g, tile_m, tile_n);
   const int m0 = tile_m * 256, n0 = tile_n * 128;
 
-  int64_t ldb;
-  const uint16_t* Bt0 = b_image_ptr(a, BKC, n0, 0, 0, ldb);
+  const BImg bi = bimg_make(a, BKC, n0);
+  const int64_t ldb = bi.ld;
   const int64_t lda = a.lda;
   uint32_t vA[2][2], vB[2];
 #pragma unroll
@@ -609,11 +655,7 @@ __global__ __launch_bounds__(512) void gemm_4ph_kernel(const GemmGroup g) {
   }
   const uint16_t* Ab0 = AK ? a.A + (int64_t)m0 * lda : a.A + m0;
   auto a_ptr = [&](int t) { return AK ? Ab0 + t * BK : Ab0 + (int64_t)t * BK * lda; };
-  auto b_ptr = [&](int t) {
-    if (a.bdim == 0) return BKC ? Bt0 + t * BK : Bt0 + (int64_t)t * BK * ldb;
-    int64_t ld;
-    return b_image_ptr(a, BKC, n0, t * BK, 0, ld);
-  };
+  auto b_ptr = [&](int t) { return bimg_ptr(bi, BKC, t * BK); };
   // image h (0 At, 1 B, 2 Ab) of K-tile t into buffer buf
   // DMA instruction `it` (of 2 per wave) of image h (0 At, 1 B, 2 Ab) of K-tile t into buffer buf
   auto stage1 = [&](int t, int buf, int h, int it) {
@@ -739,15 +781,15 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const GemmGroup g) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
+  const BImg bi = bimg_make(a, BKC, n0);
+  const int64_t lda = a.lda;
   auto stage = [&](int kt, int buf) {
     const int k0 = kt * BK;
     lds_u8* sa = smem + buf * STAGE_BYTES;
     lds_u8* sb = sa + A_BYTES;
-    const uint16_t* ga = AK ? Abase + k0 : Abase + (int64_t)k0 * a.lda;
-    stage_tile<BM, AK, NT>(ga, a.lda, sa, tid);
-    int64_t ldb;
-    const uint16_t* gb = b_image_ptr(a, BKC, n0, k0, 0, ldb);
-    stage_tile<BN, BKC, NT>(gb, ldb, sb, tid);
+    const uint16_t* ga = AK ? Abase + k0 : Abase + (int64_t)k0 * lda;
+    stage_tile<BM, AK, NT>(ga, lda, sa, tid);
+    stage_tile<BN, BKC, NT>(bimg_ptr(bi, BKC, k0), bi.ld, sb, tid);
   };
 
   const int nk = a.K / BK;
