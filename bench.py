@@ -76,6 +76,9 @@ def main():
     ap.add_argument("--grad-acc", type=int, default=32)
     ap.add_argument("--cpu-tokens", type=int, default=1024, help="tokens in the cpu_baseline sample (0 = skip)")
     ap.add_argument("--no-probe", action="store_true", help="do not time GEMM launches with events")
+    ap.add_argument("--dp-bucket", action="store_true",
+                    help="N = 1 only: run the DP path anyway (DataParallelBucket, fp32 main_grad, bucket "
+                         "all-reduce over a 1-rank RCCL group) -- the per-GPU cost of N > 1 minus the links")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -86,7 +89,13 @@ def main():
     os.environ["DEVICE"] = "cuda"
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
-    if world > 1:
+    force_dp = args.dp_bucket and world == 1
+    if world > 1 or force_dp:
+        if force_dp:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group(backend="nccl", init_method="env://", device_id=device)
 
     from picotron_amd import kernels as K
@@ -105,8 +114,9 @@ def main():
         model = Llama(cfg)
     model.to(torch.bfloat16)
     num_params = count_params(model)
-    if world > 1:
+    if world > 1 or force_dp:
         model = DataParallelBucket(model)
+        model._force_grad_sync = force_dp
     optimizer = AdamW(model.parameters(), lr=3e-4)
     loader = SyntheticMicroBatchDataLoader(args.mbs, args.seq, args.grad_acc, cfg.vocab_size, device, seed=1234)
     log(f"rank {rank}/{world}: model {num_params / 1e9:.3f} B params built in {time.time() - t0:.1f} s")
@@ -190,10 +200,10 @@ def main():
                "config": {"workload": "SmolLM-1.7B dims, 15 layers, train step (fwd+bwd+AdamW)",
                           "model": "SmolLM-1.7B", "layers": args.layers, "micro_batch": args.mbs,
                           "grad_acc": args.grad_acc, "global_batch": args.mbs * args.grad_acc * world,
-                          "seq_len": args.seq, "parallelism": f"dp{world}"},
+                          "seq_len": args.seq, "parallelism": f"dp{world}" + ("-bucket" if force_dp else "")},
                "roofline": roofline, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if world > 1 or force_dp:
         dist.destroy_process_group()
 
 

@@ -212,6 +212,9 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
           *(__attribute__((address_space(3))) uint16_t*)(st + row * ROWB + col * 2) = f2bf(acc[i][j][r]);
         }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-private staging, no barrier needed
+    // keep the epilogue's loads below the staging (the accumulators die there): hoisted above it,
+    // they would be live next to all of acc and spill
+    __builtin_amdgcn_sched_barrier(0);
     uint16_t* C = (uint16_t*)a.C[cs];
     if constexpr (EPI == EPI_ROPE && TN == 64) {
       if (ncol0 < a.rope_cols) {
@@ -246,55 +249,84 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
     }
     constexpr int CPR = TN / 8;          // 16-B chunks per row
     constexpr int RPI = 64 / CPR;        // rows per wave instruction
+    constexpr int NIT = TM / RPI;
+    typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+    // the epilogues that READ memory (g|u, the residual, the accumulated gradient) issue all their
+    // loads first, then consume them: C may alias R / the old gradient, so the compiler would keep
+    // every load behind the previous iteration's store -- one HBM round trip per row group
+    constexpr bool RD = EPI == EPI_SWIGLU_BWD || EPI == EPI_BF16_ACC || EPI == EPI_BF16_RES;
+    constexpr int NLD = EPI == EPI_SWIGLU_BWD ? 2 : 1;
+    constexpr int GRP = RD ? (NIT * NLD > 8 ? 8 / NLD : NIT) : NIT;  // <= 8 prefetched chunks (32 VGPRs)
 #pragma unroll
-    for (int it = 0; it < TM / RPI; ++it) {
-      const int row = it * RPI + lane / CPR, ch = lane % CPR;
-      typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-      const u32x4_t raw = *(const __attribute__((address_space(3))) u32x4_t*)(st + row * ROWB + ch * 16);
-      bf16x8 v;
-      v.w[0] = raw[0]; v.w[1] = raw[1]; v.w[2] = raw[2]; v.w[3] = raw[3];
-      uint16_t* dst = C + (mrow0 + row) * ldc + ncol0 + ch * 8;
-      if (EPI == EPI_SWIGLU_BWD) {  // v = dh; g|u from R; dg|du to C (swiglu.hip's bwd)
-        const uint16_t* gp = a.R + (mrow0 + row) * a.ldr + ncol0 + ch * 8;
-        float d[8], gg[8], uu[8], og[8], ou[8];
-        unpack8(v, d);
-        unpack8(ld8(gp), gg);
-        unpack8(ld8(gp + a.N), uu);
+    for (int g0 = 0; g0 < NIT; g0 += GRP) {
+      bf16x8 pre[GRP][NLD];
+      if constexpr (RD) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float sg = silu_sig(gg[e]);
-          ou[e] = d[e] * round_bf(gg[e] * sg);
-          og[e] = round_bf(d[e] * uu[e]) * (sg * (1.0f + gg[e] * (1.0f - sg)));
+        for (int q = 0; q < GRP; ++q) {
+          const int row = (g0 + q) * RPI + lane / CPR, ch = lane % CPR;
+          const uint16_t* src = EPI == EPI_BF16_ACC ? C + (mrow0 + row) * ldc + ncol0 + ch * 8
+                                                    : a.R + (mrow0 + row) * a.ldr + ncol0 + ch * 8;
+          pre[q][0] = ld8(src);
+          if constexpr (NLD == 2) pre[q][NLD - 1] = ld8(src + a.N);
         }
-        st8(dst, pack8(og));
-        st8(dst + a.N, pack8(ou));
-        continue;
       }
-      if (EPI == EPI_BF16_ACC || EPI == EPI_BF16_RES) {
-        float o[8], f[8];
-        unpack8(v, f);
-        unpack8(ld8(EPI == EPI_BF16_ACC ? dst : a.R + (mrow0 + row) * a.ldr + ncol0 + ch * 8), o);
-        // acc was rounded to bf16 once above; add in f32 and round again (== torch's bf16 add)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] += f[e];
-        v = pack8(o);
+      for (int q = 0; q < GRP; ++q) {
+        const int row = (g0 + q) * RPI + lane / CPR, ch = lane % CPR;
+        const u32x4_t raw = *(const __attribute__((address_space(3))) u32x4_t*)(st + row * ROWB + ch * 16);
+        bf16x8 v;
+        v.w[0] = raw[0]; v.w[1] = raw[1]; v.w[2] = raw[2]; v.w[3] = raw[3];
+        uint16_t* dst = C + (mrow0 + row) * ldc + ncol0 + ch * 8;
+        if constexpr (EPI == EPI_SWIGLU_BWD) {  // v = dh; g|u from R; dg|du to C (swiglu.hip's bwd)
+          float d[8], gg[8], uu[8], og[8], ou[8];
+          unpack8(v, d);
+          unpack8(pre[q][0], gg);
+          unpack8(pre[q][NLD - 1], uu);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float sg = silu_sig(gg[e]);
+            ou[e] = d[e] * round_bf(gg[e] * sg);
+            og[e] = round_bf(d[e] * uu[e]) * (sg * (1.0f + gg[e] * (1.0f - sg)));
+          }
+          st8(dst, pack8(og));
+          st8(dst + a.N, pack8(ou));
+          continue;
+        }
+        if constexpr (EPI == EPI_BF16_ACC || EPI == EPI_BF16_RES) {
+          float o[8], f[8];
+          unpack8(v, f);
+          unpack8(pre[q][0], o);
+          // acc was rounded to bf16 once above; add in f32 and round again (== torch's bf16 add)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] += f[e];
+          v = pack8(o);
+        }
+        st8(dst, v);
       }
-      st8(dst, v);
     }
   } else {
     float* C = (float*)a.C[cs];
+    // f32 accumulate: one fragment row (FN x 4 values) of old values loaded before any of its
+    // stores (rows may alias as far as the compiler knows: else one round trip per element)
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+    for (int i = 0; i < FM; ++i) {
+      float old[FN][4];
+      if (EPI == EPI_F32_ACC) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            old[j][r] = C[(mrow0 + i * 16 + (lane >> 4) * 4 + r) * ldc + ncol0 + j * 16 + (lane & 15)];
+      }
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int64_t row = mrow0 + i * 16 + (lane >> 4) * 4 + r;
           const int col = ncol0 + j * 16 + (lane & 15);
-          float* d = C + row * ldc + col;
-          if (EPI == EPI_F32_ACC) *d += acc[i][j][r];
-          else *d = acc[i][j][r];
+          C[row * ldc + col] = EPI == EPI_F32_ACC ? old[j][r] + acc[i][j][r] : acc[i][j][r];
         }
+    }
   }
 }
 

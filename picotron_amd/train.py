@@ -72,7 +72,8 @@ def train_step(model, data_loader, device, on_microbatch=None):
     """train.py:29-55 with the fused HIP cross-entropy; returns the accumulated loss (float).
     on_microbatch(i): optional hook called before micro-batch i (bench.py samples its GEMM timing)."""
     acc_loss = torch.zeros((), dtype=torch.float32, device=device)
-    requires_grad_sync = pgm.current().cp_dp_world_size > 1
+    # (bench.py --dp-bucket: a 1-rank DataParallelBucket syncs like N > 1 would)
+    requires_grad_sync = pgm.current().cp_dp_world_size > 1 or getattr(model, "_force_grad_sync", False)
     for i in range(data_loader.grad_acc_steps):
         if on_microbatch is not None:
             on_microbatch(i)
