@@ -272,7 +272,7 @@ def attention_core_bwd(do, qkv, o, lse, sh, cos, sin, scale):
 def attn_block_fwd(h2, wq, wk, wv, wo, cos, sin, sh, tp):
     """h2 [T,H] -> (a [T,H], saved).  Row-parallel out_proj: a = sum over tp of o W_o^T."""
     scale = 1.0 / math.sqrt(sh.d)
-    if _fuse() and K.rope_fusable(h2.shape[0], sh.d, sh.S):   # RoPE of q|k in the projection's epilogue
+    if _fuse() and K.rope_fusable(h2.shape[0], sh.d, sh.S, (wq.shape[0], wk.shape[0], wv.shape[0])):   # RoPE of q|k in the projection's epilogue
         qkv = K.linear_fwd_rope(h2, [wq, wk, wv], cos, sin, sh.S, sh.nh + sh.nkv, sh.d)
         o, lse = attention_core_fwd(qkv, sh, cos, sin, scale, roped=True)
     else:

@@ -354,9 +354,11 @@ def linear_fwd(x2d, weights, out=None, tile=-1, residual=None):
 EPI_SWIGLU_FWD, EPI_SWIGLU_BWD = 5, 6
 
 
-def rope_fusable(T, head_dim, seq_len):
-    """The RoPE-fused q|k|v projection tiles head_dim 64 (the wave tile width) with T % 256."""
-    return head_dim == 64 and T % 256 == 0 and T % seq_len == 0
+def rope_fusable(T, head_dim, seq_len, widths=()):
+    """The RoPE-fused q|k|v projection tiles head_dim 64 (the wave tile width) with T % 256, and the
+    phased kernels need every q / k / v segment boundary on a 128-column tile edge (e.g. TP shards
+    of 2 q heads + 1 kv head of 64 do not tile: the separate RoPE kernel runs instead)."""
+    return head_dim == 64 and T % 256 == 0 and T % seq_len == 0 and all(w % 128 == 0 for w in widths)
 
 
 def linear_fwd_rope(x2d, weights, cos, sin, seq_len, rot_heads, head_dim):

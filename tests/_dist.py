@@ -1,4 +1,4 @@
-"""Multi-process gloo harness for the CPU tests of the TP / CP / DP host logic (world_size 2-4)."""
+"""Multi-process gloo harness for the TP / CP / DP tests (world_size 2-4; CPU host logic, or all ranks on cuda:0)."""
 import os
 import socket
 import sys
@@ -16,11 +16,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, fn, args, errq):
+def _worker(rank, world, port, fn, args, errq, device):
     if ROOT not in sys.path:
         sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank), DEVICE="cpu")
+                      LOCAL_RANK=str(rank) if device == "cpu" else "0", DEVICE=device)
     try:
         dist.init_process_group("gloo", rank=rank, world_size=world)
         fn(rank, world, *args)
@@ -33,12 +33,15 @@ def _worker(rank, world, port, fn, args, errq):
             dist.destroy_process_group()
 
 
-def run(fn, world, *args):
-    """Run fn(rank, world, *args) on `world` gloo ranks; re-raise the first rank failure."""
+def run(fn, world, *args, device="cpu"):
+    """Run fn(rank, world, *args) on `world` gloo ranks; re-raise the first rank failure.
+    device="cuda": every rank drives cuda:0 (the one-GPU box) and gloo moves the CUDA tensors of
+    the collectives through host memory -- the HIP kernels under the TP / CP wrappers run for real,
+    only the transport differs from RCCL."""
     ctx = mp.get_context("spawn")
     errq = ctx.SimpleQueue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, fn, args, errq)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fn, args, errq, device)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -1,0 +1,111 @@
+"""TP and CP through the HIP kernels with two ranks: the fused decoder layers, VocabParallelEmbedding,
+the gathered lm_head, the fused CE and (CP) the ring-attention schedule over the flash kernels with
+the LSE merge in their epilogue, checked against the oracle on the full, unsharded model.
+
+Both ranks drive cuda:0 of the one-GPU box and talk over gloo, which stages the CUDA tensors of the
+collectives through host memory (tests/_dist.py): the kernels, shards, f/g collectives
+(tensor_parallel.py:116-189, tp_comm.py:19-49) and ring schedule (context_parallel.py:17-110) are
+the product path; only the transport differs from RCCL over xGMI.  Sequence 256 so that each CP
+rank holds 128 tokens (the flash kernels tile the sequence in 128-row blocks).  Tolerance: norm-relative 2e-2
+(north_star's bf16 tolerance) on the fp32 oracle evaluated from the same bf16 weights."""
+import os
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+from tests import _dist
+
+pytestmark = pytest.mark.gpu
+TOL = 2e-2
+CFG = dict(hidden_size=256, intermediate_size=512, num_attention_heads=4, num_key_value_heads=2, vocab_size=512,
+           rms_norm_eps=1e-5, rope_theta=10000.0, num_hidden_layers=2, max_position_embeddings=256)
+
+
+def _rel(a, b):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+def _shard(full, local, rank):
+    """The rank's block of a master tensor: the one dim where the shapes differ is split evenly
+    (Column: dim 0, Row: dim 1, VocabParallelEmbedding: dim 0 -- tensor_parallel.py:76-82,111-117,147-152)."""
+    if full.shape == local.shape:
+        return full
+    (d,) = [i for i, (a, b) in enumerate(zip(full.shape, local.shape)) if a != b]
+    n = local.shape[d]
+    return full.narrow(d, rank * n, n)
+
+
+def _setup(tp, cp):
+    import types
+    os.environ["FLASH_ATTEN"] = "1"
+    torch.cuda.set_device(0)
+    from oracle import picotron_oracle as O
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.context_parallel.context_parallel import apply_context_parallel
+    from picotron_amd.model import Llama
+    from picotron_amd.tensor_parallel.tensor_parallel import apply_tensor_parallel
+    m = pgm.setup_process_group_manager(tp_size=tp, cp_size=cp, pp_size=1, dp_size=1)
+    cfg = types.SimpleNamespace(**CFG)
+    full = {k: v.to(torch.bfloat16) for k, v in O.init_params(dict(CFG), seed=7).items()}
+    with torch.device("cuda"):
+        model = Llama(cfg)
+        if tp > 1:
+            apply_tensor_parallel(model)
+    apply_context_parallel(model)
+    assert os.environ["CONTEXT_PARALLEL"] == ("1" if cp > 1 else "0")
+    model.to(torch.bfloat16)
+    names = dict(model.named_parameters())
+    assert sorted(names) == sorted(full), (sorted(names), sorted(full))
+    with torch.no_grad():
+        for n, p in names.items():
+            p.copy_(_shard(full[n], p, m.tp_rank))
+    g = torch.Generator().manual_seed(11)
+    ids = torch.randint(0, CFG["vocab_size"], (2, CFG["max_position_embeddings"] + 1), generator=g)
+    # the oracle on the full model, fp32 from the same bf16 weights
+    pf = {k: v.float().requires_grad_(True) for k, v in full.items()}
+    cos, sin = O.get_cos_sin(CFG["max_position_embeddings"], 64, base=CFG["rope_theta"])
+    lo = O.llama_forward(ids[:, :-1], pf, dict(CFG), cos.float(), sin.float(), norm=O.rmsnorm_flash_semantics)
+    loss_r = F.cross_entropy(lo.reshape(-1, CFG["vocab_size"]), ids[:, 1:].reshape(-1))
+    loss_r.backward()
+    return m, model, names, pf, ids, lo, loss_r
+
+
+def _llama(rank, world, tp, cp):
+    from picotron_amd import functional as FN
+    m, model, names, pf, ids, lo, loss_r = _setup(tp, cp)
+    s = CFG["max_position_embeddings"] // cp
+    sl = slice(m.cp_rank * s, (m.cp_rank + 1) * s)                # data.py:105-109: contiguous chunks
+    x, t = ids[:, :-1][:, sl].contiguous(), ids[:, 1:][:, sl].contiguous()
+    logits = model(x.cuda())
+    assert logits.shape == (2, s, CFG["vocab_size"])             # final_proj gathers its vocab shards
+    loss = FN.cross_entropy(logits.view(-1, CFG["vocab_size"]), t.reshape(-1).cuda())
+    loss.backward()
+    torch.cuda.synchronize()
+    assert _rel(logits, lo[:, sl]) < TOL
+    lsum = loss.detach().float().cpu().view(1)
+    if cp > 1:
+        dist.all_reduce(lsum, group=m.cp_group)
+    assert abs(lsum.item() / cp - loss_r.item()) < TOL * abs(loss_r.item())
+    # each CP rank holds the grad of its chunk's mean loss; their cp_dp average (bucket.py) is the
+    # grad of the full-sequence mean loss.  TP ranks hold their shard's grad.
+    for n, p in names.items():
+        assert p.grad is not None, n
+        g = p.grad.detach().float().cpu()
+        if cp > 1:
+            dist.all_reduce(g, group=m.cp_group)
+        assert _rel(g / cp, _shard(pf[n].grad, p, m.tp_rank)) < TOL, n
+
+
+def test_tensor_parallel_llama_tp2():
+    _dist.run(_llama, 2, 2, 1, device="cuda")
+
+
+def test_context_parallel_llama_cp2():
+    _dist.run(_llama, 2, 1, 2, device="cuda")
+
+
+def test_tp2_cp2_llama():
+    _dist.run(_llama, 4, 2, 2, device="cuda")
