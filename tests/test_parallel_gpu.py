@@ -109,3 +109,61 @@ def test_context_parallel_llama_cp2():
 
 def test_tp2_cp2_llama():
     _dist.run(_llama, 4, 2, 2, device="cuda")
+
+
+def _dp_llama(rank, world, tp):
+    """DataParallelBucket (data_parallel.py:93-165, bucket.py): fp32 main_grad written by the fused
+    wgrad epilogues, grad_acc 2, bucket all-reduce on the last micro-batch; each DP rank sees its
+    own tokens.  p.grad must be the average over ranks of the oracle's grads (x tp shards)."""
+    import types
+    os.environ["FLASH_ATTEN"] = "1"
+    torch.cuda.set_device(0)
+    from oracle import picotron_oracle as O
+    from picotron_amd import functional as FN
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.context_parallel.context_parallel import apply_context_parallel
+    from picotron_amd.data_parallel.data_parallel import DataParallelBucket
+    from picotron_amd.model import Llama
+    from picotron_amd.tensor_parallel.tensor_parallel import apply_tensor_parallel
+    dp = world // tp
+    m = pgm.setup_process_group_manager(tp_size=tp, cp_size=1, pp_size=1, dp_size=dp)
+    cfg = types.SimpleNamespace(**CFG)
+    full = {k: v.to(torch.bfloat16) for k, v in O.init_params(dict(CFG), seed=9).items()}
+    with torch.device("cuda"):
+        model = Llama(cfg)
+        if tp > 1:
+            apply_tensor_parallel(model)
+    apply_context_parallel(model)
+    model.to(torch.bfloat16)
+    names = dict(model.named_parameters())
+    with torch.no_grad():
+        for n, p in names.items():
+            p.copy_(_shard(full[n], p, m.tp_rank))
+    ddp = DataParallelBucket(model)
+    ga, S, V = 2, CFG["max_position_embeddings"], CFG["vocab_size"]
+    g = torch.Generator().manual_seed(21)
+    ids = torch.randint(0, V, (dp, ga, 2, S + 1), generator=g)     # [dp, ga, mbs, seq + 1]
+    for i in range(ga):
+        ddp.require_backward_grad_sync = (i == ga - 1)
+        t = ids[m.dp_rank, i]
+        lo = ddp(t[:, :-1].cuda())
+        (FN.cross_entropy(lo.view(-1, V), t[:, 1:].reshape(-1).cuda()) / ga).backward()
+    torch.cuda.synchronize()
+    pf = {k: v.float().requires_grad_(True) for k, v in full.items()}
+    cos, sin = O.get_cos_sin(S, 64, base=CFG["rope_theta"])
+    for r in range(dp):
+        for i in range(ga):
+            t = ids[r, i]
+            lo = O.llama_forward(t[:, :-1], pf, dict(CFG), cos.float(), sin.float(), norm=O.rmsnorm_flash_semantics)
+            (F.cross_entropy(lo.reshape(-1, V), t[:, 1:].reshape(-1)) / (ga * dp)).backward()
+    for n, p in names.items():
+        assert p.grad is not None and p.grad.dtype == torch.bfloat16, n
+        assert _rel(p.grad, _shard(pf[n].grad, p, m.tp_rank)) < TOL, n
+
+
+def test_data_parallel_bucket_dp2():
+    _dist.run(_dp_llama, 2, 1, device="cuda")
+
+
+def test_data_parallel_bucket_dp2_tp2():
+    _dist.run(_dp_llama, 4, 2, device="cuda")
