@@ -67,6 +67,15 @@ int pt_swiglu_bwd(const void* dh, int64_t dh_stride, const void* g, int64_t g_st
 int pt_cross_entropy_fwd_bwd(const void* logits, int64_t logits_stride, const int64_t* targets, void* dlogits,
                              int64_t dlogits_stride, float* row_loss, int64_t rows, int64_t vocab, float scale,
                              const float* inv_count, int64_t ignore_index, hipStream_t stream);
+/* The autograd pair (train.py:49 forward, loss.backward() at train.py:51): the forward streams the
+ * logits once with an online max / sum-exp and writes row_loss and row_lse [rows] f32; the
+ * backward is elementwise from the saved LSE: dlogits = (exp(x - row_lse) - onehot) * (*scale)
+ * (a device scalar: grad_output / #valid), ignore_index rows -> 0.  dlogits may alias logits. */
+int pt_cross_entropy_fwd_lse(const void* logits, int64_t logits_stride, const int64_t* targets, float* row_loss,
+                             float* row_lse, int64_t rows, int64_t vocab, int64_t ignore_index, hipStream_t stream);
+int pt_cross_entropy_bwd_lse(const void* logits, int64_t logits_stride, const int64_t* targets, const float* row_lse,
+                             void* dlogits, int64_t dlogits_stride, int64_t rows, int64_t vocab, const float* scale,
+                             int64_t ignore_index, hipStream_t stream);
 
 /* ---- token embedding ----------------------------------------------------------------------
  * replaces model.py:224-225 (F.embedding + autograd's dense backward) and the masked lookup of

@@ -147,7 +147,140 @@ __global__ __launch_bounds__(kThreads) void ce_kernel_2pass(const uint16_t* __re
   }
 }
 
+// ---- streaming pair: the autograd forward saves the row LSE so the backward needs no reduction
+//
+// fwd: one 256-thread workgroup per row, online (max, sum-exp) over 4 chunks (32 logits) at a time
+// with the 4 loads issued together -- a handful of registers, so many rows stream at once (the
+// register-resident ce_kernel above caps occupancy at ~4 waves per SIMD for V = 49152).
+// bwd: purely elementwise  dl = (exp(x - lse_row) - onehot) * g,  4 chunks in flight per thread.
+constexpr int kUnroll = 4;
+
+__global__ __launch_bounds__(kThreads) void ce_fwd_stream_kernel(const uint16_t* __restrict__ logits, int64_t ls,
+                                                                 const int64_t* __restrict__ tgt,
+                                                                 float* __restrict__ row_loss,
+                                                                 float* __restrict__ row_lse, int V,
+                                                                 int64_t ignore_index) {
+  __shared__ float red[kThreads / 64];
+  __shared__ float red2[kThreads / 64];
+  const int64_t row = blockIdx.x;
+  const uint16_t* x = logits + row * ls;
+  const int nch = V >> 3;
+  float m = -INFINITY, s = 0.f;
+  for (int c0 = threadIdx.x; c0 < nch; c0 += kThreads * kUnroll) {
+    bf16x8 v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int c = c0 + u * kThreads;
+      if (c < nch) v[u] = ld8(x + c * 8);
+    }
+    float f[kUnroll][8];
+    float cm = m;
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int c = c0 + u * kThreads;
+      if (c < nch) {
+        unpack8(v[u], f[u]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cm = fmaxf(cm, f[u][j]);
+      }
+    }
+    if (cm == -INFINITY) continue;  // nothing finite seen yet
+    s *= __expf(m - cm);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int c = c0 + u * kThreads;
+      if (c < nch) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += __expf(f[u][j] - cm);
+      }
+    }
+    m = cm;
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64), os = __shfl_xor(s, o, 64);
+    const float nm = fmaxf(m, om);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (om == -INFINITY ? 0.f : os * __expf(om - nm));
+    m = nm;
+  }
+  if (lane == 0) { red[wid] = m; red2[wid] = s; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = red[0];
+    for (int i = 1; i < kThreads / 64; ++i) M = fmaxf(M, red[i]);
+    float S = 0.f;
+    for (int i = 0; i < kThreads / 64; ++i) S += red2[i] * __expf(red[i] - M);
+    const float lse = M + __logf(S);
+    const int64_t t = tgt[row];
+    const bool valid = t != ignore_index;
+    row_lse[row] = lse;
+    row_loss[row] = valid ? lse - bf2f(x[t]) : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void ce_bwd_stream_kernel(const uint16_t* __restrict__ logits, int64_t ls,
+                                                                 const int64_t* __restrict__ tgt,
+                                                                 const float* __restrict__ row_lse,
+                                                                 uint16_t* __restrict__ dl, int64_t ds, int V,
+                                                                 const float* __restrict__ scale_dev,
+                                                                 int64_t ignore_index) {
+  const int64_t row = blockIdx.x;
+  const uint16_t* x = logits + row * ls;
+  uint16_t* d = dl + row * ds;
+  const int nch = V >> 3;
+  const int64_t t = tgt[row];
+  const float lse = row_lse[row];
+  const float g = t != ignore_index ? *scale_dev : 0.f;
+  for (int c0 = threadIdx.x; c0 < nch; c0 += kThreads * kUnroll) {
+    bf16x8 v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int c = c0 + u * kThreads;
+      if (c < nch) v[u] = ld8(x + c * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int c = c0 + u * kThreads;
+      if (c < nch) {
+        float f[8];
+        unpack8(v[u], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = (__expf(f[j] - lse) - ((int64_t)(c * 8 + j) == t ? 1.f : 0.f)) * g;
+        st8(d + c * 8, pack8(f));
+      }
+    }
+  }
+}
+
 }  // namespace
+
+extern "C" int pt_cross_entropy_fwd_lse(const void* logits, int64_t logits_stride, const int64_t* targets,
+                                        float* row_loss, float* row_lse, int64_t rows, int64_t vocab,
+                                        int64_t ignore_index, hipStream_t stream) {
+  if (!logits || !targets || !row_loss || !row_lse || rows <= 0 || vocab <= 0) return PT_EINVAL;
+  if ((vocab & 7) || (logits_stride & 7) || !pt_aligned16(logits)) return PT_EALIGN;
+  if (rows > INT32_MAX || vocab > INT32_MAX) return PT_EUNSUPPORTED;
+  ce_fwd_stream_kernel<<<(unsigned)rows, kThreads, 0, stream>>>((const uint16_t*)logits, logits_stride, targets,
+                                                               row_loss, row_lse, (int)vocab, ignore_index);
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
+
+extern "C" int pt_cross_entropy_bwd_lse(const void* logits, int64_t logits_stride, const int64_t* targets,
+                                        const float* row_lse, void* dlogits, int64_t dlogits_stride, int64_t rows,
+                                        int64_t vocab, const float* scale, int64_t ignore_index,
+                                        hipStream_t stream) {
+  if (!logits || !targets || !row_lse || !dlogits || !scale || rows <= 0 || vocab <= 0) return PT_EINVAL;
+  if ((vocab & 7) || (logits_stride & 7) || (dlogits_stride & 7)) return PT_EALIGN;
+  if (!pt_aligned16(logits) || !pt_aligned16(dlogits)) return PT_EALIGN;
+  if (rows > INT32_MAX || vocab > INT32_MAX) return PT_EUNSUPPORTED;
+  ce_bwd_stream_kernel<<<(unsigned)rows, kThreads, 0, stream>>>((const uint16_t*)logits, logits_stride, targets,
+                                                               row_lse, (uint16_t*)dlogits, dlogits_stride,
+                                                               (int)vocab, scale, ignore_index);
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
 
 extern "C" int pt_cross_entropy_fwd_bwd(const void* logits, int64_t logits_stride, const int64_t* targets,
                                         void* dlogits, int64_t dlogits_stride, float* row_loss, int64_t rows,

@@ -452,23 +452,24 @@ def embedding(ids, weight, vocab_lo=0, vocab_hi=None, padding_idx=None):
 
 class CrossEntropyFunction(torch.autograd.Function):
     """F.cross_entropy(logits [N, V], targets [N], reduction='mean') as called at train.py:49.
-    Forward reads the logits once for the per-row loss; backward writes
-    (softmax - onehot) * grad / #valid in one more read + write, with the incoming gradient (the
-    reference's `/ grad_acc_steps`) taken from device memory -- no host synchronisation."""
+    Forward streams the logits once for the per-row loss and LSE (saved, 16 KiB at 4096 rows);
+    backward writes (exp(x - lse) - onehot) * grad / #valid elementwise in one more read + write,
+    with the incoming gradient (the reference's `/ grad_acc_steps`) taken from device memory -- no
+    host synchronisation."""
 
     @staticmethod
     def forward(ctx, logits, targets, ignore_index):
         lg = _contig2d(logits)
         tg = targets.reshape(-1)
-        loss, inv_count = K.cross_entropy_loss(lg, tg, ignore_index)
-        ctx.save_for_backward(lg, tg, inv_count)
+        loss, inv_count, row_lse = K.cross_entropy_loss_lse(lg, tg, ignore_index)
+        ctx.save_for_backward(lg, tg, inv_count, row_lse)
         ctx.ignore_index, ctx.shape = ignore_index, logits.shape
         return loss.to(logits.dtype)
 
     @staticmethod
     def backward(ctx, g):
-        lg, tg, inv_count = ctx.saved_tensors
-        dl = K.cross_entropy_grad(lg, tg, g.float().reshape(1) * inv_count, ctx.ignore_index)
+        lg, tg, inv_count, row_lse = ctx.saved_tensors
+        dl = K.cross_entropy_grad_lse(lg, tg, row_lse, g.float().reshape(1) * inv_count, ctx.ignore_index)
         return dl.view(ctx.shape), None, None
 
 

@@ -197,6 +197,38 @@ def cross_entropy_loss(logits, targets, ignore_index=-100):
     return row_loss.sum() * inv_count[0], inv_count
 
 
+def cross_entropy_loss_lse(logits, targets, ignore_index=-100):
+    """Forward of the autograd pair: (mean loss f32 scalar tensor, inv_count [1] f32, row_lse [rows]
+    f32) from one streaming read of the logits (online max / sum-exp)."""
+    _bf16_rowmajor(logits, "logits")
+    rows, vocab = logits.shape
+    _req(targets.dtype == torch.int64 and targets.numel() == rows, "targets: int64 [rows]")
+    targets = targets.contiguous()
+    inv_count = (1.0 / (targets != ignore_index).sum().clamp_min(1).to(torch.float32)).reshape(1)
+    row_loss = torch.empty(rows, dtype=torch.float32, device=logits.device)
+    row_lse = torch.empty(rows, dtype=torch.float32, device=logits.device)
+    rc = _C.lib().pt_cross_entropy_fwd_lse(_ptr(logits), logits.stride(0), _ptr(targets), _ptr(row_loss),
+                                           _ptr(row_lse), rows, vocab, int(ignore_index), _C.stream_ptr())
+    _C.check(rc, "pt_cross_entropy_fwd_lse")
+    return row_loss.sum() * inv_count[0], inv_count, row_lse
+
+
+def cross_entropy_grad_lse(logits, targets, row_lse, scale_dev, ignore_index=-100):
+    """dlogits = (exp(x - row_lse) - onehot) * scale_dev[0]: elementwise, no row reduction."""
+    _bf16_rowmajor(logits, "logits")
+    rows, vocab = logits.shape
+    targets = targets.contiguous()
+    _req(scale_dev.dtype == torch.float32 and scale_dev.numel() == 1, "scale: f32 device scalar")
+    _req(row_lse.dtype == torch.float32 and row_lse.is_contiguous() and row_lse.numel() == rows, "row_lse: f32 [rows]")
+    scale_dev = scale_dev.contiguous()
+    dl = torch.empty(rows, vocab, dtype=BF16, device=logits.device)
+    rc = _C.lib().pt_cross_entropy_bwd_lse(_ptr(logits), logits.stride(0), _ptr(targets), _ptr(row_lse), _ptr(dl),
+                                           dl.stride(0), rows, vocab, _ptr(scale_dev), int(ignore_index),
+                                           _C.stream_ptr())
+    _C.check(rc, "pt_cross_entropy_bwd_lse")
+    return dl
+
+
 def cross_entropy_grad(logits, targets, scale_dev, ignore_index=-100):
     """dlogits = (softmax - onehot) * scale_dev[0] (a device scalar, e.g. grad_output / #valid)."""
     _bf16_rowmajor(logits, "logits")

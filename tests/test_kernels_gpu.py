@@ -468,3 +468,41 @@ def test_embedding_fwd_bwd_matches_torch(lo, hi, pad):
                 acc[r - lo] += dc[i]
         gref = (gref.float() + acc.to(BF).float()).to(BF)
     assert torch.equal(w.grad.cpu(), gref)
+
+
+@pytest.mark.parametrize("V", [96, 49152, 32000, 80000, 8])
+def test_cross_entropy_lse_pair(V):
+    """The autograd pair (streaming forward saving the row LSE, elementwise backward) against
+    torch fp32 F.cross_entropy / grad_acc, with an ignore_index row, and against the reference's
+    own bf16 golden vector G9."""
+    from picotron_amd import kernels as K
+    T, ga = 64, 4
+    logits = (3 * torch.randn(T, V)).to(BF)
+    tgt = torch.randint(0, V, (T,))
+    tgt[5] = -100
+    lr = logits.float().requires_grad_(True)
+    loss_ref = torch.nn.functional.cross_entropy(lr, tgt) / ga
+    loss_ref.backward()
+    lg, tg = logits.to(DEV), tgt.to(DEV)
+    loss, inv_count, lse = K.cross_entropy_loss_lse(lg, tg)
+    lse_ref = torch.logsumexp(logits.float(), dim=1)
+    assert (lse.cpu() - lse_ref).abs().max().item() < 1e-4 * max(1.0, lse_ref.abs().max().item())
+    grad = K.cross_entropy_grad_lse(lg, tg, lse, inv_count / ga)
+    torch.cuda.synchronize()
+    assert abs(loss.item() / ga - loss_ref.item()) < 1e-3 * max(1, abs(loss_ref.item()))
+    assert rel_err(grad, lr.grad) < 1e-2
+    assert grad[5].float().abs().max().item() == 0.0
+    assert torch.equal(lg.cpu(), logits)                      # logits untouched (user-visible)
+
+
+def test_cross_entropy_lse_pair_golden_vector():
+    import os
+    from picotron_amd import kernels as K
+    g = torch.load(os.path.join(os.path.dirname(__file__), "golden", "G9.pt"), weights_only=True)
+    lg = g["logits"].view(16, -1).to(DEV)
+    tg = g["targets"].reshape(-1).to(DEV)
+    ga = int(g["grad_acc"])
+    loss, inv_count, lse = K.cross_entropy_loss_lse(lg, tg)
+    grad = K.cross_entropy_grad_lse(lg, tg, lse, inv_count / ga)
+    assert abs(loss.item() / ga - g["loss"].float().item()) < 2e-2 * abs(g["loss"].float().item())
+    assert rel_err(grad, g["dlogits"].view(16, -1)) < 2e-2
