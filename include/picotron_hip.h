@@ -159,6 +159,16 @@ int pt_attn_bwd(const void* q, const int64_t* q_str, const void* k, const int64_
                 void* dq, const int64_t* dq_str, void* dk, const int64_t* dk_str, void* dv, const int64_t* dv_str,
                 int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int64_t D, float scale, int causal,
                 int grad_f32, const void* rope_cos, const void* rope_sin, int64_t rope_stride, hipStream_t stream);
+/* pt_attn_bwd with the FA2 'D' = rowsum(dO * O) computed inside the dQ kernel (run first) from o
+ * (bf16 [B, S, H, D] strides o_str) and written to delta_out [B, H, Sq] f32, which the dK/dV kernel
+ * then reads: the separate pt_attn_bwd_delta pass disappears.  bf16 gradients only (no grad_f32). */
+int pt_attn_bwd_fused_delta(const void* q, const int64_t* q_str, const void* k, const int64_t* k_str,
+                            const void* v, const int64_t* v_str, const void* o, const int64_t* o_str,
+                            const void* dout, const int64_t* do_str, const float* lse, float* delta_out, void* dq,
+                            const int64_t* dq_str, void* dk, const int64_t* dk_str, void* dv,
+                            const int64_t* dv_str, int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk,
+                            int64_t D, float scale, int causal, const void* rope_cos, const void* rope_sin,
+                            int64_t rope_stride, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -63,6 +63,9 @@ struct AttnArgs {
   // causal load balance: each workgroup runs block x and block (n - 1 - x) one after the other,
   // so every workgroup gets the same number of tiles whatever CU slot it lands in
   int pair;
+  // bwd: when set, the dQ kernel (launched first) computes D = rowsum(dO * O) of its own rows from
+  // O (a.o, bf16) and writes it here for the dK/dV kernel -- no separate delta pass
+  float* delta_w;
 };
 
 template <int D>
@@ -532,7 +535,21 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
   }
   const int64_t ri = ((int64_t)b * a.H + h) * a.Sq + myq;
   const float nlse2 = -a.lse[ri] * kLog2e;
-  const float del = a.delta[ri];
+  float del;
+  if (a.delta_w) {  // D of this lane's row: its half of d here, the other half in lane ^ 32
+    const uint16_t* orow = (const uint16_t*)a.o + b * a.o_sb + (int64_t)myq * a.o_ss + h * a.o_sh;
+    float part = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const bf16x8_t of = ld_row_frag(orow, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part += (float)dof[ks][j] * (float)of[j];
+    }
+    del = part + __shfl_xor(part, 32, 64);
+    if (lane < 32) a.delta_w[ri] = del;
+  } else {
+    del = a.delta[ri];
+  }
   const float c2 = a.scale * kLog2e;
 
   const uint16_t* kbase = a.k + b * a.k_sb + hk * a.k_sh;
@@ -642,6 +659,13 @@ int check_common(const AttnArgs& a, int D) {
   return PT_OK;
 }
 
+int attn_bwd_impl(const void* q, const int64_t* q_str, const void* k, const int64_t* k_str, const void* v,
+                  const int64_t* v_str, const void* dout, const int64_t* do_str, const float* lse,
+                  const float* delta, void* dq, const int64_t* dq_str, void* dk, const int64_t* dk_str, void* dv,
+                  const int64_t* dv_str, int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int64_t D,
+                  float scale, int causal, int grad_f32, const void* rope_cos, const void* rope_sin,
+                  int64_t rope_stride, const void* o, const int64_t* o_str, float* delta_w, hipStream_t stream);
+
 }  // namespace
 
 extern "C" {
@@ -699,7 +723,23 @@ int pt_attn_bwd(const void* q, const int64_t* q_str, const void* k, const int64_
                 void* dq, const int64_t* dq_str, void* dk, const int64_t* dk_str, void* dv, const int64_t* dv_str,
                 int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int64_t D, float scale, int causal,
                 int grad_f32, const void* rope_cos, const void* rope_sin, int64_t rope_stride, hipStream_t stream) {
-  if (!q || !k || !v || !dout || !lse || !delta || !dq || !dk || !dv) return PT_EINVAL;
+  if (!delta) return PT_EINVAL;
+  return attn_bwd_impl(q, q_str, k, k_str, v, v_str, dout, do_str, lse, delta, dq, dq_str, dk, dk_str, dv, dv_str,
+                       B, H, HKV, Sq, Sk, D, scale, causal, grad_f32, rope_cos, rope_sin, rope_stride, nullptr,
+                       nullptr, nullptr, stream);
+}
+
+}  // extern "C"
+
+namespace {
+
+int attn_bwd_impl(const void* q, const int64_t* q_str, const void* k, const int64_t* k_str, const void* v,
+                  const int64_t* v_str, const void* dout, const int64_t* do_str, const float* lse,
+                  const float* delta, void* dq, const int64_t* dq_str, void* dk, const int64_t* dk_str, void* dv,
+                  const int64_t* dv_str, int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int64_t D,
+                  float scale, int causal, int grad_f32, const void* rope_cos, const void* rope_sin,
+                  int64_t rope_stride, const void* o, const int64_t* o_str, float* delta_w, hipStream_t stream) {
+  if (!q || !k || !v || !dout || !lse || !dq || !dk || !dv) return PT_EINVAL;
   if (rope_cos && (!rope_sin || grad_f32 || Sq != Sk || (rope_stride & 3) || !pt_aligned16(rope_cos) ||
                    !pt_aligned16(rope_sin)))
     return PT_EINVAL;
@@ -715,6 +755,10 @@ int pt_attn_bwd(const void* q, const int64_t* q_str, const void* k, const int64_
   a.B = (int)B; a.H = (int)H; a.HKV = (int)HKV; a.Sq = (int)Sq; a.Sk = (int)Sk;
   a.scale = scale; a.causal = causal; a.grad_f32 = grad_f32;
   a.rope_cos = (const uint16_t*)rope_cos; a.rope_sin = (const uint16_t*)rope_sin; a.rope_ld = rope_stride;
+  if (delta_w) {
+    a.o = const_cast<void*>(o); a.o_sb = o_str[0]; a.o_ss = o_str[1]; a.o_sh = o_str[2];
+    a.delta_w = delta_w;
+  }
   int rc = check_common(a, (int)D);
   if (rc) return rc;
   if (Sk % (NW * 32)) return PT_EUNSUPPORTED;
@@ -724,21 +768,46 @@ int pt_attn_bwd(const void* q, const int64_t* q_str, const void* k, const int64_
   a.pair = causal && nqb % 2 == 0 && nkb % 2 == 0 && pair_enabled();
   const dim3 gq((unsigned)(a.pair ? nqb / 2 : nqb), (unsigned)H, (unsigned)B);
   const dim3 gk((unsigned)(a.pair ? nkb / 2 : nkb), (unsigned)HKV, (unsigned)B);
+  // dQ first: with delta_w set it produces the D the dK/dV kernel reads (same stream, in order)
   if (D == 64) {
     set_smem(attn_bwd_dkdv_kernel<64>, smem_q);
     set_smem(attn_bwd_dq_kernel<64>, smem_kv);
-    attn_bwd_dkdv_kernel<64><<<gk, NW * 64, smem_q, stream>>>(a);
-    PT_CHECK_LAUNCH();
     attn_bwd_dq_kernel<64><<<gq, NW * 64, smem_kv, stream>>>(a);
+    PT_CHECK_LAUNCH();
+    a.delta = a.delta_w ? a.delta_w : a.delta;
+    a.delta_w = nullptr;
+    attn_bwd_dkdv_kernel<64><<<gk, NW * 64, smem_q, stream>>>(a);
   } else {
     set_smem(attn_bwd_dkdv_kernel<128>, smem_q);
     set_smem(attn_bwd_dq_kernel<128>, smem_kv);
-    attn_bwd_dkdv_kernel<128><<<gk, NW * 64, smem_q, stream>>>(a);
-    PT_CHECK_LAUNCH();
     attn_bwd_dq_kernel<128><<<gq, NW * 64, smem_kv, stream>>>(a);
+    PT_CHECK_LAUNCH();
+    a.delta = a.delta_w ? a.delta_w : a.delta;
+    a.delta_w = nullptr;
+    attn_bwd_dkdv_kernel<128><<<gk, NW * 64, smem_q, stream>>>(a);
   }
   PT_CHECK_LAUNCH();
   return PT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// pt_attn_bwd with D = rowsum(dO * O) computed inside the dQ kernel from o (bf16, strides o_str)
+// and written to delta_out [B, H, Sq] f32 (replaces the separate pt_attn_bwd_delta pass)
+int pt_attn_bwd_fused_delta(const void* q, const int64_t* q_str, const void* k, const int64_t* k_str,
+                            const void* v, const int64_t* v_str, const void* o, const int64_t* o_str,
+                            const void* dout, const int64_t* do_str, const float* lse, float* delta_out, void* dq,
+                            const int64_t* dq_str, void* dk, const int64_t* dk_str, void* dv,
+                            const int64_t* dv_str, int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk,
+                            int64_t D, float scale, int causal, const void* rope_cos, const void* rope_sin,
+                            int64_t rope_stride, hipStream_t stream) {
+  if (!o || !delta_out || !o_str) return PT_EINVAL;
+  if (!pt_aligned16(o) || (o_str[0] & 7) || (o_str[1] & 7) || (o_str[2] & 7)) return PT_EALIGN;
+  return attn_bwd_impl(q, q_str, k, k_str, v, v_str, dout, do_str, lse, nullptr, dq, dq_str, dk, dk_str, dv,
+                       dv_str, B, H, HKV, Sq, Sk, D, scale, causal, 0, rope_cos, rope_sin, rope_stride, o, o_str,
+                       delta_out, stream);
 }
 
 }  // extern "C"

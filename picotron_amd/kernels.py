@@ -7,6 +7,8 @@ validates with asserts (e.g. picotron/model.py:95-96, tensor_parallel.py:81,151,
 """
 import math
 
+import os
+
 import torch
 
 from . import _C
@@ -523,7 +525,8 @@ def attn_bwd(dout, q, k, v, out, lse, scale, causal, dq=None, dk=None, dv=None, 
     B, Sq, H, D = q.shape
     Sk, HKV = k.shape[1], k.shape[2]
     lib = _C.lib()
-    if delta is None:
+    fuse_delta = delta is None and not grad_f32 and out.dtype == BF16 and os.environ.get("PICOTRON_FUSE_DELTA", "1") != "0"
+    if delta is None and not fuse_delta:
         delta = attn_delta(dout, out)
     gdt = torch.float32 if grad_f32 else BF16
     if dq is None:
@@ -540,6 +543,15 @@ def attn_bwd(dout, q, k, v, out, lse, scale, causal, dq=None, dk=None, dv=None, 
              "attn_bwd rope tables: bf16 [S, d]")
         _req(rc_sin.stride(0) == rc_cos.stride(0), "attn_bwd rope tables share a stride")
         rstride = rc_cos.stride(0)
+    if fuse_delta:   # D = rowsum(dO * O) inside the dQ kernel (no separate pass)
+        _req(out.shape == q.shape, "attn_bwd: out must be [B, Sq, H, D]")
+        delta = torch.empty(B, H, Sq, dtype=torch.float32, device=q.device)
+        rc = lib.pt_attn_bwd_fused_delta(_ptr(q), _str3(q), _ptr(k), _str3(k), _ptr(v), _str3(v), _ptr(out), _str3(out),
+                                         _ptr(dout), _str3(dout), _ptr(lse), _ptr(delta), _ptr(dq), _str3(dq), _ptr(dk),
+                                         _str3(dk), _ptr(dv), _str3(dv), B, H, HKV, Sq, Sk, D, float(scale),
+                                         int(bool(causal)), _ptr(rc_cos), _ptr(rc_sin), rstride, _C.stream_ptr())
+        _C.check(rc, "pt_attn_bwd_fused_delta")
+        return dq, dk, dv, delta
     rc = lib.pt_attn_bwd(_ptr(q), _str3(q), _ptr(k), _str3(k), _ptr(v), _str3(v), _ptr(dout), _str3(dout),
                          _ptr(lse), _ptr(delta), _ptr(dq), _str3(dq), _ptr(dk), _str3(dk), _ptr(dv), _str3(dv),
                          B, H, HKV, Sq, Sk, D, float(scale), int(bool(causal)), int(bool(grad_f32)),
