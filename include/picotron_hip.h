@@ -140,6 +140,17 @@ typedef struct {
 } pt_gemm_problem;
 int pt_gemm_grouped(const pt_gemm_problem* probs, int nprob, int a_kcontig, int b_kcontig, int epilogue, int tile,
                     hipStream_t stream);
+/* dX = dY . [W_0; W_1; ...] (the Column/RowParallelLinear backward input grads, tensor_parallel.py:
+ * 116-189 via F.linear's autograd) as split-K pairs on the 8-phase 256x256 kernel, for the shapes
+ * where 256x256 tiles alone would leave half the CUs idle (M x N = 4096 x 2048: 128 tiles -> 256
+ * workgroups).  A = dY [M, K] K-contiguous; B_i = W_i [K_i, N] (K-segments, multiples of 64, one
+ * shared ld); epilogue 0 bf16 store / 1 bf16 accumulate.  ws: f32 workspace of
+ * (M/256)(N/256) * 65536 floats; flags: (M/256)(N/256) int32, zeroed once by the caller and then
+ * owned by this function (the lower-K workgroup of each pair publishes its partial with an epoch
+ * flag; the upper one, dispatched later, waits for it and adds in a fixed order: deterministic). */
+int pt_gemm_dgrad_splitk(const void* A, int64_t lda, const void* const* B, const int64_t* ldb,
+                         const int64_t* b_bounds, int nb, void* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                         int epilogue, float* ws, int* flags, hipStream_t stream);
 
 /* ---- flash attention ----------------------------------------------------------------------
  * replaces model.py:33-37,154 flash_attn_func(causal=True) / model.py:157 SDPA, and the ring

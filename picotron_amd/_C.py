@@ -52,6 +52,8 @@ SIGNATURES = {
     "pt_attn_bwd_fused_delta": (_i32, [_vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _vp, _vp,
                                        _i64p, _vp, _i64p, _vp, _i64p, _i64, _i64, _i64, _i64, _i64, _i64, _f32,
                                        _i32, _vp, _vp, _i64, _vp]),
+    "pt_gemm_dgrad_splitk": (_i32, [_vp, _i64, _vpp, _i64p, _i64p, _i32, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp,
+                                    _vp]),
     "pt_gemm_rope": (_i32, [_vp, _i64, _vpp, _i64p, _i64p, _i32, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _i64,
                             _i64, _i64, _i32, _vp]),
 }

@@ -459,6 +459,34 @@ def linear_dgrad_swiglu(dy2d, wd, gu):
     return dgu
 
 
+_SPLITK_WS = {}
+
+
+def _splitk_buffers(device, tiles):
+    """Per-device split-K workspace (f32, 64 Ki floats per 256x256 tile) and epoch flags (zeroed
+    once; the library owns them afterwards)."""
+    key = (device.type, device.index)
+    ws, flags = _SPLITK_WS.get(key, (None, None))
+    if ws is None or ws.numel() < tiles * 65536:
+        ws = torch.empty(tiles * 65536, dtype=torch.float32, device=device)
+        if flags is None:
+            flags = torch.zeros(4096, dtype=torch.int32, device=device)
+        _SPLITK_WS[key] = (ws, flags)
+    return ws, flags
+
+
+def splitk_dgrad_fits(T, N, Kin, ns, weights):
+    """Shapes the split-K pairs tile: 256x256 tiles that fill at most one round of the 256 CUs as
+    pairs, each K half >= 32 K-tiles (q|k|v and gate|up dX, lm_head dX at SmolLM dims).  Opt-in
+    (PICOTRON_SPLITK=1): measured in-situ equal to the 4-phase 256x128 kernel (150.8k vs 151.1k
+    tok/s, same box), so the default stays on the kernel without a cross-workgroup wait."""
+    if os.environ.get("PICOTRON_SPLITK", "0") != "1":
+        return False
+    tiles = (T // 256) * (Kin // 256)
+    return (T % 256 == 0 and Kin % 256 == 0 and tiles % 8 == 0 and 2 * tiles <= 256 and N >= 4096
+            and N % 128 == 0 and all(n % 64 == 0 for n in ns) and all(w.stride(0) == Kin for w in weights))
+
+
 def linear_dgrad(dy2d, weights, out=None, accumulate=False, tile=-1):
     """dX = dY . [W_0; W_1; ...]  where dY = [dY_0 | dY_1 | ...] is [T, sum N_i]."""
     _bf16_rowmajor(dy2d, "dy")
@@ -467,6 +495,17 @@ def linear_dgrad(dy2d, weights, out=None, accumulate=False, tile=-1):
     ns = [w.shape[0] for w in weights]
     _req(sum(ns) == N, "dgrad: dY width must equal the stacked weight rows")
     dx = out if out is not None else torch.empty(T, Kin, dtype=BF16, device=dy2d.device)
+    if tile == -1 and _PROBE is None and splitk_dgrad_fits(T, N, Kin, ns, weights):
+        _bf16_rowmajor(dx, "dx")
+        for w in weights:
+            _req(w.dtype == BF16 and w.is_contiguous() and w.shape[1] == Kin, "weight must be contiguous [N_i, Kin] bf16")
+        ws, flags = _splitk_buffers(dy2d.device, (T // 256) * (Kin // 256))
+        rc = _C.lib().pt_gemm_dgrad_splitk(_ptr(dy2d), dy2d.stride(0), _C.ptrarr([_ptr(w) for w in weights]),
+                                           _C.i64arr([Kin] * len(weights)), _C.i64arr(_bounds(ns)), len(weights),
+                                           _ptr(dx), dx.stride(0), T, Kin, N, EPI_BF16_ACC if accumulate else EPI_BF16,
+                                           _ptr(ws), _ptr(flags), _C.stream_ptr())
+        _C.check(rc, "pt_gemm_dgrad_splitk")
+        return dx
     _gemm(dy2d, dy2d.stride(0), 1, weights, [Kin] * len(weights), _bounds(ns), 0, 1, [dx], [dx.stride(0)],
           [0, T], T, Kin, N, EPI_BF16_ACC if accumulate else EPI_BF16, tile)
     return dx
