@@ -535,18 +535,15 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
   }
   const int64_t ri = ((int64_t)b * a.H + h) * a.Sq + myq;
   const float nlse2 = -a.lse[ri] * kLog2e;
-  float del;
-  if (a.delta_w) {  // D of this lane's row: its half of d here, the other half in lane ^ 32
+  // D of this lane's row (a.delta_w: computed here from O; its half of d in this lane, the other
+  // half in lane ^ 32).  The O loads are issued now and consumed after the first K/V tile's DMA
+  // has been queued, so the two latencies overlap.
+  bf16x8_t of[KS];
+  float del = 0.f;
+  if (a.delta_w) {
     const uint16_t* orow = (const uint16_t*)a.o + b * a.o_sb + (int64_t)myq * a.o_ss + h * a.o_sh;
-    float part = 0.f;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const bf16x8_t of = ld_row_frag(orow, ks, lane);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) part += (float)dof[ks][j] * (float)of[j];
-    }
-    del = part + __shfl_xor(part, 32, 64);
-    if (lane < 32) a.delta_w[ri] = del;
+    for (int ks = 0; ks < KS; ++ks) of[ks] = ld_row_frag(orow, ks, lane);
   } else {
     del = a.delta[ri];
   }
@@ -567,6 +564,15 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
   };
   stage(0, 0);
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler: its own fragment loads are done
+  if (a.delta_w) {
+    float part = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part += (float)dof[ks][j] * (float)of[ks][j];
+    del = part + __shfl_xor(part, 32, 64);
+    if (lane < 32) a.delta_w[ri] = del;
+  }
   __syncthreads();
 
   for (int kt = 0; kt < nkt; ++kt) {
