@@ -206,7 +206,8 @@ def cross_entropy_loss_lse(logits, targets, ignore_index=-100):
     rows, vocab = logits.shape
     _req(targets.dtype == torch.int64 and targets.numel() == rows, "targets: int64 [rows]")
     targets = targets.contiguous()
-    inv_count = (1.0 / (targets != ignore_index).sum().clamp_min(1).to(torch.float32)).reshape(1)
+    # no clamp: every target ignored gives 0 * inf = nan, as F.cross_entropy's mean does (grads 0)
+    inv_count = (1.0 / (targets != ignore_index).sum().to(torch.float32)).reshape(1)
     row_loss = torch.empty(rows, dtype=torch.float32, device=logits.device)
     row_lse = torch.empty(rows, dtype=torch.float32, device=logits.device)
     rc = _C.lib().pt_cross_entropy_fwd_lse(_ptr(logits), logits.stride(0), _ptr(targets), _ptr(row_loss),

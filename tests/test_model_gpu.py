@@ -293,3 +293,38 @@ def test_loss_curve_50_steps_matches_oracle(monkeypatch):
     dev_rel = [abs(a - b) / abs(b) for a, b in zip(ours, theirs)]
     assert theirs[-1] < theirs[0] - 0.5, theirs          # the curve actually moves
     assert max(dev_rel) < 1e-2, (max(dev_rel), ours[::10], theirs[::10])
+
+
+def test_cross_entropy_edge_cases_match_torch():
+    """F.cross_entropy's edge cases through the autograd pair: every target ignored (mean = nan,
+    grads 0, as torch), a single row, and a vocabulary that is not a multiple of the 256-thread
+    row stride (ragged last chunk)."""
+    from picotron_amd import functional as FN
+    for T, V, ignore_all in ((8, 96, True), (1, 49152, False), (16, 1000, False)):
+        logits = (2 * torch.randn(T, V)).to(BF)
+        tgt = torch.full((T,), -100) if ignore_all else torch.randint(0, V, (T,))
+        lg = logits.cuda().requires_grad_(True)
+        loss = FN.cross_entropy(lg, tgt.cuda())
+        loss.backward()
+        lr = logits.float().requires_grad_(True)
+        loss_r = F.cross_entropy(lr, tgt)
+        loss_r.backward()
+        if ignore_all:
+            assert math.isnan(loss.float().item()) and math.isnan(loss_r.item())
+            assert lg.grad.float().abs().max().item() == 0.0 and lr.grad.abs().max().item() == 0.0
+        else:
+            assert abs(loss.float().item() - loss_r.item()) < 1e-2 * abs(loss_r.item())
+            assert rel(lg.grad, lr.grad) < TOL
+
+
+def test_unsupported_shapes_fail_loudly():
+    """Shapes outside the kernels' tiling raise HipKernelError / ValueError -- never a silent
+    fallback (S % 128 for the flash kernels, head_dim 64 / 128)."""
+    from picotron_amd import kernels as K
+    from picotron_amd._C import HipKernelError
+    q = torch.randn(1, 100, 2, 64, device="cuda").to(BF)
+    with pytest.raises((HipKernelError, ValueError)):
+        K.attn_fwd(q, q, q, 0.125, True)
+    q = torch.randn(1, 128, 2, 32, device="cuda").to(BF)
+    with pytest.raises((HipKernelError, ValueError)):
+        K.attn_fwd(q, q, q, 0.125, True)
