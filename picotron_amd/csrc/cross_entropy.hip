@@ -154,6 +154,7 @@ __global__ __launch_bounds__(kThreads) void ce_kernel_2pass(const uint16_t* __re
 // register-resident ce_kernel above caps occupancy at ~4 waves per SIMD for V = 49152).
 // bwd: purely elementwise  dl = (exp(x - lse_row) - onehot) * g,  4 chunks in flight per thread.
 constexpr int kUnroll = 4;
+constexpr float kLog2e = 1.4426950408889634f;
 
 __global__ __launch_bounds__(kThreads) void ce_fwd_stream_kernel(const uint16_t* __restrict__ logits, int64_t ls,
                                                                  const int64_t* __restrict__ tgt,
@@ -185,13 +186,15 @@ __global__ __launch_bounds__(kThreads) void ce_fwd_stream_kernel(const uint16_t*
       }
     }
     if (cm == -INFINITY) continue;  // nothing finite seen yet
-    s *= __expf(m - cm);
+    // base-2 domain: exp(x - cm) = exp2(x log2e - cm log2e), one fma + one v_exp per logit
+    const float ncl = -cm * kLog2e;
+    s *= __builtin_amdgcn_exp2f(fmaf(m, kLog2e, ncl));
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const int c = c0 + u * kThreads;
       if (c < nch) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s += __expf(f[u][j] - cm);
+        for (int j = 0; j < 8; ++j) s += __builtin_amdgcn_exp2f(fmaf(f[u][j], kLog2e, ncl));
       }
     }
     m = cm;
