@@ -233,7 +233,7 @@ __global__ __launch_bounds__(kThreads) void ce_bwd_stream_kernel(const uint16_t*
   uint16_t* d = dl + row * ds;
   const int nch = V >> 3;
   const int64_t t = tgt[row];
-  const float lse = row_lse[row];
+  const float nl2 = -row_lse[row] * kLog2e;   // exp(x - lse) = exp2(x log2e - lse log2e)
   const float g = t != ignore_index ? *scale_dev : 0.f;
   for (int c0 = threadIdx.x; c0 < nch; c0 += kThreads * kUnroll) {
     bf16x8 v[kUnroll];
@@ -249,7 +249,8 @@ __global__ __launch_bounds__(kThreads) void ce_bwd_stream_kernel(const uint16_t*
         float f[8];
         unpack8(v[u], f);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = (__expf(f[j] - lse) - ((int64_t)(c * 8 + j) == t ? 1.f : 0.f)) * g;
+        for (int j = 0; j < 8; ++j)
+          f[j] = (__builtin_amdgcn_exp2f(fmaf(f[j], kLog2e, nl2)) - ((int64_t)(c * 8 + j) == t ? 1.f : 0.f)) * g;
         st8(d + c * 8, pack8(f));
       }
     }
