@@ -24,6 +24,11 @@ typedef struct ihipStream_t* hipStream_t;
 #define PT_EALIGN (-2)
 #define PT_EUNSUPPORTED (-3)
 
+/* Device status word (int32, caller-owned, zeroed by the caller): kernels that validate DATA (not
+ * shapes) set a bit here instead of trapping -- the analogue of torch's device-side assert.  The
+ * host reads it when it synchronises anyway (picotron_amd.kernels.device_status). */
+#define PT_STATUS_BAD_TARGET 1
+
 /* ---- RMSNorm ------------------------------------------------------------------------------
  * replaces picotron/model.py:51-65 (TritonRMSNorm -> flash-attn layer_norm_fn, mode 0) and
  * picotron/model.py:81-86 (LlamaRMSNorm, mode 1); `residual` fuses the bf16 residual add of
@@ -62,17 +67,19 @@ int pt_swiglu_bwd(const void* dh, int64_t dh_stride, const void* g, int64_t g_st
 /* ---- fused cross-entropy forward + backward -----------------------------------------------
  * replaces train.py:49 F.cross_entropy(logits, targets, 'mean') / grad_acc (+ autograd bwd) and
  * pipeline_parallel.py:103,153.  row_loss[r] = lse - logit[target]; dlogits (may alias logits) =
- * (softmax - onehot) * scale * (*inv_count if non-NULL).  targets int64, ignore_index rows -> 0.
- * dlogits == NULL: loss only (one read of the logits; the autograd forward). */
+ * (softmax - onehot) * scale * (*inv_count if non-NULL).  targets int64, ignore_index rows -> 0;
+ * a target outside [0, vocab) (not ignore_index) gives a NaN row and sets PT_STATUS_BAD_TARGET in
+ * *status (may be NULL).  dlogits == NULL: loss only (one read of the logits). */
 int pt_cross_entropy_fwd_bwd(const void* logits, int64_t logits_stride, const int64_t* targets, void* dlogits,
                              int64_t dlogits_stride, float* row_loss, int64_t rows, int64_t vocab, float scale,
-                             const float* inv_count, int64_t ignore_index, hipStream_t stream);
+                             const float* inv_count, int64_t ignore_index, int* status, hipStream_t stream);
 /* The autograd pair (train.py:49 forward, loss.backward() at train.py:51): the forward streams the
  * logits once with an online max / sum-exp and writes row_loss and row_lse [rows] f32; the
  * backward is elementwise from the saved LSE: dlogits = (exp(x - row_lse) - onehot) * (*scale)
  * (a device scalar: grad_output / #valid), ignore_index rows -> 0.  dlogits may alias logits. */
 int pt_cross_entropy_fwd_lse(const void* logits, int64_t logits_stride, const int64_t* targets, float* row_loss,
-                             float* row_lse, int64_t rows, int64_t vocab, int64_t ignore_index, hipStream_t stream);
+                             float* row_lse, int64_t rows, int64_t vocab, int64_t ignore_index, int* status,
+                             hipStream_t stream);
 int pt_cross_entropy_bwd_lse(const void* logits, int64_t logits_stride, const int64_t* targets, const float* row_lse,
                              void* dlogits, int64_t dlogits_stride, int64_t rows, int64_t vocab, const float* scale,
                              int64_t ignore_index, hipStream_t stream);
@@ -140,17 +147,16 @@ typedef struct {
 } pt_gemm_problem;
 int pt_gemm_grouped(const pt_gemm_problem* probs, int nprob, int a_kcontig, int b_kcontig, int epilogue, int tile,
                     hipStream_t stream);
-/* dX = dY . [W_0; W_1; ...] (the Column/RowParallelLinear backward input grads, tensor_parallel.py:
- * 116-189 via F.linear's autograd) as split-K pairs on the 8-phase 256x256 kernel, for the shapes
- * where 256x256 tiles alone would leave half the CUs idle (M x N = 4096 x 2048: 128 tiles -> 256
- * workgroups).  A = dY [M, K] K-contiguous; B_i = W_i [K_i, N] (K-segments, multiples of 64, one
- * shared ld); epilogue 0 bf16 store / 1 bf16 accumulate.  ws: f32 workspace of
- * (M/256)(N/256) * 65536 floats; flags: (M/256)(N/256) int32, zeroed once by the caller and then
- * owned by this function (the lower-K workgroup of each pair publishes its partial with an epoch
- * flag; the upper one, dispatched later, waits for it and adds in a fixed order: deterministic). */
-int pt_gemm_dgrad_splitk(const void* A, int64_t lda, const void* const* B, const int64_t* ldb,
-                         const int64_t* b_bounds, int nb, void* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
-                         int epilogue, float* ws, int* flags, hipStream_t stream);
+
+/* ---- ring-attention merge ------------------------------------------------------------------
+ * replaces picotron/context_parallel/context_parallel.py:157-187 update_out_and_lse (its non-first
+ * call): out_new = out - sigmoid(blse - lse) * (out - block_out), lse_new = lse - logsigmoid(lse -
+ * blse).  out / out_new f32 [rows, D]; block_out [rows, D] (dtype 0 bf16, 1 f32); lse, block_lse,
+ * lse_new [rows] in lse_dtype (0 bf16: every lse-side op rounded to bf16 as the reference's bf16
+ * ring does; 1 f32).  All contiguous; rows = B * H * S.  (The ring's own merge is fused into
+ * pt_attn_fwd's merge mode.) */
+int pt_lse_merge(const float* out, const void* block_out, int block_out_dtype, const void* lse, const void* block_lse,
+                 int lse_dtype, float* out_new, void* lse_new, int64_t rows, int64_t D, hipStream_t stream);
 
 /* ---- flash attention ----------------------------------------------------------------------
  * replaces model.py:33-37,154 flash_attn_func(causal=True) / model.py:157 SDPA, and the ring

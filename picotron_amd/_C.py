@@ -38,8 +38,8 @@ SIGNATURES = {
     "pt_rope": (_i32, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _i32, _vp]),
     "pt_swiglu_fwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp]),
     "pt_swiglu_bwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp]),
-    "pt_cross_entropy_fwd_bwd": (_i32, [_vp, _i64, _vp, _vp, _i64, _vp, _i64, _i64, _f32, _vp, _i64, _vp]),
-    "pt_cross_entropy_fwd_lse": (_i32, [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _vp]),
+    "pt_cross_entropy_fwd_bwd": (_i32, [_vp, _i64, _vp, _vp, _i64, _vp, _i64, _i64, _f32, _vp, _i64, _vp, _vp]),
+    "pt_cross_entropy_fwd_lse": (_i32, [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp]),
     "pt_cross_entropy_bwd_lse": (_i32, [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp]),
     "pt_gemm": (_i32, [_vp, _i64, _i32, _vpp, _i64p, _i64p, _i32, _i32, _i32, _vpp, _i64p, _i64p, _i32,
                        _i64, _i64, _i64, _i32, _vp, _i64, _i32, _vp]),
@@ -52,8 +52,7 @@ SIGNATURES = {
     "pt_attn_bwd_fused_delta": (_i32, [_vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _vp, _vp,
                                        _i64p, _vp, _i64p, _vp, _i64p, _i64, _i64, _i64, _i64, _i64, _i64, _f32,
                                        _i32, _vp, _vp, _i64, _vp]),
-    "pt_gemm_dgrad_splitk": (_i32, [_vp, _i64, _vpp, _i64p, _i64p, _i32, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp,
-                                    _vp]),
+    "pt_lse_merge": (_i32, [_vp, _vp, _i32, _vp, _vp, _i32, _vp, _vp, _i64, _i64, _vp]),
     "pt_gemm_rope": (_i32, [_vp, _i64, _vpp, _i64p, _i64p, _i32, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _i64,
                             _i64, _i64, _i32, _vp]),
 }
@@ -101,6 +100,12 @@ def check(rc, name):
 
 
 def stream_ptr(device=None):
+    """torch's current stream on `device` (a tensor's device).  Kernels launch on the calling
+    thread's current HIP device, so a tensor on another device is refused rather than handed to a
+    kernel on the wrong GPU with foreign pointers."""
+    if device is not None and getattr(device, "index", None) is not None and device.index != torch.cuda.current_device():
+        raise HipKernelError(f"tensor on {device} but the current HIP device is cuda:{torch.cuda.current_device()}: "
+                             f"call torch.cuda.set_device({device.index}) (train.py does) or use torch.cuda.device()")
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 

@@ -178,6 +178,27 @@ def ring_attention_forward(q, k, v, sm_scale, is_causal):
     return o.transpose(1, 2), lse
 
 
+def update_out_and_lse(out, lse, block_out, block_lse, slice_=None):
+    """context_parallel.py:157-187, same signature and contract: block_out -> fp32, block_lse
+    unsqueezed to [..., 1]; the first call (out None) returns them; later calls merge
+        out <- out - sigmoid(block_lse - lse) * (out - block_out)
+        lse <- lse - logsigmoid(lse - block_lse)
+    on the HIP merge kernel (pt_lse_merge), with lse kept in the block LSE's dtype (bf16 in a bf16
+    ring, rounded op by op as torch does).  Returns new tensors; with slice_ the merge writes
+    out[slice_] / lse[slice_] in place, as the reference does."""
+    block_out = block_out.to(torch.float32)
+    block_lse = block_lse.unsqueeze(dim=-1)
+    if out is None:
+        if slice_ is not None:
+            raise RuntimeError("first update_out_and_lse should not pass slice_ args")
+        return block_out, block_lse
+    if slice_ is not None:
+        o_new, l_new = K.lse_merge(out[slice_], block_out, lse[slice_], block_lse)   # the block is the slice's
+        out[slice_], lse[slice_] = o_new, l_new
+        return out, lse
+    return K.lse_merge(out, block_out, lse, block_lse)
+
+
 def ring_attention_backward(dO, Q, K_, V, O, softmax_lse, sm_scale, is_causal):
     """context_parallel.py:130-155: one block's (dQ, dK, dV) from the global O / LSE, [B, H, S, D]."""
     do = dO.transpose(1, 2)

@@ -10,6 +10,11 @@
 // host never synchronises).  dlogits may alias logits (in place: the logits are dead after the
 // loss, which saves a 384 MiB buffer at SmolLM-1.7B mbs4 seq1024).
 //
+// Targets are range-checked: a target outside [0, V) that is not ignore_index gives a NaN row loss
+// (and, through the saved NaN LSE, a NaN gradient row), never an out-of-bounds read, and sets bit
+// PT_STATUS_BAD_TARGET of *status (when given) -- torch's device-side assert, made observable
+// without a trap (kernels.device_status / functional.check_device_status read it).
+//
 // One 256-thread workgroup per row; the row is held in registers (NC 16-byte chunks per
 // thread) so HBM sees exactly one read and one write of the logits: 4*V bytes per row, the
 // roofline figure in DESIGN.md.  Rows longer than 256*8*32 elements take the two-pass variant.
@@ -36,15 +41,17 @@ __global__ __launch_bounds__(kThreads) void ce_kernel(const uint16_t* __restrict
                                                       const int64_t* __restrict__ tgt, uint16_t* dlogits,
                                                       int64_t ds, float* __restrict__ row_loss, int V,
                                                       float scale, const float* __restrict__ inv_count,
-                                                      int64_t ignore_index) {
+                                                      int64_t ignore_index, int* __restrict__ status) {
   __shared__ float red[kThreads / 64];
   const int64_t row = blockIdx.x;
   const uint16_t* x = logits + row * ls;
   const int nch = V >> 3;
   const int64_t t = tgt[row];
   const bool valid = t != ignore_index;
+  const bool bad = valid && (t < 0 || t >= V);
   // read the target logit before any barrier: later writes may overwrite x in place
-  const float xt = (threadIdx.x == 0 && valid) ? bf2f(x[t]) : 0.f;
+  const float xt = (threadIdx.x == 0 && valid && !bad) ? bf2f(x[t]) : 0.f;
+  if (bad && threadIdx.x == 0 && status) status[0] = PT_STATUS_BAD_TARGET;
   bf16x8 v[NC];
   float mx = -INFINITY;
 #pragma unroll
@@ -71,7 +78,7 @@ __global__ __launch_bounds__(kThreads) void ce_kernel(const uint16_t* __restrict
     }
   }
   se = block_reduce(se, red, false);
-  const float lse = mx + __logf(se);
+  const float lse = bad ? __builtin_nanf("") : mx + __logf(se);
   const float g = valid ? scale * (inv_count ? *inv_count : 1.0f) : 0.f;
   if (threadIdx.x == 0) row_loss[row] = valid ? lse - xt : 0.f;
   if (!dlogits) return;  // loss-only (forward) launch
@@ -97,7 +104,7 @@ __global__ __launch_bounds__(kThreads) void ce_kernel_2pass(const uint16_t* __re
                                                             const int64_t* __restrict__ tgt, uint16_t* dlogits,
                                                             int64_t ds, float* __restrict__ row_loss, int V,
                                                             float scale, const float* __restrict__ inv_count,
-                                                            int64_t ignore_index) {
+                                                            int64_t ignore_index, int* __restrict__ status) {
   __shared__ float red[kThreads / 64];
   __shared__ float red2[kThreads / 64];
   const int64_t row = blockIdx.x;
@@ -130,11 +137,13 @@ __global__ __launch_bounds__(kThreads) void ce_kernel_2pass(const uint16_t* __re
   for (int i = 1; i < kThreads / 64; ++i) M = fmaxf(M, red[i]);
   float S = 0.f;
   for (int i = 0; i < kThreads / 64; ++i) S += red2[i] * __expf(red[i] - M);
-  const float lse = M + __logf(S);
   const int64_t t = tgt[row];
   const bool valid = t != ignore_index;
+  const bool bad = valid && (t < 0 || t >= V);
+  const float lse = bad ? __builtin_nanf("") : M + __logf(S);
   const float g = valid ? scale * (inv_count ? *inv_count : 1.0f) : 0.f;
-  if (threadIdx.x == 0) row_loss[row] = valid ? lse - bf2f(x[t]) : 0.f;
+  if (threadIdx.x == 0) row_loss[row] = valid ? lse - (bad ? 0.f : bf2f(x[t])) : 0.f;
+  if (bad && threadIdx.x == 0 && status) status[0] = PT_STATUS_BAD_TARGET;
   __syncthreads();  // x[t] read before any in-place write
   if (!dlogits) return;
   uint16_t* d = dlogits + row * ds;
@@ -160,7 +169,7 @@ __global__ __launch_bounds__(kThreads) void ce_fwd_stream_kernel(const uint16_t*
                                                                  const int64_t* __restrict__ tgt,
                                                                  float* __restrict__ row_loss,
                                                                  float* __restrict__ row_lse, int V,
-                                                                 int64_t ignore_index) {
+                                                                 int64_t ignore_index, int* __restrict__ status) {
   __shared__ float red[kThreads / 64];
   __shared__ float red2[kThreads / 64];
   const int64_t row = blockIdx.x;
@@ -214,11 +223,13 @@ __global__ __launch_bounds__(kThreads) void ce_fwd_stream_kernel(const uint16_t*
     for (int i = 1; i < kThreads / 64; ++i) M = fmaxf(M, red[i]);
     float S = 0.f;
     for (int i = 0; i < kThreads / 64; ++i) S += red2[i] * __expf(red[i] - M);
-    const float lse = M + __logf(S);
     const int64_t t = tgt[row];
     const bool valid = t != ignore_index;
+    const bool bad = valid && (t < 0 || t >= V);
+    const float lse = bad ? __builtin_nanf("") : M + __logf(S);
     row_lse[row] = lse;
-    row_loss[row] = valid ? lse - bf2f(x[t]) : 0.f;
+    row_loss[row] = valid ? lse - (bad ? 0.f : bf2f(x[t])) : 0.f;
+    if (bad && status) status[0] = PT_STATUS_BAD_TARGET;
   }
 }
 
@@ -261,12 +272,12 @@ __global__ __launch_bounds__(kThreads) void ce_bwd_stream_kernel(const uint16_t*
 
 extern "C" int pt_cross_entropy_fwd_lse(const void* logits, int64_t logits_stride, const int64_t* targets,
                                         float* row_loss, float* row_lse, int64_t rows, int64_t vocab,
-                                        int64_t ignore_index, hipStream_t stream) {
+                                        int64_t ignore_index, int* status, hipStream_t stream) {
   if (!logits || !targets || !row_loss || !row_lse || rows <= 0 || vocab <= 0) return PT_EINVAL;
   if ((vocab & 7) || (logits_stride & 7) || !pt_aligned16(logits)) return PT_EALIGN;
   if (rows > INT32_MAX || vocab > INT32_MAX) return PT_EUNSUPPORTED;
   ce_fwd_stream_kernel<<<(unsigned)rows, kThreads, 0, stream>>>((const uint16_t*)logits, logits_stride, targets,
-                                                               row_loss, row_lse, (int)vocab, ignore_index);
+                                                               row_loss, row_lse, (int)vocab, ignore_index, status);
   PT_CHECK_LAUNCH();
   return PT_OK;
 }
@@ -289,7 +300,7 @@ extern "C" int pt_cross_entropy_bwd_lse(const void* logits, int64_t logits_strid
 extern "C" int pt_cross_entropy_fwd_bwd(const void* logits, int64_t logits_stride, const int64_t* targets,
                                         void* dlogits, int64_t dlogits_stride, float* row_loss, int64_t rows,
                                         int64_t vocab, float scale, const float* inv_count, int64_t ignore_index,
-                                        hipStream_t stream) {
+                                        int* status, hipStream_t stream) {
   if (!logits || !targets || !row_loss || rows <= 0 || vocab <= 0) return PT_EINVAL;
   if ((vocab & 7) || (logits_stride & 7) || (dlogits && (dlogits_stride & 7))) return PT_EALIGN;
   if (!pt_aligned16(logits) || (dlogits && !pt_aligned16(dlogits))) return PT_EALIGN;
@@ -297,14 +308,14 @@ extern "C" int pt_cross_entropy_fwd_bwd(const void* logits, int64_t logits_strid
   auto* D = (uint16_t*)dlogits;
   const int nc = (int)((vocab / 8 + kThreads - 1) / kThreads);
   const dim3 grid((unsigned)rows);
-#define PT_CE(N) ce_kernel<N><<<grid, kThreads, 0, stream>>>(L, logits_stride, targets, D, dlogits_stride, row_loss, (int)vocab, scale, inv_count, ignore_index)
+#define PT_CE(N) ce_kernel<N><<<grid, kThreads, 0, stream>>>(L, logits_stride, targets, D, dlogits_stride, row_loss, (int)vocab, scale, inv_count, ignore_index, status)
   if (nc <= 4) PT_CE(4);
   else if (nc <= 8) PT_CE(8);
   else if (nc <= 16) PT_CE(16);
   else if (nc <= 24) PT_CE(24);
   else if (nc <= 32) PT_CE(32);
   else ce_kernel_2pass<<<grid, kThreads, 0, stream>>>(L, logits_stride, targets, D, dlogits_stride, row_loss,
-                                                      (int)vocab, scale, inv_count, ignore_index);
+                                                      (int)vocab, scale, inv_count, ignore_index, status);
 #undef PT_CE
   PT_CHECK_LAUNCH();
   return PT_OK;

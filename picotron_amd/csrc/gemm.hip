@@ -82,13 +82,6 @@ struct GemmArgs {
   int M, N, K;
   int tiles_m, tiles_n;
   int group_m;
-  // split-K pair (8-phase kernel, one problem): workgroups [0, G/2) compute K-tiles [0, nk/2) of
-  // tile i and hand their f32 accumulators over through ws; workgroups [G/2, G) compute the upper
-  // half, wait for the flag of their lower-indexed partner (dispatched first), add, run the epilogue
-  float* ws;
-  int* flags;
-  int epoch;
-  int splitk;
 };
 
 // swizzles (chunk = 16 bytes); see tools/lds_swizzle_search.py
@@ -495,7 +488,7 @@ __device__ __forceinline__ void glds16_asm(const uint16_t* base, uint32_t voff_e
   pt_glds16(base, voff_elems * 2u, (__attribute__((address_space(3))) void*)dst);  // common.h
 }
 
-template <bool AK, bool BKC, int EPI, bool SPLIT = false>
+template <bool AK, bool BKC, int EPI>
 __global__ __launch_bounds__(512) void gemm_8ph_kernel(const GemmGroup g) {
   constexpr int NT = 512, TM = 128, TN = 64, FM = 8, FN = 4;
   constexpr int HALF = 128 * BK * 2;          // 16 KiB
@@ -506,12 +499,7 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const GemmGroup g) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   int tile_m, tile_n;
-  // split-K pair: workgroup b and b + G/2 share a tile (and an XCD: G/2 % 8 == 0, host-checked)
-  constexpr bool split = SPLIT;  // a separate instantiation: the plain kernel keeps its registers
-  const int half_g = (int)gridDim.x >> 1;
-  const int upper = split && (int)blockIdx.x >= half_g;
-  const GemmArgs& a = split ? select_problem(g, tile_m, tile_n, (int)blockIdx.x - upper * half_g, half_g)
-                            : select_problem(g, tile_m, tile_n);
+  const GemmArgs& a = select_problem(g, tile_m, tile_n);
   const int m0 = tile_m * 256, n0 = tile_n * 256;
 
   // B segment for this tile (N-segments) or the first K-segment; ld is per tile (host checks
@@ -536,11 +524,9 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const GemmGroup g) {
       vB[1][it] = himg_voff<BKC, 32>(i, lane, ldb, 32);
     }
   }
-  const int nk_all = a.K / BK;
-  const int kt0 = split && upper ? nk_all / 2 : 0;   // this workgroup's first (absolute) K-tile
   const uint16_t* Ab0 = AK ? a.A + (int64_t)m0 * lda : a.A + m0;
-  auto a_ptr = [&](int t) { return AK ? Ab0 + (t + kt0) * BK : Ab0 + (int64_t)(t + kt0) * BK * lda; };
-  auto b_ptr = [&](int t) { return bimg_ptr(bi, BKC, (t + kt0) * BK); };
+  auto a_ptr = [&](int t) { return AK ? Ab0 + t * BK : Ab0 + (int64_t)t * BK * lda; };
+  auto b_ptr = [&](int t) { return bimg_ptr(bi, BKC, t * BK); };
   // paired: rows tile_n * 128 .. +127 of W_gate (Bl) and W_up (Br), K-contiguous
   auto pair_ptr = [&](int t, int which) {
     return (which ? pairB1 : pairB0) + (int64_t)tile_n * 128 * ldb + t * BK;
@@ -564,7 +550,7 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const GemmGroup g) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = split ? (upper ? nk_all - nk_all / 2 : nk_all / 2) : nk_all;
+  const int nk = a.K / BK;
   stage(0, 0, 0); stage(0, 0, 1); stage(0, 0, 2); stage(0, 0, 3);
   if (nk > 1) {
     stage(1, 1, 0); stage(1, 1, 1); stage(1, 1, 2);
@@ -655,39 +641,6 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const GemmGroup g) {
   if (t < nk) ktile(t, std::integral_constant<int, 0>{});
   if (!late) bar();  // balance the barrier count of the two wave groups
   __syncthreads();
-  if constexpr (!PAIR) {
-    if constexpr (split) {  // hand-over in register order: thread tid's FM x FN f32x4, fully coalesced
-      const int tile_id = tile_m * a.tiles_n + tile_n;
-      f32x4_t* ws = (f32x4_t*)a.ws + (int64_t)tile_id * (FM * FN) * NT;
-      int* flag = a.flags + tile_id;
-      if (!upper) {
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j) ws[(i * FN + j) * NT + tid] = acc[i][j];
-        // the pair shares an XCD and so its L2 (the vector L1 is write-through): waiting for this
-        // workgroup's stores to be acknowledged is enough -- no L2 write-back / invalidate
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __syncthreads();
-        if (tid == 0) __hip_atomic_store(flag, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-      }
-      if (tid == 0) {  // bounded wait: the partner was dispatched first, so it is running or done
-        int spins = 0;
-        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.epoch && ++spins < (1 << 22))
-          __builtin_amdgcn_s_sleep(8);
-      }
-      __syncthreads();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const f32x4_t lo = ws[(i * FN + j) * NT + tid];
-          acc[i][j] = lo + acc[i][j];   // lower K half + upper K half, fixed order
-        }
-    }
-  }
   if constexpr (PAIR) {
     epilogue_swiglu_fwd(a, acc, smem + wave * (TM * (32 * 2 + 16)), m0 + wm * TM, tile_n * 128 + wn * 32, lane);
   } else {
@@ -977,7 +930,7 @@ int launch_t(GemmGroup g, hipStream_t stream) {
   return PT_OK;
 }
 
-template <bool AK, bool BKC, int EPI, bool SPLIT = false>
+template <bool AK, bool BKC, int EPI>
 int launch_8ph(GemmGroup g, hipStream_t stream) {
   const int tiles = group_tiles(g, 256, EPI == EPI_SWIGLU_FWD ? 128 : 256);
   constexpr int smem_main = 8 * 128 * BK * 2;
@@ -986,10 +939,10 @@ int launch_8ph(GemmGroup g, hipStream_t stream) {
   static_assert(smem <= 160 * 1024, "LDS budget");
   static bool attr_set = false;
   if (!attr_set) {
-    set_smem_once(gemm_8ph_kernel<AK, BKC, EPI, SPLIT>, smem);
+    set_smem_once(gemm_8ph_kernel<AK, BKC, EPI>, smem);
     attr_set = true;
   }
-  gemm_8ph_kernel<AK, BKC, EPI, SPLIT><<<SPLIT ? 2 * tiles : tiles, 512, smem, stream>>>(g);
+  gemm_8ph_kernel<AK, BKC, EPI><<<tiles, 512, smem, stream>>>(g);
   PT_CHECK_LAUNCH();
   return PT_OK;
 }
@@ -1234,36 +1187,6 @@ int pt_gemm_grouped(const pt_gemm_problem* probs, int nprob, int a_kcontig, int 
     if (rc) return rc;
   }
   return launch_group(g, a_kcontig, b_kcontig, epilogue, tile, stream);
-}
-
-// dX = dY . [W_0; ...] (A K-contiguous [M, K], B stored [K, N] with K-segments, epilogue bf16
-// store or accumulate) as split-K pairs on the 8-phase 256x256 kernel: 2 x (M/256)(N/256)
-// workgroups, each pair computing one tile's two K halves (see GemmArgs::splitk).  ws: f32
-// workspace of (M/256)(N/256) x 65536 floats; flags: (M/256)(N/256) ints, zero-initialised once
-// and left to this function (each call bumps the epoch they are compared with).
-int pt_gemm_dgrad_splitk(const void* A, int64_t lda, const void* const* B, const int64_t* ldb,
-                         const int64_t* b_bounds, int nb, void* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
-                         int epilogue, float* ws, int* flags, hipStream_t stream) {
-  static int epoch = 0;
-  if (!ws || !flags || (epilogue != EPI_BF16 && epilogue != EPI_BF16_ACC)) return PT_EINVAL;
-  if (M % 256 || N % 256 || K % (2 * BK)) return PT_EUNSUPPORTED;
-  const int64_t tiles = (M / 256) * (N / 256);
-  if (tiles % 8 || tiles > 4096) return PT_EUNSUPPORTED;
-  GemmGroup g{};
-  g.nprob = 1;
-  void* const Cs[1] = {C};
-  const int64_t ldcs[1] = {ldc};
-  const int rc = fill_args(g.p[0], A, lda, B, ldb, b_bounds, nb, 1, Cs, ldcs, nullptr, 1, M, N, K, epilogue, nullptr, 0);
-  if (rc) return rc;
-  if (!args_fit(g.p[0], 12)) return PT_EUNSUPPORTED;
-  GemmArgs& a = g.p[0];
-  a.ws = ws;
-  a.flags = flags;
-  epoch = epoch == INT_MAX ? 1 : epoch + 1;
-  a.epoch = epoch;
-  a.splitk = 1;
-  if (epilogue == EPI_BF16) return launch_8ph<true, false, EPI_BF16, true>(g, stream);
-  return launch_8ph<true, false, EPI_BF16_ACC, true>(g, stream);
 }
 
 // q|k|v projection with RoPE fused (EPI_ROPE): C[M,N] = A[M,K] . [B_0; ...]^T with columns

@@ -1,23 +1,39 @@
 """Gradient buckets for the DP all-reduce (RCCL over xGMI).
 
-Mirrors picotron/data_parallel/bucket.py (okoge-kaz/picotron @ 2025-03-02): Bucket (:6-57) and
-BucketManager (:59-157) -- the same greedy assignment in parameters() order (a parameter that does
-not fit opens a new bucket; one larger than the cap gets a bucket of its own), fp32 flat storage,
-`param.main_grad` views, pre-division by the group size and one async all-reduce per bucket once
-all of its parameters are ready.
+Contract of picotron/data_parallel/bucket.py (okoge-kaz/picotron @ 2025-03-02; Bucket :6-57,
+BucketManager :59-157): parameters are packed greedily, in parameters() order, into flat gradient
+buffers of at most `bucket_size` elements (a parameter that does not fit opens the next bucket; one
+larger than the cap gets a bucket of its own); every parameter's `main_grad` is a view into its
+bucket; once every parameter of a bucket has reported ready, the bucket is divided by the group size
+and all-reduced asynchronously; `wait()` joins them all; `reset()` zeroes the buffers.
 
-MI355X notes: the fused wgrad GEMMs of functional.py accumulate straight into `main_grad` (fp32
-epilogue), so no separate `main_grad += grad` pass runs for the projection weights.  Buckets are
-allocated on the parameters' device; the all-reduce runs on RCCL's stream and is waited on from
-torch's stream (no host synchronisation).
+MI355X notes.  The fused wgrad GEMMs of functional.py accumulate straight into `main_grad` (f32 or
+bf16 epilogue by the bucket dtype), so no `main_grad += grad` pass runs for the projection weights.
+The all-reduce runs on RCCL's stream; `wait()` orders torch's current stream after it (no host
+synchronisation).  `grad_type=torch.bfloat16` (the reference's own knob) halves both the
+read-modify-write traffic of the accumulation and the bytes on xGMI.
 """
-from typing import List
+from typing import Dict, List, Tuple
 
 import torch
 import torch.distributed as dist
 
 
+def plan_buckets(sizes: List[int], cap: int) -> Tuple[List[Tuple[int, int, int]], List[int]]:
+    """Greedy packing of parameter sizes (in order) into buckets of at most `cap` elements.
+    Returns ((start, end, bucket) per parameter, elements per bucket)."""
+    places, totals = [], []
+    for n in sizes:
+        if not totals or (totals[-1] > 0 and totals[-1] + n > cap):
+            totals.append(0)
+        places.append((totals[-1], totals[-1] + n, len(totals) - 1))
+        totals[-1] += n
+    return places, totals
+
+
 class Bucket:
+    """One flat gradient buffer and the parameters whose main_grad lives in it."""
+
     def __init__(self, params: List[torch.nn.Parameter], grad_data: torch.Tensor, process_group) -> None:
         self.params = set(params)
         self.params_with_grad_ready = set()
@@ -28,8 +44,10 @@ class Bucket:
         self.reset()
 
     def sync_gradient(self) -> None:
-        assert self.handle is None
-        self.grad_data /= self.process_group_size
+        """Mean over the group: pre-divide, then one async all-reduce (SUM) of the whole buffer."""
+        if self.handle is not None:
+            raise RuntimeError("bucket all-reduce launched twice in one backward")
+        self.grad_data.div_(self.process_group_size)
         self.handle = dist.all_reduce(self.grad_data, group=self.process_group, async_op=True)
 
     def reset(self) -> None:
@@ -38,11 +56,13 @@ class Bucket:
         self.grad_data.zero_()
 
     def wait(self) -> None:
-        assert self.handle is not None, "You should launch an allreduce operation before waiting for it to finish"
+        if self.handle is None:
+            raise RuntimeError("You should launch an allreduce operation before waiting for it to finish")
         self.handle.wait()
 
     def mark_param_as_ready(self, param: torch.nn.Parameter) -> None:
-        assert param in self.params and param not in self.params_with_grad_ready
+        if param not in self.params or param in self.params_with_grad_ready:
+            raise RuntimeError("parameter marked ready twice or in the wrong bucket")
         self.params_with_grad_ready.add(param)
         if len(self.params_with_grad_ready) == len(self.params):
             self.sync_gradient()
@@ -51,47 +71,23 @@ class Bucket:
 class BucketManager:
     def __init__(self, params, process_group, bucket_size: int, grad_type: torch.dtype = torch.float32) -> None:
         self.params = list(params)
-        self.device = self.params[0].device if self.params[0].is_cuda else torch.device("cpu")
-        self.buckets = []
         self.process_group = process_group
         self.process_group_size = dist.get_world_size(group=process_group)
-        self.params_to_bucket_location = {}
         self.bucket_size = bucket_size
-        self.bucket_sizes = None
-        self.grad_data_list = []
         self.grad_type = grad_type
-        self._initialize_buckets()
-
-    def _initialize_buckets(self) -> None:
-        cur_size, cur_idx = 0, 0
-        for param in self.params:
-            if not param.requires_grad:
-                continue
-            n = param.numel()
-            if cur_size == 0:
-                self.params_to_bucket_location[param] = (0, n, cur_idx)
-                cur_size = n
-            elif cur_size + n > self.bucket_size:
-                cur_idx += 1
-                self.params_to_bucket_location[param] = (0, n, cur_idx)
-                cur_size = n
-            else:
-                self.params_to_bucket_location[param] = (cur_size, cur_size + n, cur_idx)
-                cur_size += n
-        sizes = [0] * (cur_idx + 1)
-        members = [[] for _ in range(cur_idx + 1)]
-        for param, (_, end, idx) in self.params_to_bucket_location.items():
-            sizes[idx] = max(sizes[idx], end)
-            members[idx].append(param)
-        self.bucket_sizes = sizes
-        for i, s in enumerate(sizes):
-            self.grad_data_list.append(torch.zeros(s, dtype=self.grad_type, device=self.device))
-            self.buckets.append(Bucket(members[i], self.grad_data_list[i], self.process_group))
-        for param in self.params[::-1]:
-            if not param.requires_grad:
-                continue
-            start, end, idx = self.params_to_bucket_location[param]
-            param.main_grad = self.grad_data_list[idx][start:end].view(param.shape)
+        first = self.params[0]
+        self.device = first.device if first.is_cuda else torch.device("cpu")
+        trained = [p for p in self.params if p.requires_grad]
+        places, totals = plan_buckets([p.numel() for p in trained], bucket_size)
+        self.params_to_bucket_location: Dict[torch.nn.Parameter, Tuple[int, int, int]] = dict(zip(trained, places))
+        self.bucket_sizes = totals
+        self.grad_data_list = [torch.zeros(n, dtype=grad_type, device=self.device) for n in totals]
+        members = [[] for _ in totals]
+        for p, (_, _, b) in self.params_to_bucket_location.items():
+            members[b].append(p)
+        self.buckets = [Bucket(m, g, process_group) for m, g in zip(members, self.grad_data_list)]
+        for p, (lo, hi, b) in self.params_to_bucket_location.items():
+            p.main_grad = self.grad_data_list[b][lo:hi].view(p.shape)
 
     def reset(self) -> None:
         for bucket in self.buckets:

@@ -26,6 +26,13 @@ from .bucket import BucketManager
 
 
 class DataParallelNaive(nn.Module):
+    """data_parallel.py:10-60: all-reduce (mean over cp_dp_group) every parameter's gradient once it
+    is final for the backward.  Two triggers, as in DataParallelBucket: autograd's post-accumulate
+    hook for gradients autograd accumulates, and `param._pt_grad_ready` for the weights whose
+    gradient a fused kernel wrote itself (those never reach an AccumulateGrad node).
+    (The reference's hook receives the parameter and all-reduces the parameter tensor, not its
+    .grad -- a no-op on replicated weights; this averages the gradient, the documented intent.)"""
+
     def __init__(self, module):
         super().__init__()
         self.module = module
@@ -33,6 +40,7 @@ class DataParallelNaive(nn.Module):
         for p in self.module.parameters():
             if p.requires_grad:
                 p.register_post_accumulate_grad_hook(self._allreduce_grads)
+                p._pt_grad_ready = self._allreduce_grads
 
     def forward(self, *inputs, **kwargs):
         return self.module(*inputs, **kwargs)

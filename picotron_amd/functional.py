@@ -44,8 +44,8 @@ def _fuse():
 def _wgrad_target(p):
     """(buffer, epilogue) the wgrad GEMM of parameter p writes into."""
     mg = getattr(p, "main_grad", None)
-    if mg is not None:
-        return mg, K.EPI_F32_ACC
+    if mg is not None:   # DataParallelBucket's flat buffer: f32 (default) or bf16 (grad_type knob)
+        return mg, (K.EPI_F32_ACC if mg.dtype == torch.float32 else K.EPI_BF16_ACC)
     if p.grad is None:
         p.grad = torch.empty_like(p)
         return p.grad, K.EPI_BF16
@@ -60,7 +60,16 @@ def _grad_ready(p):
 
 
 def wgrad(dy2d, x2d, params):
-    """dW_i = dY_i^T X for the column segments of dY; one launch when the sinks agree."""
+    """dW_i = dY_i^T X for the column segments of dY; one launch when the sinks agree.  Parameters
+    with requires_grad=False get no gradient (autograd leaves their .grad alone)."""
+    if not all(p.requires_grad for p in params):
+        lo = 0
+        for p in params:
+            n = p.shape[0]
+            if p.requires_grad:
+                wgrad(dy2d[:, lo:lo + n], x2d, [p])
+            lo += n
+        return
     targets = [_wgrad_target(p) for p in params]
     epis = {e for _, e in targets}
     if len(epis) == 1:
@@ -78,9 +87,10 @@ def wgrad(dy2d, x2d, params):
 def wgrad_group(jobs):
     """Several wgrads [(dy2d, x2d, params), ...] in one grouped launch when every sink takes the
     same epilogue (else one wgrad() per job)."""
-    targets = [[_wgrad_target(p) for p in params] for _, _, params in jobs]
+    frozen = any(not p.requires_grad for _, _, params in jobs for p in params)
+    targets = [] if frozen else [[_wgrad_target(p) for p in params] for _, _, params in jobs]
     epis = {e for tg in targets for _, e in tg}
-    if len(epis) != 1:
+    if frozen or len(epis) != 1:
         for dy2d, x2d, params in jobs:
             wgrad(dy2d, x2d, params)
         return
@@ -99,7 +109,7 @@ def norm_bwd(dy2, z, weight, rstd, mode, dres=None, need_dw=True):
         return dx
     mg = getattr(weight, "main_grad", None)
     if mg is not None:
-        buf, sink = mg, K.DW_ACC_F32
+        buf, sink = mg, (K.DW_ACC_F32 if mg.dtype == torch.float32 else K.DW_ACC_BF16)
     elif weight.grad is None:
         weight.grad = torch.empty_like(weight)
         buf, sink = weight.grad, 0
@@ -413,7 +423,7 @@ class DecoderLayerFunction(torch.autograd.Function):
         dh2 = mlp_block_bwd(dout2, h2, (gu, hh), wg, wu, wd, tp)
         dz = norm_bwd(dh2, z, w2, rstd2, mode, dres=dout2)
         dh1 = attn_block_bwd(dz, h1, (qkv, o, lse), wq, wk, wv, wo, cos, sin, sh, tp)
-        dx = norm_bwd(dh1, x2, w1, rstd1, mode, dres=dz)
+        dx = norm_bwd(dh1, x2, w1, rstd1, mode, dres=dz)   # (norm_bwd skips dW of frozen weights)
         return (dx.view(sh.B, sh.S, -1),) + (None,) * 16
 
 
@@ -433,9 +443,11 @@ class EmbeddingFunction(torch.autograd.Function):
     def backward(ctx, dy):
         (ids,) = ctx.saved_tensors
         weight = ctx.weight
+        if not weight.requires_grad:
+            return None, None, None, None, None
         mg = getattr(weight, "main_grad", None)
         if mg is not None:
-            buf, sink = mg, K.DW_ACC_F32
+            buf, sink = mg, (K.DW_ACC_F32 if mg.dtype == torch.float32 else K.DW_ACC_BF16)
         else:
             if weight.grad is None:   # untouched rows of a fresh gradient are zero, as autograd's
                 weight.grad = torch.zeros_like(weight)
@@ -473,8 +485,63 @@ class CrossEntropyFunction(torch.autograd.Function):
         return dl.view(ctx.shape), None, None
 
 
+class HipLogits(torch.Tensor):
+    """The lm_head output (model.py:270): an ordinary tensor -- same storage, same autograd history
+    (Tensor.as_subclass) -- whose F.cross_entropy runs the fused HIP cross-entropy.  So the
+    reference's unchanged callers, `F.cross_entropy(outputs.view(-1, V), targets)` (train.py:49) and
+    `F.cross_entropy(output.transpose(1, 2), target)` (pipeline_parallel.py:103,153), reach
+    csrc/cross_entropy.hip without an edit.  View-like methods keep the type (the callers reshape
+    first); every other op returns plain tensors."""
+
+    _KEEP = frozenset([torch.Tensor.view, torch.Tensor.reshape, torch.Tensor.transpose, torch.Tensor.permute,
+                       torch.Tensor.flatten, torch.Tensor.contiguous])
+
+    @classmethod
+    def __torch_function__(cls, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        if func is torch.nn.functional.cross_entropy:
+            return _dispatch_cross_entropy(*args, **kwargs)
+        if func in cls._KEEP:
+            return super().__torch_function__(func, types, args, kwargs)
+        with torch._C.DisableTorchFunctionSubclass():
+            return func(*args, **kwargs)
+
+
+def _plain(t):
+    return t.as_subclass(torch.Tensor) if isinstance(t, HipLogits) else t
+
+
+def _dispatch_cross_entropy(input, target, weight=None, size_average=None, ignore_index=-100, reduce=None,
+                            reduction="mean", label_smoothing=0.0):
+    if weight is not None or size_average is not None or reduce is not None or label_smoothing != 0.0:
+        raise NotImplementedError("picotron_amd cross_entropy: class weights / label smoothing / legacy reduction "
+                                  "arguments are not on picotron's path (train.py:49)")
+    return cross_entropy(_plain(input), _plain(target), reduction=reduction, ignore_index=ignore_index)
+
+
+def as_logits(t):
+    """Tag an lm_head output so F.cross_entropy on it (or on its views) takes the HIP kernel."""
+    return t.as_subclass(HipLogits)
+
+
 def cross_entropy(input, target, reduction="mean", ignore_index=-100):
-    """Drop-in for F.cross_entropy(outputs [N, V], target_ids [N], reduction='mean') of train.py:49."""
+    """Drop-in for F.cross_entropy(..., reduction='mean') at the reference's two call sites:
+      * train.py:49                     input [N, V], target [N];
+      * pipeline_parallel.py:103,153    input = output.transpose(1, 2), i.e. [B, V, S] with the class
+        dim 1 (a view of the [B, S, V] stage output), target [B, S].
+    The [B, V, S] form is read as the [B*S, V] rows it views (no copy when the underlying [B, S, V]
+    is contiguous); the gradient flows back through the same views."""
     if reduction != "mean":
         raise ValueError("picotron_amd.cross_entropy implements reduction='mean' (train.py:49)")
+    input, target = _plain(input), _plain(target)
+    if input.dim() == 3:
+        B, V, S = input.shape
+        if tuple(target.shape) != (B, S):
+            raise ValueError(f"cross_entropy: input [B, V, S] = {tuple(input.shape)} needs target [B, S], got "
+                             f"{tuple(target.shape)}")
+        rows = input.transpose(1, 2).reshape(B * S, V)
+        return CrossEntropyFunction.apply(rows, target.reshape(-1), ignore_index)
+    if input.dim() != 2 or target.dim() != 1 or target.shape[0] != input.shape[0]:
+        raise ValueError(f"cross_entropy: expected input [N, V] and target [N] (or [B, V, S] / [B, S]), got "
+                         f"{tuple(input.shape)} / {tuple(target.shape)}")
     return CrossEntropyFunction.apply(input, target, ignore_index)

@@ -50,7 +50,7 @@ def rmsnorm_fwd(x, weight, eps, mode=MODE_TRITON, residual=None):
         _req(residual.shape == x.shape and residual.dtype == BF16, "residual shape/dtype")
         z = torch.empty_like(x)
     rc = lib.pt_rmsnorm_fwd(_ptr(x), _ptr(residual), _ptr(weight), _ptr(y), _ptr(z), _ptr(rstd), rows, cols,
-                            float(eps), int(mode), _C.stream_ptr())
+                            float(eps), int(mode), _C.stream_ptr(x.device))
     _C.check(rc, "pt_rmsnorm_fwd")
     return y, rstd, z
 
@@ -76,7 +76,7 @@ def rmsnorm_bwd(dy, z, weight, rstd, mode=MODE_TRITON, dres=None, dw_out=None, d
     if dres is not None:
         dres = dres.contiguous()
     rc = lib.pt_rmsnorm_bwd(_ptr(dy), _ptr(z), _ptr(weight), _ptr(rstd), _ptr(dres), _ptr(dx), _ptr(dw_out),
-                            _ptr(partial), rows, cols, int(mode) | int(dw_sink), _C.stream_ptr())
+                            _ptr(partial), rows, cols, int(mode) | int(dw_sink), _C.stream_ptr(z.device))
     _C.check(rc, "pt_rmsnorm_bwd")
     return dx, dw_out
 
@@ -90,7 +90,7 @@ def embedding_fwd(ids, weight, vocab_lo=0, vocab_hi=None):
     H = weight.shape[1]
     out = torch.empty(flat.numel(), H, dtype=BF16, device=weight.device)
     rc = _C.lib().pt_embedding_fwd(_ptr(flat), flat.numel(), _ptr(weight), weight.stride(0), int(vocab_lo),
-                                   int(vocab_hi), _ptr(out), out.stride(0), H, _C.stream_ptr())
+                                   int(vocab_hi), _ptr(out), out.stride(0), H, _C.stream_ptr(weight.device))
     _C.check(rc, "pt_embedding_fwd")
     return out.view(*ids.shape, H)
 
@@ -108,7 +108,7 @@ def embedding_bwd(ids, dy2d, dweight, sink, vocab_lo=0, vocab_hi=None, padding_i
     sorted_ids, perm = torch.sort(keyed, stable=True)
     rc = _C.lib().pt_embedding_bwd(_ptr(sorted_ids), _ptr(perm), flat.numel(), _ptr(dy2d), dy2d.stride(0),
                                    int(vocab_lo), _ptr(dweight), dweight.stride(0), dy2d.shape[1], int(sink),
-                                   _C.stream_ptr())
+                                   _C.stream_ptr(dy2d.device))
     _C.check(rc, "pt_embedding_bwd")
 
 
@@ -128,7 +128,7 @@ def adamw_step(p, grad, exp_avg, exp_avg_sq, decay, w1, beta2, c2, bc2_sqrt, eps
         raise _C.HipKernelError(f"adamw: unsupported dtype {p.dtype}")
     rc = _C.lib().pt_adamw_step(_ptr(p), _ptr(grad), _ptr(exp_avg), _ptr(exp_avg_sq), p.numel(), dt, float(decay),
                                 float(w1), float(beta2), float(c2), float(bc2_sqrt), float(eps), float(step_size),
-                                _C.stream_ptr())
+                                _C.stream_ptr(p.device))
     _C.check(rc, "pt_adamw_step")
 
 
@@ -140,7 +140,7 @@ def rope_(x2d, nheads, head_dim, cos, sin, seq_len, inverse=False):
     _req(cos.shape[0] >= seq_len, "rope: table shorter than the sequence")
     rows = x2d.shape[0]
     rc = _C.lib().pt_rope(_ptr(x2d), rows, x2d.stride(0), nheads, head_dim, _ptr(cos), _ptr(sin), seq_len,
-                          cos.stride(0), 1 if inverse else 0, _C.stream_ptr())
+                          cos.stride(0), 1 if inverse else 0, _C.stream_ptr(x2d.device))
     _C.check(rc, "pt_rope")
     return x2d
 
@@ -150,7 +150,7 @@ def swiglu_fwd(g, u, out=None):
     rows, cols = g.shape
     h = out if out is not None else torch.empty(rows, cols, dtype=BF16, device=g.device)
     rc = _C.lib().pt_swiglu_fwd(_ptr(g), g.stride(0), _ptr(u), u.stride(0), _ptr(h), h.stride(0), rows, cols,
-                                _C.stream_ptr())
+                                _C.stream_ptr(g.device))
     _C.check(rc, "pt_swiglu_fwd")
     return h
 
@@ -161,9 +161,47 @@ def swiglu_bwd(dh, g, u, dg=None, du=None):
     dg = dg if dg is not None else torch.empty(rows, cols, dtype=BF16, device=g.device)
     du = du if du is not None else torch.empty(rows, cols, dtype=BF16, device=g.device)
     rc = _C.lib().pt_swiglu_bwd(_ptr(dh), dh.stride(0), _ptr(g), g.stride(0), _ptr(u), u.stride(0), _ptr(dg),
-                                dg.stride(0), _ptr(du), du.stride(0), rows, cols, _C.stream_ptr())
+                                dg.stride(0), _ptr(du), du.stride(0), rows, cols, _C.stream_ptr(g.device))
     _C.check(rc, "pt_swiglu_bwd")
     return dg, du
+
+
+# ---------------------------------------------------------------------------- device status
+STATUS_BAD_TARGET = 1   # PT_STATUS_BAD_TARGET (include/picotron_hip.h)
+_STATUS = {}
+
+
+def status_word(device):
+    """The per-device int32 status word data-validating kernels OR their error bits into."""
+    w = _STATUS.get(device.index)
+    if w is None:
+        w = torch.zeros(1, dtype=torch.int32, device=device)
+        _STATUS[device.index] = w
+    return w
+
+
+def device_status(device=None, reset=True):
+    """Read (a host synchronisation) and optionally clear the status word of `device`."""
+    device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    w = _STATUS.get(device.index)
+    if w is None:
+        return 0
+    v = int(w.item())
+    if reset and v:
+        w.zero_()
+    return v
+
+
+def check_device_status(device=None):
+    """Raise what torch's device-side asserts would have: called where the host synchronises anyway
+    (train.train_step after the step's loss read) or by anyone after a suspicious NaN."""
+    v = device_status(device)
+    if v & STATUS_BAD_TARGET:
+        raise _C.HipKernelError("cross_entropy: a target index is outside [0, vocab) and is not ignore_index "
+                                "(torch: 'Assertion `t >= 0 && t < n_classes` failed'); its row loss and "
+                                "gradient were set to NaN")
+    if v:
+        raise _C.HipKernelError(f"device status word {v:#x}")
 
 
 # ---------------------------------------------------------------------------- cross entropy
@@ -179,7 +217,7 @@ def cross_entropy_fwd_bwd(logits, targets, scale=1.0, ignore_index=-100, inplace
     dlogits = logits if inplace else torch.empty_like(logits)
     rc = _C.lib().pt_cross_entropy_fwd_bwd(_ptr(logits), logits.stride(0), _ptr(targets), _ptr(dlogits),
                                            dlogits.stride(0), _ptr(row_loss), rows, vocab, float(scale),
-                                           _ptr(inv_count), int(ignore_index), _C.stream_ptr())
+                                           _ptr(inv_count), int(ignore_index), _ptr(status_word(logits.device)), _C.stream_ptr(logits.device))
     _C.check(rc, "pt_cross_entropy_fwd_bwd")
     loss = row_loss.sum() * inv_count[0]
     return loss, dlogits, inv_count
@@ -194,7 +232,7 @@ def cross_entropy_loss(logits, targets, ignore_index=-100):
     inv_count = (1.0 / (targets != ignore_index).sum().clamp_min(1).to(torch.float32)).reshape(1)
     row_loss = torch.empty(rows, dtype=torch.float32, device=logits.device)
     rc = _C.lib().pt_cross_entropy_fwd_bwd(_ptr(logits), logits.stride(0), _ptr(targets), None, 0, _ptr(row_loss),
-                                           rows, vocab, 1.0, None, int(ignore_index), _C.stream_ptr())
+                                           rows, vocab, 1.0, None, int(ignore_index), _ptr(status_word(logits.device)), _C.stream_ptr(logits.device))
     _C.check(rc, "pt_cross_entropy_fwd_bwd(loss)")
     return row_loss.sum() * inv_count[0], inv_count
 
@@ -211,7 +249,7 @@ def cross_entropy_loss_lse(logits, targets, ignore_index=-100):
     row_loss = torch.empty(rows, dtype=torch.float32, device=logits.device)
     row_lse = torch.empty(rows, dtype=torch.float32, device=logits.device)
     rc = _C.lib().pt_cross_entropy_fwd_lse(_ptr(logits), logits.stride(0), _ptr(targets), _ptr(row_loss),
-                                           _ptr(row_lse), rows, vocab, int(ignore_index), _C.stream_ptr())
+                                           _ptr(row_lse), rows, vocab, int(ignore_index), _ptr(status_word(logits.device)), _C.stream_ptr(logits.device))
     _C.check(rc, "pt_cross_entropy_fwd_lse")
     return row_loss.sum() * inv_count[0], inv_count, row_lse
 
@@ -227,7 +265,7 @@ def cross_entropy_grad_lse(logits, targets, row_lse, scale_dev, ignore_index=-10
     dl = torch.empty(rows, vocab, dtype=BF16, device=logits.device)
     rc = _C.lib().pt_cross_entropy_bwd_lse(_ptr(logits), logits.stride(0), _ptr(targets), _ptr(row_lse), _ptr(dl),
                                            dl.stride(0), rows, vocab, _ptr(scale_dev), int(ignore_index),
-                                           _C.stream_ptr())
+                                           _C.stream_ptr(logits.device))
     _C.check(rc, "pt_cross_entropy_bwd_lse")
     return dl
 
@@ -243,7 +281,7 @@ def cross_entropy_grad(logits, targets, scale_dev, ignore_index=-100):
     row_loss = torch.empty(rows, dtype=torch.float32, device=logits.device)
     rc = _C.lib().pt_cross_entropy_fwd_bwd(_ptr(logits), logits.stride(0), _ptr(targets), _ptr(dl), dl.stride(0),
                                            _ptr(row_loss), rows, vocab, 1.0, _ptr(scale_dev), int(ignore_index),
-                                           _C.stream_ptr())
+                                           _ptr(status_word(logits.device)), _C.stream_ptr(logits.device))
     _C.check(rc, "pt_cross_entropy_fwd_bwd(grad)")
     return dl
 
@@ -307,7 +345,7 @@ def _gemm(A, lda, a_kcontig, Bs, ldbs, b_bounds, b_kcontig, b_seg_dim, Cs, ldcs,
     rc = lib.pt_gemm(_ptr(A), lda, int(a_kcontig), _C.ptrarr([_ptr(b) for b in Bs]), _C.i64arr(ldbs),
                      _C.i64arr(b_bounds), nb, int(b_kcontig), int(b_seg_dim), _C.ptrarr([_ptr(c) for c in Cs]),
                      _C.i64arr(ldcs), _C.i64arr(c_bounds), nc, M, N, K, int(epilogue), _ptr(residual), int(ldr),
-                     int(tile), _C.stream_ptr())
+                     int(tile), _C.stream_ptr(A.device))
     _C.check(rc, f"pt_gemm(M={M}, N={N}, K={K}, a_k={a_kcontig}, b_k={b_kcontig}, epi={epilogue})")
     if probe is not None:
         ev1.record()
@@ -358,7 +396,7 @@ def linear_wgrad_grouped(jobs, epilogue=EPI_BF16, tile=-1):
     if probe is not None:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
-    rc = _C.lib().pt_gemm_grouped(probs, len(jobs), 0, 0, int(epilogue), int(tile), _C.stream_ptr())
+    rc = _C.lib().pt_gemm_grouped(probs, len(jobs), 0, 0, int(epilogue), int(tile), _C.stream_ptr(jobs[0][0].device))
     _C.check(rc, f"pt_gemm_grouped({len(jobs)} problems, epi={epilogue})")
     if probe is not None:
         ev1.record()
@@ -415,7 +453,7 @@ def linear_fwd_rope(x2d, weights, cos, sin, seq_len, rot_heads, head_dim):
         ev0.record()
     rc = _C.lib().pt_gemm_rope(_ptr(x2d), x2d.stride(0), _C.ptrarr([_ptr(w) for w in weights]), _C.i64arr([K] * len(weights)),
                                _C.i64arr(_bounds(ns)), len(weights), _ptr(y), y.stride(0), T, N, K, _ptr(cos), _ptr(sin),
-                               cos.stride(0), seq_len, rot_heads * head_dim, head_dim, -1, _C.stream_ptr())
+                               cos.stride(0), seq_len, rot_heads * head_dim, head_dim, -1, _C.stream_ptr(x2d.device))
     _C.check(rc, "pt_gemm_rope")
     if probe is not None:
         ev1.record()
@@ -460,34 +498,6 @@ def linear_dgrad_swiglu(dy2d, wd, gu):
     return dgu
 
 
-_SPLITK_WS = {}
-
-
-def _splitk_buffers(device, tiles):
-    """Per-device split-K workspace (f32, 64 Ki floats per 256x256 tile) and epoch flags (zeroed
-    once; the library owns them afterwards)."""
-    key = (device.type, device.index)
-    ws, flags = _SPLITK_WS.get(key, (None, None))
-    if ws is None or ws.numel() < tiles * 65536:
-        ws = torch.empty(tiles * 65536, dtype=torch.float32, device=device)
-        if flags is None:
-            flags = torch.zeros(4096, dtype=torch.int32, device=device)
-        _SPLITK_WS[key] = (ws, flags)
-    return ws, flags
-
-
-def splitk_dgrad_fits(T, N, Kin, ns, weights):
-    """Shapes the split-K pairs tile: 256x256 tiles that fill at most one round of the 256 CUs as
-    pairs, each K half >= 32 K-tiles (q|k|v and gate|up dX, lm_head dX at SmolLM dims).  Opt-in
-    (PICOTRON_SPLITK=1): measured in-situ equal to the 4-phase 256x128 kernel (150.8k vs 151.1k
-    tok/s, same box), so the default stays on the kernel without a cross-workgroup wait."""
-    if os.environ.get("PICOTRON_SPLITK", "0") != "1":
-        return False
-    tiles = (T // 256) * (Kin // 256)
-    return (T % 256 == 0 and Kin % 256 == 0 and tiles % 8 == 0 and 2 * tiles <= 256 and N >= 4096
-            and N % 128 == 0 and all(n % 64 == 0 for n in ns) and all(w.stride(0) == Kin for w in weights))
-
-
 def linear_dgrad(dy2d, weights, out=None, accumulate=False, tile=-1):
     """dX = dY . [W_0; W_1; ...]  where dY = [dY_0 | dY_1 | ...] is [T, sum N_i]."""
     _bf16_rowmajor(dy2d, "dy")
@@ -496,17 +506,6 @@ def linear_dgrad(dy2d, weights, out=None, accumulate=False, tile=-1):
     ns = [w.shape[0] for w in weights]
     _req(sum(ns) == N, "dgrad: dY width must equal the stacked weight rows")
     dx = out if out is not None else torch.empty(T, Kin, dtype=BF16, device=dy2d.device)
-    if tile == -1 and _PROBE is None and splitk_dgrad_fits(T, N, Kin, ns, weights):
-        _bf16_rowmajor(dx, "dx")
-        for w in weights:
-            _req(w.dtype == BF16 and w.is_contiguous() and w.shape[1] == Kin, "weight must be contiguous [N_i, Kin] bf16")
-        ws, flags = _splitk_buffers(dy2d.device, (T // 256) * (Kin // 256))
-        rc = _C.lib().pt_gemm_dgrad_splitk(_ptr(dy2d), dy2d.stride(0), _C.ptrarr([_ptr(w) for w in weights]),
-                                           _C.i64arr([Kin] * len(weights)), _C.i64arr(_bounds(ns)), len(weights),
-                                           _ptr(dx), dx.stride(0), T, Kin, N, EPI_BF16_ACC if accumulate else EPI_BF16,
-                                           _ptr(ws), _ptr(flags), _C.stream_ptr())
-        _C.check(rc, "pt_gemm_dgrad_splitk")
-        return dx
     _gemm(dy2d, dy2d.stride(0), 1, weights, [Kin] * len(weights), _bounds(ns), 0, 1, [dx], [dx.stride(0)],
           [0, T], T, Kin, N, EPI_BF16_ACC if accumulate else EPI_BF16, tile)
     return dx
@@ -523,6 +522,26 @@ def linear_wgrad(dy2d, x2d, outs, epilogue=EPI_BF16, tile=-1):
     _gemm(dy2d, dy2d.stride(0), 0, [x2d], [x2d.stride(0)], [0, Kin], 0, 0, outs, [o.stride(0) for o in outs],
           _bounds(ns), N, Kin, T, epilogue, tile)
     return outs
+
+
+# ------------------------------------------------------------------------------- LSE merge
+def lse_merge(out, block_out, lse, block_lse):
+    """(out_new f32, lse_new) = update_out_and_lse's non-first step (context_parallel.py:157-187) over
+    contiguous out / block_out [..., D] and lse / block_lse [...] (lse in bf16 or f32)."""
+    _req(out.dtype == torch.float32 and out.is_cuda, "lse_merge: out must be an f32 device tensor")
+    _req(block_out.shape == out.shape and block_out.dtype in (BF16, torch.float32), "lse_merge: block_out")
+    _req(lse.dtype == block_lse.dtype and lse.dtype in (BF16, torch.float32), "lse_merge: lse dtypes")
+    D = out.shape[-1]
+    rows = out.numel() // D
+    _req(lse.numel() == rows and block_lse.numel() == rows, "lse_merge: one lse per output row")
+    out, block_out, lse, block_lse = (t.contiguous() for t in (out, block_out, lse, block_lse))
+    out_new = torch.empty_like(out)
+    lse_new = torch.empty_like(lse)
+    rc = _C.lib().pt_lse_merge(_ptr(out), _ptr(block_out), 0 if block_out.dtype == BF16 else 1, _ptr(lse),
+                               _ptr(block_lse), 0 if lse.dtype == BF16 else 1, _ptr(out_new), _ptr(lse_new), rows, D,
+                               _C.stream_ptr(out.device))
+    _C.check(rc, "pt_lse_merge")
+    return out_new, lse_new
 
 
 # ------------------------------------------------------------------------------- attention
@@ -543,7 +562,7 @@ def attn_fwd(q, k, v, scale, causal, out=None, lse=None, merge=False):
     _req(lse.is_contiguous() and lse.shape == (B, H, Sq), "lse must be contiguous [B, H, Sq] f32")
     rc = _C.lib().pt_attn_fwd(_ptr(q), _str3(q), _ptr(k), _str3(k), _ptr(v), _str3(v), _ptr(out), _str3(out),
                               _ptr(lse), B, H, HKV, Sq, Sk, D, float(scale), int(bool(causal)), int(bool(merge)),
-                              _C.stream_ptr())
+                              _C.stream_ptr(q.device))
     _C.check(rc, "pt_attn_fwd")
     return out, lse
 
@@ -553,7 +572,7 @@ def attn_delta(dout, out):
     B, Sq, H, D = out.shape
     delta = torch.empty(B, H, Sq, dtype=torch.float32, device=out.device)
     rc = _C.lib().pt_attn_bwd_delta(_ptr(dout), _str3(dout), _ptr(out), _str3(out), _ptr(delta), B, H, Sq, D,
-                                    _C.stream_ptr())
+                                    _C.stream_ptr(out.device))
     _C.check(rc, "pt_attn_bwd_delta")
     return delta
 
@@ -589,12 +608,12 @@ def attn_bwd(dout, q, k, v, out, lse, scale, causal, dq=None, dk=None, dv=None, 
         rc = lib.pt_attn_bwd_fused_delta(_ptr(q), _str3(q), _ptr(k), _str3(k), _ptr(v), _str3(v), _ptr(out), _str3(out),
                                          _ptr(dout), _str3(dout), _ptr(lse), _ptr(delta), _ptr(dq), _str3(dq), _ptr(dk),
                                          _str3(dk), _ptr(dv), _str3(dv), B, H, HKV, Sq, Sk, D, float(scale),
-                                         int(bool(causal)), _ptr(rc_cos), _ptr(rc_sin), rstride, _C.stream_ptr())
+                                         int(bool(causal)), _ptr(rc_cos), _ptr(rc_sin), rstride, _C.stream_ptr(q.device))
         _C.check(rc, "pt_attn_bwd_fused_delta")
         return dq, dk, dv, delta
     rc = lib.pt_attn_bwd(_ptr(q), _str3(q), _ptr(k), _str3(k), _ptr(v), _str3(v), _ptr(dout), _str3(dout),
                          _ptr(lse), _ptr(delta), _ptr(dq), _str3(dq), _ptr(dk), _str3(dk), _ptr(dv), _str3(dv),
                          B, H, HKV, Sq, Sk, D, float(scale), int(bool(causal)), int(bool(grad_f32)),
-                         _ptr(rc_cos), _ptr(rc_sin), rstride, _C.stream_ptr())
+                         _ptr(rc_cos), _ptr(rc_sin), rstride, _C.stream_ptr(q.device))
     _C.check(rc, "pt_attn_bwd")
     return dq, dk, dv, delta

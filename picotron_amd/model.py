@@ -169,7 +169,10 @@ class Linear(nn.Module):
 
     def forward(self, x):
         y = FN.linear(x, self.weight)
-        return y if self.bias is None else y + self.bias
+        y = y if self.bias is None else y + self.bias
+        # the lm_head (Llama tags its final_proj): keep F.cross_entropy on the HIP kernel also when
+        # a caller other than Llama.forward runs it (PipelineParallel.forward, model.py:63)
+        return FN.as_logits(y) if getattr(self, "_pt_lm_head", False) else y
 
 
 def _init_uniform_fan_in(tensor):
@@ -298,6 +301,7 @@ class Llama(nn.Module):
         self.embedding = Embedding(self.vocab_size, self.hidden_size)
         self.decoder_layers = nn.ModuleList([DecoderLayer(config, layer_idx=i) for i in range(self.num_layers)])
         self.final_proj = Linear(self.hidden_size, self.vocab_size, bias=False)
+        self.final_proj._pt_lm_head = True
         RMSNorm = TritonRMSNorm if _flash() else LlamaRMSNorm
         self.final_norm = RMSNorm(self.hidden_size, eps=config.rms_norm_eps)
         self.reset_parameters()
@@ -317,5 +321,17 @@ class Llama(nn.Module):
         for layer in self.decoder_layers:
             x = layer(x)
         x = self.final_norm(x)
-        logits = self.final_proj(x)
-        return logits
+        return lm_head(self.final_proj, x)
+
+
+def lm_head(final_proj, x):
+    """model.py:270 `self.final_proj(x)` on the MFMA GEMM whatever module holds the weight: the
+    build's Linear / ColumnParallelLinear call it themselves; a plain torch nn.Linear -- what
+    init_model_with_materialized_weights swaps in (checkpoint.py:89-91) -- is run through
+    functional.linear on its weight (+ bias) instead of torch's GEMM."""
+    if type(final_proj) is nn.Linear:
+        y = FN.linear(x, final_proj.weight)
+        y = y if final_proj.bias is None else y + final_proj.bias
+    else:
+        y = final_proj(x)
+    return FN.as_logits(y)

@@ -1,11 +1,16 @@
 """The 4-D process grid (dp, pp, cp, tp) -- the topology the hot path's collectives run over.
 
-Mirrors picotron/process_group_manager.py:5-67 of the reference (same grid order
-`arange(world).view(dp, pp, cp, tp)`, TP innermost, same attribute names, module-global
-`process_group_manager` set by `setup_process_group_manager`), so the TP/CP/DP code of this
-package reads the same groups the reference's does.  One addition: without an initialised
-torch.distributed job (a single-GPU bench or test) the manager describes a 1-rank grid with no
-groups instead of failing.
+Same contract as picotron/process_group_manager.py:5-67 of the reference: ranks laid out as
+`arange(world).view(dp, pp, cp, tp)` (TP innermost, so a TP group is a run of consecutive ranks --
+on one 8-GPU node the TP all-reduce stays inside the xGMI mesh), the same attribute names
+(`tp_group`, `cp_send_rank`, `pp_is_last_stage`, `cp_dp_world_size`, ...) and the module-global
+`process_group_manager` set by `setup_process_group_manager`, so the reference's own callers
+(utils.py, checkpoint.py, pipeline_parallel/) read it unchanged.
+
+Built differently: every group family is "the ranks that vary along some grid axes while the others
+stay fixed", computed by one permute + reshape of the grid (`_axis_groups`) instead of a nested
+comprehension per family.  Addition: without an initialised torch.distributed job (a single-GPU
+bench or test) the manager describes a 1-rank grid with no process groups instead of failing.
 """
 import os
 
@@ -13,6 +18,22 @@ import torch
 import torch.distributed as dist
 
 process_group_manager = None
+
+DP, PP, CP, TP = 0, 1, 2, 3   # grid axes
+
+
+def _axis_groups(grid, axes):
+    """All rank lists that run over `axes` (row-major in grid order) with the other axes fixed; the
+    fixed axes are enumerated outermost-first, the order every rank creates the groups in."""
+    fixed = [a for a in range(grid.dim()) if a not in axes]
+    span = 1
+    for a in axes:
+        span *= grid.shape[a]
+    return grid.permute(*fixed, *axes).reshape(-1, span).tolist()
+
+
+def _mine(lists, rank):
+    return next(ranks for ranks in lists if rank in ranks)
 
 
 class ProcessGroupManager:
@@ -24,48 +45,36 @@ class ProcessGroupManager:
         assert self.world_size == tp_size * cp_size * pp_size * dp_size, (
             f"World size ({self.world_size}) != TP ({tp_size}) * CP ({cp_size}) * PP ({pp_size}) * DP ({dp_size})")
         self.grid = torch.arange(self.world_size).view(dp_size, pp_size, cp_size, tp_size)
-        self.dp_rank, self.pp_rank, self.cp_rank, self.tp_rank = (self.grid == self.global_rank).nonzero().flatten().tolist()
+        coord = (self.grid == self.global_rank).nonzero()[0].tolist()
+        self.dp_rank, self.pp_rank, self.cp_rank, self.tp_rank = coord
 
-        g = self.grid
-        if distributed:
-            def sub(ranks_lists):
-                return dist.new_subgroups_by_enumeration(ranks_lists)[0]
-            self.tp_group = sub([g[d, p, c, :].tolist() for d in range(dp_size) for p in range(pp_size) for c in range(cp_size)])
-            self.cp_group = sub([g[d, p, :, t].tolist() for d in range(dp_size) for p in range(pp_size) for t in range(tp_size)])
-            self.pp_group = sub([g[d, :, c, t].tolist() for d in range(dp_size) for c in range(cp_size) for t in range(tp_size)])
-            self.dp_group = sub([g[:, p, c, t].tolist() for p in range(pp_size) for c in range(cp_size) for t in range(tp_size)])
-            self.cp_dp_group = sub([g[:, p, :, t].flatten().tolist() for p in range(pp_size) for t in range(tp_size)])
-            self.pp_dp_group = sub([g[:, :, c, t].flatten().tolist() for c in range(cp_size) for t in range(tp_size)])
-            self.world_group = dist.group.WORLD
-        else:
-            self.tp_group = self.cp_group = self.pp_group = self.dp_group = None
-            self.cp_dp_group = self.pp_dp_group = self.world_group = None
+        families = {"tp": (TP,), "cp": (CP,), "pp": (PP,), "dp": (DP,), "cp_dp": (DP, CP), "pp_dp": (DP, PP)}
+        lists = {name: _axis_groups(self.grid, axes) for name, axes in families.items()}
+        for name, ranks in lists.items():
+            # new_subgroups_by_enumeration creates every group of the family on every rank (a
+            # collective call) and returns the one this rank belongs to
+            group = dist.new_subgroups_by_enumeration(ranks)[0] if distributed else None
+            setattr(self, f"{name}_group", group)
+            if name != "pp_dp":
+                setattr(self, f"{name}_group_ids", _mine(ranks, self.global_rank))
+        self.world_group = dist.group.WORLD if distributed else None
 
-        dr, pr, cr, tr = self.dp_rank, self.pp_rank, self.cp_rank, self.tp_rank
-        self.tp_group_ids = g[dr, pr, cr, :].tolist()
-        self.cp_group_ids = g[dr, pr, :, tr].tolist()
-        self.pp_group_ids = g[dr, :, cr, tr].tolist()
-        self.dp_group_ids = g[:, pr, cr, tr].tolist()
-        self.cp_dp_group_ids = g[:, pr, :, tr].flatten().tolist()
-
-        self.tp_world_size = tp_size
-        self.tp_first_rank, self.tp_last_rank = self.tp_group_ids[0], self.tp_group_ids[-1]
-
-        self.cp_world_size = cp_size
-        self.cp_first_rank, self.cp_last_rank = self.cp_group_ids[0], self.cp_group_ids[-1]
-        self.cp_send_rank = self.cp_group_ids[(cr + 1) % cp_size]
-        self.cp_recv_rank = self.cp_group_ids[(cr - 1) % cp_size]
-
-        self.pp_world_size = pp_size
-        self.pp_first_rank, self.pp_last_rank = self.pp_group_ids[0], self.pp_group_ids[-1]
-        self.pp_is_first_stage = pr == 0
-        self.pp_is_last_stage = pr == pp_size - 1
-        self.pp_next_rank = None if pr == pp_size - 1 else int(g[dr, pr + 1, cr, tr].item())
-        self.pp_prev_rank = None if pr == 0 else int(g[dr, pr - 1, cr, tr].item())
-
-        self.dp_world_size = dp_size
-        self.dp_first_rank, self.dp_last_rank = self.dp_group_ids[0], self.dp_group_ids[-1]
+        self.tp_world_size, self.cp_world_size, self.pp_world_size, self.dp_world_size = (
+            tp_size, cp_size, pp_size, dp_size)
         self.cp_dp_world_size = cp_size * dp_size
+        for name in ("tp", "cp", "pp", "dp"):
+            ids = getattr(self, f"{name}_group_ids")
+            setattr(self, f"{name}_first_rank", ids[0])
+            setattr(self, f"{name}_last_rank", ids[-1])
+
+        # CP ring neighbours (rank r sends its K/V shard to r+1, receives from r-1)
+        self.cp_send_rank = self.cp_group_ids[(self.cp_rank + 1) % cp_size]
+        self.cp_recv_rank = self.cp_group_ids[(self.cp_rank - 1) % cp_size]
+        # PP neighbours (global ranks; None at the ends)
+        self.pp_is_first_stage = self.pp_rank == 0
+        self.pp_is_last_stage = self.pp_rank == pp_size - 1
+        self.pp_next_rank = None if self.pp_is_last_stage else self.pp_group_ids[self.pp_rank + 1]
+        self.pp_prev_rank = None if self.pp_is_first_stage else self.pp_group_ids[self.pp_rank - 1]
 
     def __str__(self):
         return (f"TP({self.tp_world_size})-CP({self.cp_world_size})-PP({self.pp_world_size})-"

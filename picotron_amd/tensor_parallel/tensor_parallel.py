@@ -34,6 +34,8 @@ def apply_tensor_parallel(model):
         else:
             new = VocabParallelEmbedding(num_embeddings=linear_layer.num_embeddings,
                                          embedding_dim=linear_layer.embedding_dim)
+        if getattr(linear_layer, "_pt_lm_head", False):   # keep F.cross_entropy on the HIP kernel
+            new._pt_lm_head = True
         setattr(_module, _linear_proj_name, new)
 
     mapping = [
@@ -88,7 +90,7 @@ class ColumnParallelLinear(torch.nn.Module):
             output = linear_with_all_reduce(x, self.weight, self.bias)
         if self.gather_output:
             output = GatherFromModelParallelRegion.apply(output)
-        return output
+        return FN.as_logits(output) if getattr(self, "_pt_lm_head", False) else output
 
 
 class RowParallelLinear(nn.Module):

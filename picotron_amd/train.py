@@ -19,6 +19,7 @@ import types
 import torch
 
 from . import functional as FN
+from . import kernels as K
 from . import process_group_manager as pgm
 
 SMOLLM_1_7B = dict(hidden_size=2048, intermediate_size=8192, num_attention_heads=32, num_key_value_heads=32,
@@ -89,7 +90,9 @@ def train_step(model, data_loader, device, on_microbatch=None):
         loss = FN.cross_entropy(outputs, target_ids, reduction="mean") / data_loader.grad_acc_steps
         loss.backward()
         acc_loss += loss.detach().float()
-    return acc_loss.item()
+    out = acc_loss.item()
+    K.check_device_status(torch.device(device))   # the host has synchronised: surface device asserts
+    return out
 
 
 def count_params(model):

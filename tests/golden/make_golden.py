@@ -34,6 +34,121 @@ def _fake_pgm(pgm_mod):
         dp_world_size=1, cp_dp_world_size=1, pp_is_first_stage=True, pp_is_last_stage=True)
 
 
+# ---------------------------------------------------------------- multi-rank fixtures (gloo, CPU)
+def _dist_worker(rank, world, port, ref, fn, out_dir):
+    os.environ.update(DEVICE="cpu", LOCAL_RANK=str(rank), FLASH_ATTEN="0", MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path.insert(0, ref)
+    _install_stubs()
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = fn(rank, world)
+        torch.save({k: (v.contiguous() if torch.is_tensor(v) else v) for k, v in res.items()},
+                   os.path.join(out_dir, f"_part{rank}.pt"))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_dist(fn, world, ref, name):
+    """Run fn(rank, world) -> dict on `world` gloo ranks; save {rank{r}.key: tensor} as <name>.pt."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    mp.spawn(_dist_worker, args=(world, port, ref, fn, OUT), nprocs=world, join=True)
+    merged = {}
+    for r in range(world):
+        part = os.path.join(OUT, f"_part{r}.pt")
+        for k, v in torch.load(part, weights_only=True).items():
+            merged[f"rank{r}.{k}"] = v
+        os.remove(part)
+    torch.save(merged, os.path.join(OUT, f"{name}.pt"))
+
+
+def g7_tensor_parallel(rank, world):
+    """G7: the reference's own TP pin, tests/test_tensor_parallel.py:20-73, run on gloo/CPU at shapes
+    the MFMA GEMM tiles (B 2, S 64, in 128, out 256; the test's own are 2 x 4 x 8 -> 16), bias=True,
+    ColumnParallelLinear(gather_output=True) with and without async_all_reduce, RowParallelLinear,
+    and VocabParallelEmbedding (tensor_parallel.py:191-270) -- all against a dense layer."""
+    from picotron.process_group_manager import setup_process_group_manager
+    from picotron.tensor_parallel.tensor_parallel import (ColumnParallelLinear, RowParallelLinear,
+                                                          VocabParallelEmbedding)
+    setup_process_group_manager(tp_size=world, cp_size=1, pp_size=1, dp_size=1)
+    torch.manual_seed(42)
+    B, S, IN, OUT_ = 2, 64, 128, 256
+    res = {}
+    for async_ar in (False, True):
+        x = torch.randn(B, S, IN, requires_grad=True)
+        xc = x.clone().detach().requires_grad_(True)
+        xr = x.clone().chunk(world, dim=-1)[rank].detach().requires_grad_(True)
+        col = ColumnParallelLinear(IN, OUT_, bias=True, gather_output=True, async_all_reduce=async_ar)
+        row = RowParallelLinear(IN, OUT_, bias=True)
+        dense = torch.nn.Linear(IN, OUT_, bias=True)
+        col.weight = torch.nn.Parameter(dense.weight.chunk(world, dim=0)[rank])
+        row.weight = torch.nn.Parameter(dense.weight.chunk(world, dim=1)[rank])
+        col.bias = torch.nn.Parameter(dense.bias.chunk(world, dim=0)[rank])
+        row.bias = torch.nn.Parameter(dense.bias)
+        y, yc, yr = dense(x), col(xc), row(xr)
+        y.backward(torch.ones_like(y))
+        yc.backward(torch.ones_like(yc))
+        yr.backward(torch.ones_like(yr))
+        t = "async." if async_ar else ""
+        res.update({t + "x": x.detach(), t + "dense_w": dense.weight.detach(), t + "dense_b": dense.bias.detach(),
+                    t + "y_dense": y.detach(), t + "y_col": yc.detach(), t + "y_row": yr.detach(),
+                    t + "dx_dense": x.grad, t + "dx_col": xc.grad, t + "dx_row": xr.grad,
+                    t + "dw_col": col.weight.grad, t + "db_col": col.bias.grad,
+                    t + "dw_row": row.weight.grad, t + "db_row": row.bias.grad,
+                    t + "dw_dense": dense.weight.grad, t + "db_dense": dense.bias.grad})
+    V, H = 512, 128
+    emb = VocabParallelEmbedding(V, H)
+    ids = torch.randint(0, V, (2, 64))
+    ye = emb(ids)
+    dye = torch.randn(ye.shape)
+    ye.backward(dye)
+    res.update(emb_ids=ids, emb_w=emb.weight.detach(), emb_y=ye.detach(), emb_dy=dye, emb_dw=emb.weight.grad,
+               emb_lo=torch.tensor(emb.vocab_start_index), emb_hi=torch.tensor(emb.vocab_end_index))
+    return res
+
+
+G8_CFG = dict(hidden_size=128, intermediate_size=256, num_attention_heads=2, num_key_value_heads=2,
+              rms_norm_eps=1e-5, max_position_embeddings=128, rope_theta=10000.0, vocab_size=256,
+              num_hidden_layers=2)
+
+
+def g8_data_parallel(rank, world):
+    """G8: DataParallelBucket (data_parallel.py:62-170, bucket.py) at dp=2 over the reference's tiny
+    Llama (FLASH_ATTEN=0, fp32): grad_acc 2, sync on the last micro-batch only (train.py:39-41), each
+    rank its own tokens; the averaged p.grad (= main_grad after _post_backward) per rank."""
+    import torch.nn.functional as F
+    from picotron.process_group_manager import setup_process_group_manager
+    setup_process_group_manager(tp_size=1, cp_size=1, pp_size=1, dp_size=world)
+    from picotron import model as M
+    from picotron.data_parallel.data_parallel import DataParallelBucket
+    cfg = types.SimpleNamespace(**G8_CFG)
+    torch.manual_seed(7)
+    llama = M.Llama(cfg)
+    for layer in llama.decoder_layers:
+        layer.cos, layer.sin = layer.cos.float(), layer.sin.float()
+    init = {n: p.detach().clone() for n, p in llama.named_parameters()}
+    dp = DataParallelBucket(llama)
+    g = torch.Generator().manual_seed(99)
+    ids = torch.randint(0, cfg.vocab_size, (world, 2, 2, 129), generator=g)   # [dp, ga, mbs, seq+1]
+    ga = 2
+    for i in range(ga):
+        dp.require_backward_grad_sync = (i == ga - 1)
+        t = ids[rank, i]
+        lo = dp(input_ids=t[:, :-1])
+        loss = F.cross_entropy(lo.reshape(-1, cfg.vocab_size), t[:, 1:].reshape(-1)) / ga
+        loss.backward()
+    res = {"ids": ids}
+    res.update({f"param.{n}": v for n, v in init.items()})
+    res.update({f"grad.{n}": p.grad.detach().clone() for n, p in llama.named_parameters()})
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -149,7 +264,9 @@ def main():
     for name, d in gold.items():
         torch.save({k: (v.contiguous() if torch.is_tensor(v) else v) for k, v in d.items()},
                    os.path.join(OUT, f"{name}.pt"))
-    print("wrote", sorted(gold))
+    _run_dist(g7_tensor_parallel, 2, args.ref, "G7")
+    _run_dist(g8_data_parallel, 2, args.ref, "G8")
+    print("wrote", sorted(gold) + ["G7", "G8"])
 
 
 if __name__ == "__main__":

@@ -1,0 +1,184 @@
+"""The reference API surface around the hot path on the GPU (HIP kernels through the C ABI):
+
+  * update_out_and_lse (context_parallel.py:157-187) on the HIP merge kernel vs the reference's own
+    outputs (G4, fp32 and the bf16-LSE behaviour);
+  * ring_attention_backward (context_parallel.py:130-155) as a pure function vs the oracle;
+  * F.cross_entropy as the reference's callers write it -- on the lm_head's output (HipLogits) and in
+    the pipeline engine's [B, V, S] transpose form (pipeline_parallel.py:103,153) -- on the HIP
+    kernel, and a target outside the vocabulary surfacing as an error (torch's device assert);
+  * the lm_head after init_model_with_materialized_weights swaps in a torch nn.Linear
+    (checkpoint.py:89-91): still the MFMA GEMM, same logits;
+  * frozen (requires_grad=False) weights get no gradient from the fused kernels (autograd semantics).
+Tolerances are stated per assertion."""
+import math
+import os
+import types
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import picotron_oracle as O
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+BF = torch.bfloat16
+
+
+def rel(a, b):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+@pytest.fixture(autouse=True)
+def _env(monkeypatch):
+    monkeypatch.setenv("DEVICE", "cuda")
+    monkeypatch.setenv("LOCAL_RANK", "0")
+    monkeypatch.setenv("CONTEXT_PARALLEL", "0")
+    monkeypatch.setenv("FLASH_ATTEN", "1")
+    from picotron_amd import process_group_manager as pgm
+    pgm.setup_process_group_manager(1, 1, 1, 1)
+
+
+@pytest.mark.parametrize("tag", ["f32", "bf16"])
+def test_update_out_and_lse_matches_reference_g4(tag):
+    from picotron_amd.context_parallel.context_parallel import update_out_and_lse
+    g = torch.load(os.path.join(GOLD, f"G4_{tag}.pt"), weights_only=True)
+    dev = torch.device("cuda")
+    out, lse = update_out_and_lse(None, None, g["o_causal"].to(dev), g["lse_causal"].to(dev))
+    assert out.dtype == torch.float32 and lse.dtype == g["lse_causal"].dtype and lse.shape[-1] == 1
+    out, lse = update_out_and_lse(out, lse, g["o_full"].to(dev), g["lse_full"].to(dev))
+    assert lse.dtype == g["merged_lse"].dtype and lse.shape == g["merged_lse"].shape
+    if tag == "f32":
+        torch.testing.assert_close(out.cpu(), g["merged_out"], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(lse.cpu(), g["merged_lse"], rtol=1e-6, atol=1e-6)
+    else:
+        # the bf16 LSE path rounds op by op as torch's bf16 ops do: the reference's values to within
+        # one bf16 ulp (the f32 transcendental may differ in its last bit before the rounding)
+        ulp = g["merged_lse"].float().abs() * 2 ** -7
+        assert ((lse.cpu().float() - g["merged_lse"].float()).abs() <= ulp + 1e-6).all()
+        assert rel(out, g["merged_out"]) < 1e-2
+    # slice_ form: merge rows [0, 4) of the sequence in place
+    o2, l2 = update_out_and_lse(None, None, g["o_causal"].to(dev), g["lse_causal"].to(dev))
+    sl = (slice(None), slice(None), slice(0, 4))
+    o2, l2 = update_out_and_lse(o2, l2, g["o_full"][sl].to(dev), g["lse_full"][sl].to(dev), slice_=sl)
+    assert rel(o2[sl], out[sl]) < 1e-6 and torch.equal(l2[sl].cpu(), lse[sl].cpu())
+
+
+def test_ring_attention_backward_pure_function():
+    from picotron_amd.context_parallel import context_parallel as CP
+    B, H, S, D = 2, 4, 256, 64
+    sc = 1 / math.sqrt(D)
+    g = torch.Generator().manual_seed(3)
+    q, k, v, do = (torch.randn(B, H, S, D, generator=g).to(BF) for _ in range(4))
+    for causal in (True, False):
+        o, lse = O.attention_lse(q.float(), k.float(), v.float(), sc, causal)
+        dq, dk, dv = CP.ring_attention_backward(do.cuda(), q.cuda(), k.cuda(), v.cuda(), o.to(BF).cuda(),
+                                                lse.cuda(), sc, causal)
+        rq, rk, rv = O.ring_attention_backward(do.float(), q.float(), k.float(), v.float(), o.to(BF).float(), lse,
+                                               sc, causal)
+        assert rel(dq, rq) < 2e-2 and rel(dk, rk) < 2e-2 and rel(dv, rv) < 2e-2
+
+
+def _tiny_llama(layers=1):
+    from picotron_amd.model import Llama
+    cfg = types.SimpleNamespace(hidden_size=256, intermediate_size=512, num_attention_heads=4, num_key_value_heads=2,
+                                vocab_size=512, rms_norm_eps=1e-5, rope_theta=10000.0, num_hidden_layers=layers,
+                                max_position_embeddings=128)
+    torch.manual_seed(0)
+    with torch.device("cuda"):
+        m = Llama(cfg)
+    return m.to(BF), cfg
+
+
+def test_reference_call_sites_take_the_hip_cross_entropy():
+    """train.py:49 and pipeline_parallel.py:103 call torch's F.cross_entropy on the model output;
+    the output is HipLogits, so both forms run csrc/cross_entropy.hip -- same loss and gradient as
+    torch's kernel on the same bf16 logits (rel 1e-2 / 2e-2)."""
+    from picotron_amd import functional as FN
+    model, cfg = _tiny_llama()
+    ids = torch.randint(0, cfg.vocab_size, (2, 129), generator=torch.Generator().manual_seed(4)).cuda()
+    logits = model(ids[:, :-1])
+    assert isinstance(logits, FN.HipLogits) and isinstance(logits.view(-1, cfg.vocab_size), FN.HipLogits)
+    calls = []
+    orig = FN.cross_entropy
+
+    def spy(*a, **k):
+        calls.append(a[0].shape)
+        return orig(*a, **k)
+    FN.cross_entropy = spy
+    try:
+        l1 = F.cross_entropy(logits.view(-1, cfg.vocab_size), ids[:, 1:].reshape(-1), reduction="mean")
+        l2 = F.cross_entropy(logits.transpose(1, 2), ids[:, 1:], reduction="mean")
+    finally:
+        FN.cross_entropy = orig
+    assert len(calls) == 2 and type(l1) is torch.Tensor
+    plain = logits.detach().as_subclass(torch.Tensor).float().requires_grad_(True)
+    ref = F.cross_entropy(plain.view(-1, cfg.vocab_size), ids[:, 1:].reshape(-1))
+    assert abs(l1.float().item() - ref.item()) < 1e-2 * abs(ref.item())
+    assert abs(l2.float().item() - ref.item()) < 1e-2 * abs(ref.item())
+    # the transpose form's gradient flows back through the views
+    lg = logits.detach().as_subclass(torch.Tensor).clone().requires_grad_(True)
+    FN.cross_entropy(lg.transpose(1, 2), ids[:, 1:]).backward()
+    ref.backward()
+    assert rel(lg.grad, plain.grad) < 2e-2
+
+
+def test_cross_entropy_bad_target_is_an_error():
+    """A target outside [0, V) (not ignore_index): no out-of-bounds read, a NaN loss, and the device
+    status word raises at the next check (train_step checks after its per-step host read)."""
+    from picotron_amd import functional as FN
+    from picotron_amd import kernels as K
+    from picotron_amd._C import HipKernelError
+    K.device_status(torch.device("cuda"))   # clear
+    lg = torch.randn(16, 1000, device="cuda").to(BF).requires_grad_(True)
+    tgt = torch.randint(0, 1000, (16,), device="cuda")
+    tgt[5] = 1000
+    loss = FN.cross_entropy(lg, tgt)
+    assert math.isnan(loss.float().item())
+    with pytest.raises(HipKernelError, match="outside"):
+        K.check_device_status(torch.device("cuda"))
+    K.check_device_status(torch.device("cuda"))   # cleared by the read
+    tgt[5] = -7
+    FN.cross_entropy(lg, tgt).backward()
+    assert torch.isnan(lg.grad[5].float()).all() and not torch.isnan(lg.grad[4].float()).any()
+    with pytest.raises(HipKernelError):
+        K.check_device_status(torch.device("cuda"))
+
+
+def test_lm_head_swapped_for_torch_linear_stays_on_hip_gemm():
+    """checkpoint.py:89-91 replaces final_proj by a torch nn.Linear; Llama.forward still runs it on
+    the MFMA GEMM (bit-identical logits to the build's own Linear with the same weight)."""
+    from picotron_amd import functional as FN
+    model, cfg = _tiny_llama()
+    ids = torch.randint(0, cfg.vocab_size, (2, 128), generator=torch.Generator().manual_seed(5)).cuda()
+    before = model(ids).detach().clone()
+    w = model.final_proj.weight.detach().clone()
+    model.final_proj = torch.nn.Linear(cfg.hidden_size, cfg.vocab_size, bias=False, device="cuda", dtype=BF)
+    with torch.no_grad():
+        model.final_proj.weight.copy_(w)
+    calls = []
+    orig = FN.linear
+    FN.linear = lambda *a, **k: (calls.append(a[1].shape), orig(*a, **k))[1]
+    try:
+        after = model(ids)
+    finally:
+        FN.linear = orig
+    assert calls == [w.shape] and isinstance(after, FN.HipLogits)
+    assert torch.equal(after.detach().as_subclass(torch.Tensor), before.as_subclass(torch.Tensor))
+
+
+def test_frozen_weights_get_no_gradient():
+    from picotron_amd import functional as FN
+    model, cfg = _tiny_llama()
+    frozen = [model.decoder_layers[0].attention.k_proj.weight, model.decoder_layers[0].mlp.up_proj.weight,
+              model.decoder_layers[0].input_layernorm.weight, model.embedding.weight]
+    for p in frozen:
+        p.requires_grad_(False)
+    ids = torch.randint(0, cfg.vocab_size, (2, 129), generator=torch.Generator().manual_seed(6)).cuda()
+    FN.cross_entropy(model(ids[:, :-1]).view(-1, cfg.vocab_size), ids[:, 1:].reshape(-1)).backward()
+    for p in frozen:
+        assert p.grad is None
+    for n, p in model.named_parameters():
+        if p.requires_grad:
+            assert p.grad is not None and torch.isfinite(p.grad.float()).all(), n
