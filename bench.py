@@ -9,7 +9,18 @@ all-reduce of the gradients over RCCL (dp = N, weak scaling: per-GPU work fixed)
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
-        bench.py --gpus N --steps K --warmup W
+        bench.py --gpus N --steps K --warmup W [--model llama2-7b] [--tp T] [--cp C] [--seq S]
+
+The other BASELINE configs through the same step (process grid from
+setup_process_group_manager(tp, cp, 1, N / (tp cp)), train.py:95-100; apply_tensor_parallel /
+apply_context_parallel / DataParallelBucket in train.py's order):
+    config 3  --tp 8                                  (SmolLM-1.7B TP=8 over xGMI, strong scaling)
+    config 4  --model llama2-7b --tp 2 (--gpus 4: dp2 tp2; PP is the reference's engine, not here)
+    config 5  --model llama2-7b --cp 8 --seq 32768 --mbs 1   (ring attention at 32k)
+One-GPU per-rank compute proxies (no collectives; what one rank of the multi-GPU run computes):
+    --tp-proxy 8      the decoder stack + lm_head with TP=8 shard widths (q|k|v 3 x 256, I 1024)
+    --cp-proxy 8      Llama-2-7B at 32k, CP=8: the ring's critical rank (the last: 1 causal + 7 full
+                      4096 x 4096 d128 blocks per layer) -- attention blocks and the layer's GEMMs
 
 Rank 0 prints ONE JSON line.  `value` is whole-job tokens/s (max wall time over ranks);
 tokens/s/GPU and MFU (utils.py:42-48 formula, N counted once, 2.5 PF bf16 dense peak) ride along.
@@ -32,9 +43,9 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
-# HBM bytes per GEMM launch from rocprofv3 PMC passes (tools/gpu_round.sh <tag> pmc, then
+# HBM bytes per GEMM launch from rocprofv3 PMC passes (tools/r02_baseline.sh: bench.py --grad-acc 2, then
 # tools/traffic_summary.py); read for the roofline's `traffic`
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_gemm_traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_gemm_traffic_ga2.json")
 
 
 def log(*a):
@@ -65,12 +76,166 @@ def cpu_baseline(cfg, tokens):
                       f"micro-batch ({dt:.1f} s)"}
 
 
+MODELS = {"smollm-1.7b": ("SmolLM-1.7B", "SMOLLM_1_7B", 15), "llama2-7b": ("Llama-2-7B", "LLAMA2_7B", 32)}
+
+
+def _events_time(fn, reps):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e-3
+
+
+def tp_proxy(args, base, layers):
+    """One TP rank's compute for a micro-batch (no collectives): `layers` decoder layers with the
+    shard widths (heads / tp, I / tp; the layer kernels read shards exactly like this inside the
+    TP model), the embedding lookup and the lm_head's vocab shard (ColumnParallel, V / tp) plus the
+    cross-entropy over the gathered vocabulary, fwd + bwd.  Returns the JSON line."""
+    import math
+    from picotron_amd import functional as FN
+    from picotron_amd import kernels as K
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.train import MI355X_BF16_DENSE_PEAK, make_config
+    pgm.setup_process_group_manager(1, 1, 1, 1)
+    tp = args.tp_proxy
+    cfg = make_config(base, args.seq, num_hidden_layers=layers)
+    H, I, V = cfg.hidden_size, cfg.intermediate_size // tp, cfg.vocab_size
+    nh, nkv, d = cfg.num_attention_heads // tp, cfg.num_key_value_heads // tp, cfg.hidden_size // cfg.num_attention_heads
+    T = args.mbs * args.seq
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(0)
+
+    def u(o, i):
+        return torch.nn.Parameter(((torch.rand(o, i, device=dev, generator=g) * 2 - 1) / math.sqrt(i)).to(torch.bfloat16))
+    stack = [[torch.nn.Parameter(torch.ones(H, device=dev, dtype=torch.bfloat16)) for _ in range(2)] +
+             [u(nh * d, H), u(nkv * d, H), u(nkv * d, H), u(H, nh * d), u(I, H), u(I, H), u(H, I)] for _ in range(layers)]
+    emb = torch.nn.Parameter(torch.randn(V // tp, H, device=dev, generator=g).to(torch.bfloat16))
+    head = u(V // tp, H)
+    cos = torch.ones(args.seq, d, device=dev, dtype=torch.bfloat16)
+    sin = torch.zeros(args.seq, d, device=dev, dtype=torch.bfloat16)
+    ids = torch.randint(0, V // tp, (args.mbs, args.seq), device=dev, generator=g)
+    tgt = torch.randint(0, V, (T,), device=dev, generator=g)
+
+    def micro_batch():
+        x = FN.embedding(ids, emb)
+        for w in stack:
+            x = FN.DecoderLayerFunction.apply(x, *w, cos, sin, cfg.rms_norm_eps, 0, nh, nkv, d)
+        lg = FN.linear(x.view(T, H), head)                         # this rank's vocab shard
+        full = torch.cat([lg] * tp, dim=1) if tp > 1 else lg         # stands in for the all-gather
+        FN.cross_entropy(full, tgt).backward()
+    probe = K.GemmProbe()
+    for _ in range(args.warmup + 1):
+        micro_batch()
+    torch.cuda.synchronize()
+    t = _events_time(micro_batch, args.steps)
+    with probe:
+        micro_batch()
+    s = probe.summary()
+    fpt_rank = 6 * sum(p.numel() for w in stack for p in w) + 6 * head.numel() + 12 * layers * nh * d * args.seq
+    ach = s["avg_flop"] / (s["avg_ms"] * 1e-3) / 1e12
+    tok_gpu = T / t / tp          # tp ranks share these tokens
+    from picotron_amd.train import SMOLLM_1_7B  # noqa: F401
+    return {"metric": f"TP={tp} per-rank compute proxy (1 GPU, no collectives)", "value": tok_gpu,
+            "unit": "tokens/s/GPU (compute-only upper bound)", "ms_per_microbatch": t * 1e3,
+            "mfu_upper_bound": tok_gpu * (fpt_rank * tp) / MI355X_BF16_DENSE_PEAK,
+            "config": {"model": cfg_name(base), "layers": layers, "micro_batch": args.mbs, "seq_len": args.seq,
+                       "shard": {"q|k|v": 3 * nh * d, "I": I, "heads": nh, "vocab": V // tp}},
+            "roofline": {"bound": "mfma", "kernel": "gemm (every GEMM launch of one micro-batch)", "achieved": ach,
+                         "peak": MI355X_BF16_DENSE_PEAK / 1e12, "unit": "TFLOP/s",
+                         "frac": ach / (MI355X_BF16_DENSE_PEAK / 1e12), "launches": s["launches"],
+                         "gemm_share": s["total_ms"] * 1e-3 / t}}
+
+
+def cp_proxy(args, base, layers):
+    """The critical rank of a CP ring (the last: it computes all C blocks) for one layer of
+    Llama-2-7B at seq = C x S_local: the layer's GEMMs + its causal diagonal block (the fused layer at
+    S_local) and C - 1 full S_local x S_local blocks (forward with the LSE merge epilogue, backward
+    from the global LSE, f32 dQ / dK / dV as the ring keeps them), fwd + bwd.  No p2p."""
+    import math
+    from picotron_amd import functional as FN
+    from picotron_amd import kernels as K
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.train import MI355X_BF16_DENSE_PEAK, make_config
+    pgm.setup_process_group_manager(1, 1, 1, 1)
+    C = args.cp_proxy
+    cfg = make_config(base, args.seq, num_hidden_layers=layers)
+    S = args.seq // C
+    H, I = cfg.hidden_size, cfg.intermediate_size
+    nh, nkv, d = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.hidden_size // cfg.num_attention_heads
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(0)
+    B = args.mbs
+
+    def r(*shape):
+        return torch.randn(*shape, device=dev, generator=g).to(torch.bfloat16)
+
+    def u(o, i):
+        return torch.nn.Parameter(((torch.rand(o, i, device=dev, generator=g) * 2 - 1) / math.sqrt(i)).to(torch.bfloat16))
+    w = [torch.nn.Parameter(torch.ones(H, device=dev, dtype=torch.bfloat16)) for _ in range(2)] + \
+        [u(nh * d, H), u(nkv * d, H), u(nkv * d, H), u(H, nh * d), u(I, H), u(I, H), u(H, I)]
+    cos = torch.ones(S, d, device=dev, dtype=torch.bfloat16)
+    sin = torch.zeros(S, d, device=dev, dtype=torch.bfloat16)
+    x = r(B, S, H).requires_grad_(True)
+    q, k, v, do = r(B, S, nh, d), r(B, S, nkv, d), r(B, S, nkv, d), r(B, S, nh, d)
+    sc = 1 / math.sqrt(d)
+    acc = torch.zeros(B, S, nh, d, device=dev)
+    lse = torch.zeros(B, nh, S, device=dev)
+    o = r(B, S, nh, d)
+    dq = torch.zeros(B, S, nh, d, device=dev)
+    dk, dv = torch.zeros(B, S, nkv, d, device=dev), torch.zeros(B, S, nkv, d, device=dev)
+    delta = K.attn_delta(do, o)
+
+    def layer():
+        FN.DecoderLayerFunction.apply(x, *w, cos, sin, cfg.rms_norm_eps, 0, nh, nkv, d).backward(r(B, S, H))
+
+    def block_fwd():
+        K.attn_fwd(q, k, v, sc, False, out=acc, lse=lse, merge=True)
+
+    def block_bwd():
+        K.attn_bwd(do, q, k, v, o, lse, sc, False, dq=dq, dk=dk, dv=dv, grad_f32=True, delta=delta)
+    t_layer = _events_time(layer, args.steps)
+    t_f = _events_time(block_fwd, args.steps * 4)
+    t_b = _events_time(block_bwd, args.steps * 4)
+    blk_flop = 4.0 * B * nh * S * S * d           # full block: QK^T + PV
+    t_rank = t_layer + (C - 1) * (t_f + t_b)      # per layer on the critical rank
+    layer_flop_model = 6 * (2 * H * nh * d + 2 * H * nkv * d + 3 * H * I) + 12 * H * args.seq   # per token
+    tok_gpu = B * S / (t_rank * layers) / 1   # each rank holds S tokens; the ring's pace = critical rank
+    return {"metric": f"CP={C} critical-rank compute proxy (1 GPU, no p2p)", "value": tok_gpu,
+            "unit": "tokens/s/GPU (compute-only upper bound, lm_head/embedding excluded)",
+            "config": {"model": cfg_name(base), "layers": layers, "micro_batch": B, "seq_len": args.seq,
+                       "S_local": S, "head_dim": d},
+            "layer_ms": t_layer * 1e3, "block_fwd_ms": t_f * 1e3, "block_bwd_ms": t_b * 1e3,
+            "critical_rank_layer_ms": t_rank * 1e3,
+            "mfu_upper_bound": tok_gpu * layer_flop_model * layers / MI355X_BF16_DENSE_PEAK,
+            "roofline": {"bound": "mfma", "kernel": "attention block S_local x S_local d128 (fwd merge + bwd)",
+                         "achieved": (blk_flop * 3.5) / (t_f + t_b) / 1e12, "peak": MI355X_BF16_DENSE_PEAK / 1e12,
+                         "unit": "TFLOP/s", "frac": (blk_flop * 3.5) / (t_f + t_b) / MI355X_BF16_DENSE_PEAK,
+                         "fwd_frac": blk_flop / t_f / MI355X_BF16_DENSE_PEAK,
+                         "bwd_frac": blk_flop * 2.5 / t_b / MI355X_BF16_DENSE_PEAK}}
+
+
+def cfg_name(base):
+    return {v[1]: v[0] for v in MODELS.values()}.get(base.get("_name"), "custom")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--layers", type=int, default=15)
+    ap.add_argument("--model", choices=sorted(MODELS), default="smollm-1.7b")
+    ap.add_argument("--layers", type=int, default=0, help="decoder layers (0 = the config's: 15 / 32)")
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (N GPUs = dp x tp x cp)")
+    ap.add_argument("--cp", type=int, default=1, help="context-parallel (ring attention) degree")
+    ap.add_argument("--tp-proxy", type=int, default=0, help="1 GPU: one TP rank's compute at this degree")
+    ap.add_argument("--cp-proxy", type=int, default=0, help="1 GPU: the CP ring's critical rank at this degree")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="gloo: rehearse an N-rank grid with every rank on cuda:0 (one-GPU box); timing meaningless")
     ap.add_argument("--mbs", type=int, default=4)
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--grad-acc", type=int, default=32)
@@ -87,6 +252,9 @@ def main():
     os.environ.setdefault("LOCAL_RANK", str(local_rank))
     os.environ.setdefault("FLASH_ATTEN", "1")
     os.environ["DEVICE"] = "cuda"
+    if args.backend == "gloo":
+        local_rank = 0
+        os.environ["LOCAL_RANK"] = "0"
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
     force_dp = args.dp_bucket and world == 1
@@ -96,25 +264,45 @@ def main():
             os.environ.setdefault("MASTER_PORT", "29533")
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
-        dist.init_process_group(backend="nccl", init_method="env://", device_id=device)
+        if args.backend == "gloo":
+            dist.init_process_group(backend="gloo", init_method="env://")
+        else:
+            dist.init_process_group(backend="nccl", init_method="env://", device_id=device)
 
     from picotron_amd import kernels as K
+    from picotron_amd import train as TR
+    from picotron_amd.context_parallel.context_parallel import apply_context_parallel
     from picotron_amd.data_parallel.data_parallel import DataParallelBucket
     from picotron_amd.model import Llama
     from picotron_amd.optim import AdamW
     from picotron_amd.process_group_manager import setup_process_group_manager
-    from picotron_amd.train import (SMOLLM_1_7B, SyntheticMicroBatchDataLoader, count_params, flops_per_token,
-                                    make_config, train_step, MI355X_BF16_DENSE_PEAK)
+    from picotron_amd.tensor_parallel.tensor_parallel import apply_tensor_parallel
+    from picotron_amd.train import (SyntheticMicroBatchDataLoader, count_params, flops_per_token, make_config,
+                                    train_step, MI355X_BF16_DENSE_PEAK)
 
-    setup_process_group_manager(tp_size=1, cp_size=1, pp_size=1, dp_size=world)
+    model_name, base_name, default_layers = MODELS[args.model]
+    base = dict(getattr(TR, base_name), _name=base_name)
+    layers = args.layers or default_layers
+    if args.tp_proxy or args.cp_proxy:
+        out = tp_proxy(args, base, layers) if args.tp_proxy else cp_proxy(args, base, layers)
+        print(json.dumps(out), flush=True)
+        return
+    tp, cp = args.tp, args.cp
+    if world % (tp * cp):
+        raise SystemExit(f"--gpus {world} is not a multiple of tp {tp} x cp {cp}")
+    dp = world // (tp * cp)
+    m = setup_process_group_manager(tp_size=tp, cp_size=cp, pp_size=1, dp_size=dp)
     torch.manual_seed(42)
-    cfg = make_config(SMOLLM_1_7B, args.seq, num_hidden_layers=args.layers)
+    cfg = make_config({k: v for k, v in base.items() if k != "_name"}, args.seq, num_hidden_layers=layers)
     t0 = time.time()
     with torch.device(device):
-        model = Llama(cfg)
+        model = Llama(cfg)            # train.py:174-186 order: build, TP swap, (PP), CP, dtype, DP wrap
+        if tp > 1:
+            apply_tensor_parallel(model)
+    apply_context_parallel(model)
     model.to(torch.bfloat16)
     num_params = count_params(model)
-    if world > 1 or force_dp:
+    if m.cp_dp_world_size > 1 or force_dp:
         model = DataParallelBucket(model)
         model._force_grad_sync = force_dp
     optimizer = AdamW(model.parameters(), lr=3e-4)
@@ -161,7 +349,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
 
-    tokens = world * args.grad_acc * args.mbs * args.seq * args.steps
+    tokens = dp * args.grad_acc * args.mbs * args.seq * args.steps    # tp / cp ranks share their tokens
     value = tokens / elapsed
     per_gpu = value / world
     fpt = flops_per_token(num_params, cfg)
@@ -186,21 +374,23 @@ def main():
                     "gemm_share_of_step": s["total_ms"] * 1e-3 * args.grad_acc / elapsed}
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_tokens > 0:
+    if rank == 0 and world == 1 and args.cpu_tokens > 0 and args.model == "smollm-1.7b":
         log("cpu baseline ...")
         cpu = cpu_baseline(cfg, args.cpu_tokens)
 
     if rank == 0:
+        par = "-".join(f"{k}{v}" for k, v in (("dp", dp), ("tp", tp), ("cp", cp)) if v > 1 or k == "dp")
         out = {"metric": "tokens/s/GPU and MFU, SmolLM-1.7B seq1024 at 1/2/4/8 MI355X", "value": value,
                "unit": "tokens/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-               "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+               "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+               "scaling": "weak" if tp * cp == 1 else "strong",
                "vs_baseline": None, "dtype": "bf16", "data": "synthetic (seeded random tokens, random init)",
                "tokens_per_s_per_gpu": per_gpu, "mfu": mfu, "flops_per_token": fpt, "num_params": num_params,
                "final_loss": losses[-1] if losses else None,
-               "config": {"workload": "SmolLM-1.7B dims, 15 layers, train step (fwd+bwd+AdamW)",
-                          "model": "SmolLM-1.7B", "layers": args.layers, "micro_batch": args.mbs,
-                          "grad_acc": args.grad_acc, "global_batch": args.mbs * args.grad_acc * world,
-                          "seq_len": args.seq, "parallelism": f"dp{world}" + ("-bucket" if force_dp else "")},
+               "config": {"workload": f"{model_name} dims, {layers} layers, train step (fwd+bwd+AdamW)",
+                          "model": model_name, "layers": layers, "micro_batch": args.mbs,
+                          "grad_acc": args.grad_acc, "global_batch": args.mbs * args.grad_acc * dp,
+                          "seq_len": args.seq, "parallelism": par + ("-bucket" if force_dp else "")},
                "roofline": roofline, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
     if world > 1 or force_dp:

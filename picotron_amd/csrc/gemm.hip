@@ -1086,27 +1086,41 @@ bool args_fit(const GemmArgs& a, int tile) {
   return true;
 }
 
-// auto tile for a group: the phased kernels when every problem divides -- 256x256 or 256x128,
-// whichever fills the CUs' last round better over the whole group (ties -> 256x256) -- else the
-// 128x128 two-stage kernel, else 64x64
+// auto tile for a group.  The phased kernels (256x256 8-phase, 256x128 4-phase), whichever fills the
+// CUs' last round better (ties -> 256x256), as long as that puts at least 128 tiles on the 256 CUs:
+// on the SmolLM-1.7B / Llama-2-7B TP=1 shapes they measure fastest (profiles/r01_gemm_tiles_8ph.md).
+// Below that -- the TP shards (N 256-1024 at TP=8: 24-96 phased tiles) -- the candidate with the
+// smallest modelled time, rounds x tile work / the kernel's sustained rate (one CU per workgroup:
+// ceil(tiles / 256) rounds; in-situ TF/s 1.30 / 1.20 / 0.85 / 0.45 for 256x256 / 256x128 / 128x128
+// / 64x64), which trades the phased kernels' rate for the smaller tiles' parallelism.
 int pick_group_tile(const GemmGroup& g) {
   auto fits = [&](int t) {
     for (int i = 0; i < g.nprob; ++i)
       if (!args_fit(g.p[i], t)) return false;
     return true;
   };
-  auto fill = [&](int t) {
+  auto ntiles = [&](int t) {
     int64_t tiles = 0;
     for (int i = 0; i < g.nprob; ++i) tiles += (int64_t)(g.p[i].M / kTileBM[t]) * (g.p[i].N / kTileBN[t]);
-    const int64_t rounds = (tiles + 255) / 256;
-    return (double)tiles / (double)(rounds * 256);
+    return tiles;
+  };
+  auto fill = [&](int t) {
+    const int64_t tiles = ntiles(t);
+    return (double)tiles / (double)(((tiles + 255) / 256) * 256);
   };
   const bool f12 = fits(12), f13 = fits(13);
-  if (f12 && (!f13 || fill(12) >= fill(13))) return 12;
-  if (f13) return 13;
-  if (fits(2)) return 2;
-  if (fits(3)) return 3;
-  return -1;
+  const int phased = f12 && (!f13 || fill(12) >= fill(13)) ? 12 : (f13 ? 13 : -1);
+  if (phased >= 0 && ntiles(phased) >= 128) return phased;
+  const int cand[4] = {12, 13, 2, 3};
+  const double rate[4] = {1.30, 1.20, 0.85, 0.45};
+  int best = -1;
+  double best_cost = 0.0;
+  for (int i = 0; i < 4; ++i) {
+    if (!fits(cand[i])) continue;
+    const double c = (double)((ntiles(cand[i]) + 255) / 256) * kTileBM[cand[i]] * kTileBN[cand[i]] / rate[i];
+    if (best < 0 || c < best_cost) best = cand[i], best_cost = c;
+  }
+  return best;
 }
 
 int launch_swiglu(GemmGroup& g, int a_kcontig, int b_kcontig, int epilogue, int tile, hipStream_t stream);
@@ -1114,8 +1128,11 @@ int launch_swiglu(GemmGroup& g, int a_kcontig, int b_kcontig, int epilogue, int 
 int launch_group(GemmGroup& g, int a_kcontig, int b_kcontig, int epilogue, int tile, hipStream_t stream) {
   if (epilogue == EPI_SWIGLU_FWD || epilogue == EPI_SWIGLU_BWD)
     return launch_swiglu(g, a_kcontig, b_kcontig, epilogue, tile, stream);
+  // RoPE: wave tiles 64 columns wide, the phased kernels only; the 256x128 one (twice the tiles) when
+  // it divides -- the q|k|v projection never fills more than a few rounds of 256x256 tiles
+  if (epilogue == EPI_ROPE && tile < 0) tile = args_fit(g.p[0], 13) ? 13 : 12;
   if (tile < 0) tile = pick_group_tile(g);
-  if (epilogue == EPI_ROPE) {  // wave tiles 64 columns wide: the phased kernels only
+  if (epilogue == EPI_ROPE) {
     if (!a_kcontig || !b_kcontig) return PT_EUNSUPPORTED;
     for (int i = 0; i < g.nprob; ++i)
       if (!args_fit(g.p[i], tile)) return PT_EUNSUPPORTED;

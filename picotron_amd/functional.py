@@ -103,8 +103,9 @@ def wgrad_group(jobs):
 
 def norm_bwd(dy2, z, weight, rstd, mode, dres=None, need_dw=True):
     """RMSNorm backward with the weight gradient summed straight into p's sink (bf16 .grad store or
-    accumulate -- autograd's AccumulateGrad -- or the f32 main_grad of DataParallelBucket)."""
-    if not need_dw:
+    accumulate -- autograd's AccumulateGrad -- or the f32 main_grad of DataParallelBucket).  A frozen
+    weight (requires_grad=False) gets no gradient, as under autograd."""
+    if not (need_dw and weight.requires_grad):
         dx, _ = K.rmsnorm_bwd(dy2, z, weight, rstd, mode, dres=dres)
         return dx
     mg = getattr(weight, "main_grad", None)

@@ -171,19 +171,23 @@ STATUS_BAD_TARGET = 1   # PT_STATUS_BAD_TARGET (include/picotron_hip.h)
 _STATUS = {}
 
 
+def _dev_index(device):
+    device = torch.device(device) if device is not None else torch.device("cuda")
+    return device.index if device.index is not None else torch.cuda.current_device()
+
+
 def status_word(device):
     """The per-device int32 status word data-validating kernels OR their error bits into."""
-    w = _STATUS.get(device.index)
+    w = _STATUS.get(_dev_index(device))
     if w is None:
-        w = torch.zeros(1, dtype=torch.int32, device=device)
-        _STATUS[device.index] = w
+        w = torch.zeros(1, dtype=torch.int32, device=torch.device("cuda", _dev_index(device)))
+        _STATUS[_dev_index(device)] = w
     return w
 
 
 def device_status(device=None, reset=True):
     """Read (a host synchronisation) and optionally clear the status word of `device`."""
-    device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
-    w = _STATUS.get(device.index)
+    w = _STATUS.get(_dev_index(device))
     if w is None:
         return 0
     v = int(w.item())

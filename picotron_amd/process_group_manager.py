@@ -44,7 +44,8 @@ class ProcessGroupManager:
         self.local_rank = int(os.environ.get("LOCAL_RANK", self.global_rank % self.world_size))
         assert self.world_size == tp_size * cp_size * pp_size * dp_size, (
             f"World size ({self.world_size}) != TP ({tp_size}) * CP ({cp_size}) * PP ({pp_size}) * DP ({dp_size})")
-        self.grid = torch.arange(self.world_size).view(dp_size, pp_size, cp_size, tp_size)
+        # on the CPU whatever device context the caller builds the model under (meta, cuda)
+        self.grid = torch.arange(self.world_size, device="cpu").view(dp_size, pp_size, cp_size, tp_size)
         coord = (self.grid == self.global_rank).nonzero()[0].tolist()
         self.dp_rank, self.pp_rank, self.cp_rank, self.tp_rank = coord
 

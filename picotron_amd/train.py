@@ -96,12 +96,18 @@ def train_step(model, data_loader, device, on_microbatch=None):
 
 
 def count_params(model):
-    """Parameters of the whole model, every tensor once (TP shards x tp except replicated ones)."""
-    m = pgm.current()
+    """Parameters of the whole model, every tensor once: a tensor-parallel shard counts tp times
+    (Column / VocabParallel weights and biases, RowParallel weights), a replicated tensor once.
+    (utils.py:50-79 matches names instead, which counts the replicated dense lm_head of train.py tp
+    times -- SURVEY.md §5; here the lm_head is whatever module holds it.)"""
+    from .tensor_parallel.tensor_parallel import ColumnParallelLinear, RowParallelLinear, VocabParallelEmbedding
+    tp = pgm.current().tp_world_size
     n = 0
-    for name, p in model.named_parameters():
-        sharded = any(k in name.lower() for k in ("attention", "mlp", "embed")) and "norm" not in name.lower()
-        n += p.numel() * (m.tp_world_size if sharded else 1)
+    for mod in model.modules():
+        for name, p in mod.named_parameters(recurse=False):
+            sharded = isinstance(mod, (ColumnParallelLinear, VocabParallelEmbedding)) or (
+                isinstance(mod, RowParallelLinear) and name == "weight")
+            n += p.numel() * (tp if sharded else 1)
     return n
 
 

@@ -27,6 +27,9 @@ def short(name):
     return name.split("(")[0] if "<" not in name else name.split(">")[0] + ">"
 
 
+GRAD_ACC = 2
+
+
 def main(fetch, write, out):
     f, w = per_dispatch(fetch), per_dispatch(write)
     kinds = collections.defaultdict(list)
@@ -41,7 +44,7 @@ def main(fetch, write, out):
         if "gemm" in name:
             gemm.append(b)
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py --steps 1 --warmup 0 "
-                     "--grad-acc 1; bytes = 2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction)",
+                     f"--grad-acc {GRAD_ACC}; bytes = 2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction)",
            "gemm_launches": len(gemm), "gemm_avg_bytes_per_launch": sum(gemm) / max(len(gemm), 1),
            "kernels": {f"{k} [{g} WG]": {"launches": len(v), "avg_bytes": sum(v) / len(v)}
                        for (k, g), v in sorted(kinds.items(), key=lambda kv: -sum(kv[1]))[:30]}}
