@@ -104,6 +104,20 @@ int pt_embedding_bwd(const int64_t* sorted_ids, const int64_t* perm, int64_t T, 
 int pt_adamw_step(void* param, const void* grad, void* exp_avg, void* exp_avg_sq, int64_t n, int dtype,
                   float decay, float w1, float beta2, float c2, float bc2_sqrt, float eps, float step_size,
                   hipStream_t stream);
+/* The same update over a LIST of bf16 tensors in one launch (torch's foreach AdamW is a list op
+ * too): `tensors` is a device array of pt_adam_tensor (every pointer 16-byte aligned),
+ * `chunk_start` a device int64 [ntensors + 1] of prefix sums of ceil(n / 8), total_chunks its last
+ * entry.  The caller builds and caches both (the pointers only change when tensors are re-made). */
+typedef struct {
+  void* param;
+  const void* grad;
+  void* exp_avg;
+  void* exp_avg_sq;
+  int64_t n;
+} pt_adam_tensor;
+int pt_adamw_step_multi(const void* tensors, const int64_t* chunk_start, int ntensors, int64_t total_chunks,
+                        float decay, float w1, float beta2, float c2, float bc2_sqrt, float eps, float step_size,
+                        hipStream_t stream);
 
 /* ---- bf16 GEMM, f32 accumulate -------------------------------------------------------------
  * replaces every F.linear / matmul of the layer: model.py:124-126,161,186,270,

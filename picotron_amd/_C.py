@@ -34,6 +34,7 @@ SIGNATURES = {
     "pt_embedding_fwd": (_i32, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _i64, _vp]),
     "pt_embedding_bwd": (_i32, [_vp, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _vp]),
     "pt_adamw_step": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _vp]),
+    "pt_adamw_step_multi": (_i32, [_vp, _vp, _i32, _i64, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _vp]),
     "pt_rmsnorm_bwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp]),
     "pt_rope": (_i32, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _i32, _vp]),
     "pt_swiglu_fwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp]),
@@ -67,16 +68,19 @@ class HipKernelError(RuntimeError):
     pass
 
 
-def load_library(path=LIB_PATH):
-    """dlopen the kernel library and bind every symbol; does not touch the GPU."""
+def load_library(path=LIB_PATH, strict=True):
+    """dlopen the kernel library and bind every symbol; does not touch the GPU.  strict=False (A/B
+    runs against another build) skips symbols that build does not export."""
     global _lib
-    if _lib is not None:
+    if _lib is not None and path == LIB_PATH:
         return _lib
     if not os.path.exists(path):
         raise HipKernelError(f"picotron_amd HIP library not built: {path} (run python -m picotron_amd.build)")
     import torch  # noqa: F401  -- its HIP runtime must be the one our SONAME binds to
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
+        if not strict and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

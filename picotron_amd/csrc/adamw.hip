@@ -80,6 +80,62 @@ __global__ __launch_bounds__(256) void adamw_scalar_kernel(T* __restrict__ param
   }
 }
 
+// Multi-tensor form: ONE launch per step over every bf16 parameter (torch's foreach AdamW works on
+// the whole list too).  The tensors are a virtual concatenation of 8-element chunks; workgroup b
+// owns a contiguous run of chunks, finds the tensor its run starts in by binary search over the
+// chunk prefix sums (read from the caller's descriptor table), then walks forward.  A tensor whose
+// length is not a multiple of 8 finishes its last chunk element by element.
+struct AdamTensor {   // pt_adam_tensor (include/picotron_hip.h)
+  uint16_t* p;
+  const uint16_t* g;
+  uint16_t* m;
+  uint16_t* v;
+  int64_t n;
+};
+
+__global__ __launch_bounds__(256) void adamw_multi_bf16_kernel(const AdamTensor* __restrict__ ts,
+                                                               const int64_t* __restrict__ chunk_start, int nt,
+                                                               int64_t per_block, AdamScalars s) {
+  const int64_t total = chunk_start[nt];
+  const int64_t lo = (int64_t)blockIdx.x * per_block;
+  const int64_t hi = lo + per_block < total ? lo + per_block : total;
+  if (lo >= hi) return;
+  // the tensor holding chunk lo: largest t with chunk_start[t] <= lo
+  int a = 0, b = nt - 1;
+  while (a < b) {
+    const int mid = (a + b + 1) >> 1;
+    if (chunk_start[mid] <= lo) a = mid; else b = mid - 1;
+  }
+  for (int t = a; t < nt && chunk_start[t] < hi; ++t) {
+    const AdamTensor T = ts[t];
+    const int64_t c0 = chunk_start[t], c1 = chunk_start[t + 1];
+    const int64_t from = (lo > c0 ? lo : c0) - c0, to = (hi < c1 ? hi : c1) - c0;   // chunk range in t
+    const int64_t full = T.n >> 3;
+    for (int64_t c = from + threadIdx.x; c < to; c += blockDim.x) {
+      if (c < full) {
+        float p[8], g[8], m[8], v[8];
+        unpack8(ld8(T.p + c * 8), p);
+        unpack8(ld8(T.g + c * 8), g);
+        unpack8(ld8(T.m + c * 8), m);
+        unpack8(ld8(T.v + c * 8), v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) adam_elem(p[j], g[j], m[j], v[j], s, true);
+        st8(T.p + c * 8, pack8(p));
+        st8(T.m + c * 8, pack8(m));
+        st8(T.v + c * 8, pack8(v));
+      } else {   // the ragged last chunk
+        for (int64_t i = c * 8; i < T.n; ++i) {
+          float p = bf2f(T.p[i]), g = bf2f(T.g[i]), m = bf2f(T.m[i]), v = bf2f(T.v[i]);
+          adam_elem(p, g, m, v, s, true);
+          T.p[i] = f2bf(p);
+          T.m[i] = f2bf(m);
+          T.v[i] = f2bf(v);
+        }
+      }
+    }
+  }
+}
+
 int grid_for(int64_t work) {
   int64_t g = (work + 255) / 256;
   return (int)(g < PT_STREAM_GRID_CAP ? (g < 1 ? 1 : g) : PT_STREAM_GRID_CAP);
@@ -119,6 +175,23 @@ int pt_adamw_step(void* param, const void* grad, void* exp_avg, void* exp_avg_sq
   } else {
     return PT_EINVAL;
   }
+  return PT_OK;
+}
+
+// bf16 tensors (every pointer 16-byte aligned), one launch.  tensors: device array of ntensors
+// pt_adam_tensor; chunk_start: device int64 [ntensors + 1], chunk_start[i] = sum over j < i of
+// ceil(n_j / 8) -- both built (and cached) by the caller.  total_chunks = chunk_start[ntensors].
+int pt_adamw_step_multi(const void* tensors, const int64_t* chunk_start, int ntensors, int64_t total_chunks,
+                        float decay, float w1, float beta2, float c2, float bc2_sqrt, float eps, float step_size,
+                        hipStream_t stream) {
+  if (!tensors || !chunk_start || ntensors <= 0 || total_chunks < 0) return PT_EINVAL;
+  if (total_chunks == 0) return PT_OK;
+  const AdamScalars s{decay, w1, beta2, c2, bc2_sqrt, eps, step_size};
+  const int64_t blocks = grid_for(total_chunks);
+  const int64_t per_block = (total_chunks + blocks - 1) / blocks;
+  adamw_multi_bf16_kernel<<<(unsigned)blocks, 256, 0, stream>>>((const AdamTensor*)tensors, chunk_start, ntensors,
+                                                                per_block, s);
+  PT_CHECK_LAUNCH();
   return PT_OK;
 }
 

@@ -42,6 +42,9 @@ typedef __attribute__((address_space(3))) uint8_t lds_u8;
 namespace {
 
 constexpr int BK = 64;
+#ifndef PT_SWIGLU_GRP
+#define PT_SWIGLU_GRP 2
+#endif
 
 // EPI_BF16_RES: C = bf16(R + bf16(acc)) -- the residual add of model.py:207-208 fused into the
 // producing GEMM (R may alias C).
@@ -257,7 +260,10 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
     // every load behind the previous iteration's store -- one HBM round trip per row group
     constexpr bool RD = EPI == EPI_SWIGLU_BWD || EPI == EPI_BF16_ACC || EPI == EPI_BF16_RES;
     constexpr int NLD = EPI == EPI_SWIGLU_BWD ? 2 : 1;
-    constexpr int GRP = RD ? (NIT * NLD > 8 ? 8 / NLD : NIT) : NIT;  // <= 8 prefetched chunks (32 VGPRs)
+    // prefetched chunks per group: the accumulate / residual epilogues 8 (32 VGPRs); the SwiGLU
+    // backward 2 (x2 loads: g, u) -- measured over 1 / 2 / 4 / 8 on the layer's shape, 8 is 40 %
+    // slower (profiles/r02_notes.md), 1-4 within 2 %
+    constexpr int GRP = EPI == EPI_SWIGLU_BWD ? PT_SWIGLU_GRP : (RD ? (NIT * NLD > 8 ? 8 / NLD : NIT) : NIT);
 #pragma unroll
     for (int g0 = 0; g0 < NIT; g0 += GRP) {
       bf16x8 pre[GRP][NLD];
@@ -968,7 +974,10 @@ int launch_4ph(GemmGroup g, hipStream_t stream) {
 //           8 / 9 = simple 256x256 / 128x128 with both k-substeps' fragments in flight,
 //           12 = 8-phase 256x256 (two half-image wave groups, one wait per K-tile)
 //           13 = 4-phase 256x128 (three K-tiles resident)
-//           (ids 0, 1, 6, 7, 10, 11 were pipelining experiments, measured slower and retired)
+//           (ids 0, 1, 6, 7, 10, 11 were pipelining experiments, measured slower and retired; so
+//           was round 2's 14: the 8-phase tile with ONE barrier per K-tile and free-running
+//           phases, 3-13 % slower on every layer shape -- the per-phase ping-pong pays for its
+//           barriers)
 constexpr int kNumTiles = 14;
 const int kTileBM[kNumTiles] = {0, 0, 128, 64, 256, 256, 0, 0, 256, 128, 0, 0, 256, 256};
 const int kTileBN[kNumTiles] = {0, 0, 128, 64, 256, 128, 0, 0, 256, 128, 0, 0, 256, 128};

@@ -132,6 +132,36 @@ def adamw_step(p, grad, exp_avg, exp_avg_sq, decay, w1, beta2, c2, bc2_sqrt, eps
     _C.check(rc, "pt_adamw_step")
 
 
+_ADAM_DESC = {}
+
+
+def adamw_step_multi(items, decay, w1, beta2, c2, bc2_sqrt, eps, step_size):
+    """One launch of the fused AdamW update over a list of bf16 (param, grad, exp_avg, exp_avg_sq)
+    tuples (pt_adamw_step_multi).  The device descriptor table is cached per pointer set (the
+    tensors of a model stay put across steps; a re-allocated gradient makes a new table)."""
+    for p, g, m, v in items:
+        for t in (p, g, m, v):
+            _req(t.dtype == BF16 and t.is_contiguous() and t.numel() == p.numel() and t.data_ptr() % 16 == 0,
+                 "adamw multi: contiguous, 16-byte aligned bf16 tensors of one length per parameter")
+    key = tuple((p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel()) for p, g, m, v in items)
+    ent = _ADAM_DESC.get(key)
+    if ent is None:
+        dev = items[0][0].device
+        desc = torch.tensor([list(k) for k in key], dtype=torch.int64).to(dev, non_blocking=False)
+        chunks = [0]
+        for k in key:
+            chunks.append(chunks[-1] + (k[4] + 7) // 8)
+        ent = (desc, torch.tensor(chunks, dtype=torch.int64).to(dev), chunks[-1])
+        if len(_ADAM_DESC) > 64:
+            _ADAM_DESC.clear()
+        _ADAM_DESC[key] = ent
+    desc, chunk_t, total = ent
+    rc = _C.lib().pt_adamw_step_multi(_ptr(desc), _ptr(chunk_t), len(items), int(total), float(decay), float(w1),
+                                      float(beta2), float(c2), float(bc2_sqrt), float(eps), float(step_size),
+                                      _C.stream_ptr(items[0][0].device))
+    _C.check(rc, "pt_adamw_step_multi")
+
+
 # ------------------------------------------------------------------------------------ RoPE
 def rope_(x2d, nheads, head_dim, cos, sin, seq_len, inverse=False):
     """In-place rotate the first `nheads` heads of every row of x2d ([rows, row_stride] view)."""

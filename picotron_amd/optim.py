@@ -22,12 +22,16 @@ class AdamW(torch.optim.Optimizer):
 
     @torch.no_grad()
     def step(self, closure=None):
+        """torch.optim.AdamW.step (foreach, decoupled weight decay) on the HIP kernel: the bf16 tensors
+        that share a step count go through ONE multi-tensor launch; anything else (f32, unaligned)
+        per tensor."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
         for group in self.param_groups:
             lr, (beta1, beta2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
+            batches = {}
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -40,8 +44,18 @@ class AdamW(torch.optim.Optimizer):
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st["step"] += 1
                 t = st["step"].item()
+                item = (p, p.grad, st["exp_avg"], st["exp_avg_sq"])
+                multi = p.dtype == torch.bfloat16 and all(x.is_contiguous() and x.data_ptr() % 16 == 0 for x in item) \
+                    and p.grad.dtype == p.dtype
+                batches.setdefault((t, multi), []).append(item)
+            for (t, multi), items in batches.items():
                 bc1 = 1 - beta1 ** t
                 bc2 = 1 - beta2 ** t
-                K.adamw_step(p, p.grad, st["exp_avg"], st["exp_avg_sq"], decay=1 - lr * wd, w1=1 - beta1,
-                             beta2=beta2, c2=1 - beta2, bc2_sqrt=bc2 ** 0.5, eps=eps, step_size=(lr / bc1) * -1)
+                sc = dict(decay=1 - lr * wd, w1=1 - beta1, beta2=beta2, c2=1 - beta2, bc2_sqrt=bc2 ** 0.5, eps=eps,
+                          step_size=(lr / bc1) * -1)
+                if multi:
+                    K.adamw_step_multi(items, **sc)
+                else:
+                    for p, g, m, v in items:
+                        K.adamw_step(p, g, m, v, **sc)
         return loss

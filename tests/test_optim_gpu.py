@@ -57,3 +57,34 @@ def test_adamw_state_dict_roundtrip():
     torch.cuda.synchronize()
     for p, q in zip(ref, ours.param_groups[0]["params"]):
         assert (p.float() - q.float()).abs().max().item() <= 1e-2 * p.float().abs().max().item()
+
+
+def test_multi_tensor_launch_equals_per_tensor():
+    """pt_adamw_step_multi (one launch over the list, ragged tails included) == pt_adamw_step per
+    tensor, bit for bit; a re-made gradient (new pointer) gets a new descriptor table."""
+    from picotron_amd import kernels as K
+    g = torch.Generator().manual_seed(3)
+    shapes = [(2048,), (1001,), (512, 2048), (37,), (3, 5, 7), (8,)]
+
+    def mk():
+        return [torch.randn(s, generator=g).to(torch.bfloat16).to(DEV) for s in shapes]
+    P, G, M, V = mk(), mk(), [t.abs() * 0.01 for t in mk()], [t.abs() * 1e-4 for t in mk()]
+    sc = dict(decay=1 - 3e-4 * 0.01, w1=0.1, beta2=0.999, c2=0.001, bc2_sqrt=(1 - 0.999 ** 3) ** 0.5, eps=1e-8,
+              step_size=-3e-4 / (1 - 0.9 ** 3))
+    a = [[t.clone() for t in L] for L in (P, G, M, V)]
+    b = [[t.clone() for t in L] for L in (P, G, M, V)]
+    for i in range(len(shapes)):
+        K.adamw_step(a[0][i], a[1][i], a[2][i], a[3][i], **sc)
+    K.adamw_step_multi(list(zip(*b)), **sc)
+    torch.cuda.synchronize()
+    for la, lb in zip(a, b):
+        for x, y in zip(la, lb):
+            assert torch.equal(x, y)
+    b[1] = [t.clone() for t in G]   # new gradient tensors: new pointers
+    K.adamw_step_multi(list(zip(*b)), **sc)
+    for i in range(len(shapes)):
+        K.adamw_step(a[0][i], G[i].clone(), a[2][i], a[3][i], **sc)
+    torch.cuda.synchronize()
+    for la, lb in zip((a[0], a[2], a[3]), (b[0], b[2], b[3])):
+        for x, y in zip(la, lb):
+            assert torch.equal(x, y)

@@ -103,6 +103,24 @@ def main():
 
 def one(shape, tile, reps):
     """Launch a single (shape, tile) `reps` times -- for rocprofv3 --pmc passes."""
+    if shape in ("swiglu_bwd", "swiglu_fwd"):   # the epilogue-fused MLP GEMMs at the layer's shape
+        x = (torch.rand(T, H, device="cuda") * 2 - 1).to(torch.bfloat16)
+        wd = (torch.rand(H, I, device="cuda") * 0.02).to(torch.bfloat16)
+        wg = (torch.rand(I, H, device="cuda") * 0.02).to(torch.bfloat16)
+        wu = (torch.rand(I, H, device="cuda") * 0.02).to(torch.bfloat16)
+        gu, _ = K.linear_swiglu_fwd(x, wg, wu)
+        fn = (lambda: K.linear_dgrad_swiglu(x, wd, gu)) if shape == "swiglu_bwd" else (lambda: K.linear_swiglu_fwd(x, wg, wu))
+        for _ in range(3):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        print(json.dumps({"shape": shape, "us": round(ms * 1e3, 1), "tflops": round(2.0 * T * 2 * I * H / ms / 1e9 / (2 if shape == "swiglu_bwd" else 1), 1)}))
+        return
     for name, M, N, Kd, ak, bk in SHAPES:
         if name == shape:
             tf, err, ms = run(name, M, N, Kd, ak, bk, tile, reps=reps)
@@ -110,6 +128,8 @@ def one(shape, tile, reps):
 
 
 if __name__ == "__main__":
+    if os.environ.get("PT_LIB"):   # A/B: load another build of the library (before any launch)
+        K._C.load_library(os.path.abspath(os.environ["PT_LIB"]), strict=False)
     if len(sys.argv) > 1 and sys.argv[1] == "one":
         one(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]) if len(sys.argv) > 4 else 5)
     else:
