@@ -53,7 +53,9 @@ def log(*a):
 
 
 def cpu_baseline(cfg, tokens):
-    """The oracle's fwd+bwd of the full model over one [1, tokens] micro-batch on the host cores."""
+    """The oracle's training step -- fwd + bwd of the full model and torch's AdamW over every
+    parameter -- on one [1, tokens] micro-batch, on this host's cores (the reference's own path cannot
+    run on the GPU box; the oracle restates it in plain torch)."""
     from oracle import picotron_oracle as O
     import torch.nn.functional as F
     c = dict(hidden_size=cfg.hidden_size, intermediate_size=cfg.intermediate_size,
@@ -62,6 +64,7 @@ def cpu_baseline(cfg, tokens):
     params = O.init_params(c, seed=42)
     for p in params.values():
         p.requires_grad_(True)
+    opt = torch.optim.AdamW(list(params.values()), lr=3e-4)
     d = cfg.hidden_size // cfg.num_attention_heads
     cos, sin = O.get_cos_sin(tokens, d, base=cfg.rope_theta)
     g = torch.Generator().manual_seed(1234)
@@ -70,10 +73,13 @@ def cpu_baseline(cfg, tokens):
     logits = O.llama_forward(ids[:, :-1], params, c, cos.float(), sin.float(), norm=O.rmsnorm_flash_semantics)
     loss = F.cross_entropy(logits.reshape(-1, cfg.vocab_size), ids[:, 1:].reshape(-1))
     loss.backward()
+    opt.step()
     dt = time.perf_counter() - t0
-    return {"value": tokens / dt, "unit": "tokens/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"oracle fp32 fwd+bwd of the same {cfg.num_hidden_layers}-layer model on one [1, {tokens}] "
-                      f"micro-batch ({dt:.1f} s)"}
+    return {"value": tokens / dt, "unit": "tokens/s", "cores": torch.get_num_threads(), "nproc": os.cpu_count(),
+            "kind": "port",
+            "sample": f"oracle fp32 train step (fwd + bwd + torch AdamW) of the same {cfg.num_hidden_layers}-layer "
+                      f"model on one [1, {tokens}] micro-batch ({dt:.1f} s, {torch.get_num_threads()} threads of "
+                      f"{os.cpu_count()} host CPUs)"}
 
 
 MODELS = {"smollm-1.7b": ("SmolLM-1.7B", "SMOLLM_1_7B", 15), "llama2-7b": ("Llama-2-7B", "LLAMA2_7B", 32)}
@@ -241,6 +247,9 @@ def main():
     ap.add_argument("--grad-acc", type=int, default=32)
     ap.add_argument("--cpu-tokens", type=int, default=1024, help="tokens in the cpu_baseline sample (0 = skip)")
     ap.add_argument("--no-probe", action="store_true", help="do not time GEMM launches with events")
+    ap.add_argument("--bucket-mb", type=float, default=25, help="DataParallelBucket bucket_cap_mb (reference: 25)")
+    ap.add_argument("--grad-type", choices=["fp32", "bf16"], default="fp32",
+                    help="DataParallelBucket grad_type: fp32 main_grad (reference default) or bf16")
     ap.add_argument("--dp-bucket", action="store_true",
                     help="N = 1 only: run the DP path anyway (DataParallelBucket, fp32 main_grad, bucket "
                          "all-reduce over a 1-rank RCCL group) -- the per-GPU cost of N > 1 minus the links")
@@ -303,7 +312,8 @@ def main():
     model.to(torch.bfloat16)
     num_params = count_params(model)
     if m.cp_dp_world_size > 1 or force_dp:
-        model = DataParallelBucket(model)
+        model = DataParallelBucket(model, bucket_cap_mb=args.bucket_mb,
+                                   grad_type=torch.bfloat16 if args.grad_type == "bf16" else torch.float32)
         model._force_grad_sync = force_dp
     optimizer = AdamW(model.parameters(), lr=3e-4)
     loader = SyntheticMicroBatchDataLoader(args.mbs, args.seq, args.grad_acc, cfg.vocab_size, device, seed=1234)
@@ -390,7 +400,9 @@ def main():
                "config": {"workload": f"{model_name} dims, {layers} layers, train step (fwd+bwd+AdamW)",
                           "model": model_name, "layers": layers, "micro_batch": args.mbs,
                           "grad_acc": args.grad_acc, "global_batch": args.mbs * args.grad_acc * dp,
-                          "seq_len": args.seq, "parallelism": par + ("-bucket" if force_dp else "")},
+                          "seq_len": args.seq, "parallelism": par + ("-bucket" if force_dp else ""),
+                          **({"bucket_mb": args.bucket_mb, "grad_type": args.grad_type}
+                             if (m.cp_dp_world_size > 1 or force_dp) else {})},
                "roofline": roofline, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
     if world > 1 or force_dp:

@@ -219,6 +219,21 @@ def main():
         gold[f"G4_{tag}"] = dict(q=q, k=k, v=v, o_causal=o_c, lse_causal=l_c, o_full=o_f, lse_full=l_f,
                                  merged_out=out, merged_lse=lse, dO=dO, dq=dq, dk=dk, dv=dv)
 
+    # G4b: one ring step of rank 1 at a shape the flash kernels tile ([1, 2, 128, 64]): the causal
+    # diagonal block, then the full block of rank 0's K/V, merged by update_out_and_lse -- in bf16
+    # (the reference's bf16 LSE) and in f32 from the SAME bf16-representable inputs
+    g4 = torch.Generator().manual_seed(4242)   # its own stream: the later fixtures stay as they were
+    base = [torch.randn(1, 2, 128, 64, generator=g4).to(torch.bfloat16) for _ in range(5)]
+    for dt in (torch.float32, torch.bfloat16):
+        tag = "f32" if dt == torch.float32 else "bf16"
+        q1, k0, v0, k1, v1 = (t.to(dt) for t in base)
+        sc = 1 / math.sqrt(64)
+        o_c, l_c = CP.ring_attention_forward(q1, k1, v1, sc, True)
+        o_f, l_f = CP.ring_attention_forward(q1, k0, v0, sc, False)
+        out, lse = CP.update_out_and_lse(None, None, o_c, l_c)
+        out, lse = CP.update_out_and_lse(out, lse, o_f, l_f)
+        gold[f"G4b_{tag}"] = dict(q1=q1, k0=k0, v0=v0, k1=k1, v1=v1, out=out, lse=lse)
+
     # G5: MLP fwd/bwd
     mlp = M.MLP(cfg)
     x = torch.randn(2, 5, 64, generator=g, requires_grad=True)

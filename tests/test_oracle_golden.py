@@ -169,3 +169,18 @@ def test_data_parallel_bucket_golden():
     for r in range(dp):
         for n, p in params.items():
             close(g[f"rank{r}.grad.{n}"], p.grad, rtol=1e-4, atol=1e-5)
+
+
+def test_ring_step_golden_g4b():
+    """G4b: rank 1's ring step (causal diagonal + full off-diagonal block, update_out_and_lse) as
+    the reference computes it, in f32 and bf16 -- the oracle's pieces reproduce both."""
+    for tag in ("f32", "bf16"):
+        g = load(f"G4b_{tag}")
+        sc = 1 / math.sqrt(64)
+        o_c, l_c = O.ring_attention_forward(g["q1"], g["k1"], g["v1"], sc, True)
+        o_f, l_f = O.ring_attention_forward(g["q1"], g["k0"], g["v0"], sc, False)
+        out, lse = O.update_out_and_lse(None, None, o_c, l_c)
+        out, lse = O.update_out_and_lse(out, lse, o_f, l_f)
+        tol = dict(rtol=1e-5, atol=1e-6) if tag == "f32" else dict(rtol=0, atol=0)
+        close(out, g["out"], **tol)
+        close(lse, g["lse"], **tol)
