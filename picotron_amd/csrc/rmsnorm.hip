@@ -8,56 +8,91 @@
 //   * picotron/model.py:207-208 the residual `x + f(x)` in bf16, fused in front of the
 //     following norm:   z = bf16(x + r), y = norm(z); z is written out as the new residual stream.
 //
-// Layout: rows x cols, row-major bf16, cols % 8 == 0.  One wavefront owns one row
-// (grid-strided); each lane holds NCH 16-byte chunks of the row in registers, so x
-// is read from HBM exactly once.  HBM-bound: fwd moves 4*rows*cols bytes (6 with the
-// residual), bwd 6*rows*cols (+2 with the fused residual gradient).
+// Layout: rows x cols, row-major bf16, cols % 8 == 0.  One wavefront owns one row at a time; each
+// lane holds NCH 16-byte chunks of the row in registers, so every input is read from HBM exactly
+// once.  HBM-bound: fwd moves 4*rows*cols bytes (8 with the residual: x, r in; z, y out), bwd
+// 8*rows*cols with the fused residual gradient (dy, z, dres in; dx out).
+//
+// Rows are grid-strided over a grid sized so that every block is resident at once (at the layer's
+// 4096 rows: one row per wave, all loads in flight from the start); the register budget is kept
+// at <= 128 VGPRs for that (see the backward's second pass).
 #include "common.h"
+
+#include <stdlib.h>
 
 namespace {
 
-constexpr int kWavesPerBlock = 4;
-constexpr int kThreads = kWavesPerBlock * PT_WAVE;
+constexpr int kCUs = 256;
+
+// launch shape: waves per block and blocks per CU (grid cap) of the forward and backward kernels.
+// Measured at T 4096 (tools/norm_bench.py, profiles/r02_norm_bench.log): 4 x 4 / 8 x 2; PT_NORM
+// ("fwd_wpb,fwd_bpc,bwd_wpb,bwd_bpc", read once) overrides it for such sweeps.
+struct NormCfg { int fwd_wpb, fwd_bpc, bwd_wpb, bwd_bpc; };
+
+const NormCfg& norm_cfg() {
+  static const NormCfg cfg = [] {
+    NormCfg c{4, 4, 8, 2};
+    if (const char* e = getenv("PT_NORM")) sscanf(e, "%d,%d,%d,%d", &c.fwd_wpb, &c.fwd_bpc, &c.bwd_wpb, &c.bwd_bpc);
+    return c;
+  }();
+  return cfg;
+}
 
 template <int NCH>
-__global__ __launch_bounds__(kThreads) void rmsnorm_fwd_kernel(
+__device__ __forceinline__ void load_row(const uint16_t* __restrict__ p, int lane, int nchunk, bf16x8 (&v)[NCH]) {
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int c = lane + i * PT_WAVE;
+    if (c < nchunk) v[i] = ld8(p + c * 8);
+  }
+}
+
+// waves per SIMD the register allocation must allow: every block resident at once (NCH <= 4)
+template <int NCH>
+constexpr int min_waves() { return NCH <= 4 ? 4 : 2; }
+
+template <int NCH, int WPB>
+__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(min_waves<NCH>()))) void rmsnorm_fwd_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ res, const uint16_t* __restrict__ w,
     uint16_t* __restrict__ y, uint16_t* __restrict__ z_out, float* __restrict__ rstd_out,
     int64_t rows, int cols, float eps, int mode) {
   const int lane = threadIdx.x & 63;
-  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
+  const int64_t stride = (int64_t)gridDim.x * WPB;
+  int64_t row = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
   const int nchunk = cols >> 3;
   const float inv_cols = 1.0f / (float)cols;
 
-  // weight chunks are row-invariant: keep them in registers across rows
-  float wf[NCH][8];
-#pragma unroll
-  for (int i = 0; i < NCH; ++i) {
-    const int c = lane + i * PT_WAVE;
-    if (c < nchunk) unpack8(ld8(w + c * 8), wf[i]);
-  }
+  bf16x8 wv[NCH];  // row-invariant weight chunks
+  load_row<NCH>(w, lane, nchunk, wv);
 
-  for (int64_t row = wave; row < rows; row += nwaves) {
-    const uint16_t* xr = x + row * cols;
-    float v[NCH][8];
+  for (; row < rows; row += stride) {
+    bf16x8 xc[NCH], rc[NCH];
+    load_row<NCH>(x + row * cols, lane, nchunk, xc);
+    if (res) load_row<NCH>(res + row * cols, lane, nchunk, rc);
     float ss = 0.f;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int c = lane + i * PT_WAVE;
       if (c < nchunk) {
-        unpack8(ld8(xr + c * 8), v[i]);
+        float v[8];
+        unpack8(xc[i], v);
         if (res) {
           float r[8];
-          unpack8(ld8(res + row * cols + c * 8), r);
+          unpack8(rc[i], r);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[i][j] = round_bf(v[i][j] + r[j]);  // bf16 residual stream
-          st8(z_out + row * cols + c * 8, pack8(v[i]));
+          for (int j = 0; j < 8; ++j) v[j] = round_bf(v[j] + r[j]);  // bf16 residual stream
+          xc[i] = pack8(v);                                           // exact: v is bf16-valued
+          st8(z_out + row * cols + c * 8, xc[i]);
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+        for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
       }
     }
+    // keep the row packed (bf16) across the reduction, not as 8*NCH f32 registers
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) asm volatile("" : "+v"(xc[i].w[k]), "+v"(wv[i].w[k]));
     ss = wave_sum(ss);
     const float rstd = rsqrtf(ss * inv_cols + eps);
     if (lane == 0) rstd_out[row] = rstd;
@@ -65,13 +100,15 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_fwd_kernel(
     for (int i = 0; i < NCH; ++i) {
       const int c = lane + i * PT_WAVE;
       if (c < nchunk) {
-        float o[8];
+        float v[8], o[8], wf[8];
+        unpack8(xc[i], v);
+        unpack8(wv[i], wf);
         if (mode == 0) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = v[i][j] * rstd * wf[i][j];
+          for (int j = 0; j < 8; ++j) o[j] = v[j] * rstd * wf[j];
         } else {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = wf[i][j] * round_bf(v[i][j] * rstd);
+          for (int j = 0; j < 8; ++j) o[j] = wf[j] * round_bf(v[j] * rstd);
         }
         st8(y + row * cols + c * 8, pack8(o));
       }
@@ -81,73 +118,73 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_fwd_kernel(
 
 // dz = rstd * (dxh - xh * mean(dxh * xh)),  dxh = dy * w,  xh = z * rstd
 // dx = dz (+ dres when the residual branch gradient is fused in)
-// dw partial per block: sum over this block's rows of dy * xh (mode 1: dy * bf16(xh))
-// One row per wave at a time, kBwdWaves(NCH) waves per block (rows grid-strided): every load of a
-// row (z, dy, dres) is issued before the row's reduction, and many waves per SIMD keep HBM busy
-// (the kernel is HBM-bound: 8 bytes per element with the fused residual gradient).
-template <int NCH>
-constexpr int bwd_waves() { return NCH <= 4 ? 8 : 4; }
-constexpr int kBwdGridCap = 1024;
-
-template <int NCH>
-__global__ __launch_bounds__(bwd_waves<NCH>() * 64) void rmsnorm_bwd_kernel(
+// dw partial per block: sum over this block's rows of dy * xh (mode 1: dy * bf16(xh)), the block's
+// waves combined through LDS in a fixed order -> one partial row per block (deterministic).
+template <int NCH, int WPB>
+__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(min_waves<NCH>()))) void rmsnorm_bwd_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ z, const uint16_t* __restrict__ w,
     const float* __restrict__ rstd_in, const uint16_t* __restrict__ dres, uint16_t* __restrict__ dx,
     float* __restrict__ dw_partial, int64_t rows, int cols, int mode) {
-  constexpr int WPB = bwd_waves<NCH>();
-  __shared__ float red[WPB][NCH * PT_WAVE * 8];
+  extern __shared__ float red[];  // [WPB][cols]
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int nchunk = cols >> 3;
   const float inv_cols = 1.0f / (float)cols;
+  const int64_t stride = (int64_t)gridDim.x * WPB;
+  int64_t row = (int64_t)blockIdx.x * WPB + wid;
 
   bf16x8 wv[NCH];
-  float dwacc[NCH][8];
-#pragma unroll
-  for (int i = 0; i < NCH; ++i) {
-    const int c = lane + i * PT_WAVE;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dwacc[i][j] = 0.f;
-    if (c < nchunk) wv[i] = ld8(w + c * 8);
+  load_row<NCH>(w, lane, nchunk, wv);
+  // the wave's dw accumulator is its own LDS row (not 8*NCH registers): read-modify-written once
+  // per chunk per row, no barrier needed until the cross-wave combine
+  float* dwrow = red + wid * cols;
+  for (int c = lane; c < nchunk; c += PT_WAVE) {
+    *(float4*)(dwrow + c * 8) = make_float4(0.f, 0.f, 0.f, 0.f);
+    *(float4*)(dwrow + c * 8 + 4) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 
-  for (int64_t row = (int64_t)blockIdx.x * WPB + wid; row < rows; row += (int64_t)gridDim.x * WPB) {
-    bf16x8 zr[NCH], dr[NCH], rr[NCH];
+  for (; row < rows; row += stride) {
+    bf16x8 zc[NCH], dc[NCH], rc[NCH];
+    load_row<NCH>(z + row * cols, lane, nchunk, zc);
+    load_row<NCH>(dy + row * cols, lane, nchunk, dc);
+    if (dres) load_row<NCH>(dres + row * cols, lane, nchunk, rc);
     const float rstd = rstd_in[row];
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int c = lane + i * PT_WAVE;
-      if (c < nchunk) {
-        zr[i] = ld8(z + row * cols + c * 8);
-        dr[i] = ld8(dy + row * cols + c * 8);
-        if (dres) rr[i] = ld8(dres + row * cols + c * 8);
-      }
-    }
     float dot = 0.f;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int c = lane + i * PT_WAVE;
       if (c < nchunk) {
-        float zz[8], d[8], wf[8];
-        unpack8(zr[i], zz);
-        unpack8(dr[i], d);
+        float zz[8], d[8], wf[8], g[8];
+        unpack8(zc[i], zz);
+        unpack8(dc[i], d);
         unpack8(wv[i], wf);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float xh = zz[j] * rstd;
           dot += d[j] * wf[j] * xh;
-          dwacc[i][j] += d[j] * (mode == 0 ? xh : round_bf(xh));
+          g[j] = d[j] * (mode == 0 ? xh : round_bf(xh));
         }
+        float4* acc = (float4*)(dwrow + c * 8);
+        float4 a0 = acc[0], a1 = acc[1];
+        a0.x += g[0]; a0.y += g[1]; a0.z += g[2]; a0.w += g[3];
+        a1.x += g[4]; a1.y += g[5]; a1.z += g[6]; a1.w += g[7];
+        acc[0] = a0; acc[1] = a1;
       }
     }
+    // the f32 unpacked row is not kept live across the reduction (it would double the VGPRs
+    // and halve the waves per CU): the second pass re-expands the packed chunks
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) asm volatile("" : "+v"(zc[i].w[k]), "+v"(dc[i].w[k]), "+v"(wv[i].w[k]));
     dot = wave_sum(dot) * inv_cols;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int c = lane + i * PT_WAVE;
       if (c < nchunk) {
         float zz[8], d[8], wf[8], o[8];
-        unpack8(zr[i], zz);
-        unpack8(dr[i], d);
+        unpack8(zc[i], zz);
+        unpack8(dc[i], d);
         unpack8(wv[i], wf);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -156,7 +193,7 @@ __global__ __launch_bounds__(bwd_waves<NCH>() * 64) void rmsnorm_bwd_kernel(
         }
         if (dres) {
           float r[8];
-          unpack8(rr[i], r);
+          unpack8(rc[i], r);
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] += r[j];
         }
@@ -166,64 +203,42 @@ __global__ __launch_bounds__(bwd_waves<NCH>() * 64) void rmsnorm_bwd_kernel(
   }
 
   // combine the block's waves (fixed order), one partial row per block
-#pragma unroll
-  for (int i = 0; i < NCH; ++i) {
-    const int c = lane + i * PT_WAVE;
-    if (c < nchunk) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) red[wid][c * 8 + j] = dwacc[i][j];
-    }
-  }
   __syncthreads();
   for (int col = threadIdx.x; col < cols; col += WPB * 64) {
     float s = 0.f;
 #pragma unroll
-    for (int k = 0; k < WPB; ++k) s += red[k][col];
+    for (int k = 0; k < WPB; ++k) s += red[k * cols + col];
     dw_partial[(int64_t)blockIdx.x * cols + col] = s;
   }
 }
 
-template <int NCH>
-int bwd_grid(int64_t rows) {
-  const int64_t g = (rows + bwd_waves<NCH>() - 1) / bwd_waves<NCH>();
-  return (int)(g < kBwdGridCap ? g : kBwdGridCap);
-}
-
-// dw[col] = sum_p partial[p][col]  -- fixed summation order, deterministic.  One block per 8
-// columns (256 blocks for cols 2048: every CU): thread t sums partial rows t, t + 256, ... of its
-// block's 8 columns (two 16-B loads per row), then a fixed-shape LDS tree over the 256 threads.
+// dw[col] = sum_p partial[p][col]  -- fixed summation order, deterministic.  One block per 32
+// columns: 8 lanes x 16 B cover a partial row's 32 columns (128 contiguous bytes per row), the 32
+// lane groups of the block stride over the partial rows, then a fixed-order sum over the groups.
 // Sink (flags): 0 store bf16, DW_ACC_BF16 bf16 accumulate (= autograd's grad + bf16(new)),
 // DW_ACC_F32 f32 accumulate (DataParallelBucket main_grad).
-constexpr int kColsumThreads = 256;
-__global__ __launch_bounds__(kColsumThreads) void colsum_kernel(const float* __restrict__ partial, int nparts,
-                                                                int cols, void* __restrict__ out, int sink) {
-  __shared__ float red[kColsumThreads][9];  // +1 pad
-  const int t = threadIdx.x;
-  const int col0 = blockIdx.x * 8;
-  float s[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) s[j] = 0.f;
-  for (int p = t; p < nparts; p += kColsumThreads) {
-    const float4 a = *(const float4*)(partial + (int64_t)p * cols + col0);
-    const float4 b = *(const float4*)(partial + (int64_t)p * cols + col0 + 4);
-    s[0] += a.x; s[1] += a.y; s[2] += a.z; s[3] += a.w;
-    s[4] += b.x; s[5] += b.y; s[6] += b.z; s[7] += b.w;
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) red[t][j] = s[j];
-  __syncthreads();
-  for (int w = kColsumThreads / 2; w >= 8; w >>= 1) {
-    if (t < w) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) red[t][j] += red[t + w][j];
+constexpr int kCsCols = 32, kCsThreads = 256, kCsGroups = kCsThreads / (kCsCols / 4);
+__global__ __launch_bounds__(kCsThreads) void colsum_kernel(const float* __restrict__ partial, int nparts,
+                                                            int cols, void* __restrict__ out, int sink) {
+  __shared__ float red[kCsGroups][kCsCols + 1];
+  const int t = threadIdx.x, ch = t & 7, grp = t >> 3;
+  const int col4 = blockIdx.x * kCsCols + ch * 4;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (col4 < cols) {
+#pragma unroll 4
+    for (int p = grp; p < nparts; p += kCsGroups) {
+      const float4 a = *(const float4*)(partial + (int64_t)p * cols + col4);
+      s0 += a.x; s1 += a.y; s2 += a.z; s3 += a.w;
     }
-    __syncthreads();
   }
-  if (t < 8) {
+  red[grp][ch * 4 + 0] = s0; red[grp][ch * 4 + 1] = s1;
+  red[grp][ch * 4 + 2] = s2; red[grp][ch * 4 + 3] = s3;
+  __syncthreads();
+  const int col = blockIdx.x * kCsCols + t;
+  if (t < kCsCols && col < cols) {
     float v = 0.f;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v += red[k][t];
-    const int col = col0 + t;
+    for (int g = 0; g < kCsGroups; ++g) v += red[g][t];
     if (sink == PT_DW_ACC_F32) {
       ((float*)out)[col] += v;
     } else if (sink == PT_DW_ACC_BF16) {
@@ -244,9 +259,26 @@ int nch_for(int cols) {
   return -1;
 }
 
-int fwd_grid(int64_t rows) {
-  int64_t g = (rows + kWavesPerBlock - 1) / kWavesPerBlock;
-  return (int)(g < PT_STREAM_GRID_CAP ? g : PT_STREAM_GRID_CAP);
+int grid_for(int64_t rows, int wpb, int bpc) {
+  const int64_t g = (rows + wpb - 1) / wpb, cap = (int64_t)kCUs * bpc;
+  return (int)(g < cap ? g : cap);
+}
+
+int bwd_wpb(int nch, const NormCfg& c) { return nch == 8 ? 4 : c.bwd_wpb; }  // LDS: wpb * cols * 4 <= 64 KiB
+
+template <int NCH>
+void launch_fwd(int wpb, int grid, hipStream_t s, const uint16_t* X, const uint16_t* R, const uint16_t* W,
+                uint16_t* Y, uint16_t* Z, float* rstd, int64_t rows, int cols, float eps, int mode) {
+  if (wpb == 8) rmsnorm_fwd_kernel<NCH, 8><<<grid, 512, 0, s>>>(X, R, W, Y, Z, rstd, rows, cols, eps, mode);
+  else rmsnorm_fwd_kernel<NCH, 4><<<grid, 256, 0, s>>>(X, R, W, Y, Z, rstd, rows, cols, eps, mode);
+}
+
+template <int NCH>
+void launch_bwd(int wpb, int grid, hipStream_t s, const uint16_t* DY, const uint16_t* Z, const uint16_t* W,
+                const float* rstd, const uint16_t* DR, uint16_t* DX, float* part, int64_t rows, int cols, int mode) {
+  const size_t lds = (size_t)wpb * cols * sizeof(float);
+  if (wpb == 8) rmsnorm_bwd_kernel<NCH, 8><<<grid, 512, lds, s>>>(DY, Z, W, rstd, DR, DX, part, rows, cols, mode);
+  else rmsnorm_bwd_kernel<NCH, 4><<<grid, 256, lds, s>>>(DY, Z, W, rstd, DR, DX, part, rows, cols, mode);
 }
 
 }  // namespace
@@ -254,13 +286,10 @@ int fwd_grid(int64_t rows) {
 extern "C" {
 
 int pt_rmsnorm_bwd_partials(int64_t rows, int cols) {
-  switch (nch_for(cols)) {  // one partial row per bwd block
-    case 1: return bwd_grid<1>(rows);
-    case 2: return bwd_grid<2>(rows);
-    case 4: return bwd_grid<4>(rows);
-    case 8: return bwd_grid<8>(rows);
-    default: return PT_EUNSUPPORTED;
-  }
+  const int nch = nch_for(cols);
+  if (nch < 0) return PT_EUNSUPPORTED;
+  const NormCfg& c = norm_cfg();
+  return grid_for(rows, bwd_wpb(nch, c), c.bwd_bpc);  // one partial row per bwd block
 }
 
 int pt_rmsnorm_fwd(const void* x, const void* residual, const void* weight, void* y, void* z_out,
@@ -269,18 +298,19 @@ int pt_rmsnorm_fwd(const void* x, const void* residual, const void* weight, void
   if (residual && !z_out) return PT_EINVAL;
   if (!pt_aligned16(x) || !pt_aligned16(weight) || !pt_aligned16(y)) return PT_EALIGN;
   if (residual && (!pt_aligned16(residual) || !pt_aligned16(z_out))) return PT_EALIGN;
-  const int nch = nch_for((int)cols);
+  const NormCfg& c = norm_cfg();
+  const int wpb = c.fwd_wpb == 8 ? 8 : 4;
+  const int grid = grid_for(rows, wpb, c.fwd_bpc);
   const auto* X = (const uint16_t*)x;
   const auto* R = (const uint16_t*)residual;
   const auto* W = (const uint16_t*)weight;
   auto* Y = (uint16_t*)y;
   auto* Z = (uint16_t*)z_out;
-  const dim3 grid(fwd_grid(rows)), block(kThreads);
-  switch (nch) {
-    case 1: rmsnorm_fwd_kernel<1><<<grid, block, 0, stream>>>(X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
-    case 2: rmsnorm_fwd_kernel<2><<<grid, block, 0, stream>>>(X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
-    case 4: rmsnorm_fwd_kernel<4><<<grid, block, 0, stream>>>(X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
-    case 8: rmsnorm_fwd_kernel<8><<<grid, block, 0, stream>>>(X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
+  switch (nch_for((int)cols)) {
+    case 1: launch_fwd<1>(wpb, grid, stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
+    case 2: launch_fwd<2>(wpb, grid, stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
+    case 4: launch_fwd<4>(wpb, grid, stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
+    case 8: launch_fwd<8>(wpb, grid, stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
     default: return PT_EUNSUPPORTED;
   }
   PT_CHECK_LAUNCH();
@@ -298,24 +328,25 @@ int pt_rmsnorm_bwd(const void* dy, const void* z, const void* weight, const floa
   if (nch < 0) return PT_EUNSUPPORTED;
   const int nmode = mode & 3;
   if (nmode > 1 || (mode & PT_DW_ACC_BF16 && mode & PT_DW_ACC_F32)) return PT_EINVAL;
-  const int nparts = pt_rmsnorm_bwd_partials(rows, (int)cols);
+  const NormCfg& c = norm_cfg();
+  const int wpb = bwd_wpb(nch, c) == 8 ? 8 : 4;
+  const int grid = grid_for(rows, wpb, c.bwd_bpc);
   const auto* DY = (const uint16_t*)dy;
   const auto* Z = (const uint16_t*)z;
   const auto* W = (const uint16_t*)weight;
   const auto* DR = (const uint16_t*)dres;
   auto* DX = (uint16_t*)dx;
   switch (nch) {
-    case 1: rmsnorm_bwd_kernel<1><<<bwd_grid<1>(rows), bwd_waves<1>() * 64, 0, stream>>>(DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
-    case 2: rmsnorm_bwd_kernel<2><<<bwd_grid<2>(rows), bwd_waves<2>() * 64, 0, stream>>>(DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
-    case 4: rmsnorm_bwd_kernel<4><<<bwd_grid<4>(rows), bwd_waves<4>() * 64, 0, stream>>>(DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
-    case 8: rmsnorm_bwd_kernel<8><<<bwd_grid<8>(rows), bwd_waves<8>() * 64, 0, stream>>>(DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
+    case 1: launch_bwd<1>(wpb, grid, stream, DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
+    case 2: launch_bwd<2>(wpb, grid, stream, DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
+    case 4: launch_bwd<4>(wpb, grid, stream, DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
+    case 8: launch_bwd<8>(wpb, grid, stream, DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
     default: return PT_EUNSUPPORTED;
   }
   PT_CHECK_LAUNCH();
   if (dweight) {
-    if (cols % 8) return PT_EUNSUPPORTED;
-    colsum_kernel<<<(int)(cols / 8), kColsumThreads, 0, stream>>>(dw_partial, nparts, (int)cols, dweight,
-                                                                  mode & (PT_DW_ACC_BF16 | PT_DW_ACC_F32));
+    colsum_kernel<<<(int)((cols + kCsCols - 1) / kCsCols), kCsThreads, 0, stream>>>(
+        dw_partial, grid, (int)cols, dweight, mode & (PT_DW_ACC_BF16 | PT_DW_ACC_F32));
     PT_CHECK_LAUNCH();
   }
   return PT_OK;
