@@ -83,6 +83,12 @@ int pt_cross_entropy_fwd_lse(const void* logits, int64_t logits_stride, const in
 int pt_cross_entropy_bwd_lse(const void* logits, int64_t logits_stride, const int64_t* targets, const float* row_lse,
                              void* dlogits, int64_t dlogits_stride, int64_t rows, int64_t vocab, const float* scale,
                              int64_t ignore_index, hipStream_t stream);
+/* The same forward from the lm_head GEMM's statistics (pt_gemm_ce_stats) instead of a second pass
+ * over the logits: float2 stats[b * rows + row] = (max, sum exp(x - max)) of the row's bf16 logits
+ * in column tile b < nblk (vocab / nblk columns each); only x[row, target] is read. */
+int pt_cross_entropy_fwd_stats(const void* logits, int64_t logits_stride, const int64_t* targets,
+                               const float* stats, int64_t nblk, float* row_loss, float* row_lse, int64_t rows,
+                               int64_t vocab, int64_t ignore_index, int* status, hipStream_t stream);
 
 /* ---- token embedding ----------------------------------------------------------------------
  * replaces model.py:224-225 (F.embedding + autograd's dense backward) and the masked lookup of
@@ -140,6 +146,12 @@ int pt_gemm_rope(const void* A, int64_t lda, const void* const* B, const int64_t
                  void* C, int64_t ldc, int64_t M, int64_t N, int64_t K, const void* cos_table, const void* sin_table,
                  int64_t table_stride, int64_t seq_len, int64_t rot_cols, int64_t head_dim, int tile,
                  hipStream_t stream);
+/* The lm_head (model.py:270, logits consumed by F.cross_entropy at train.py:49) with the CE forward's
+ * statistics fused into its epilogue: C[M, N] = A[M, K] . W[N, K]^T stored bf16, and per row and
+ * `block`-column tile b the (max, sum exp(x - max)) of the stored values as float2
+ * stats[b * M + row] (block 256 or 128; M % 256 == 0, N % block == 0, K % 64 == 0). */
+int pt_gemm_ce_stats(const void* A, int64_t lda, const void* W, int64_t ldw, void* C, int64_t ldc, float* stats,
+                     int64_t block, int64_t M, int64_t N, int64_t K, hipStream_t stream);
 /* Grouped GEMM: nprob (<= 4) independent problems in ONE launch, each described like pt_gemm's
  * arguments, sharing layouts (a_kcontig, b_kcontig), epilogue and tile (-1 = auto over the
  * group).  Used where one problem alone would leave CUs idle (dW of q|k|v + dW of o_proj). */

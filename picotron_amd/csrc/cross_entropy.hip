@@ -233,6 +233,48 @@ __global__ __launch_bounds__(kThreads) void ce_fwd_stream_kernel(const uint16_t*
   }
 }
 
+// Forward from the lm_head GEMM's statistics (gemm.hip EPI_CE_STATS): float2 stats[b][row] =
+// (m_b, s_b = sum exp(x - m_b)) over the nblk column tiles -> lse = M + log(sum_b s_b exp(m_b - M)),
+// M = max_b m_b; row_loss = lse - x[t].  A block = 32 rows x 8 tile groups: each lane merges every
+// 8th tile of its row online (32 lanes read 256 contiguous bytes of one tile's pairs), then the 8
+// partial merges of a row are combined in a fixed order.  The [rows, V] logits are not read again
+// (only x[t]).
+constexpr int kStatRows = 32, kStatGroups = 8;
+__global__ __launch_bounds__(kStatRows * kStatGroups) void ce_fwd_stats_kernel(
+    const uint16_t* __restrict__ logits, int64_t ls, const int64_t* __restrict__ tgt,
+    const float2* __restrict__ stats, int nblk, float* __restrict__ row_loss, float* __restrict__ row_lse,
+    int64_t rows, int V, int64_t ignore_index, int* __restrict__ status) {
+  __shared__ float2 part[kStatGroups][kStatRows];
+  const int r = threadIdx.x % kStatRows, grp = threadIdx.x / kStatRows;
+  const int64_t row = (int64_t)blockIdx.x * kStatRows + r;
+  float m = -INFINITY, s = 0.f;
+  if (row < rows) {
+    for (int b = grp; b < nblk; b += kStatGroups) {
+      const float2 p = stats[(int64_t)b * rows + row];
+      const float nm = fmaxf(m, p.x);
+      s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (p.x == -INFINITY ? 0.f : p.y * __expf(p.x - nm));
+      m = nm;
+    }
+  }
+  part[grp][r] = make_float2(m, s);
+  __syncthreads();
+  if (grp == 0 && row < rows) {
+    for (int g = 1; g < kStatGroups; ++g) {
+      const float2 p = part[g][r];
+      const float nm = fmaxf(m, p.x);
+      s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (p.x == -INFINITY ? 0.f : p.y * __expf(p.x - nm));
+      m = nm;
+    }
+    const int64_t t = tgt[row];
+    const bool valid = t != ignore_index;
+    const bool bad = valid && (t < 0 || t >= V);
+    const float lse = bad ? __builtin_nanf("") : m + __logf(s);
+    row_lse[row] = lse;
+    row_loss[row] = valid ? lse - (bad ? 0.f : bf2f(logits[row * ls + t])) : 0.f;
+    if (bad && status) status[0] = PT_STATUS_BAD_TARGET;
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void ce_bwd_stream_kernel(const uint16_t* __restrict__ logits, int64_t ls,
                                                                  const int64_t* __restrict__ tgt,
                                                                  const float* __restrict__ row_lse,
@@ -317,6 +359,22 @@ extern "C" int pt_cross_entropy_fwd_bwd(const void* logits, int64_t logits_strid
   else ce_kernel_2pass<<<grid, kThreads, 0, stream>>>(L, logits_stride, targets, D, dlogits_stride, row_loss,
                                                       (int)vocab, scale, inv_count, ignore_index, status);
 #undef PT_CE
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
+
+// Forward (per-row loss + LSE) from the lm_head GEMM's statistics (pt_gemm_ce_stats): float2
+// stats[b * rows + row] = (max, sum exp(x - max)) of the row's logits in column tile b < nblk.
+extern "C" int pt_cross_entropy_fwd_stats(const void* logits, int64_t logits_stride, const int64_t* targets,
+                                          const float* stats, int64_t nblk, float* row_loss, float* row_lse,
+                                          int64_t rows, int64_t vocab, int64_t ignore_index, int* status,
+                                          hipStream_t stream) {
+  if (!logits || !targets || !stats || !row_loss || !row_lse || rows <= 0 || vocab <= 0 || nblk <= 0) return PT_EINVAL;
+  if (vocab % nblk || !pt_aligned16(stats)) return PT_EINVAL;
+  const unsigned grid = (unsigned)((rows + kStatRows - 1) / kStatRows);
+  ce_fwd_stats_kernel<<<grid, kStatRows * kStatGroups, 0, stream>>>((const uint16_t*)logits, logits_stride, targets,
+                                                                  (const float2*)stats, (int)nblk, row_loss, row_lse,
+                                                                  rows, (int)vocab, ignore_index, status);
   PT_CHECK_LAUNCH();
   return PT_OK;
 }

@@ -58,7 +58,13 @@ enum Epilogue {
   EPI_SWIGLU_FWD = 5, EPI_SWIGLU_BWD = 6,
   // EPI_ROPE: the q|k|v projection with RoPE (model.py:136-137) on its q|k columns in the
   // epilogue; head_dim 64 = the wave tile's width, so (d, d + 32) pairs sit in one lane
-  EPI_ROPE = 7
+  EPI_ROPE = 7,
+  // EPI_CE_STATS: the lm_head (model.py:270) storing bf16 logits AND, per row and per output tile
+  // (BN = 256 / 128 columns), the cross-entropy forward's statistics of the stored bf16 values:
+  // (max m, sum exp(x - m)) as float2 stats[(col / BN) * M + row] (tile-major: each workgroup
+  // writes its rows' pairs as one contiguous run) -- the CE forward (train.py:49) then combines
+  // N / BN pairs per row instead of streaming the [M, N] logits again
+  EPI_CE_STATS = 8
 };
 
 // SwiGLU element math, the same expressions as csrc/swiglu.hip (torch's bf16 roundings)
@@ -82,6 +88,7 @@ struct GemmArgs {
   const uint16_t* rope_sin;
   int64_t rope_ld;
   int rope_seq, rope_cols;   // position = row % rope_seq; columns [0, rope_cols) are rotated
+  float* stats;              // EPI_CE_STATS: float2 [N / BN][M], (max, sumexp) per row and tile
   int M, N, K;
   int tiles_m, tiles_n;
   int group_m;
@@ -196,15 +203,53 @@ __device__ __forceinline__ const GemmArgs& select_problem(const GemmGroup& g, in
 
 // Write the wave's TM x TN accumulator tile (FM x FN 16x16 fragments) at output (m0 + wm*TM,
 // n0 + wn*TN).  `st` is this wave's private LDS staging area (TM * (2*TN + 16) bytes).
+// sum / max over the 8 consecutive lanes of a lane's group (lane & ~7): DPP, no LDS round trip
+template <int CTRL>
+__device__ __forceinline__ float dpp8(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float max8(float v) {
+  v = fmaxf(v, dpp8<0xB1>(v));    // quad_perm [1,0,3,2]
+  v = fmaxf(v, dpp8<0x4E>(v));    // quad_perm [2,3,0,1]
+  return fmaxf(v, dpp8<0x141>(v));  // row_half_mirror: lane i <-> 7 - i, the other quad
+}
+__device__ __forceinline__ float sum8(float v) {
+  v += dpp8<0xB1>(v);
+  v += dpp8<0x4E>(v);
+  return v + dpp8<0x141>(v);
+}
+
+// EPI_CE_STATS, after every wave's epilogue wrote its rows' (max, sumexp) over its TN columns into
+// xs[(wm * WN + wn) * TM + row] (and a barrier): the WN = 0 waves merge the WN pairs of each of
+// their TM rows and store them contiguously at stats[(n0 / (WN * TN)) * M + row].
+template <int WN, int TM, int TN>
+__device__ __forceinline__ void ce_stats_merge(const GemmArgs& a, const float2* xs, int m0, int n0, int wm, int lane) {
+  float2* out = (float2*)a.stats + (int64_t)(n0 / (WN * TN)) * a.M + m0 + wm * TM;
+#pragma unroll
+  for (int r = lane; r < TM; r += 64) {
+    float2 p[WN];
+#pragma unroll
+    for (int w = 0; w < WN; ++w) p[w] = xs[(wm * WN + w) * TM + r];
+    float M = p[0].x;
+#pragma unroll
+    for (int w = 1; w < WN; ++w) M = fmaxf(M, p[w].x);
+    float S = 0.f;
+#pragma unroll
+    for (int w = 0; w < WN; ++w) S += p[w].y * __expf(p[w].x - M);
+    out[r] = make_float2(M, S);
+  }
+}
+
 template <int TM, int TN, int EPI>
 __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)[TM / 16][TN / 16], lds_u8* st,
-                                         int m0, int n0, int wm, int wn, int lane) {
+                                         int m0, int n0, int wm, int wn, int lane, float2* xs_wave = nullptr) {
   constexpr int FM = TM / 16, FN = TN / 16;
   const int cs = find_seg(a.cseg, a.ncseg, m0);
   const int64_t ldc = a.ldc[cs];
   const int64_t mrow0 = m0 - a.cseg[cs] + wm * TM;
   const int ncol0 = n0 + wn * TN;
-  if (EPI == EPI_BF16 || EPI == EPI_BF16_ACC || EPI == EPI_BF16_RES || EPI == EPI_SWIGLU_BWD || EPI == EPI_ROPE) {
+  if (EPI == EPI_BF16 || EPI == EPI_BF16_ACC || EPI == EPI_BF16_RES || EPI == EPI_SWIGLU_BWD || EPI == EPI_ROPE ||
+      EPI == EPI_CE_STATS) {
     constexpr int ROWB = TN * 2 + 16;  // +16 B pad: spreads the column-wise 2-B writes over banks
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -298,6 +343,21 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
           st8(dst, pack8(og));
           st8(dst + a.N, pack8(ou));
           continue;
+        }
+        if constexpr (EPI == EPI_CE_STATS) {
+          // the row's TN = 64 columns of this wave are the CPR = 8 consecutive lanes sharing
+          // lane / 8: max and sum-exp of the stored (bf16) values over the 8 x 8, one pair per row
+          static_assert(TN == 64, "CE statistics: 64-column wave tiles (8 lanes per row)");
+          float f[8];
+          unpack8(v, f);
+          const float mx = max8(fmaxf(fmaxf(fmaxf(f[0], f[1]), fmaxf(f[2], f[3])),
+                                      fmaxf(fmaxf(f[4], f[5]), fmaxf(f[6], f[7]))));
+          const float nm = -mx * 1.4426950408889634f;
+          float se = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) se += __builtin_amdgcn_exp2f(fmaf(f[e], 1.4426950408889634f, nm));
+          se = sum8(se);
+          if (ch == 0) xs_wave[row] = make_float2(mx, se);
         }
         if constexpr (EPI == EPI_BF16_ACC || EPI == EPI_BF16_RES) {
           float o[8], f[8];
@@ -650,7 +710,13 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const GemmGroup g) {
   if constexpr (PAIR) {
     epilogue_swiglu_fwd(a, acc, smem + wave * (TM * (32 * 2 + 16)), m0 + wm * TM, tile_n * 128 + wn * 32, lane);
   } else {
-    epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane);
+    // EPI_CE_STATS: per-wave row statistics beside the 8 staging areas (launch_8ph sizes the LDS)
+    float2* xs = (float2*)(smem + 8 * (TM * (TN * 2 + 16)));
+    epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane, xs + wave * TM);
+    if constexpr (EPI == EPI_CE_STATS) {
+      __syncthreads();
+      if (wn == 0) ce_stats_merge<4, TM, TN>(a, xs, m0, n0, wm, lane);
+    }
   }
 }
 
@@ -793,7 +859,12 @@ __global__ __launch_bounds__(512) void gemm_4ph_kernel(const GemmGroup g) {
   if (t + 1 < nk) ktile(t + 1, std::integral_constant<int, 1>{});
   if (!late) bar();
   __syncthreads();
-  epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane);
+  float2* xs = (float2*)(smem + 8 * (TM * (TN * 2 + 16)));  // EPI_CE_STATS row statistics
+  epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane, xs + wave * TM);
+  if constexpr (EPI == EPI_CE_STATS) {
+    __syncthreads();
+    if (wn == 0) ce_stats_merge<2, TM, TN>(a, xs, m0, n0, wm, lane);
+  }
 }
 
 // ================================================================================= simple
@@ -940,7 +1011,7 @@ template <bool AK, bool BKC, int EPI>
 int launch_8ph(GemmGroup g, hipStream_t stream) {
   const int tiles = group_tiles(g, 256, EPI == EPI_SWIGLU_FWD ? 128 : 256);
   constexpr int smem_main = 8 * 128 * BK * 2;
-  constexpr int smem_epi = 8 * 128 * (64 * 2 + 16);
+  constexpr int smem_epi = 8 * 128 * (64 * 2 + 16) + (EPI == EPI_CE_STATS ? 8 * 128 * 8 : 0);
   constexpr int smem = smem_main > smem_epi ? smem_main : smem_epi;
   static_assert(smem <= 160 * 1024, "LDS budget");
   static bool attr_set = false;
@@ -957,7 +1028,7 @@ template <bool AK, bool BKC, int EPI>
 int launch_4ph(GemmGroup g, hipStream_t stream) {
   const int tiles = group_tiles(g, 256, 128);
   constexpr int smem_main = 9 * 128 * BK * 2;
-  constexpr int smem_epi = 8 * 64 * (64 * 2 + 16);
+  constexpr int smem_epi = 8 * 64 * (64 * 2 + 16) + (EPI == EPI_CE_STATS ? 8 * 64 * 8 : 0);
   constexpr int smem = smem_main > smem_epi ? smem_main : smem_epi;
   static_assert(smem <= 160 * 1024, "LDS budget");
   static bool attr_set = false;
@@ -1159,6 +1230,11 @@ int launch_group(GemmGroup& g, int a_kcontig, int b_kcontig, int epilogue, int t
     case EPI_BF16_RES:  // forward projections only (weights K-contiguous)
       if (!a_kcontig || !b_kcontig) return PT_EUNSUPPORTED;
       return launch_layout<true, true, EPI_BF16_RES>(g, tile, stream);
+    case EPI_CE_STATS:  // the lm_head forward: the phased kernels (64-column wave tiles)
+      if (!a_kcontig || !b_kcontig) return PT_EUNSUPPORTED;
+      if (tile == 12) return launch_8ph<true, true, EPI_CE_STATS>(g, stream);
+      if (tile == 13) return launch_4ph<true, true, EPI_CE_STATS>(g, stream);
+      return PT_EUNSUPPORTED;
     default: return PT_EINVAL;
   }
 }
@@ -1236,6 +1312,30 @@ int pt_gemm_rope(const void* A, int64_t lda, const void* const* B, const int64_t
   a.rope_seq = (int)seq_len;
   a.rope_cols = (int)rot_cols;
   return launch_group(g, 1, 1, EPI_ROPE, tile, stream);
+}
+
+// lm_head with the cross-entropy forward statistics fused (EPI_CE_STATS): logits C[M, N] = A[M, K] .
+// W[N, K]^T stored bf16, and float2 stats[N / block][M] = (max, sum exp(x - max)) of the stored
+// values per row and block-column tile (block 256: the 8-phase 256x256 kernel, 128: the 4-phase
+// 256x128 one).  M % 256 == 0, N % block == 0.
+int pt_gemm_ce_stats(const void* A, int64_t lda, const void* W, int64_t ldw, void* C, int64_t ldc, float* stats,
+                     int64_t block, int64_t M, int64_t N, int64_t K, hipStream_t stream) {
+  if (!stats || !pt_aligned16(stats)) return PT_EINVAL;
+  if (block != 256 && block != 128) return PT_EUNSUPPORTED;
+  const int tile = block == 256 ? 12 : 13;
+  GemmGroup g{};
+  g.nprob = 1;
+  const void* const Bs[1] = {W};
+  const int64_t ldbs[1] = {ldw};
+  void* const Cs[1] = {C};
+  const int64_t ldcs[1] = {ldc};
+  const int rc = fill_args(g.p[0], A, lda, Bs, ldbs, nullptr, 1, 0, Cs, ldcs, nullptr, 1, M, N, K, EPI_CE_STATS,
+                           nullptr, 0);
+  if (rc) return rc;
+  if (!args_fit(g.p[0], tile)) return PT_EUNSUPPORTED;
+  if (ldc & 7) return PT_EALIGN;
+  g.p[0].stats = stats;
+  return launch_group(g, 1, 1, EPI_CE_STATS, tile, stream);
 }
 
 // Tile the auto-pick chooses for one [M, N] problem with the given segment boundaries (see

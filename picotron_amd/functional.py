@@ -24,6 +24,7 @@ notify the gradient owner through `param._pt_grad_ready`.
 """
 import math
 import os
+import weakref
 
 import torch
 import torch.distributed as dist
@@ -225,6 +226,67 @@ class LinearFunction(torch.autograd.Function):
 
 def linear(x, weight, tp_reduce_fwd=False, tp_reduce_bwd=False):
     return LinearFunction.apply(x, weight, tp_reduce_fwd, tp_reduce_bwd)
+
+
+# ------------------------------------------------------------------------ lm_head + CE statistics
+# The lm_head GEMM leaves, next to the logits, the CE forward's per-row (max, sum-exp) of the stored
+# bf16 values for each 256- (128-) column output tile (csrc/gemm.hip EPI_CE_STATS).  They travel beside the logits, keyed by the
+# logits' storage: F.cross_entropy on those logits (or a view of them, unmodified -- same version
+# counter) combines V/256 pairs per row instead of streaming the [T, V] logits a second time; any
+# other consumer sees ordinary logits.
+_CE_STATS = {}
+
+
+def _stash_ce_stats(y, stats):
+    for key in [k for k, e in _CE_STATS.items() if e[0]() is None]:
+        del _CE_STATS[key]
+    _CE_STATS[y.data_ptr()] = (weakref.ref(y), y._version, y.numel(), stats)
+
+
+def _take_ce_stats(lg):
+    e = _CE_STATS.pop(lg.data_ptr(), None)
+    if e is None:
+        return None
+    ref, version, numel, stats = e
+    if ref() is None or lg._version != version or lg.numel() != numel or stats.shape[1] != lg.shape[0]:
+        return None
+    return stats
+
+
+def ce_stats_enabled():
+    return os.getenv("PICOTRON_CE_STATS", "1") != "0"
+
+
+class LMHeadFunction(torch.autograd.Function):
+    """final_proj(x) (model.py:270, no bias, tp 1) on the GEMM with the CE statistics epilogue; the
+    backward is LinearFunction's."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        x2 = _contig2d(x)
+        y, stats = K.linear_ce_stats(x2, weight)
+        _stash_ce_stats(y, stats)
+        ctx.save_for_backward(x2, weight)
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight = ctx.saved_tensors
+        dy2 = _contig2d(dy)
+        dx = K.linear_dgrad(dy2, [weight]) if ctx.needs_input_grad[0] else None
+        if ctx.needs_input_grad[1]:
+            wgrad(dy2, x2, [weight])
+        return (dx.view(ctx.xshape) if dx is not None else None), None
+
+
+def lm_head_linear(x, weight):
+    """Y = x W^T for the lm_head: with the CE statistics when the shape tiles, else plain linear."""
+    T = x.numel() // x.shape[-1]
+    if (ce_stats_enabled() and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
+            and K.ce_stats_fusable(T, weight.shape[0]) and x.shape[-1] % 64 == 0):
+        return LMHeadFunction.apply(x, weight)
+    return linear(x, weight)
 
 
 # ------------------------------------------------------------------------ attention block
@@ -474,7 +536,11 @@ class CrossEntropyFunction(torch.autograd.Function):
     def forward(ctx, logits, targets, ignore_index):
         lg = _contig2d(logits)
         tg = targets.reshape(-1)
-        loss, inv_count, row_lse = K.cross_entropy_loss_lse(lg, tg, ignore_index)
+        stats = _take_ce_stats(lg)   # the lm_head GEMM's statistics of exactly these logits, if any
+        if stats is not None:
+            loss, inv_count, row_lse = K.cross_entropy_loss_lse_stats(lg, tg, stats, ignore_index)
+        else:
+            loss, inv_count, row_lse = K.cross_entropy_loss_lse(lg, tg, ignore_index)
         ctx.save_for_backward(lg, tg, inv_count, row_lse)
         ctx.ignore_index, ctx.shape = ignore_index, logits.shape
         return loss.to(logits.dtype)

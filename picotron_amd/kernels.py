@@ -495,6 +495,66 @@ def linear_fwd_rope(x2d, weights, cos, sin, seq_len, rot_heads, head_dim):
     return y
 
 
+EPI_CE_STATS = 8
+
+
+def ce_stats_block(T, V):
+    """Column tile of the lm_head GEMM's CE statistics: 256 (8-phase 256x256 kernel) when V divides,
+    else 128 (4-phase 256x128); None when the shape does not tile (T % 256)."""
+    if T % 256:
+        return None
+    return 256 if V % 256 == 0 else (128 if V % 128 == 0 else None)
+
+
+def ce_stats_fusable(T, V):
+    return ce_stats_block(T, V) is not None
+
+
+def linear_ce_stats(x2d, weight):
+    """lm_head (model.py:270) with the CE forward's statistics in the GEMM epilogue: returns (logits
+    [T, V] bf16, stats [V / block, T, 2] f32 = per column tile and row (max, sum exp(x - max)) of
+    the stored bf16 logits)."""
+    _bf16_rowmajor(x2d, "x")
+    T, K = x2d.shape
+    V = weight.shape[0]
+    _req(weight.dtype == BF16 and weight.is_contiguous() and weight.shape[1] == K, "weight must be contiguous [V, K] bf16")
+    block = ce_stats_block(T, V)
+    _req(block is not None and K % 64 == 0, "linear_ce_stats: T % 256, V % 128, K % 64")
+    y = torch.empty(T, V, dtype=BF16, device=x2d.device)
+    stats = torch.empty(V // block, T, 2, dtype=torch.float32, device=x2d.device)
+    probe = _PROBE
+    if probe is not None:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    rc = _C.lib().pt_gemm_ce_stats(_ptr(x2d), x2d.stride(0), _ptr(weight), K, _ptr(y), y.stride(0), _ptr(stats),
+                                   block, T, V, K, _C.stream_ptr(x2d.device))
+    _C.check(rc, "pt_gemm_ce_stats")
+    if probe is not None:
+        ev1.record()
+        probe.records.append((ev0, ev1, 2.0 * T * V * K, _alg_bytes(T, V, K, EPI_BF16)))
+    return y, stats
+
+
+def cross_entropy_loss_lse_stats(logits, targets, stats, ignore_index=-100):
+    """cross_entropy_loss_lse from the lm_head GEMM's statistics (linear_ce_stats): same outputs,
+    the logits are not streamed again (only x[row, target] is read)."""
+    _bf16_rowmajor(logits, "logits")
+    rows, vocab = logits.shape
+    _req(targets.dtype == torch.int64 and targets.numel() == rows, "targets: int64 [rows]")
+    _req(stats.dtype == torch.float32 and stats.is_contiguous() and stats.dim() == 3 and stats.shape[1:] == (rows, 2)
+         and vocab % stats.shape[0] == 0, "stats: f32 [nblk, rows, 2]")
+    targets = targets.contiguous()
+    inv_count = (1.0 / (targets != ignore_index).sum().to(torch.float32)).reshape(1)
+    row_loss = torch.empty(rows, dtype=torch.float32, device=logits.device)
+    row_lse = torch.empty(rows, dtype=torch.float32, device=logits.device)
+    rc = _C.lib().pt_cross_entropy_fwd_stats(_ptr(logits), logits.stride(0), _ptr(targets), _ptr(stats),
+                                             stats.shape[0], _ptr(row_loss), _ptr(row_lse), rows, vocab,
+                                             int(ignore_index), _ptr(status_word(logits.device)),
+                                             _C.stream_ptr(logits.device))
+    _C.check(rc, "pt_cross_entropy_fwd_stats")
+    return row_loss.sum() * inv_count[0], inv_count, row_lse
+
+
 def swiglu_fusable(T, I, backward=False):
     """Shapes the SwiGLU-fused projections tile (8-phase kernel: T % 256, I % 128 (fwd) / 256 (bwd))."""
     return T % 256 == 0 and I % (256 if backward else 128) == 0

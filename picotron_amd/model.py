@@ -168,6 +168,8 @@ class Linear(nn.Module):
             nn.init.uniform_(self.bias, -bound, bound)
 
     def forward(self, x):
+        if getattr(self, "_pt_lm_head", False) and self.bias is None:
+            return FN.as_logits(FN.lm_head_linear(x, self.weight))
         y = FN.linear(x, self.weight)
         y = y if self.bias is None else y + self.bias
         # the lm_head (Llama tags its final_proj): keep F.cross_entropy on the HIP kernel also when
@@ -330,8 +332,10 @@ def lm_head(final_proj, x):
     init_model_with_materialized_weights swaps in (checkpoint.py:89-91) -- is run through
     functional.linear on its weight (+ bias) instead of torch's GEMM."""
     if type(final_proj) is nn.Linear:
-        y = FN.linear(x, final_proj.weight)
-        y = y if final_proj.bias is None else y + final_proj.bias
+        if final_proj.bias is None:
+            y = FN.lm_head_linear(x, final_proj.weight)
+        else:
+            y = FN.linear(x, final_proj.weight) + final_proj.bias
     else:
         y = final_proj(x)
     return FN.as_logits(y)

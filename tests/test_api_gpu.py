@@ -182,12 +182,12 @@ def test_lm_head_swapped_for_torch_linear_stays_on_hip_gemm():
     with torch.no_grad():
         model.final_proj.weight.copy_(w)
     calls = []
-    orig = FN.linear
-    FN.linear = lambda *a, **k: (calls.append(a[1].shape), orig(*a, **k))[1]
+    orig = FN.lm_head_linear
+    FN.lm_head_linear = lambda *a, **k: (calls.append(a[1].shape), orig(*a, **k))[1]
     try:
         after = model(ids)
     finally:
-        FN.linear = orig
+        FN.lm_head_linear = orig
     assert calls == [w.shape] and isinstance(after, FN.HipLogits)
     assert torch.equal(after.detach().as_subclass(torch.Tensor), before.as_subclass(torch.Tensor))
 
@@ -206,3 +206,83 @@ def test_frozen_weights_get_no_gradient():
     for n, p in model.named_parameters():
         if p.requires_grad:
             assert p.grad is not None and torch.isfinite(p.grad.float()).all(), n
+
+
+def test_lm_head_ce_statistics_epilogue():
+    """pt_gemm_ce_stats: the logits are bit-identical to the plain lm_head GEMM on the same tile, and
+    each row's (max, sum exp(x - max)) per 256- (8-phase) or 128-column (4-phase) tile equals torch's
+    on the stored bf16 logits (max exact, sum rel 1e-5)."""
+    from picotron_amd import kernels as K
+    g = torch.Generator(device="cuda").manual_seed(11)
+    for T, H, V in ((512, 256, 1536), (256, 128, 640)):   # block 256 / block 128
+        x = (torch.randn(T, H, device="cuda", generator=g)).to(BF)
+        w = (torch.randn(V, H, device="cuda", generator=g) * 0.2).to(BF)
+        y, stats = K.linear_ce_stats(x, w)
+        block = K.ce_stats_block(T, V)
+        assert stats.shape == (V // block, T, 2)
+        assert torch.equal(y, K.linear_fwd(x, [w], tile=12 if block == 256 else 13))
+        blk = y.float().view(T, V // block, block).transpose(0, 1)
+        m = blk.amax(-1)
+        se = torch.exp(blk - m[..., None]).sum(-1)
+        torch.testing.assert_close(stats[..., 0], m, rtol=0, atol=0)
+        torch.testing.assert_close(stats[..., 1], se, rtol=1e-5, atol=1e-6)
+
+
+def test_cross_entropy_from_lm_head_statistics():
+    """Llama forward + F.cross_entropy with the lm_head's statistics (PICOTRON_CE_STATS=1, default)
+    against the streaming CE kernel (=0): loss within 1e-6 relative, every gradient within 1e-3;
+    the statistics are used only for the unmodified logits they were computed from."""
+    from picotron_amd import functional as FN
+    from picotron_amd import kernels as K
+    ids = torch.randint(0, 512, (2, 129), generator=torch.Generator().manual_seed(8)).cuda()
+    res = {}
+    for flag in ("1", "0"):
+        os.environ["PICOTRON_CE_STATS"] = flag
+        try:
+            model, cfg = _tiny_llama()
+            used = []
+            orig = K.cross_entropy_loss_lse_stats
+            K.cross_entropy_loss_lse_stats = lambda *a, **k: (used.append(1), orig(*a, **k))[1]
+            try:
+                loss = F.cross_entropy(model(ids[:, :-1]).view(-1, cfg.vocab_size), ids[:, 1:].reshape(-1))
+            finally:
+                K.cross_entropy_loss_lse_stats = orig
+            loss.backward()
+            res[flag] = (loss.float().item(), {n: p.grad.float().clone() for n, p in model.named_parameters()}, used)
+        finally:
+            os.environ.pop("PICOTRON_CE_STATS", None)
+    assert res["1"][2] == [1] and res["0"][2] == []
+    assert abs(res["1"][0] - res["0"][0]) <= 1e-6 * abs(res["0"][0])
+    for n, gr in res["0"][1].items():
+        assert rel(res["1"][1][n], gr) < 1e-3, n
+    # logits changed in place after the GEMM: the statistics no longer describe them -> streaming path
+    model, cfg = _tiny_llama()
+    used = []
+    orig = K.cross_entropy_loss_lse_stats
+    K.cross_entropy_loss_lse_stats = lambda *a, **k: (used.append(1), orig(*a, **k))[1]
+    try:
+        with torch.no_grad():
+            logits = model(ids[:, :-1])
+            logits.mul_(0.5)
+            l_mod = F.cross_entropy(logits.view(-1, cfg.vocab_size), ids[:, 1:].reshape(-1))
+    finally:
+        K.cross_entropy_loss_lse_stats = orig
+    plain = logits.detach().as_subclass(torch.Tensor).float()
+    ref = F.cross_entropy(plain.view(-1, cfg.vocab_size), ids[:, 1:].reshape(-1))
+    assert used == [] and abs(l_mod.float().item() - ref.item()) < 1e-2 * abs(ref.item())
+
+
+def test_cross_entropy_stats_bad_target():
+    from picotron_amd import functional as FN
+    from picotron_amd import kernels as K
+    from picotron_amd._C import HipKernelError
+    K.device_status(torch.device("cuda"))
+    x = torch.randn(256, 128, device="cuda").to(BF)
+    w = (torch.randn(1024, 128, device="cuda") * 0.1).to(BF)
+    y = FN.LMHeadFunction.apply(x, w)
+    tgt = torch.randint(0, 1024, (256,), device="cuda")
+    tgt[3] = 5000
+    loss = FN.cross_entropy(y, tgt)
+    assert math.isnan(loss.float().item())
+    with pytest.raises(HipKernelError, match="outside"):
+        K.check_device_status(torch.device("cuda"))

@@ -1,8 +1,13 @@
 """Attention microbenchmark at the decoder layer's shape (SmolLM-1.7B: B 4, S 1024, 32 heads, d 64,
-causal), q/k/v as strided views of one fused [T, 3 H d] projection like the model.  Prints us and
-TF/s (causal FLOP: fwd 2 GEMMs, bwd dK/dV kernel 4, dQ kernel 3, each 2 B h S^2 d / 2).
+causal), q/k/v as strided views of one fused [T, 3 H d] projection like the model.  Prints us per
+call from a HIP graph of `reps` back-to-back calls (no host gaps between launches) and TF/s (causal
+FLOP: fwd 2 GEMMs, bwd 5 = the algorithm's, bwd_kernel 7 = what the dK/dV (4) + dQ (3) kernels run;
+each 2 B h S^2 d / 2).
 
-    python tools/attn_bench.py [--reps 20] [--B 4 --S 1024 --H 32 --D 64]
+    python tools/attn_bench.py [--reps 20] [--B 4 --S 1024 --H 32 --D 64] [--old lib.so]
+
+--old: a library holding another build of the pt_attn_* entry points, timed in the same process
+(rounds interleaved) and compared element-wise with this build's outputs.
 """
 import argparse
 import json
@@ -12,19 +17,33 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from picotron_amd import _C  # noqa: E402
 from picotron_amd import kernels as K  # noqa: E402
 
 
-def timeit(fn, reps):
-    for _ in range(3):
-        fn()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        fn()
-    e1.record()
+def graph_us(fn, reps, rounds=3):
+    fn()
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / reps * 1e3
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    best = []
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        best.append(e0.elapsed_time(e1) / reps * 1e3)
+    return min(best)
 
 
 def main():
@@ -34,27 +53,36 @@ def main():
     ap.add_argument("--S", type=int, default=1024)
     ap.add_argument("--H", type=int, default=32)
     ap.add_argument("--D", type=int, default=64)
-    ap.add_argument("--lib", default="", help="load this libpicotron_hip.so instead (A/B runs)")
+    ap.add_argument("--old", default="")
     a = ap.parse_args()
-    if a.lib:
-        K._C.load_library(os.path.abspath(a.lib))
     B, S, H, D = a.B, a.S, a.H, a.D
     g = torch.Generator(device="cuda").manual_seed(0)
     qkv = torch.randn(B, S, 3, H, D, device="cuda", generator=g).to(torch.bfloat16)
     q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
     do = torch.randn(B, S, H, D, device="cuda", generator=g).to(torch.bfloat16)
     scale = D ** -0.5
-    o, lse = K.attn_fwd(q, k, v, scale, True)
-    delta = K.attn_delta(do, o)
     unit = 2.0 * B * H * S * S * D / 2
-    t_fwd = timeit(lambda: K.attn_fwd(q, k, v, scale, True, out=o, lse=lse), a.reps)
-    t_delta = timeit(lambda: K.attn_delta(do, o), a.reps)
-    t_bwd = timeit(lambda: K.attn_bwd(do, q, k, v, o, lse, scale, True, delta=delta), a.reps)
-    print(json.dumps({"lib": a.lib or "in-tree", "B": B, "S": S, "H": H, "D": D,
-                      "fwd_us": round(t_fwd, 1), "fwd_tflops": round(2 * unit / t_fwd / 1e6, 1),
-                      "delta_us": round(t_delta, 1),
-                      "bwd_us": round(t_bwd, 1), "bwd_tflops": round(5 * unit / t_bwd / 1e6, 1),
-                      "bwd_kernel_flop_tflops": round(7 * unit / t_bwd / 1e6, 1)}), flush=True)
+    libs = {"new": _C.load_library()}
+    if a.old:
+        libs["old"] = _C.load_library(os.path.abspath(a.old), strict=False)
+    outs = {}
+    for rnd in range(2):
+        for name, lib in libs.items():
+            _C._lib = lib
+            o, lse = K.attn_fwd(q, k, v, scale, True)
+            delta = K.attn_delta(do, o)
+            dq, dk, dv, _ = K.attn_bwd(do, q, k, v, o, lse, scale, True, delta=delta)
+            outs[name] = [t.clone() for t in (o, lse, dq, dk, dv)]
+            t_fwd = graph_us(lambda: K.attn_fwd(q, k, v, scale, True, out=o, lse=lse), a.reps)
+            t_bwd = graph_us(lambda: K.attn_bwd(do, q, k, v, o, lse, scale, True, delta=delta), a.reps)
+            print(json.dumps({"lib": f"{name}:r{rnd}", "B": B, "S": S, "H": H, "D": D,
+                              "fwd_us": round(t_fwd, 1), "fwd_tflops": round(2 * unit / t_fwd / 1e6, 1),
+                              "bwd_us": round(t_bwd, 1), "bwd_tflops": round(5 * unit / t_bwd / 1e6, 1),
+                              "bwd_kernel_flop_tflops": round(7 * unit / t_bwd / 1e6, 1)}), flush=True)
+    _C._lib = libs["new"]
+    if "old" in outs:
+        rel = [((x.float() - y.float()).norm() / y.float().norm()).item() for x, y in zip(outs["new"], outs["old"])]
+        print(json.dumps({"new_vs_old_rel_o_lse_dq_dk_dv": rel}), flush=True)
 
 
 if __name__ == "__main__":
