@@ -90,6 +90,12 @@ int pt_cross_entropy_fwd_stats(const void* logits, int64_t logits_stride, const 
                                const float* stats, int64_t nblk, float* row_loss, float* row_lse, int64_t rows,
                                int64_t vocab, int64_t ignore_index, int* status, hipStream_t stream);
 
+/* train.py:49's reduction='mean' over the per-row losses: loss = sum(row_loss) / #(target !=
+ * ignore_index) in one deterministic launch; inv_count = 1 / #valid (the backward's scale);
+ * loss_f32 / out (bf16 when out_bf16, else f32) optional. */
+int pt_cross_entropy_mean(const float* row_loss, const int64_t* targets, int64_t rows, int64_t ignore_index,
+                          float* loss_f32, float* inv_count, void* out, int out_bf16, hipStream_t stream);
+
 /* ---- token embedding ----------------------------------------------------------------------
  * replaces model.py:224-225 (F.embedding + autograd's dense backward) and the masked lookup of
  * VocabParallelEmbedding (tensor_parallel.py:246-270): rows of ids outside [vocab_lo, vocab_hi)
@@ -101,6 +107,12 @@ int pt_embedding_fwd(const int64_t* ids, int64_t T, const void* weight, int64_t 
                      void* out, int64_t ldo, int64_t H, hipStream_t stream);
 int pt_embedding_bwd(const int64_t* sorted_ids, const int64_t* perm, int64_t T, const void* dy, int64_t ldy,
                      int64_t vocab_lo, void* dweight, int64_t lddw, int64_t H, int sink, hipStream_t stream);
+/* The backward's segment order: ids keyed (0 = skipped: outside [vocab_lo, vocab_hi) or padding_idx
+ * when has_padding; else id - vocab_lo + 1) and stably sorted in one launch -> sorted_ids (-1 =
+ * skip) and perm (token positions), the inputs of pt_embedding_bwd.  T <= 16384 (else
+ * PT_EUNSUPPORTED). */
+int pt_embedding_sort(const int64_t* ids, int64_t T, int64_t vocab_lo, int64_t vocab_hi, int has_padding,
+                      int64_t padding_idx, int64_t* sorted_ids, int64_t* perm, hipStream_t stream);
 
 /* ---- fused AdamW step ---------------------------------------------------------------------
  * replaces train.py:209 torch.optim.AdamW(...).step() for one tensor: the eight foreach passes of

@@ -275,6 +275,45 @@ __global__ __launch_bounds__(kStatRows * kStatGroups) void ce_fwd_stats_kernel(
   }
 }
 
+// mean over the valid rows (train.py:49's reduction='mean'): loss = sum(row_loss) / #valid, in ONE
+// block with a fixed-shape reduction (deterministic); also 1/#valid for the backward and the loss in
+// the logits' dtype.  #valid == 0 gives 0 * inf = NaN, as F.cross_entropy's mean does.
+constexpr int kMeanThreads = 1024;
+__global__ __launch_bounds__(kMeanThreads) void ce_mean_kernel(const float* __restrict__ row_loss,
+                                                               const int64_t* __restrict__ tgt, int64_t rows,
+                                                               int64_t ignore_index, float* __restrict__ loss_f32,
+                                                               float* __restrict__ inv_count, void* __restrict__ out,
+                                                               int out_bf16) {
+  __shared__ float ssum[kMeanThreads];
+  __shared__ int scnt[kMeanThreads];
+  float s = 0.f;
+  int c = 0;
+  for (int64_t r = threadIdx.x; r < rows; r += kMeanThreads) {
+    s += row_loss[r];
+    c += tgt[r] != ignore_index;
+  }
+  ssum[threadIdx.x] = s;
+  scnt[threadIdx.x] = c;
+  __syncthreads();
+  for (int w = kMeanThreads / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      ssum[threadIdx.x] += ssum[threadIdx.x + w];
+      scnt[threadIdx.x] += scnt[threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float inv = 1.0f / (float)scnt[0];
+    const float loss = ssum[0] * inv;
+    inv_count[0] = inv;
+    if (loss_f32) loss_f32[0] = loss;
+    if (out) {
+      if (out_bf16) *(uint16_t*)out = f2bf(loss);
+      else *(float*)out = loss;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void ce_bwd_stream_kernel(const uint16_t* __restrict__ logits, int64_t ls,
                                                                  const int64_t* __restrict__ tgt,
                                                                  const float* __restrict__ row_lse,
@@ -375,6 +414,17 @@ extern "C" int pt_cross_entropy_fwd_stats(const void* logits, int64_t logits_str
   ce_fwd_stats_kernel<<<grid, kStatRows * kStatGroups, 0, stream>>>((const uint16_t*)logits, logits_stride, targets,
                                                                   (const float2*)stats, (int)nblk, row_loss, row_lse,
                                                                   rows, (int)vocab, ignore_index, status);
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
+
+// loss = mean of row_loss over the rows whose target is not ignore_index; inv_count = 1 / #valid;
+// out (optional) = loss in bf16 (out_bf16) or f32.  One launch, deterministic.
+extern "C" int pt_cross_entropy_mean(const float* row_loss, const int64_t* targets, int64_t rows, int64_t ignore_index,
+                                     float* loss_f32, float* inv_count, void* out, int out_bf16, hipStream_t stream) {
+  if (!row_loss || !targets || !inv_count || rows <= 0) return PT_EINVAL;
+  ce_mean_kernel<<<1, kMeanThreads, 0, stream>>>(row_loss, targets, rows, ignore_index, loss_f32, inv_count, out,
+                                                 out_bf16);
   PT_CHECK_LAUNCH();
   return PT_OK;
 }

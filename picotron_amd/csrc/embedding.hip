@@ -79,6 +79,92 @@ __global__ __launch_bounds__(256) void embedding_bwd_kernel(const int64_t* __res
   }
 }
 
+// The backward's key preparation + stable sort in ONE single-workgroup launch (T <= 16384): key =
+// 0 for a skipped token (outside [lo, hi) or padding_idx), id - lo + 1 otherwise, carried with its
+// position as (key << 32 | position).  LSD radix sort, one key bit per pass (bits = bit length of
+// hi - lo): each pass is a stable split -- zeros keep their order ahead of the ones -- ranked by
+// wave ballots and one 64-entry prefix over (round, wave), scattered through LDS.  Stable by
+// construction, so equal ids keep ascending positions (== torch.sort(stable=True) of the keyed ids;
+// the backward's fixed summation order).  Element i = r * 1024 + tid lives in thread tid's
+// register r.  Writes sorted_ids (-1 = skip, first) and perm as int64.
+constexpr int kSortThreads = 1024, kSortMax = 16384, kSortRounds = kSortMax / kSortThreads;
+__global__ __launch_bounds__(kSortThreads) void embedding_sort_kernel(const int64_t* __restrict__ ids, int T,
+                                                                      int rounds, int bits, int64_t lo, int64_t hi,
+                                                                      int has_pad, int64_t pad,
+                                                                      int64_t* __restrict__ sorted_ids,
+                                                                      int64_t* __restrict__ perm) {
+  extern __shared__ uint64_t buf[];             // [rounds * 1024]
+  __shared__ int zc[kSortRounds * 16];          // zeros per (round, wave), then their exclusive prefix
+  __shared__ int ztotal;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t lt_mask = (1ull << lane) - 1;
+  uint64_t c[kSortRounds];
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    const int i = r * kSortThreads + tid;
+    c[r] = ~0ull;  // padding: all key bits set -> sorts last
+    if (r < rounds && i < T) {
+      const int64_t id = ids[i];
+      const bool skip = id < lo || id >= hi || (has_pad && id == pad);
+      c[r] = ((uint64_t)(skip ? 0 : (uint32_t)(id - lo + 1)) << 32) | (uint32_t)i;
+    }
+  }
+  for (int b = 0; b < bits; ++b) {
+    int zr[kSortRounds];
+#pragma unroll
+    for (int r = 0; r < kSortRounds; ++r) {
+      if (r < rounds) {
+        const bool zero = ((c[r] >> (32 + b)) & 1) == 0;
+        const uint64_t m = __ballot(zero);
+        zr[r] = __popcll(m & lt_mask);          // zeros before this lane in its wave-round
+        if (lane == 0) zc[r * 16 + wave] = __popcll(m);
+      }
+    }
+    __syncthreads();
+    if (wave == 0) {  // exclusive prefix of the zero counts in (round, wave) order: <= 256 entries
+      const int n = rounds * 16;
+      int carry = 0;
+      for (int base = 0; base < n; base += 64) {
+        const int v = base + lane < n ? zc[base + lane] : 0;
+        int x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int y = __shfl_up(x, o, 64);
+          if (lane >= o) x += y;
+        }
+        if (base + lane < n) zc[base + lane] = carry + x - v;
+        carry += __shfl(x, 63, 64);
+      }
+      if (lane == 0) ztotal = carry;
+    }
+    __syncthreads();
+    const int Z = ztotal;
+#pragma unroll
+    for (int r = 0; r < kSortRounds; ++r) {
+      if (r < rounds) {
+        const int zb = zc[r * 16 + wave] + zr[r];  // zeros before this element
+        const int i = r * kSortThreads + tid;
+        const bool zero = ((c[r] >> (32 + b)) & 1) == 0;
+        buf[zero ? zb : Z + (i - zb)] = c[r];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kSortRounds; ++r)
+      if (r < rounds) c[r] = buf[r * kSortThreads + tid];
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    const int i = r * kSortThreads + tid;
+    if (r < rounds && i < T) {
+      const uint32_t key = (uint32_t)(c[r] >> 32);
+      sorted_ids[i] = key == 0 ? -1 : (int64_t)key - 1 + lo;
+      perm[i] = (int64_t)(uint32_t)c[r];
+    }
+  }
+}
+
 int grid_for(int64_t work, int per_block) {
   int64_t g = (work + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -108,6 +194,30 @@ int pt_embedding_bwd(const int64_t* sorted_ids, const int64_t* perm, int64_t T, 
   if (T == 0) return PT_OK;
   embedding_bwd_kernel<<<grid_for(T, 4), 256, 0, stream>>>(sorted_ids, perm, T, (const uint16_t*)dy, ldy, vocab_lo,
                                                            dweight, lddw, (int)H, sink);
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
+
+// Key preparation + stable sort of the backward's token ids (embedding_sort_kernel): T <= 16384
+// (PT_EUNSUPPORTED above; the caller sorts otherwise).  has_padding / padding_idx: F.embedding's.
+int pt_embedding_sort(const int64_t* ids, int64_t T, int64_t vocab_lo, int64_t vocab_hi, int has_padding,
+                      int64_t padding_idx, int64_t* sorted_ids, int64_t* perm, hipStream_t stream) {
+  if (!ids || !sorted_ids || !perm || T < 0 || vocab_hi < vocab_lo || vocab_hi - vocab_lo >= (1ll << 31) - 1)
+    return PT_EINVAL;
+  if (T > kSortMax) return PT_EUNSUPPORTED;
+  if (T == 0) return PT_OK;
+  const int rounds = (int)((T + kSortThreads - 1) / kSortThreads);
+  int bits = 1;
+  while (bits < 31 && ((vocab_hi - vocab_lo) >> bits) != 0) ++bits;  // keys <= hi - lo
+  const int smem = rounds * kSortThreads * (int)sizeof(uint64_t);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)embedding_sort_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kSortMax * (int)sizeof(uint64_t));
+    attr = true;
+  }
+  embedding_sort_kernel<<<1, kSortThreads, smem, stream>>>(ids, (int)T, rounds, bits, vocab_lo, vocab_hi,
+                                                           has_padding, padding_idx, sorted_ids, perm);
   PT_CHECK_LAUNCH();
   return PT_OK;
 }

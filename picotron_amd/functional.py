@@ -537,13 +537,14 @@ class CrossEntropyFunction(torch.autograd.Function):
         lg = _contig2d(logits)
         tg = targets.reshape(-1)
         stats = _take_ce_stats(lg)   # the lm_head GEMM's statistics of exactly these logits, if any
+        odt = logits.dtype if logits.dtype in (torch.bfloat16, torch.float32) else torch.float32
         if stats is not None:
-            loss, inv_count, row_lse = K.cross_entropy_loss_lse_stats(lg, tg, stats, ignore_index)
+            loss, inv_count, row_lse = K.cross_entropy_loss_lse_stats(lg, tg, stats, ignore_index, out_dtype=odt)
         else:
-            loss, inv_count, row_lse = K.cross_entropy_loss_lse(lg, tg, ignore_index)
+            loss, inv_count, row_lse = K.cross_entropy_loss_lse(lg, tg, ignore_index, out_dtype=odt)
         ctx.save_for_backward(lg, tg, inv_count, row_lse)
         ctx.ignore_index, ctx.shape = ignore_index, logits.shape
-        return loss.to(logits.dtype)
+        return loss if loss.dtype == logits.dtype else loss.to(logits.dtype)
 
     @staticmethod
     def backward(ctx, g):

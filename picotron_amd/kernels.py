@@ -99,13 +99,21 @@ def embedding_bwd(ids, dy2d, dweight, sink, vocab_lo=0, vocab_hi=None, padding_i
     """Sum the dY rows of every id into dweight (sink: 0 / DW_ACC_BF16 / DW_ACC_F32); ids outside
     [vocab_lo, vocab_hi) and padding_idx contribute nothing (F.embedding's backward)."""
     _bf16_rowmajor(dy2d, "dy")
-    flat = ids.reshape(-1).to(torch.int64)
+    flat = ids.reshape(-1).to(torch.int64).contiguous()
     vocab_hi = vocab_lo + dweight.shape[0] if vocab_hi is None else vocab_hi
-    skip = (flat < vocab_lo) | (flat >= vocab_hi)
-    if padding_idx is not None:
-        skip = skip | (flat == padding_idx)
-    keyed = torch.where(skip, torch.full_like(flat, -1), flat)
-    sorted_ids, perm = torch.sort(keyed, stable=True)
+    T = flat.numel()
+    sorted_ids = torch.empty(T, dtype=torch.int64, device=flat.device)
+    perm = torch.empty(T, dtype=torch.int64, device=flat.device)
+    rc = _C.lib().pt_embedding_sort(_ptr(flat), T, int(vocab_lo), int(vocab_hi), int(padding_idx is not None),
+                                    int(padding_idx if padding_idx is not None else 0), _ptr(sorted_ids), _ptr(perm),
+                                    _C.stream_ptr(flat.device))
+    if rc == -3:   # more tokens than the one-workgroup sort holds: torch's (stable) device sort
+        skip = (flat < vocab_lo) | (flat >= vocab_hi)
+        if padding_idx is not None:
+            skip = skip | (flat == padding_idx)
+        sorted_ids, perm = torch.sort(torch.where(skip, torch.full_like(flat, -1), flat), stable=True)
+    else:
+        _C.check(rc, "pt_embedding_sort")
     rc = _C.lib().pt_embedding_bwd(_ptr(sorted_ids), _ptr(perm), flat.numel(), _ptr(dy2d), dy2d.stride(0),
                                    int(vocab_lo), _ptr(dweight), dweight.stride(0), dy2d.shape[1], int(sink),
                                    _C.stream_ptr(dy2d.device))
@@ -271,21 +279,33 @@ def cross_entropy_loss(logits, targets, ignore_index=-100):
     return row_loss.sum() * inv_count[0], inv_count
 
 
-def cross_entropy_loss_lse(logits, targets, ignore_index=-100):
+def _ce_mean(row_loss, targets, ignore_index, out_dtype):
+    """(mean loss over the valid rows in out_dtype, inv_count [1] f32) in one launch."""
+    rows = row_loss.numel()
+    _req(out_dtype in (BF16, torch.float32), "cross_entropy: loss dtype bf16 / f32")
+    inv_count = torch.empty(1, dtype=torch.float32, device=row_loss.device)
+    loss = torch.empty((), dtype=out_dtype, device=row_loss.device)
+    rc = _C.lib().pt_cross_entropy_mean(_ptr(row_loss), _ptr(targets), rows, int(ignore_index), None, _ptr(inv_count),
+                                        _ptr(loss), int(out_dtype == BF16), _C.stream_ptr(row_loss.device))
+    _C.check(rc, "pt_cross_entropy_mean")
+    return loss, inv_count
+
+
+def cross_entropy_loss_lse(logits, targets, ignore_index=-100, out_dtype=torch.float32):
     """Forward of the autograd pair: (mean loss f32 scalar tensor, inv_count [1] f32, row_lse [rows]
     f32) from one streaming read of the logits (online max / sum-exp)."""
     _bf16_rowmajor(logits, "logits")
     rows, vocab = logits.shape
     _req(targets.dtype == torch.int64 and targets.numel() == rows, "targets: int64 [rows]")
     targets = targets.contiguous()
-    # no clamp: every target ignored gives 0 * inf = nan, as F.cross_entropy's mean does (grads 0)
-    inv_count = (1.0 / (targets != ignore_index).sum().to(torch.float32)).reshape(1)
     row_loss = torch.empty(rows, dtype=torch.float32, device=logits.device)
     row_lse = torch.empty(rows, dtype=torch.float32, device=logits.device)
     rc = _C.lib().pt_cross_entropy_fwd_lse(_ptr(logits), logits.stride(0), _ptr(targets), _ptr(row_loss),
                                            _ptr(row_lse), rows, vocab, int(ignore_index), _ptr(status_word(logits.device)), _C.stream_ptr(logits.device))
     _C.check(rc, "pt_cross_entropy_fwd_lse")
-    return row_loss.sum() * inv_count[0], inv_count, row_lse
+    # no clamp: every target ignored gives 0 * inf = nan, as F.cross_entropy's mean does (grads 0)
+    loss, inv_count = _ce_mean(row_loss, targets, ignore_index, out_dtype)
+    return loss, inv_count, row_lse
 
 
 def cross_entropy_grad_lse(logits, targets, row_lse, scale_dev, ignore_index=-100):
@@ -535,7 +555,7 @@ def linear_ce_stats(x2d, weight):
     return y, stats
 
 
-def cross_entropy_loss_lse_stats(logits, targets, stats, ignore_index=-100):
+def cross_entropy_loss_lse_stats(logits, targets, stats, ignore_index=-100, out_dtype=torch.float32):
     """cross_entropy_loss_lse from the lm_head GEMM's statistics (linear_ce_stats): same outputs,
     the logits are not streamed again (only x[row, target] is read)."""
     _bf16_rowmajor(logits, "logits")
@@ -544,7 +564,6 @@ def cross_entropy_loss_lse_stats(logits, targets, stats, ignore_index=-100):
     _req(stats.dtype == torch.float32 and stats.is_contiguous() and stats.dim() == 3 and stats.shape[1:] == (rows, 2)
          and vocab % stats.shape[0] == 0, "stats: f32 [nblk, rows, 2]")
     targets = targets.contiguous()
-    inv_count = (1.0 / (targets != ignore_index).sum().to(torch.float32)).reshape(1)
     row_loss = torch.empty(rows, dtype=torch.float32, device=logits.device)
     row_lse = torch.empty(rows, dtype=torch.float32, device=logits.device)
     rc = _C.lib().pt_cross_entropy_fwd_stats(_ptr(logits), logits.stride(0), _ptr(targets), _ptr(stats),
@@ -552,7 +571,8 @@ def cross_entropy_loss_lse_stats(logits, targets, stats, ignore_index=-100):
                                              int(ignore_index), _ptr(status_word(logits.device)),
                                              _C.stream_ptr(logits.device))
     _C.check(rc, "pt_cross_entropy_fwd_stats")
-    return row_loss.sum() * inv_count[0], inv_count, row_lse
+    loss, inv_count = _ce_mean(row_loss, targets, ignore_index, out_dtype)
+    return loss, inv_count, row_lse
 
 
 def swiglu_fusable(T, I, backward=False):

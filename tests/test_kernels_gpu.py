@@ -524,3 +524,46 @@ def test_dgrad_k_segmented(ns, T, Kin, acc):
     assert rel_err(dx, want) < 1e-2
     one = K.linear_dgrad(dy, ws, out=base.clone() if acc else None, accumulate=acc, tile=13)
     assert rel_err(dx, one.float()) < 5e-3
+
+
+@pytest.mark.parametrize("T,lo,hi,pad", [(4096, 0, 49152, None), (1000, 100, 300, 150), (17, 0, 8, 3),
+                                         (20000, 0, 512, None)])
+def test_embedding_sort_equals_torch_stable_sort(T, lo, hi, pad):
+    """pt_embedding_sort (one-workgroup LDS bitonic sort of (key, position)) == torch.sort(stable) of
+    the keyed ids, bit for bit; T > 16384 takes torch's device sort (same result by construction)."""
+    from picotron_amd import _C
+    from picotron_amd import kernels as K
+    g = torch.Generator().manual_seed(T)
+    ids = torch.randint(0, max(hi + 50, 64), (T,), generator=g).to(DEV)
+    skip = (ids < lo) | (ids >= hi)
+    if pad is not None:
+        skip = skip | (ids == pad)
+    ref_ids, ref_perm = torch.sort(torch.where(skip, torch.full_like(ids, -1), ids), stable=True)
+    s_ids = torch.empty(T, dtype=torch.int64, device=DEV)
+    perm = torch.empty(T, dtype=torch.int64, device=DEV)
+    rc = _C.lib().pt_embedding_sort(K._ptr(ids), T, lo, hi, int(pad is not None), pad or 0, K._ptr(s_ids),
+                                    K._ptr(perm), _C.stream_ptr(ids.device))
+    if T > 16384:
+        assert rc == -3
+        return
+    assert rc == 0
+    assert torch.equal(s_ids, ref_ids) and torch.equal(perm, ref_perm)
+
+
+def test_cross_entropy_mean_kernel():
+    """pt_cross_entropy_mean: mean over the valid rows (ignore_index excluded), 1/#valid, bf16 / f32
+    output; all rows ignored -> NaN (torch's mean of an empty selection)."""
+    from picotron_amd import kernels as K
+    rows = 4096
+    rl = torch.rand(rows, device=DEV) * 5
+    tg = torch.randint(0, 100, (rows,), device=DEV)
+    tg[::7] = -100
+    rl[::7] = 0.0
+    valid = (tg != -100).sum().item()
+    for dt in (torch.float32, BF):
+        loss, inv = K._ce_mean(rl, tg, -100, dt)
+        assert loss.dtype == dt and abs(inv.item() - 1.0 / valid) < 1e-9
+        ref = rl.double().sum().item() / valid
+        assert abs(loss.float().item() - ref) <= (1e-6 if dt == torch.float32 else 2 ** -8) * ref
+    loss, _ = K._ce_mean(torch.zeros_like(rl), torch.full_like(tg, -100), -100, torch.float32)  # rows all 0
+    assert math.isnan(loss.item())
