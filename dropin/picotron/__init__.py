@@ -16,6 +16,8 @@ Replaced (reference path -> module object):
     picotron/tensor_parallel/{tensor_parallel,tp_communications}.py
     picotron/context_parallel/{context_parallel,cp_communications}.py
     picotron/data_parallel/{data_parallel,bucket}.py
+    picotron/pipeline_parallel/pp_communications.py   picotron_amd.pipeline_parallel.pp_communications
+                                                   (the PipelineParallel engine itself stays the checkout's)
 """
 import importlib
 import os
@@ -29,7 +31,8 @@ if _REPO not in sys.path:
 REPLACED = ("process_group_manager", "model",
             "tensor_parallel", "tensor_parallel.tensor_parallel", "tensor_parallel.tp_communications",
             "context_parallel", "context_parallel.context_parallel", "context_parallel.cp_communications",
-            "data_parallel", "data_parallel.data_parallel", "data_parallel.bucket")
+            "data_parallel", "data_parallel.data_parallel", "data_parallel.bucket",
+            "pipeline_parallel.pp_communications")
 
 
 def _checkout_dir():
@@ -54,4 +57,5 @@ for _name in REPLACED:
     _mod = importlib.import_module("picotron_amd." + _name)
     sys.modules[__name__ + "." + _name] = _mod
     _parent, _, _leaf = (__name__ + "." + _name).rpartition(".")
-    setattr(sys.modules[_parent], _leaf, _mod)
+    if _parent in sys.modules:   # picotron.pipeline_parallel (the checkout's) is not imported here:
+        setattr(sys.modules[_parent], _leaf, _mod)   # its `from ...pp_communications import` finds ours

@@ -111,7 +111,27 @@ __global__ __launch_bounds__(256) void adamw_multi_bf16_kernel(const AdamTensor*
     const int64_t c0 = chunk_start[t], c1 = chunk_start[t + 1];
     const int64_t from = (lo > c0 ? lo : c0) - c0, to = (hi < c1 ? hi : c1) - c0;   // chunk range in t
     const int64_t full = T.n >> 3;
-    for (int64_t c = from + threadIdx.x; c < to; c += blockDim.x) {
+    // two full chunks per thread per iteration: all 8 loads in flight before the first use
+    int64_t c = from + threadIdx.x;
+    for (; c + blockDim.x < to && c + blockDim.x < full; c += 2 * blockDim.x) {
+      const int64_t c2 = c + blockDim.x;
+      const bf16x8 p0 = ld8(T.p + c * 8), g0 = ld8(T.g + c * 8), m0 = ld8(T.m + c * 8), v0 = ld8(T.v + c * 8);
+      const bf16x8 p1 = ld8(T.p + c2 * 8), g1 = ld8(T.g + c2 * 8), m1 = ld8(T.m + c2 * 8), v1 = ld8(T.v + c2 * 8);
+      float p[8], g[8], m[8], v[8];
+      unpack8(p0, p); unpack8(g0, g); unpack8(m0, m); unpack8(v0, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) adam_elem(p[j], g[j], m[j], v[j], s, true);
+      st8(T.p + c * 8, pack8(p));
+      st8(T.m + c * 8, pack8(m));
+      st8(T.v + c * 8, pack8(v));
+      unpack8(p1, p); unpack8(g1, g); unpack8(m1, m); unpack8(v1, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) adam_elem(p[j], g[j], m[j], v[j], s, true);
+      st8(T.p + c2 * 8, pack8(p));
+      st8(T.m + c2 * 8, pack8(m));
+      st8(T.v + c2 * 8, pack8(v));
+    }
+    for (; c < to; c += blockDim.x) {
       if (c < full) {
         float p[8], g[8], m[8], v[8];
         unpack8(ld8(T.p + c * 8), p);
@@ -187,7 +207,9 @@ int pt_adamw_step_multi(const void* tensors, const int64_t* chunk_start, int nte
   if (!tensors || !chunk_start || ntensors <= 0 || total_chunks < 0) return PT_EINVAL;
   if (total_chunks == 0) return PT_OK;
   const AdamScalars s{decay, w1, beta2, c2, bc2_sqrt, eps, step_size};
-  const int64_t blocks = grid_for(total_chunks);
+  // one resident round: 4 blocks of 4 waves per CU at <= 128 VGPRs (2 chunks per thread in flight)
+  const int64_t cap = 1024, want = (total_chunks + 511) / 512;
+  const int64_t blocks = want < 1 ? 1 : (want < cap ? want : cap);
   const int64_t per_block = (total_chunks + blocks - 1) / blocks;
   adamw_multi_bf16_kernel<<<(unsigned)blocks, 256, 0, stream>>>((const AdamTensor*)tensors, chunk_start, ntensors,
                                                                 per_block, s);

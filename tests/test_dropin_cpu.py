@@ -29,7 +29,7 @@ def test_overlay_aliases_the_hot_path_modules():
 import importlib, picotron
 names = ["process_group_manager", "model", "tensor_parallel.tensor_parallel", "tensor_parallel.tp_communications",
          "context_parallel.context_parallel", "context_parallel.cp_communications",
-         "data_parallel.data_parallel", "data_parallel.bucket"]
+         "data_parallel.data_parallel", "data_parallel.bucket", "pipeline_parallel.pp_communications"]
 for n in names:
     assert importlib.import_module("picotron." + n) is importlib.import_module("picotron_amd." + n), n
 import picotron.process_group_manager as pgm
@@ -61,6 +61,10 @@ from picotron.pipeline_parallel.pipeline_parallel import PipelineParallel
 import picotron.utils as U
 import picotron.checkpoint as ck
 assert PipelineParallel.__module__ == "picotron.pipeline_parallel.pipeline_parallel"
+import picotron.pipeline_parallel.pipeline_parallel as PPm
+import picotron_amd.pipeline_parallel.pp_communications as PC
+assert PPm.pipeline_communicate is PC.pipeline_communicate
+assert PPm.bidirectional_pipeline_communicate is PC.bidirectional_pipeline_communicate
 assert U.pgm is pgm and ck.pgm is pgm
 pgm.setup_process_group_manager(tp_size=1, cp_size=1, pp_size=1, dp_size=1)
 from picotron.model import Llama

@@ -229,3 +229,55 @@ def _ring(rank, world, nh, nkv):
 @pytest.mark.parametrize("world,nh,nkv", [(2, 2, 2), (4, 4, 2)])
 def test_ring_attention_schedule_matches_full_attention(world, nh, nkv):
     _dist.run(_ring, world, nh, nkv)
+
+
+# ----------------------------------------------------------------------------- PP p2p
+def _pp_p2p(rank, world):
+    """pp_communications.py:8-45 semantics on a pp=world pipeline: None at the pipeline ends, the
+    received tensor equal to the peer's sent one (requires_grad, given shape / dtype), and the
+    batched bidirectional exchange of the 1F1B steady state (pipeline_parallel.py:150-190)."""
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.pipeline_parallel import pp_communications as PC
+    m = pgm.setup_process_group_manager(tp_size=1, cp_size=1, pp_size=world, dp_size=1)
+    assert m.pp_rank == rank
+    shape, dt = (2, 3, 4), torch.float32
+    act = torch.full(shape, float(rank + 1))
+    # forward: recv from the previous stage, send to the next one
+    got = PC.pipeline_communicate("recv_forward", "cpu", dt, shapes=shape) if rank % 2 else None
+    if rank % 2 == 0:
+        assert PC.pipeline_communicate("send_forward", "cpu", dt, tensor=act) is None
+        got = PC.pipeline_communicate("recv_forward", "cpu", dt, shapes=shape)
+    else:
+        PC.pipeline_communicate("send_forward", "cpu", dt, tensor=act)
+    if rank == 0:
+        assert got is None
+    else:
+        assert got.requires_grad and got.shape == shape and torch.equal(got.detach(), torch.full(shape, float(rank)))
+    # backward: recv from the next stage, send to the previous one
+    grad = torch.full(shape, -float(rank + 1))
+    if rank % 2 == 0:
+        gb = PC.pipeline_communicate("recv_backward", "cpu", dt, shapes=shape)
+        PC.pipeline_communicate("send_backward", "cpu", dt, tensor=grad)
+    else:
+        PC.pipeline_communicate("send_backward", "cpu", dt, tensor=grad)
+        gb = PC.pipeline_communicate("recv_backward", "cpu", dt, shapes=shape)
+    if rank == world - 1:
+        assert gb is None
+    else:
+        assert torch.equal(gb.detach(), torch.full(shape, -float(rank + 2)))
+    # 1F1B steady state between stages 0 and 1: one batched isend + irecv each way
+    if rank == 0:
+        r = PC.bidirectional_pipeline_communicate("send_fwd_recv_bwd", act, shape, "cpu", dt)
+        assert torch.equal(r.detach(), torch.full(shape, -2.0))
+    elif rank == 1:
+        r = PC.bidirectional_pipeline_communicate("send_bwd_recv_fwd", grad, shape, "cpu", dt)
+        assert torch.equal(r.detach(), torch.full(shape, 1.0))
+    if rank == world - 1:
+        assert PC.bidirectional_pipeline_communicate("send_fwd_recv_bwd", act, shape, "cpu", dt) is None
+    if rank == 0:
+        assert PC.bidirectional_pipeline_communicate("send_bwd_recv_fwd", grad, shape, "cpu", dt) is None
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pp_p2p(world):
+    _dist.run(_pp_p2p, world)
