@@ -54,6 +54,7 @@ def main():
     ap.add_argument("--H", type=int, default=32)
     ap.add_argument("--D", type=int, default=64)
     ap.add_argument("--old", default="")
+    ap.add_argument("--rounds", type=int, default=2, help="interleaved rounds; medians are printed at the end")
     a = ap.parse_args()
     B, S, H, D = a.B, a.S, a.H, a.D
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -66,7 +67,8 @@ def main():
     if a.old:
         libs["old"] = _C.load_library(os.path.abspath(a.old), strict=False)
     outs = {}
-    for rnd in range(2):
+    med = {name: {"fwd": [], "bwd": []} for name in libs}
+    for rnd in range(a.rounds):
         for name, lib in libs.items():
             _C._lib = lib
             o, lse = K.attn_fwd(q, k, v, scale, True)
@@ -75,11 +77,16 @@ def main():
             outs[name] = [t.clone() for t in (o, lse, dq, dk, dv)]
             t_fwd = graph_us(lambda: K.attn_fwd(q, k, v, scale, True, out=o, lse=lse), a.reps)
             t_bwd = graph_us(lambda: K.attn_bwd(do, q, k, v, o, lse, scale, True, delta=delta), a.reps)
+            med[name]["fwd"].append(t_fwd)
+            med[name]["bwd"].append(t_bwd)
             print(json.dumps({"lib": f"{name}:r{rnd}", "B": B, "S": S, "H": H, "D": D,
                               "fwd_us": round(t_fwd, 1), "fwd_tflops": round(2 * unit / t_fwd / 1e6, 1),
                               "bwd_us": round(t_bwd, 1), "bwd_tflops": round(5 * unit / t_bwd / 1e6, 1),
                               "bwd_kernel_flop_tflops": round(7 * unit / t_bwd / 1e6, 1)}), flush=True)
     _C._lib = libs["new"]
+    for name, m in med.items():
+        f, b = sorted(m["fwd"])[len(m["fwd"]) // 2], sorted(m["bwd"])[len(m["bwd"]) // 2]
+        print(json.dumps({"median": name, "fwd_us": round(f, 1), "bwd_us": round(b, 1)}), flush=True)
     if "old" in outs:
         rel = [((x.float() - y.float()).norm() / y.float().norm()).item() for x, y in zip(outs["new"], outs["old"])]
         print(json.dumps({"new_vs_old_rel_o_lse_dq_dk_dv": rel}), flush=True)
