@@ -586,7 +586,8 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
     const int kv0 = kt * KT;
     if (!a.causal || kv0 <= q0 + 31) {
       const bool diag = a.causal && (kv0 + KT - 1 > q0);
-      f32x16_t ds[2];
+      // each 32-key half's dS feeds its two dQ k-steps right away: one dS tile live, not two
+      // (16 VGPRs: d128's dQ kernel fits 2 waves per SIMD)
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh) {
         f32x16_t s = zero16(), dp = zero16();
@@ -606,13 +607,13 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
           const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, nlse2));
           s[r] = p * (dp[r] - del);
         }
-        ds[kh] = s;
-      }
 #pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        const bf16x8_t db = acc_as_b(ds[st >> 1], st & 1);
+        for (int sh = 0; sh < 2; ++sh) {
+          const int st = 2 * kh + sh;
+          const bf16x8_t db = acc_as_b(s, sh);
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt) dq[dt] = mfma(rd_tr<D>(sk, st, dt, lane), db, dq[dt]);
+          for (int dt = 0; dt < DT; ++dt) dq[dt] = mfma(rd_tr<D>(sk, st, dt, lane), db, dq[dt]);
+        }
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -636,7 +637,8 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
 }
 
 template <int D>
-__global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnArgs a) {
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(D == 128 ? 2 : 1)))
+void attn_bwd_dq_kernel(AttnArgs a) {
   int bx, hh, b;
   attn_coords(bx, hh, b);
   for (int pass = 0; pass <= a.pair; ++pass) {  // one inlined body: no register growth

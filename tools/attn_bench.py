@@ -69,7 +69,8 @@ def main():
     outs = {}
     med = {name: {"fwd": [], "bwd": []} for name in libs}
     for rnd in range(a.rounds):
-        for name, lib in libs.items():
+        order = list(libs.items())
+        for name, lib in (order if rnd % 2 == 0 else order[::-1]):   # alternate who goes first
             _C._lib = lib
             o, lse = K.attn_fwd(q, k, v, scale, True)
             delta = K.attn_delta(do, o)
