@@ -40,6 +40,9 @@ def _dist_worker(rank, world, port, ref, fn, out_dir):
                       MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     sys.path.insert(0, ref)
     _install_stubs()
+    # the reference calls torch.cuda.synchronize() after every ring p2p (cp_comm.py:51); there is no
+    # GPU here, and on CPU tensors gloo's wait() already completed the transfer (SURVEY.md §4 probe)
+    torch.cuda.synchronize = lambda *a, **k: None
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -146,6 +149,90 @@ def g8_data_parallel(rank, world):
     res = {"ids": ids}
     res.update({f"param.{n}": v for n, v in init.items()})
     res.update({f"grad.{n}": p.grad.detach().clone() for n, p in llama.named_parameters()})
+    return res
+
+
+G10M_CFG = dict(hidden_size=128, intermediate_size=256, num_attention_heads=2, num_key_value_heads=2,
+                rms_norm_eps=1e-5, max_position_embeddings=256, rope_theta=10000.0, vocab_size=256,
+                num_hidden_layers=2)
+G10M_STEPS, G10M_GA, G10M_MBS, G10M_LR = 4, 2, 2, 1e-2
+
+
+def _g10m_data():
+    """[steps, dp 2, ga, mbs, seq + 1] tokens shared by every topology (seed 1234): the same batch
+    every step, so the loss curve falls steeply (memorisation) and a 1 % bar separates real
+    training from a broken update."""
+    g = torch.Generator().manual_seed(1234)
+    S = G10M_CFG["max_position_embeddings"]
+    one = torch.randint(0, G10M_CFG["vocab_size"], (1, 2, G10M_GA, G10M_MBS, S + 1), generator=g)
+    return one.expand(G10M_STEPS, -1, -1, -1, -1).contiguous()
+
+
+def _g10m_shard(full, local, rank):
+    if full.shape == local.shape:
+        return full
+    (d,) = [i for i, (a, b) in enumerate(zip(full.shape, local.shape)) if a != b]
+    n = local.shape[d]
+    return full.narrow(d, rank * n, n)
+
+
+def g10m_multirank(rank, world, tp, cp, dp):
+    """G10 multi-rank: train.py's loop (train_step 29-55, the step loop 232-249) run by the reference
+    itself on gloo/CPU, fp32, FLASH_ATTEN=0, at tp / cp / dp = 2: G10M_STEPS AdamW steps (lr 1e-2,
+    torch defaults), grad_acc 2, mbs 2, seq 256 (each cp rank its contiguous half, data.py:105-109);
+    every topology starts from the SAME full weights (one tp=1 init, seed 7, sharded as
+    apply_tensor_parallel shards).  DataParallelBucket wraps the model only when dp > 1, as
+    train.py:194-195 does (so at cp 2 / dp 1 the two cp ranks' replicas train on their own
+    gradients, the reference's behaviour).  Records the logged loss per step
+    (average_loss_across_dp_cp_ranks, utils.py:93-98) and the full initial weights (rank 0)."""
+    import torch.nn.functional as F
+    import picotron.process_group_manager as pgm
+    pgm.setup_process_group_manager(tp_size=tp, cp_size=cp, pp_size=1, dp_size=dp)
+    m = pgm.process_group_manager
+    from picotron import model as M
+    from picotron.context_parallel.context_parallel import apply_context_parallel
+    from picotron.data_parallel.data_parallel import DataParallelBucket
+    from picotron.tensor_parallel.tensor_parallel import apply_tensor_parallel
+    from picotron.utils import average_loss_across_dp_cp_ranks
+    cfg = types.SimpleNamespace(**G10M_CFG)
+    torch.manual_seed(7)
+    model = M.Llama(cfg)
+    full = {n: p.detach().clone() for n, p in model.named_parameters()}
+    if tp > 1:
+        model = apply_tensor_parallel(model)
+    if cp > 1:
+        model = apply_context_parallel(model)
+    for layer in model.decoder_layers:
+        layer.cos, layer.sin = layer.cos.float(), layer.sin.float()
+    with torch.no_grad():
+        for n, p in model.named_parameters():
+            p.copy_(_g10m_shard(full[n], p, m.tp_rank))
+    if dp > 1:
+        model = DataParallelBucket(model)
+    opt = torch.optim.AdamW(model.parameters(), lr=G10M_LR)
+    ids = _g10m_data()
+    S, V = G10M_CFG["max_position_embeddings"], G10M_CFG["vocab_size"]
+    sl = slice(m.cp_rank * S // cp, (m.cp_rank + 1) * S // cp)
+    losses = []
+    for step in range(G10M_STEPS):
+        opt.zero_grad()
+        acc = 0.0
+        for i in range(G10M_GA):
+            if m.cp_dp_world_size > 1:
+                model.require_backward_grad_sync = (i == G10M_GA - 1)
+            t = ids[step, m.dp_rank, i]
+            x, y = t[:, :-1][:, sl].contiguous(), t[:, 1:][:, sl].contiguous()
+            out = model(input_ids=x)
+            loss = F.cross_entropy(out.reshape(-1, V), y.reshape(-1), reduction="mean") / G10M_GA
+            loss.backward()
+            acc += loss.item()
+        losses.append(average_loss_across_dp_cp_ranks(acc, "cpu"))
+        opt.step()
+        if hasattr(model, "reset"):
+            model.reset()
+    res = {"losses": torch.tensor(losses, dtype=torch.float64)}
+    if rank == 0:
+        res.update({f"param.{n}": v for n, v in full.items()})
     return res
 
 
@@ -281,7 +368,10 @@ def main():
                    os.path.join(OUT, f"{name}.pt"))
     _run_dist(g7_tensor_parallel, 2, args.ref, "G7")
     _run_dist(g8_data_parallel, 2, args.ref, "G8")
-    print("wrote", sorted(gold) + ["G7", "G8"])
+    import functools
+    for name, (tp, cp, dp) in (("G10m_tp2", (2, 1, 1)), ("G10m_cp2", (1, 2, 1)), ("G10m_dp2", (1, 1, 2))):
+        _run_dist(functools.partial(g10m_multirank, tp=tp, cp=cp, dp=dp), 2, args.ref, name)
+    print("wrote", sorted(gold) + ["G7", "G8", "G10m_tp2", "G10m_cp2", "G10m_dp2"])
 
 
 if __name__ == "__main__":

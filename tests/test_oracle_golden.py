@@ -184,3 +184,19 @@ def test_ring_step_golden_g4b():
         tol = dict(rtol=1e-5, atol=1e-6) if tag == "f32" else dict(rtol=0, atol=0)
         close(out, g["out"], **tol)
         close(lse, g["lse"], **tol)
+
+
+def test_g10m_fixtures_are_reference_loss_curves():
+    """G10m_{tp2,cp2,dp2}: 4 finite, falling losses, identical on both ranks (the logged, cp_dp-
+    averaged value), and the same initial weights in every topology."""
+    import torch
+    base = None
+    for tag in ("tp2", "cp2", "dp2"):
+        g = load(f"G10m_{tag}")
+        l0, l1 = g["rank0.losses"], g["rank1.losses"]
+        assert torch.equal(l0, l1) and l0.numel() == 4 and torch.isfinite(l0).all()
+        assert (l0[1:] < l0[:-1]).all()
+        w = {k: v for k, v in g.items() if k.startswith("rank0.param.")}
+        if base is None:
+            base = w
+        assert w.keys() == base.keys() and all(torch.equal(w[k], base[k]) for k in w)
