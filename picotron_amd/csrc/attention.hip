@@ -146,6 +146,16 @@ __device__ __forceinline__ void attn_coords(int& x, int& y, int& z) {
 
 __device__ __forceinline__ int nqb_of(const AttnArgs& a) { return a.Sq / (NW * 32); }
 
+// v + (v of lane ^ 32) and max(v, v of lane ^ 32): one v_permlane32_swap (no LDS round trip)
+__device__ __forceinline__ float xor32_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xor32_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
 __device__ __forceinline__ f32x16_t zero16() {
   f32x16_t z;
 #pragma unroll
@@ -252,13 +262,11 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler: its own fragment loads are done
   __syncthreads();
 
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nkt) stage(kt + 1, buf ^ 1);
-    const lds_u8* sk = smem + buf * 2 * TILE_B;
+  // one K/V tile (a lambda, not a loop body: the causal skip is an early return)
+  auto tile = [&](const lds_u8* sk, int kv0) {
     const lds_u8* sv = sk + TILE_B;
-    const int kv0 = kt * KT;
-    if (!a.causal || kv0 <= q0 + 31) {  // wave-uniform: skip tiles fully above the diagonal
+    if (a.causal && kv0 > q0 + 31) return;  // wave-uniform: skip tiles fully above the diagonal
+    {
       f32x16_t s[2];
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh) {
@@ -280,7 +288,7 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
       for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
         for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[kh][r]);
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * c2;  // log2 units (c2 > 0)
+      mt = xor32_max(mt) * c2;  // log2 units (c2 > 0)
       // lazy rescale (FA-style deferred max): only when some query's max grew by > 2^8; P may then
       // exceed 1 by at most 2^8, harmless in f32 accumulation and in bf16 (relative precision)
       if (__any(mt > m + kRescaleLog2)) {
@@ -309,11 +317,17 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
         for (int dt = 0; dt < DT; ++dt) o[dt] = mfma(rd_tr<D>(sv, st, dt, lane), pb, o[dt]);
       }
     }
+  };
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nkt) stage(kt + 1, buf ^ 1);
+    tile(smem + buf * 2 * TILE_B, kt * KT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
-  l += __shfl_xor(l, 32, 64);
+  l = xor32_sum(l);
   const float inv_l = 1.0f / l;
   const float lse = m * kLn2 + __logf(l);
   float* lse_p = a.lse + ((int64_t)b * a.H + h) * a.Sq + myq;
@@ -414,34 +428,33 @@ __device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, i
   // q tiles: causal -> only those that can see this block's keys
   const int qt_begin = a.causal ? (kb * NW * 32) / KT : 0;
   const int nqt = a.Sq / KT;
-  const int n_iter = (nqt - qt_begin) * group;
-  // LDS: 2 x {Q tile, dO tile, lse[64], delta[64]}
+  const int nq = nqt - qt_begin;  // q tiles per query head
+  const int n_iter = nq * group;
+  // LDS: 2 x {Q tile, dO tile, lse * log2(e) [64], delta[64]}
   constexpr int STAGE_B = 2 * TILE_B + 2 * KT * 4;
 
-  auto stage = [&](int it, int buf) {
-    const int hq = hk * group + it / (nqt - qt_begin);
-    const int qt = qt_begin + it % (nqt - qt_begin);
+  // the LSE rows go through wave 0's registers (one load per lane, scaled by log2(e) and written to
+  // LDS at the end of the iteration): the exponent below is then one fma per score, not two ops
+  float lse_next = 0.f;
+  auto stage = [&](int hq, int qt, int buf) {
     lds_u8* sq = smem + buf * STAGE_B;
     stage_rows<D>(a.q + b * a.q_sb + (int64_t)qt * KT * a.q_ss + hq * a.q_sh, a.q_ss, sq, wave, lane);
     stage_rows<D>(a.dout + b * a.do_sb + (int64_t)qt * KT * a.do_ss + hq * a.do_sh, a.do_ss, sq + TILE_B, wave, lane);
-    if (wave == 0) {  // 64 lse + 64 delta floats = 2 x 256 B: one 4-byte DMA per lane each
+    if (wave == 0) {  // 64 delta floats = 256 B: one 4-byte DMA per lane
       const int64_t ro = ((int64_t)b * a.H + hq) * a.Sq + qt * KT;
-      pt_glds4(a.lse + ro, lane * 4u, (__attribute__((address_space(3))) void*)(sq + 2 * TILE_B));
+      lse_next = a.lse[ro + lane];
       pt_glds4(a.delta + ro, lane * 4u, (__attribute__((address_space(3))) void*)(sq + 2 * TILE_B + KT * 4));
     }
   };
-  if (n_iter > 0) stage(0, 0);
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler: its own fragment loads are done
-  __syncthreads();
+  auto put_lse = [&](int buf) {  // after the iteration's vmcnt(0), before its barrier
+    if (wave == 0) ((__attribute__((address_space(3))) float*)(smem + buf * STAGE_B + 2 * TILE_B))[lane] = lse_next * kLog2e;
+  };
 
-  for (int it = 0; it < n_iter; ++it) {
-    const int buf = it & 1;
-    if (it + 1 < n_iter) stage(it + 1, buf ^ 1);
-    const int qt = qt_begin + it % (nqt - qt_begin);
-    const lds_u8* sq = smem + buf * STAGE_B;
+  // one (query head, q tile) step
+  auto tile = [&](const lds_u8* sq, int qt) {
     const lds_u8* sdo = sq + TILE_B;
-    const float* slse = (const float*)(sq + 2 * TILE_B);
-    const float* sdel = slse + KT;
+    const float* sl2 = (const float*)(sq + 2 * TILE_B);
+    const float* sdel = sl2 + KT;
 #pragma unroll
     for (int qh = 0; qh < 2; ++qh) {
       const int qs = qt * KT + 32 * qh;
@@ -462,7 +475,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, i
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qi = 32 * qh + crow(r, lane);
-        const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -slse[qi] * kLog2e));
+        const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -sl2[qi]));
         s[r] = p;                             // P
         dp[r] = p * (dp[r] - sdel[qi]);       // dS
       }
@@ -476,7 +489,24 @@ __device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, i
         }
       }
     }
+  };
+
+  // (head, tile) counters for this step and the staged one (no divisions in the loop)
+  int cur_h = hk * group, cur_t = 0, nxt_h = cur_h, nxt_t = 0;
+  if (n_iter > 0) stage(cur_h, qt_begin, 0);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler: its own fragment loads are done
+  if (n_iter > 0) put_lse(0);
+  __syncthreads();
+
+  for (int it = 0; it < n_iter; ++it) {
+    const int buf = it & 1;
+    if (++nxt_t == nq) { nxt_t = 0; ++nxt_h; }
+    if (it + 1 < n_iter) stage(nxt_h, qt_begin + nxt_t, buf ^ 1);
+    const lds_u8* sq = smem + buf * STAGE_B;
+    tile(sq, qt_begin + cur_t);
+    cur_h = nxt_h; cur_t = nxt_t;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (it + 1 < n_iter) put_lse(buf ^ 1);
     __syncthreads();
   }
 
@@ -504,7 +534,8 @@ __device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, i
 }
 
 template <int D>
-__global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv_kernel(AttnArgs a) {
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(D == 64 ? 2 : 1)))
+void attn_bwd_dkdv_kernel(AttnArgs a) {
   int bx, hh, b;
   attn_coords(bx, hh, b);
   for (int pass = 0; pass <= a.pair; ++pass) {  // one inlined body: no register growth
@@ -573,49 +604,50 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int j = 0; j < 8; ++j) part += (float)dof[ks][j] * (float)of[ks][j];
-    del = part + __shfl_xor(part, 32, 64);
+    del = xor32_sum(part);
     if (lane < 32) a.delta_w[ri] = del;
   }
   __syncthreads();
 
+  // one K/V tile
+  auto tile = [&](const lds_u8* sk, int kv0) {
+    const lds_u8* sv = sk + TILE_B;
+    if (a.causal && kv0 > q0 + 31) return;  // wave-uniform: every key of the tile is after my queries
+    // each 32-key half's dS feeds its two dQ k-steps right away: one dS tile live, not two
+    // (16 VGPRs: d128's dQ kernel fits 2 waves per SIMD)
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      f32x16_t s = zero16(), dp = zero16();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        s = mfma(rd_row<D>(sk, 32 * kh, ks, lane), qf[ks], s);
+        dp = mfma(rd_row<D>(sv, 32 * kh, ks, lane), dof[ks], dp);
+      }
+      if (a.causal && kv0 + KT - 1 > q0) {  // key row 32 kh + crow(r) visible iff <= thr
+        const int thr = myq - kv0 - 32 * kh - 4 * (lane >> 5);
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if ((r & 3) + 8 * (r >> 2) > thr) s[r] = -INFINITY;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, nlse2));
+        s[r] = p * (dp[r] - del);
+      }
+#pragma unroll
+      for (int sh = 0; sh < 2; ++sh) {
+        const int st = 2 * kh + sh;
+        const bf16x8_t db = acc_as_b(s, sh);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) dq[dt] = mfma(rd_tr<D>(sk, st, dt, lane), db, dq[dt]);
+      }
+    }
+  };
+
   for (int kt = 0; kt < nkt; ++kt) {
     const int buf = kt & 1;
     if (kt + 1 < nkt) stage(kt + 1, buf ^ 1);
-    const lds_u8* sk = smem + buf * 2 * TILE_B;
-    const lds_u8* sv = sk + TILE_B;
-    const int kv0 = kt * KT;
-    if (!a.causal || kv0 <= q0 + 31) {
-      const bool diag = a.causal && (kv0 + KT - 1 > q0);
-      // each 32-key half's dS feeds its two dQ k-steps right away: one dS tile live, not two
-      // (16 VGPRs: d128's dQ kernel fits 2 waves per SIMD)
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) {
-        f32x16_t s = zero16(), dp = zero16();
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          s = mfma(rd_row<D>(sk, 32 * kh, ks, lane), qf[ks], s);
-          dp = mfma(rd_row<D>(sv, 32 * kh, ks, lane), dof[ks], dp);
-        }
-        if (diag) {  // key row 32 kh + crow(r) visible iff <= thr
-          const int thr = myq - kv0 - 32 * kh - 4 * (lane >> 5);
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if ((r & 3) + 8 * (r >> 2) > thr) s[r] = -INFINITY;
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, nlse2));
-          s[r] = p * (dp[r] - del);
-        }
-#pragma unroll
-        for (int sh = 0; sh < 2; ++sh) {
-          const int st = 2 * kh + sh;
-          const bf16x8_t db = acc_as_b(s, sh);
-#pragma unroll
-          for (int dt = 0; dt < DT; ++dt) dq[dt] = mfma(rd_tr<D>(sk, st, dt, lane), db, dq[dt]);
-        }
-      }
-    }
+    tile(smem + buf * 2 * TILE_B, kt * KT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }

@@ -6,8 +6,8 @@ each 2 B h S^2 d / 2).
 
     python tools/attn_bench.py [--reps 20] [--B 4 --S 1024 --H 32 --D 64] [--old lib.so]
 
---old: a library holding another build of the pt_attn_* entry points, timed in the same process
-(rounds interleaved) and compared element-wise with this build's outputs.
+--old: libraries (comma-separated) holding other builds of the pt_attn_* entry points, timed in the
+same process (rounds interleaved, first one rotated) and compared element-wise with this build's outputs.
 """
 import argparse
 import json
@@ -64,13 +64,14 @@ def main():
     scale = D ** -0.5
     unit = 2.0 * B * H * S * S * D / 2
     libs = {"new": _C.load_library()}
-    if a.old:
-        libs["old"] = _C.load_library(os.path.abspath(a.old), strict=False)
+    for i, path in enumerate(x for x in a.old.split(",") if x):   # comma-separated: old, old1, old2 ...
+        libs["old" if i == 0 else f"old{i}"] = _C.load_library(os.path.abspath(path), strict=False)
     outs = {}
     med = {name: {"fwd": [], "bwd": []} for name in libs}
     for rnd in range(a.rounds):
         order = list(libs.items())
-        for name, lib in (order if rnd % 2 == 0 else order[::-1]):   # alternate who goes first
+        order = order[rnd % len(order):] + order[:rnd % len(order)]   # rotate who goes first
+        for name, lib in order:
             _C._lib = lib
             o, lse = K.attn_fwd(q, k, v, scale, True)
             delta = K.attn_delta(do, o)
@@ -88,9 +89,11 @@ def main():
     for name, m in med.items():
         f, b = sorted(m["fwd"])[len(m["fwd"]) // 2], sorted(m["bwd"])[len(m["bwd"]) // 2]
         print(json.dumps({"median": name, "fwd_us": round(f, 1), "bwd_us": round(b, 1)}), flush=True)
-    if "old" in outs:
-        rel = [((x.float() - y.float()).norm() / y.float().norm()).item() for x, y in zip(outs["new"], outs["old"])]
-        print(json.dumps({"new_vs_old_rel_o_lse_dq_dk_dv": rel}), flush=True)
+    for name in outs:
+        if name == "new":
+            continue
+        rel = [((x.float() - y.float()).norm() / y.float().norm()).item() for x, y in zip(outs["new"], outs[name])]
+        print(json.dumps({f"new_vs_{name}_rel_o_lse_dq_dk_dv": rel}), flush=True)
 
 
 if __name__ == "__main__":
