@@ -186,6 +186,17 @@ typedef struct {
 int pt_gemm_grouped(const pt_gemm_problem* probs, int nprob, int a_kcontig, int b_kcontig, int epilogue, int tile,
                     hipStream_t stream);
 
+/* Two independent groups in ONE launch of 256x256 tiles, each with its own layouts and epilogue:
+ * group 0 = dX (A = dY [M, K] K-contiguous, B = W [K, N] N-contiguous; epilogue 0 or 6 = the
+ * SwiGLU backward, residual = g|u), group 1 = wgrad (dY^T X; both operands MN-contiguous;
+ * epilogue 0, 1 or 3).  The dX of a layer's projection beside its dW (both read only dY and saved
+ * activations): the down_proj dX's HBM-bound SwiGLU-backward tail overlaps the dW's MFMA work.
+ * order: 0 group 0 first, 1 group 1 first, inside each XCD's share.
+ * PT_EUNSUPPORTED when a problem does not tile by 256 x 256 or a group's tile count % 8 != 0. */
+int pt_gemm_dual(const pt_gemm_problem* p0, int n0, int a_kcontig0, int b_kcontig0, int epilogue0,
+                 const pt_gemm_problem* p1, int n1, int a_kcontig1, int b_kcontig1, int epilogue1, int order,
+                 hipStream_t stream);
+
 /* ---- ring-attention merge ------------------------------------------------------------------
  * replaces picotron/context_parallel/context_parallel.py:157-187 update_out_and_lse (its non-first
  * call): out_new = out - sigmoid(blse - lse) * (out - block_out), lse_new = lse - logsigmoid(lse -

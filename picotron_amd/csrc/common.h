@@ -29,6 +29,10 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
 }
 // round an f32 through bf16 and back (models a bf16 storage round trip)
 __device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
+// sigmoid(x) = 1 / (1 + e^-x) with the hardware reciprocal (v_rcp_f32, 1 ulp) instead of the IEEE
+// division sequence (v_div_scale / fmas / fixup, ~10 instructions): every SwiGLU kernel uses this
+// one expression, so the fused epilogues and csrc/swiglu.hip stay bit-identical
+__device__ __forceinline__ float pt_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
 __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
   return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);

@@ -42,9 +42,6 @@ typedef __attribute__((address_space(3))) uint8_t lds_u8;
 namespace {
 
 constexpr int BK = 64;
-#ifndef PT_SWIGLU_GRP
-#define PT_SWIGLU_GRP 2
-#endif
 
 // EPI_BF16_RES: C = bf16(R + bf16(acc)) -- the residual add of model.py:207-208 fused into the
 // producing GEMM (R may alias C).
@@ -68,7 +65,7 @@ enum Epilogue {
 };
 
 // SwiGLU element math, the same expressions as csrc/swiglu.hip (torch's bf16 roundings)
-__device__ __forceinline__ float silu_sig(float x) { return 1.0f / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float silu_sig(float x) { return pt_sigmoid(x); }
 
 struct GemmArgs {
   const uint16_t* A;
@@ -182,9 +179,9 @@ struct GemmGroup {
 // then group `group_m` tile-rows so an XCD's 32 consecutive tiles form a compact block of the
 // output (A and B panels shared through that XCD's L2): 8 for 256x256 tiles, 4 for 256x128
 // (32 tiles = 1024 x 1024 elements either way)
-__device__ __forceinline__ const GemmArgs& select_problem(const GemmGroup& g, int& tile_m, int& tile_n,
-                                                          int bid = -1, int nwg = -1) {
-  const int pid_all = bid < 0 ? xcd_remap(blockIdx.x, gridDim.x) : xcd_remap(bid, nwg);
+// tile id pid_all (already in XCD order) of group g -> its problem and (tile_m, tile_n)
+__device__ __forceinline__ const GemmArgs& select_problem_pid(const GemmGroup& g, int pid_all, int& tile_m,
+                                                              int& tile_n) {
   int pi = 0;
 #pragma unroll
   for (int i = 1; i < kMaxProb; ++i)
@@ -199,6 +196,12 @@ __device__ __forceinline__ const GemmArgs& select_problem(const GemmGroup& g, in
   tile_m = first_m + (pid % group_span) % gsize;
   tile_n = (pid % group_span) / gsize;
   return a;
+}
+
+__device__ __forceinline__ const GemmArgs& select_problem(const GemmGroup& g, int& tile_m, int& tile_n,
+                                                          int bid = -1, int nwg = -1) {
+  const int pid_all = bid < 0 ? xcd_remap(blockIdx.x, gridDim.x) : xcd_remap(bid, nwg);
+  return select_problem_pid(g, pid_all, tile_m, tile_n);
 }
 
 // Write the wave's TM x TN accumulator tile (FM x FN 16x16 fragments) at output (m0 + wm*TM,
@@ -240,6 +243,114 @@ __device__ __forceinline__ void ce_stats_merge(const GemmArgs& a, const float2* 
   }
 }
 
+// EPI_SWIGLU_BWD tail: the wave's TM x TN dh tile is staged (bf16) in `st`; read g|u, write
+// dg|du (swiglu.hip's backward), SG chunks of g and u per group, row-group bases in SGPRs (one
+// address VGPR per lane).  The tail is HBM-bound -- the 256 tiles of a round reach it together and
+// move 134 MB at ~4.5 TB/s -- and a stream that alternates loads and stores runs it fastest:
+// issuing all 2 x NIT loads before any math measured 3 % slower than 2 chunks per group
+// (profiles/r02_notes.md).
+#ifndef PT_SWIGLU_GRP
+#define PT_SWIGLU_GRP 2
+#endif
+template <int TM, int TN>
+__device__ __forceinline__ void swiglu_bwd_tail(const GemmArgs& a, const lds_u8* st, int64_t mrow0, int ncol0,
+                                                int64_t ldc, uint16_t* C, int lane) {
+  constexpr int ROWB = TN * 2 + 16, CPR = TN / 8, RPI = 64 / CPR, NIT = TM / RPI, SG = PT_SWIGLU_GRP;
+  static_assert(NIT % SG == 0, "chunk groups");
+  typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+  const int lrow = lane / CPR, ch = lane % CPR;
+  const uint32_t roff = (uint32_t)(lrow * a.ldr + ch * 8) * 2u;  // bytes from the row group's base
+  const uint32_t coff = (uint32_t)(lrow * ldc + ch * 8) * 2u;
+  const int64_t r0 = (int64_t)__builtin_amdgcn_readfirstlane((int)mrow0);
+  const int c0 = __builtin_amdgcn_readfirstlane(ncol0);
+  const uint8_t* gbase = (const uint8_t*)(a.R + r0 * a.ldr + c0);
+  uint8_t* cbase = (uint8_t*)(C + r0 * ldc + c0);
+  const int64_t rstep = (int64_t)RPI * a.ldr * 2, cstep = (int64_t)RPI * ldc * 2, ustep = (int64_t)a.N * 2;
+#pragma unroll
+  for (int q0 = 0; q0 < NIT; q0 += SG) {
+    bf16x8 g[SG], u[SG];
+#pragma unroll
+    for (int k = 0; k < SG; ++k) {
+      g[k] = ld8((const uint16_t*)(gbase + (q0 + k) * rstep + roff));
+      u[k] = ld8((const uint16_t*)(gbase + (q0 + k) * rstep + ustep + roff));
+    }
+#pragma unroll
+    for (int k = 0; k < SG; ++k) {
+      const int q = q0 + k, row = q * RPI + lrow;
+      const u32x4_t raw = *(const __attribute__((address_space(3))) u32x4_t*)(st + row * ROWB + ch * 16);
+      bf16x8 v;
+      v.w[0] = raw[0]; v.w[1] = raw[1]; v.w[2] = raw[2]; v.w[3] = raw[3];
+      float d[8], gg[8], uu[8], og[8], ou[8];
+      unpack8(v, d);
+      unpack8(g[k], gg);
+      unpack8(u[k], uu);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float sg = silu_sig(gg[e]);
+        ou[e] = d[e] * round_bf(gg[e] * sg);
+        og[e] = round_bf(d[e] * uu[e]) * (sg * (1.0f + gg[e] * (1.0f - sg)));
+      }
+      st8((uint16_t*)(cbase + q * cstep + coff), pack8(og));
+      st8((uint16_t*)(cbase + q * cstep + ustep + coff), pack8(ou));
+    }
+  }
+}
+
+// EPI_F32_ACC (the f32 main_grad sink of DataParallelBucket): C += acc in two TM / 2-row passes
+// through this wave's LDS staging area (TM / 2 x 64 f32 + pad fits the TM x (64 bf16 + pad) area
+// the bf16 epilogues use) so that every global access is a
+// whole 16-byte chunk of a row (the accumulator layout gives 4-byte pieces of 16 rows); the old
+// values of BOTH passes are loaded before the first store (one memory round trip per wave, was
+// one per 16-row fragment row), pass 1's loads issued once pass 0's accumulators are staged.
+template <int TM, int TN>
+__device__ __forceinline__ void f32_acc_tail(const f32x4_t (&acc)[TM / 16][TN / 16], lds_u8* st, int64_t mrow0,
+                                             int ncol0, int64_t ldc, float* C, int lane) {
+  constexpr int HR = TM / 2, NP = 2, FP = HR / 16, FN = TN / 16;
+  static_assert(HR * (TN * 4 + 16) <= TM * (TN * 2 + 16), "f32 pass fits the staging area");
+  constexpr int ROWB = TN * 4 + 16, CPR = TN / 4, RPI = 64 / CPR, NIT = HR / RPI;
+  const int lrow = lane / CPR, ch = lane % CPR;
+  const int64_t r0 = (int64_t)__builtin_amdgcn_readfirstlane((int)mrow0);
+  const int c0 = __builtin_amdgcn_readfirstlane(ncol0);
+  uint8_t* cbase = (uint8_t*)(C + r0 * ldc + c0);
+  const uint32_t coff = (uint32_t)(lrow * ldc + ch * 4) * 4u;
+  const int64_t rstep = (int64_t)RPI * ldc * 4;
+  f32x4_t old[NP][NIT];
+  auto load_pass = [&](int p) {
+#pragma unroll
+    for (int q = 0; q < NIT; ++q) old[p][q] = *(const f32x4_t*)(cbase + (p * NIT + q) * rstep + coff);
+  };
+  auto stage_pass = [&](int p) {
+#pragma unroll
+    for (int i = 0; i < FP; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = i * 16 + (lane >> 4) * 4 + r, col = j * 16 + (lane & 15);
+          *(__attribute__((address_space(3))) float*)(st + row * ROWB + col * 4) = acc[p * FP + i][j][r];
+        }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-private staging
+  };
+  load_pass(0);
+  stage_pass(0);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int p = 1; p < NP; ++p) load_pass(p);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    if (p > 0) stage_pass(p);
+#pragma unroll
+    for (int q = 0; q < NIT; ++q) {
+      asm volatile("" : "+v"(old[p][q]));
+      const f32x4_t v = *(const __attribute__((address_space(3))) f32x4_t*)(st + (q * RPI + lrow) * ROWB + ch * 16);
+      *(f32x4_t*)(cbase + (p * NIT + q) * rstep + coff) = old[p][q] + v;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // this pass's LDS reads done before the next staging
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 template <int TM, int TN, int EPI>
 __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)[TM / 16][TN / 16], lds_u8* st,
                                          int m0, int n0, int wm, int wn, int lane, float2* xs_wave = nullptr) {
@@ -265,6 +376,10 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
     // they would be live next to all of acc and spill
     __builtin_amdgcn_sched_barrier(0);
     uint16_t* C = (uint16_t*)a.C[cs];
+    if constexpr (EPI == EPI_SWIGLU_BWD) {
+      swiglu_bwd_tail<TM, TN>(a, st, mrow0, ncol0, ldc, C, lane);
+      return;
+    }
     if constexpr (EPI == EPI_ROPE && TN == 64) {
       if (ncol0 < a.rope_cols) {
         // the wave's 64 columns are one head: lane = (row, chunk ch < 4) rotates chunk ch with
@@ -303,15 +418,13 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
     // the epilogues that READ memory (g|u, the residual, the accumulated gradient) issue all their
     // loads first, then consume them: C may alias R / the old gradient, so the compiler would keep
     // every load behind the previous iteration's store -- one HBM round trip per row group
-    constexpr bool RD = EPI == EPI_SWIGLU_BWD || EPI == EPI_BF16_ACC || EPI == EPI_BF16_RES;
-    constexpr int NLD = EPI == EPI_SWIGLU_BWD ? 2 : 1;
-    // prefetched chunks per group: the accumulate / residual epilogues 8 (32 VGPRs); the SwiGLU
-    // backward 2 (x2 loads: g, u) -- measured over 1 / 2 / 4 / 8 on the layer's shape, 8 is 40 %
-    // slower (profiles/r02_notes.md), 1-4 within 2 %
-    constexpr int GRP = EPI == EPI_SWIGLU_BWD ? PT_SWIGLU_GRP : (RD ? (NIT * NLD > 8 ? 8 / NLD : NIT) : NIT);
+    // (all NIT chunks -- 4 NIT VGPRs, the accumulators are dead once staged -- before any store,
+    // so the wave's epilogue is one memory round trip)
+    constexpr bool RD = EPI == EPI_BF16_ACC || EPI == EPI_BF16_RES;
+    constexpr int GRP = NIT;
 #pragma unroll
     for (int g0 = 0; g0 < NIT; g0 += GRP) {
-      bf16x8 pre[GRP][NLD];
+      bf16x8 pre[GRP][1];
       if constexpr (RD) {
 #pragma unroll
         for (int q = 0; q < GRP; ++q) {
@@ -319,8 +432,8 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
           const uint16_t* src = EPI == EPI_BF16_ACC ? C + (mrow0 + row) * ldc + ncol0 + ch * 8
                                                     : a.R + (mrow0 + row) * a.ldr + ncol0 + ch * 8;
           pre[q][0] = ld8(src);
-          if constexpr (NLD == 2) pre[q][NLD - 1] = ld8(src + a.N);
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
       for (int q = 0; q < GRP; ++q) {
@@ -329,21 +442,6 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
         bf16x8 v;
         v.w[0] = raw[0]; v.w[1] = raw[1]; v.w[2] = raw[2]; v.w[3] = raw[3];
         uint16_t* dst = C + (mrow0 + row) * ldc + ncol0 + ch * 8;
-        if constexpr (EPI == EPI_SWIGLU_BWD) {  // v = dh; g|u from R; dg|du to C (swiglu.hip's bwd)
-          float d[8], gg[8], uu[8], og[8], ou[8];
-          unpack8(v, d);
-          unpack8(pre[q][0], gg);
-          unpack8(pre[q][NLD - 1], uu);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float sg = silu_sig(gg[e]);
-            ou[e] = d[e] * round_bf(gg[e] * sg);
-            og[e] = round_bf(d[e] * uu[e]) * (sg * (1.0f + gg[e] * (1.0f - sg)));
-          }
-          st8(dst, pack8(og));
-          st8(dst + a.N, pack8(ou));
-          continue;
-        }
         if constexpr (EPI == EPI_CE_STATS) {
           // the row's TN = 64 columns of this wave are the CPR = 8 consecutive lanes sharing
           // lane / 8: max and sum-exp of the stored (bf16) values over the 8 x 8, one pair per row
@@ -360,6 +458,8 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
           if (ch == 0) xs_wave[row] = make_float2(mx, se);
         }
         if constexpr (EPI == EPI_BF16_ACC || EPI == EPI_BF16_RES) {
+          // opaque: keeps chunk q's unpacking (and so its wait) here, after every load is issued
+          asm volatile("" : "+v"(pre[q][0].w[0]), "+v"(pre[q][0].w[1]), "+v"(pre[q][0].w[2]), "+v"(pre[q][0].w[3]));
           float o[8], f[8];
           unpack8(v, f);
           unpack8(pre[q][0], o);
@@ -373,8 +473,12 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
     }
   } else {
     float* C = (float*)a.C[cs];
-    // f32 accumulate: one fragment row (FN x 4 values) of old values loaded before any of its
-    // stores (rows may alias as far as the compiler knows: else one round trip per element)
+    if constexpr (EPI == EPI_F32_ACC && TN == 64) {
+      f32_acc_tail<TM, TN>(acc, st, mrow0, ncol0, ldc, C, lane);
+      return;
+    }
+    // f32 store (and accumulate for other wave tiles): one fragment row (FN x 4 values) of old
+    // values loaded before any of its stores
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       float old[FN][4];
@@ -554,9 +658,10 @@ __device__ __forceinline__ void glds16_asm(const uint16_t* base, uint32_t voff_e
   pt_glds16(base, voff_elems * 2u, (__attribute__((address_space(3))) void*)dst);  // common.h
 }
 
+// one 256x256 output tile (tile_m, tile_n) of problem `a` by the whole 512-thread workgroup
 template <bool AK, bool BKC, int EPI>
-__global__ __launch_bounds__(512) void gemm_8ph_kernel(const GemmGroup g) {
-  constexpr int NT = 512, TM = 128, TN = 64, FM = 8, FN = 4;
+__device__ __forceinline__ void gemm_8ph_tile(const GemmArgs& a, const int tile_m, const int tile_n) {
+  constexpr int TM = 128, TN = 64, FM = 8, FN = 4;
   constexpr int HALF = 128 * BK * 2;          // 16 KiB
   constexpr int BUF = 4 * HALF;               // At, Bl, Br, Ab
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
@@ -564,8 +669,6 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const GemmGroup g) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
-  int tile_m, tile_n;
-  const GemmArgs& a = select_problem(g, tile_m, tile_n);
   const int m0 = tile_m * 256, n0 = tile_n * 256;
 
   // B segment for this tile (N-segments) or the first K-segment; ld is per tile (host checks
@@ -717,6 +820,50 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const GemmGroup g) {
       __syncthreads();
       if (wn == 0) ce_stats_merge<4, TM, TN>(a, xs, m0, n0, wm, lane);
     }
+  }
+}
+
+template <bool AK, bool BKC, int EPI>
+__global__ __launch_bounds__(512) void gemm_8ph_kernel(const GemmGroup g) {
+  int tile_m, tile_n;
+  const GemmArgs& a = select_problem(g, tile_m, tile_n);
+  gemm_8ph_tile<AK, BKC, EPI>(a, tile_m, tile_n);
+}
+
+// ---------------------------------------------------------------------------- dual launch
+// Two INDEPENDENT groups in one launch of 256x256 8-phase tiles, each with its own layouts and
+// epilogue: the down_proj dX with the SwiGLU backward in its epilogue beside the down_proj dW
+// (both read only dY and saved activations).  One launch instead of two: the dX tiles' HBM-bound
+// epilogue tail (the g|u read and dg|du write, ~4.5 TB/s while every CU is in it) shares the launch
+// with the dW tiles' main loops -- measured 271 vs 280 us for the two launches at SmolLM-1.7B
+// shapes.  Each XCD (blocks b, b + 8, ... share one) takes an equal, contiguous share of each
+// group's tiles (n0 / n1 per XCD), so both keep their XCD-grouped L2 reuse; `order` 0 runs an
+// XCD's group-0 tiles first, 1 its group-1 tiles first.  (Interleaving the groups inside an XCD,
+// in proportion or with the CUs split between them by work, measured 4-7 % slower: two GEMMs'
+// panels then share each L2; profiles/r02_notes.md.)
+struct DualMap {
+  int n0, n1, order;
+};
+
+__device__ __forceinline__ int dual_select(const DualMap& m, int& pid) {
+  const int bid = blockIdx.x, xcd = bid & 7, li = bid >> 3;
+  const int nfirst = m.order == 0 ? m.n0 : m.n1;
+  const bool first = li < nfirst;
+  const int which = (m.order == 0) ? !first : first;
+  const int local = first ? li : li - nfirst;
+  pid = xcd * (which ? m.n1 : m.n0) + local;
+  return which;
+}
+
+template <bool AK0, bool BKC0, int EPI0, bool AK1, bool BKC1, int EPI1>
+__global__ __launch_bounds__(512) void gemm_8ph_dual_kernel(const GemmGroup g0, const GemmGroup g1, const DualMap m) {
+  int pid, tile_m, tile_n;
+  if (dual_select(m, pid) == 0) {
+    const GemmArgs& a = select_problem_pid(g0, pid, tile_m, tile_n);
+    gemm_8ph_tile<AK0, BKC0, EPI0>(a, tile_m, tile_n);
+  } else {
+    const GemmArgs& a = select_problem_pid(g1, pid, tile_m, tile_n);
+    gemm_8ph_tile<AK1, BKC1, EPI1>(a, tile_m, tile_n);
   }
 }
 
@@ -1024,6 +1171,23 @@ int launch_8ph(GemmGroup g, hipStream_t stream) {
   return PT_OK;
 }
 
+template <bool AK0, bool BKC0, int EPI0, bool AK1, bool BKC1, int EPI1>
+int launch_dual_t(GemmGroup g0, GemmGroup g1, int order, hipStream_t stream) {
+  const int t0 = group_tiles(g0, 256, 256), t1 = group_tiles(g1, 256, 256);
+  if (t0 % 8 || t1 % 8) return PT_EUNSUPPORTED;  // equal per-XCD shares of both groups
+  const DualMap m{t0 / 8, t1 / 8, order};
+  constexpr int smem = 8 * 128 * (64 * 2 + 16);  // epilogue staging (> the 128 KiB main loop)
+  static_assert(smem <= 160 * 1024, "LDS budget");
+  static bool attr_set = false;
+  if (!attr_set) {
+    set_smem_once(gemm_8ph_dual_kernel<AK0, BKC0, EPI0, AK1, BKC1, EPI1>, smem);
+    attr_set = true;
+  }
+  gemm_8ph_dual_kernel<AK0, BKC0, EPI0, AK1, BKC1, EPI1><<<t0 + t1, 512, smem, stream>>>(g0, g1, m);
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
+
 template <bool AK, bool BKC, int EPI>
 int launch_4ph(GemmGroup g, hipStream_t stream) {
   const int tiles = group_tiles(g, 256, 128);
@@ -1255,6 +1419,32 @@ int launch_swiglu(GemmGroup& g, int a_kcontig, int b_kcontig, int epilogue, int 
   return launch_8ph<true, false, EPI_SWIGLU_BWD>(g, stream);
 }
 
+// group 0: dX (A = dY K-contiguous, B = W N-contiguous) with EPI_BF16 or EPI_SWIGLU_BWD;
+// group 1: wgrad (dY^T X: both operands MN-contiguous) into a bf16 / bf16-accumulate / f32-accumulate sink
+template <int EPI0>
+int launch_dual_e1(GemmGroup& g0, GemmGroup& g1, int e1, int order, hipStream_t s) {
+  switch (e1) {
+    case EPI_BF16: return launch_dual_t<true, false, EPI0, false, false, EPI_BF16>(g0, g1, order, s);
+    case EPI_BF16_ACC: return launch_dual_t<true, false, EPI0, false, false, EPI_BF16_ACC>(g0, g1, order, s);
+    case EPI_F32_ACC: return launch_dual_t<true, false, EPI0, false, false, EPI_F32_ACC>(g0, g1, order, s);
+    default: return PT_EUNSUPPORTED;
+  }
+}
+
+int launch_dual(GemmGroup& g0, int ak0, int bk0, int e0, GemmGroup& g1, int ak1, int bk1, int e1, int order,
+                hipStream_t s) {
+  if (!ak0 || bk0 || ak1 || bk1 || order < 0 || order > 1) return PT_EUNSUPPORTED;
+  for (int i = 0; i < g0.nprob; ++i) {
+    if (!args_fit(g0.p[i], 12)) return PT_EUNSUPPORTED;
+    if (e0 == EPI_SWIGLU_BWD && (g0.p[i].ncseg != 1 || g0.p[i].bdim != 0 || g0.p[i].nbseg != 1)) return PT_EUNSUPPORTED;
+  }
+  for (int i = 0; i < g1.nprob; ++i)
+    if (!args_fit(g1.p[i], 12)) return PT_EUNSUPPORTED;
+  if (e0 == EPI_BF16) return launch_dual_e1<EPI_BF16>(g0, g1, e1, order, s);
+  if (e0 == EPI_SWIGLU_BWD) return launch_dual_e1<EPI_SWIGLU_BWD>(g0, g1, e1, order, s);
+  return PT_EUNSUPPORTED;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1289,6 +1479,30 @@ int pt_gemm_grouped(const pt_gemm_problem* probs, int nprob, int a_kcontig, int 
     if (rc) return rc;
   }
   return launch_group(g, a_kcontig, b_kcontig, epilogue, tile, stream);
+}
+
+// Two independent groups in ONE launch of 256x256 8-phase tiles (see gemm_8ph_dual_kernel): a dX
+// group and a wgrad group of the same layer, each with its own epilogue.  PT_EUNSUPPORTED when a
+// problem does not tile by 256x256 or a group's tile count is not a multiple of 8 (the caller
+// then launches the two groups separately).
+int pt_gemm_dual(const pt_gemm_problem* p0, int n0, int a_kcontig0, int b_kcontig0, int epilogue0,
+                 const pt_gemm_problem* p1, int n1, int a_kcontig1, int b_kcontig1, int epilogue1, int order,
+                 hipStream_t stream) {
+  if (!p0 || !p1 || n0 < 1 || n0 > kMaxProb || n1 < 1 || n1 > kMaxProb) return PT_EINVAL;
+  GemmGroup g[2]{};
+  const pt_gemm_problem* ps[2] = {p0, p1};
+  const int ns[2] = {n0, n1}, es[2] = {epilogue0, epilogue1};
+  for (int k = 0; k < 2; ++k) {
+    g[k].nprob = ns[k];
+    for (int i = 0; i < ns[k]; ++i) {
+      const pt_gemm_problem& q = ps[k][i];
+      const int rc = fill_args(g[k].p[i], q.A, q.lda, q.B, q.ldb, q.b_bounds, q.nb, q.b_seg_dim, q.C, q.ldc,
+                               q.c_bounds, q.nc, q.M, q.N, q.K, es[k], q.residual, q.ldr);
+      if (rc) return rc;
+    }
+  }
+  return launch_dual(g[0], a_kcontig0, b_kcontig0, epilogue0, g[1], a_kcontig1, b_kcontig1, epilogue1, order,
+                     stream);
 }
 
 // q|k|v projection with RoPE fused (EPI_ROPE): C[M,N] = A[M,K] . [B_0; ...]^T with columns

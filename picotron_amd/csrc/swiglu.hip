@@ -13,7 +13,7 @@
 
 namespace {
 
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float sigmoidf_(float x) { return pt_sigmoid(x); }
 
 __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const uint16_t* __restrict__ g, int64_t gs,
                                                          const uint16_t* __restrict__ u, int64_t us,

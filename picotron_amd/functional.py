@@ -102,6 +102,40 @@ def wgrad_group(jobs):
             _grad_ready(p)
 
 
+def dgrad_with_wgrad(dy2d, weights, wjobs, gu=None):
+    """dX = dY . [W_0; ...] (with gu: the down_proj dX's SwiGLU backward, dg|du) AND the wgrads
+    wjobs [(dy2d, x2d, params)] of the same layer in ONE launch (K.linear_dgrad_dual) when the
+    shapes tile for it and every sink takes one epilogue; otherwise the separate launches.
+    Returns dX / dg|du."""
+    frozen = any(not p.requires_grad for _, _, params in wjobs for p in params)
+    mns = [(dy.shape[1], x.shape[1]) for dy, x, _ in wjobs]
+    dmn = (dy2d.shape[0], gu.shape[1] // 2 if gu is not None else weights[0].shape[1])
+    if K.dual_enabled() and not frozen and K.dual_fits(dmn, mns):
+        targets = [[_wgrad_target(p) for p in params] for _, _, params in wjobs]
+        epis = {e for tg in targets for _, e in tg}
+        if len(epis) == 1:
+            epi = epis.pop()
+            wk = [(dy, x, [t for t, _ in tg]) for (dy, x, _), tg in zip(wjobs, targets)]
+            dx = K.linear_dgrad_dual(dy2d, weights, wk, epi, gu=gu)
+            if dx is None:   # not tileable after all: the same sinks, separate launches
+                dx = K.linear_dgrad_swiglu(dy2d, weights[0], gu) if gu is not None else K.linear_dgrad(dy2d, weights)
+                K.linear_wgrad_grouped(wk, epilogue=epi)
+        else:   # mixed sinks: one launch per parameter (the targets exist now)
+            dx = K.linear_dgrad_swiglu(dy2d, weights[0], gu) if gu is not None else K.linear_dgrad(dy2d, weights)
+            for (dy, x, params), tg in zip(wjobs, targets):
+                lo = 0
+                for p, (t, e) in zip(params, tg):
+                    K.linear_wgrad(dy[:, lo:lo + p.shape[0]], x, [t], epilogue=e)
+                    lo += p.shape[0]
+        for _, _, params in wjobs:
+            for p in params:
+                _grad_ready(p)
+        return dx
+    dx = K.linear_dgrad_swiglu(dy2d, weights[0], gu) if gu is not None else K.linear_dgrad(dy2d, weights)
+    wgrad_group(wjobs)
+    return dx
+
+
 def norm_bwd(dy2, z, weight, rstd, mode, dres=None, need_dw=True):
     """RMSNorm backward with the weight gradient summed straight into p's sink (bf16 .grad store or
     accumulate -- autograd's AccumulateGrad -- or the f32 main_grad of DataParallelBucket).  A frozen
@@ -416,12 +450,14 @@ def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True):
     gu, hh = saved
     I = wg.shape[0]
     if _fuse() and K.swiglu_fusable(dm.shape[0], I, backward=True):   # SwiGLU bwd in the down dX epilogue
-        dgu = K.linear_dgrad_swiglu(dm, wd, gu)
+        # ... in one launch with the down_proj dW: the epilogue's HBM-bound g|u / dg|du tail
+        # overlaps the dW's MFMA work (K.linear_dgrad_dual)
+        dgu = dgrad_with_wgrad(dm, [wd], [(dm, hh, [wd])], gu=gu)
     else:
         dhh = K.linear_dgrad(dm, [wd])
         dgu = torch.empty_like(gu)
         K.swiglu_bwd(dhh, gu[:, :I], gu[:, I:], dg=dgu[:, :I], du=dgu[:, I:])
-    wgrad(dm, hh, [wd])
+        wgrad(dm, hh, [wd])
     dh = handle = None
     if need_dx:
         dh = K.linear_dgrad(dgu, [wg, wu])

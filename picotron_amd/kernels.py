@@ -625,6 +625,76 @@ def linear_dgrad(dy2d, weights, out=None, accumulate=False, tile=-1):
     return dx
 
 
+def dual_enabled():
+    """PICOTRON_DUAL=0 launches a layer's dX and dW GEMMs separately (A/B measurement only)."""
+    return os.environ.get("PICOTRON_DUAL", "1") != "0"
+
+
+def _dual_order():
+    return int(os.environ.get("PICOTRON_DUAL_ORDER", "0"))
+
+
+def dual_fits(dgrad_mn, wgrad_mns):
+    """Whether pt_gemm_dual tiles these problems: every [M, N] by 256 x 256 and each group's tile
+    count a multiple of 8 (equal shares per XCD)."""
+    def ok(mns):
+        return all(m % 256 == 0 and n % 256 == 0 for m, n in mns) and sum(m * n for m, n in mns) // 65536 % 8 == 0
+    return ok([dgrad_mn]) and ok(wgrad_mns)
+
+
+def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None):
+    """dX = dY . [W_0; ...] (or, with gu, the SwiGLU backward dg|du of the down_proj dX:
+    linear_dgrad_swiglu) AND the wgrads wjobs [(dy2d, x2d, outs)] (linear_wgrad, epilogue
+    wepilogue) in ONE launch (pt_gemm_dual).  Returns dX / dg|du, or None (nothing launched) when
+    the problems do not tile for it -- the caller then launches them separately."""
+    _bf16_rowmajor(dy2d, "dy")
+    T, N = dy2d.shape
+    if gu is not None:
+        wd = weights[0]
+        I = wd.shape[1]
+        _bf16_rowmajor(gu, "gu")
+        _req(len(weights) == 1 and wd.is_contiguous() and wd.shape[0] == N and tuple(gu.shape) == (T, 2 * I),
+             "dual: down weight [H, I], gu [T, 2I]")
+        dx = torch.empty(T, 2 * I, dtype=BF16, device=dy2d.device)
+        p0 = _problem(dy2d, dy2d.stride(0), [wd], [I], [0, I], 0, [dx], [dx.stride(0)], [0, T], T, I, N)
+        p0.residual, p0.ldr = _ptr(gu), gu.stride(0)
+        e0, flops, nbytes = EPI_SWIGLU_BWD, 2.0 * T * I * N, _alg_bytes(T, I, N, EPI_SWIGLU_BWD)
+    else:
+        Kin = weights[0].shape[1]
+        ns = [w.shape[0] for w in weights]
+        _req(sum(ns) == N, "dgrad: dY width must equal the stacked weight rows")
+        dx = torch.empty(T, Kin, dtype=BF16, device=dy2d.device)
+        p0 = _problem(dy2d, dy2d.stride(0), weights, [Kin] * len(weights), _bounds(ns), 1, [dx], [dx.stride(0)],
+                      [0, T], T, Kin, N)
+        e0, flops, nbytes = EPI_BF16, 2.0 * T * Kin * N, _alg_bytes(T, Kin, N, EPI_BF16)
+    p0s = (_C.GemmProblem * 1)(p0)
+    p1s = (_C.GemmProblem * len(wjobs))()
+    for j, (wdy, x2d, outs) in enumerate(wjobs):
+        _bf16_rowmajor(wdy, "dy")
+        _bf16_rowmajor(x2d, "x")
+        Tw, Nw = wdy.shape
+        Kin = x2d.shape[1]
+        ns = [o.shape[0] for o in outs]
+        _req(sum(ns) == Nw and x2d.shape[0] == Tw, "wgrad: output rows must cover dY's width")
+        p1s[j] = _problem(wdy, wdy.stride(0), [x2d], [x2d.stride(0)], [0, Kin], 0, outs, [o.stride(0) for o in outs],
+                          _bounds(ns), Nw, Kin, Tw)
+        flops += 2.0 * Nw * Kin * Tw
+        nbytes += _alg_bytes(Nw, Kin, Tw, wepilogue)
+    probe = _PROBE
+    if probe is not None:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    rc = _C.lib().pt_gemm_dual(p0s, 1, 1, 0, e0, p1s, len(wjobs), 0, 0, int(wepilogue),
+                               _dual_order() if order is None else int(order), _C.stream_ptr(dy2d.device))
+    if rc == -3:   # PT_EUNSUPPORTED: outside the dual tiling (e.g. C segments not on 256 rows)
+        return None
+    _C.check(rc, f"pt_gemm_dual(dX epi {e0}, {len(wjobs)} wgrads epi {wepilogue})")
+    if probe is not None:
+        ev1.record()
+        probe.records.append((ev0, ev1, flops, nbytes))
+    return dx
+
+
 def linear_wgrad(dy2d, x2d, outs, epilogue=EPI_BF16, tile=-1):
     """dW_i = dY_i^T . X for the column segments dY_i of dY (widths = outs[i].shape[0]); one launch."""
     _bf16_rowmajor(dy2d, "dy")

@@ -273,6 +273,59 @@ def test_gemm_swiglu_fused(T, H, I):
     assert torch.equal(dgu[:, I:], du)
 
 
+@pytest.mark.parametrize("swiglu", [True, False])
+@pytest.mark.parametrize("epi", [0, 1, 3])
+@pytest.mark.parametrize("order", [0, 1])
+def test_gemm_dual_equals_separate(swiglu, epi, order):
+    """pt_gemm_dual (a dX group and a wgrad group in one launch, every dispatch order) == the two
+    groups as separate 256x256 launches, bit for bit: the down_proj dX with the SwiGLU backward
+    beside its dW, and a K-segmented q|k|v dX beside the q|k|v + o_proj dWs"""
+    from picotron_amd import kernels as K_
+    T, H = 1024, 512
+    dt = torch.float32 if epi == 3 else BF
+    if swiglu:
+        I = 1024
+        dm = torch.randn(T, H).to(BF).to(DEV)
+        wd = (torch.randn(H, I) / math.sqrt(I)).to(BF).to(DEV)
+        gu = torch.randn(T, 2 * I).to(BF).to(DEV)
+        hh = torch.randn(T, I).to(BF).to(DEV)
+        init = [torch.randn(H, I).to(dt).to(DEV)]
+        wj = lambda outs: [(dm, hh, outs)]
+        outs = [t.clone() for t in init]
+        dx = K_.linear_dgrad_dual(dm, [wd], wj(outs), epi, gu=gu, order=order)
+        ref_dx = K_.linear_dgrad_swiglu(dm, wd, gu)
+    else:
+        H, nkv = 1024, 512
+        dqkv = torch.randn(T, H + 2 * nkv).to(BF).to(DEV)
+        ws = [(torch.randn(n, H) / math.sqrt(H)).to(BF).to(DEV) for n in (H, nkv, nkv)]
+        h, da, o = [torch.randn(T, H).to(BF).to(DEV) for _ in range(3)]
+        init = [torch.randn(n, H).to(dt).to(DEV) for n in (H, nkv, nkv, H)]
+        outs = [t.clone() for t in init]
+        wj = lambda o_: [(dqkv, h, o_[:3]), (da, o, o_[3:])]
+        dx = K_.linear_dgrad_dual(dqkv, ws, wj(outs), epi, order=order)
+        ref_dx = K_.linear_dgrad(dqkv, ws, tile=12)
+    assert dx is not None
+    refs = [t.clone() for t in init]
+    K_.linear_wgrad_grouped(wj(refs), epilogue=epi, tile=12)
+    torch.cuda.synchronize()
+    assert torch.equal(dx, ref_dx)
+    for a, b in zip(outs, refs):
+        assert torch.equal(a, b)
+
+
+def test_gemm_dual_unsupported_returns_none():
+    """a group whose tile count is not a multiple of 8 is refused before anything runs"""
+    from picotron_amd import kernels as K_
+    T, H = 256, 512   # dX: 1 x 2 tiles
+    dy = torch.randn(T, H).to(BF).to(DEV)
+    w = torch.randn(H, H).to(BF).to(DEV)
+    out = torch.zeros(H, H, dtype=BF, device=DEV)
+    assert not K_.dual_fits((T, H), [(H, H)])
+    assert K_.linear_dgrad_dual(dy, [w], [(dy, dy, [out])], 0) is None
+    torch.cuda.synchronize()
+    assert not out.any()
+
+
 @pytest.mark.parametrize("nh,nkv,S", [(4, 2, 256), (8, 8, 128), (32, 32, 1024)])
 def test_gemm_rope_fused(nh, nkv, S):
     """q|k|v projection with RoPE in the epilogue == projection + rope kernel, bit for bit"""
