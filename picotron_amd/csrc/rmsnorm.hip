@@ -25,13 +25,14 @@ namespace {
 constexpr int kCUs = 256;
 
 // launch shape: waves per block and blocks per CU (grid cap) of the forward and backward kernels.
-// Measured at T 4096 (tools/norm_bench.py, profiles/r02_norm_bench.log): 4 x 4 / 8 x 2; PT_NORM
-// ("fwd_wpb,fwd_bpc,bwd_wpb,bwd_bpc", read once) overrides it for such sweeps.
+// Measured at T 4096 (tools/norm_bench.py, profiles/r02_norm_bench.log, r02_notes.md): 4 x 4 /
+// 16 x 1 (backward + column sum 17.5-18.4 us vs 19.2 with 8 x 2: one 1024-thread block per CU
+// halves the partial rows); PT_NORM ("fwd_wpb,fwd_bpc,bwd_wpb,bwd_bpc", read once) overrides it.
 struct NormCfg { int fwd_wpb, fwd_bpc, bwd_wpb, bwd_bpc; };
 
 const NormCfg& norm_cfg() {
   static const NormCfg cfg = [] {
-    NormCfg c{4, 4, 8, 2};
+    NormCfg c{4, 4, 16, 1};
     if (const char* e = getenv("PT_NORM")) sscanf(e, "%d,%d,%d,%d", &c.fwd_wpb, &c.fwd_bpc, &c.bwd_wpb, &c.bwd_bpc);
     return c;
   }();
@@ -213,20 +214,32 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(min_wa
 }
 
 // dw[col] = sum_p partial[p][col]  -- fixed summation order, deterministic.  One block per 32
-// columns: 8 lanes x 16 B cover a partial row's 32 columns (128 contiguous bytes per row), the 32
-// lane groups of the block stride over the partial rows, then a fixed-order sum over the groups.
+// columns: 8 lanes x 16 B cover a partial row's 32 columns (128 contiguous bytes per row), the 128
+// lane groups of the 1024-thread block take every 128th partial row (all of a thread's rows loaded
+// before any is added), then a fixed-order two-level sum over the groups (4 groups per thread, then
+// 32).  (256 threads and 32 groups: 16 dependent rows per thread, one wave per CU -- 4.9 us for
+// the 4 MB of partials at T 4096.)
 // Sink (flags): 0 store bf16, DW_ACC_BF16 bf16 accumulate (= autograd's grad + bf16(new)),
 // DW_ACC_F32 f32 accumulate (DataParallelBucket main_grad).
-constexpr int kCsCols = 32, kCsThreads = 256, kCsGroups = kCsThreads / (kCsCols / 4);
+constexpr int kCsCols = 32, kCsThreads = 1024, kCsGroups = kCsThreads / (kCsCols / 4);
 __global__ __launch_bounds__(kCsThreads) void colsum_kernel(const float* __restrict__ partial, int nparts,
                                                             int cols, void* __restrict__ out, int sink) {
   __shared__ float red[kCsGroups][kCsCols + 1];
+  __shared__ float red2[kCsThreads / kCsCols][kCsCols + 1];
   const int t = threadIdx.x, ch = t & 7, grp = t >> 3;
   const int col4 = blockIdx.x * kCsCols + ch * 4;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (col4 < cols) {
-#pragma unroll 4
-    for (int p = grp; p < nparts; p += kCsGroups) {
+    constexpr int kPre = 4;  // rows in flight per thread (nparts <= 4 x 128 at the layer's shapes)
+    int p = grp;
+    for (; p + (kPre - 1) * kCsGroups < nparts; p += kPre * kCsGroups) {
+      float4 a[kPre];
+#pragma unroll
+      for (int k = 0; k < kPre; ++k) a[k] = *(const float4*)(partial + (int64_t)(p + k * kCsGroups) * cols + col4);
+#pragma unroll
+      for (int k = 0; k < kPre; ++k) { s0 += a[k].x; s1 += a[k].y; s2 += a[k].z; s3 += a[k].w; }
+    }
+    for (; p < nparts; p += kCsGroups) {
       const float4 a = *(const float4*)(partial + (int64_t)p * cols + col4);
       s0 += a.x; s1 += a.y; s2 += a.z; s3 += a.w;
     }
@@ -234,11 +247,20 @@ __global__ __launch_bounds__(kCsThreads) void colsum_kernel(const float* __restr
   red[grp][ch * 4 + 0] = s0; red[grp][ch * 4 + 1] = s1;
   red[grp][ch * 4 + 2] = s2; red[grp][ch * 4 + 3] = s3;
   __syncthreads();
+  {  // level 1: thread (part, c) sums groups 4 part .. 4 part + 3 of column c
+    const int c = t & (kCsCols - 1), part = t / kCsCols;
+    constexpr int per = kCsGroups / (kCsThreads / kCsCols);
+    float v = 0.f;
+#pragma unroll
+    for (int g = 0; g < per; ++g) v += red[part * per + g][c];
+    red2[part][c] = v;
+  }
+  __syncthreads();
   const int col = blockIdx.x * kCsCols + t;
   if (t < kCsCols && col < cols) {
     float v = 0.f;
 #pragma unroll
-    for (int g = 0; g < kCsGroups; ++g) v += red[g][t];
+    for (int g = 0; g < kCsThreads / kCsCols; ++g) v += red2[g][t];
     if (sink == PT_DW_ACC_F32) {
       ((float*)out)[col] += v;
     } else if (sink == PT_DW_ACC_BF16) {
@@ -264,7 +286,8 @@ int grid_for(int64_t rows, int wpb, int bpc) {
   return (int)(g < cap ? g : cap);
 }
 
-int bwd_wpb(int nch, const NormCfg& c) { return nch == 8 ? 4 : c.bwd_wpb; }  // LDS: wpb * cols * 4 <= 64 KiB
+// LDS: wpb * cols * 4 (<= 64 KiB at 8 waves, 128 KiB at 16)
+int bwd_wpb(int nch, const NormCfg& c) { return nch == 8 ? 4 : (nch > 4 && c.bwd_wpb == 16 ? 8 : c.bwd_wpb); }
 
 template <int NCH>
 void launch_fwd(int wpb, int grid, hipStream_t s, const uint16_t* X, const uint16_t* R, const uint16_t* W,
@@ -277,8 +300,19 @@ template <int NCH>
 void launch_bwd(int wpb, int grid, hipStream_t s, const uint16_t* DY, const uint16_t* Z, const uint16_t* W,
                 const float* rstd, const uint16_t* DR, uint16_t* DX, float* part, int64_t rows, int cols, int mode) {
   const size_t lds = (size_t)wpb * cols * sizeof(float);
-  if (wpb == 8) rmsnorm_bwd_kernel<NCH, 8><<<grid, 512, lds, s>>>(DY, Z, W, rstd, DR, DX, part, rows, cols, mode);
-  else rmsnorm_bwd_kernel<NCH, 4><<<grid, 256, lds, s>>>(DY, Z, W, rstd, DR, DX, part, rows, cols, mode);
+  if (wpb == 16) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)rmsnorm_bwd_kernel<NCH, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+      attr = true;
+    }
+    rmsnorm_bwd_kernel<NCH, 16><<<grid, 1024, lds, s>>>(DY, Z, W, rstd, DR, DX, part, rows, cols, mode);
+  } else if (wpb == 8) {
+    rmsnorm_bwd_kernel<NCH, 8><<<grid, 512, lds, s>>>(DY, Z, W, rstd, DR, DX, part, rows, cols, mode);
+  } else {
+    rmsnorm_bwd_kernel<NCH, 4><<<grid, 256, lds, s>>>(DY, Z, W, rstd, DR, DX, part, rows, cols, mode);
+  }
 }
 
 }  // namespace
@@ -329,7 +363,7 @@ int pt_rmsnorm_bwd(const void* dy, const void* z, const void* weight, const floa
   const int nmode = mode & 3;
   if (nmode > 1 || (mode & PT_DW_ACC_BF16 && mode & PT_DW_ACC_F32)) return PT_EINVAL;
   const NormCfg& c = norm_cfg();
-  const int wpb = bwd_wpb(nch, c) == 8 ? 8 : 4;
+  const int wpb = bwd_wpb(nch, c);
   const int grid = grid_for(rows, wpb, c.bwd_bpc);
   const auto* DY = (const uint16_t*)dy;
   const auto* Z = (const uint16_t*)z;
