@@ -230,6 +230,11 @@ def cfg_name(base):
 
 
 def main():
+    # stdout carries exactly ONE line, the JSON result: anything else written to fd 1 (RCCL prints
+    # its version banner there when a communicator is created) is sent to stderr
+    result_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -294,7 +299,7 @@ def main():
     layers = args.layers or default_layers
     if args.tp_proxy or args.cp_proxy:
         out = tp_proxy(args, base, layers) if args.tp_proxy else cp_proxy(args, base, layers)
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=result_out, flush=True)
         return
     tp, cp = args.tp, args.cp
     if world % (tp * cp):
@@ -404,7 +409,7 @@ def main():
                           **({"bucket_mb": args.bucket_mb, "grad_type": args.grad_type}
                              if (m.cp_dp_world_size > 1 or force_dp) else {})},
                "roofline": roofline, "cpu_baseline": cpu}
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=result_out, flush=True)
     if world > 1 or force_dp:
         dist.destroy_process_group()
 

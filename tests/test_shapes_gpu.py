@@ -50,15 +50,20 @@ def _weights(H, I, nh, nkv, d, seed):
             "mlp.gate_proj.weight": u(I, H), "mlp.up_proj.weight": u(I, H), "mlp.down_proj.weight": u(H, I)}
 
 
-def _layer_parity(B, S, H, I, nh, nkv, d, seed=0):
+def _layer_parity(B, S, H, I, nh, nkv, d, seed=0, main_grad=False):
     """One decoder layer (model.py:204-209) fwd + bwd through functional.DecoderLayerFunction (the
-    node model.DecoderLayer runs) at these dims vs the oracle."""
+    node model.DecoderLayer runs) at these dims vs the oracle.  main_grad: every weight carries an
+    f32 `main_grad` as DataParallelBucket gives it (data_parallel.py:122-144), so each wgrad
+    epilogue (the dual down_proj dX + dW launch included) accumulates in f32."""
     from picotron_amd import functional as FN
     from picotron_amd import process_group_manager as pgm
     pgm.setup_process_group_manager(1, 1, 1, 1)
     w = _weights(H, I, nh, nkv, d, seed)
     dev = torch.device("cuda")
     params = {k: torch.nn.Parameter(v.to(dev)) for k, v in w.items()}
+    if main_grad:
+        for p in params.values():
+            p.main_grad = torch.zeros(p.shape, dtype=torch.float32, device=dev)
     cos, sin = O.get_cos_sin(S, d, base=10000.0)
     g = torch.Generator().manual_seed(seed + 1)
     x = torch.randn(B, S, H, generator=g).to(BF)
@@ -73,13 +78,17 @@ def _layer_parity(B, S, H, I, nh, nkv, d, seed=0):
     yr.backward(dy.float())
     errs = {"y": rel(y, yr), "dx": rel(xg.grad, xr.grad)}
     for n in NAMES:
-        errs["d" + n] = rel(params[n].grad, pr[n].grad)
+        errs["d" + n] = rel(params[n].main_grad if main_grad else params[n].grad, pr[n].grad)
     bad = {k: v for k, v in errs.items() if not v < TOL}
     assert not bad, (bad, errs)
 
 
 def test_smollm_1_7b_layer_mbs4_seq1024():
     _layer_parity(B=4, S=1024, H=2048, I=8192, nh=32, nkv=32, d=64)
+
+
+def test_smollm_1_7b_layer_f32_main_grad():
+    _layer_parity(B=4, S=1024, H=2048, I=8192, nh=32, nkv=32, d=64, seed=7, main_grad=True)
 
 
 def test_llama2_7b_layer_seq1024():
