@@ -385,20 +385,33 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
         // the wave's 64 columns are one head: lane = (row, chunk ch < 4) rotates chunk ch with
         // its partner ch + 4 (d, d + 32) from the bf16 staging, as csrc/rope.hip does
         typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+        // every row's cos / sin chunk loaded before the first store (C may alias the tables as far
+        // as the compiler knows: loaded per row, they were one table round trip per 16 rows)
+        constexpr int NR = TM / 16;
+        bf16x8 cv[NR], sv[NR];
 #pragma unroll
-        for (int it = 0; it < TM / 16; ++it) {
+        for (int it = 0; it < NR; ++it) {
           const int row = it * 16 + lane / 4, ch = lane % 4;
+          const int64_t pos = (mrow0 + row) % a.rope_seq;
+          cv[it] = ld8(a.rope_cos + pos * a.rope_ld + ch * 8);
+          sv[it] = ld8(a.rope_sin + pos * a.rope_ld + ch * 8);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int it = 0; it < NR; ++it) {
+          const int row = it * 16 + lane / 4, ch = lane % 4;
+          asm volatile("" : "+v"(cv[it].w[0]), "+v"(cv[it].w[1]), "+v"(cv[it].w[2]), "+v"(cv[it].w[3]));
+          asm volatile("" : "+v"(sv[it].w[0]), "+v"(sv[it].w[1]), "+v"(sv[it].w[2]), "+v"(sv[it].w[3]));
           const u32x4_t r1 = *(const __attribute__((address_space(3))) u32x4_t*)(st + row * ROWB + ch * 16);
           const u32x4_t r2 = *(const __attribute__((address_space(3))) u32x4_t*)(st + row * ROWB + (ch + 4) * 16);
-          const int64_t pos = (mrow0 + row) % a.rope_seq;
           float x1[8], x2[8], c[8], sn[8], o1[8], o2[8];
           bf16x8 v1, v2;
           v1.w[0] = r1[0]; v1.w[1] = r1[1]; v1.w[2] = r1[2]; v1.w[3] = r1[3];
           v2.w[0] = r2[0]; v2.w[1] = r2[1]; v2.w[2] = r2[2]; v2.w[3] = r2[3];
           unpack8(v1, x1);
           unpack8(v2, x2);
-          unpack8(ld8(a.rope_cos + pos * a.rope_ld + ch * 8), c);
-          unpack8(ld8(a.rope_sin + pos * a.rope_ld + ch * 8), sn);
+          unpack8(cv[it], c);
+          unpack8(sv[it], sn);
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             o1[e] = fmaf(x1[e], c[e], -(x2[e] * sn[e]));
