@@ -43,6 +43,19 @@ namespace {
 
 constexpr int BK = 64;
 
+// Accumulator layout.  Every MFMA is fed (B fragment, A fragment), so a 16x16 accumulator holds
+// C^T of its block: lane l has row (l & 15), columns 4 (l >> 4) .. +3 -- four consecutive columns
+// of one row.  The epilogue then stages each (i, j) fragment with ONE 8-byte (bf16) / 16-byte
+// (f32) LDS write instead of four 2- / 4-byte ones (a wave's 128 x 64 bf16 tile: 32 instead of
+// 128 LDS write instructions).  Same products and summation order as the (A, B) order.
+__device__ __forceinline__ int acc_row(int i, int lane) { return i * 16 + (lane & 15); }
+__device__ __forceinline__ int acc_col(int j, int r, int lane) { return j * 16 + (lane >> 4) * 4 + r; }
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+template <typename V, typename A>
+__device__ __forceinline__ A mfma16(const V& a, const V& b, const A& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, c, 0, 0, 0);
+}
+
 // EPI_BF16_RES: C = bf16(R + bf16(acc)) -- the residual add of model.py:207-208 fused into the
 // producing GEMM (R may alias C).
 // EPI_SWIGLU_FWD: the gate|up projection with SwiGLU (model.py:186) in its epilogue: B = {W_gate,
@@ -323,12 +336,9 @@ __device__ __forceinline__ void f32_acc_tail(const f32x4_t (&acc)[TM / 16][TN / 
 #pragma unroll
     for (int i = 0; i < FP; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = i * 16 + (lane >> 4) * 4 + r, col = j * 16 + (lane & 15);
-          *(__attribute__((address_space(3))) float*)(st + row * ROWB + col * 4) = acc[p * FP + i][j][r];
-        }
+      for (int j = 0; j < FN; ++j)  // the fragment's 4 columns of one row: one 16-byte write
+        *(__attribute__((address_space(3))) f32x4_t*)(st + acc_row(i, lane) * ROWB + acc_col(j, 0, lane) * 4) =
+            acc[p * FP + i][j];
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-private staging
   };
   load_pass(0);
@@ -361,16 +371,14 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
   const int ncol0 = n0 + wn * TN;
   if (EPI == EPI_BF16 || EPI == EPI_BF16_ACC || EPI == EPI_BF16_RES || EPI == EPI_SWIGLU_BWD || EPI == EPI_ROPE ||
       EPI == EPI_CE_STATS) {
-    constexpr int ROWB = TN * 2 + 16;  // +16 B pad: spreads the column-wise 2-B writes over banks
+    constexpr int ROWB = TN * 2 + 16;  // +16 B pad: spreads the staging writes over banks
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = i * 16 + (lane >> 4) * 4 + r, col = j * 16 + (lane & 15);
-          *(__attribute__((address_space(3))) uint16_t*)(st + row * ROWB + col * 2) = f2bf(acc[i][j][r]);
-        }
+      for (int j = 0; j < FN; ++j) {  // 4 consecutive columns of one row: one 8-byte write
+        const u32x2_t w = {pack_bf2(acc[i][j][0], acc[i][j][1]), pack_bf2(acc[i][j][2], acc[i][j][3])};
+        *(__attribute__((address_space(3))) u32x2_t*)(st + acc_row(i, lane) * ROWB + acc_col(j, 0, lane) * 2) = w;
+      }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-private staging, no barrier needed
     // keep the epilogue's loads below the staging (the accumulators die there): hoisted above it,
     // they would be live next to all of acc and spill
@@ -500,35 +508,32 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
         for (int j = 0; j < FN; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            old[j][r] = C[(mrow0 + i * 16 + (lane >> 4) * 4 + r) * ldc + ncol0 + j * 16 + (lane & 15)];
+            old[j][r] = C[(mrow0 + acc_row(i, lane)) * ldc + ncol0 + acc_col(j, r, lane)];
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int64_t row = mrow0 + i * 16 + (lane >> 4) * 4 + r;
-          const int col = ncol0 + j * 16 + (lane & 15);
+          const int64_t row = mrow0 + acc_row(i, lane);
+          const int col = ncol0 + acc_col(j, r, lane);
           C[row * ldc + col] = EPI == EPI_F32_ACC ? old[j][r] + acc[i][j][r] : acc[i][j][r];
         }
     }
   }
 }
 
-// Stage a 128 x 32 bf16 tile (values f(i, j, r) at wave row 16 i + 4 (lane >> 4) + r, column
-// 16 j + (lane & 15)) through this wave's LDS area and write it at dst (+ row * ld) as 16-B row
-// segments.
+// Stage a 128 x 32 bf16 tile (value f(i, j, r) at wave row acc_row(i), column acc_col(j, r))
+// through this wave's LDS area and write it at dst (+ row * ld) as 16-B row segments.
 template <typename F>
 __device__ __forceinline__ void write_128x32(lds_u8* st, int lane, uint16_t* dst, int64_t ld, F f) {
   constexpr int ROWB = 32 * 2 + 16;
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = i * 16 + (lane >> 4) * 4 + r, col = j * 16 + (lane & 15);
-        *(__attribute__((address_space(3))) uint16_t*)(st + row * ROWB + col * 2) = f2bf(f(i, j, r));
-      }
+    for (int j = 0; j < 2; ++j) {
+      const u32x2_t w = {pack_bf2(f(i, j, 0), f(i, j, 1)), pack_bf2(f(i, j, 2), f(i, j, 3))};
+      *(__attribute__((address_space(3))) u32x2_t*)(st + acc_row(i, lane) * ROWB + acc_col(j, 0, lane) * 2) = w;
+    }
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
 #pragma unroll
   for (int it = 0; it < 128 / 16; ++it) {
@@ -756,7 +761,7 @@ __device__ __forceinline__ void gemm_8ph_tile(const GemmArgs& a, const int tile_
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i][s], Bf[j][s], acc[i0 + i][j0 + j], 0, 0, 0);
+          acc[i0 + i][j0 + j] = mfma16(A[i][s], Bf[j][s], acc[i0 + i][j0 + j]);
     __builtin_amdgcn_s_setprio(0);
   };
   const bool late = __builtin_amdgcn_readfirstlane(wm) == 1;
@@ -964,7 +969,7 @@ __global__ __launch_bounds__(512) void gemm_4ph_kernel(const GemmGroup g) {
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i0 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bf[j][s], acc[i0 + i][j], 0, 0, 0);
+          acc[i0 + i][j] = mfma16(af[i][s], bf[j][s], acc[i0 + i][j]);
     __builtin_amdgcn_s_setprio(0);
   };
   const bool late = __builtin_amdgcn_readfirstlane(wm) >= 2;
@@ -1084,7 +1089,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const GemmGroup g) {
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -1105,12 +1110,12 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const GemmGroup g) {
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], b0[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16(a0[i], b0[j], acc[i][j]);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16(a1[i], b1[j], acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();

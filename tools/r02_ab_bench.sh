@@ -9,6 +9,7 @@ T=$1; LIBS=$2; ROUNDS=${3:-2}
 LIB=picotron_amd/lib/libpicotron_hip.so
 IFS=, read -ra L <<< "$LIBS"
 for f in "${L[@]}"; do [ -f "$f" ] || { echo "missing $f on the box"; exit 1; }; done
+[ $(md5sum "${L[@]}" | cut -d' ' -f1 | sort -u | wc -l) -eq ${#L[@]} ] || { echo "identical builds in $LIBS"; exit 1; }
 cp "${L[0]}" $LIB || exit 1
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${T}_pytest.log 2>&1 || { echo pytest failed; grep -E "Error|FAILED|assert" gpurun_out/${T}_pytest.log | head -30; exit 1; }
 tail -1 gpurun_out/${T}_pytest.log
