@@ -899,7 +899,7 @@ __global__ __launch_bounds__(512) void gemm_8ph_dual_kernel(const GemmGroup g0, 
 // (At in phase 1, B and Ab in phase 2), and the one wait per K-tile (phase 2, vmcnt(6)) retires
 // K-tile t+1 with t+2 in flight -- every DMA has >= 1.5 K-tiles to land.
 template <bool AK, bool BKC, int EPI>
-__global__ __launch_bounds__(512) void gemm_4ph_kernel(const GemmGroup g) {
+__device__ __forceinline__ void gemm_4ph_tile(const GemmArgs& a, const int tile_m, const int tile_n) {
   constexpr int TM = 64, TN = 64, FM = 4, FN = 4;
   constexpr int IMG = 128 * BK * 2;           // 16 KiB
   constexpr int BUF = 3 * IMG;                // At, B, Ab
@@ -908,8 +908,6 @@ __global__ __launch_bounds__(512) void gemm_4ph_kernel(const GemmGroup g) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  int tile_m, tile_n;
-  const GemmArgs& a = select_problem(g, tile_m, tile_n);
   const int m0 = tile_m * 256, n0 = tile_n * 128;
 
   const BImg bi = bimg_make(a, BKC, n0);
@@ -1029,6 +1027,45 @@ __global__ __launch_bounds__(512) void gemm_4ph_kernel(const GemmGroup g) {
   if constexpr (EPI == EPI_CE_STATS) {
     __syncthreads();
     if (wn == 0) ce_stats_merge<2, TM, TN>(a, xs, m0, n0, wm, lane);
+  }
+}
+
+template <bool AK, bool BKC, int EPI>
+__global__ __launch_bounds__(512) void gemm_4ph_kernel(const GemmGroup g) {
+  int tile_m, tile_n;
+  const GemmArgs& a = select_problem(g, tile_m, tile_n);
+  gemm_4ph_tile<AK, BKC, EPI>(a, tile_m, tile_n);
+}
+
+// ------------------------------------------------------------------- mixed-tile launch (q|k|v)
+// One problem whose output columns [0, n_split) are covered by 256x256 8-phase tiles and
+// [n_split, N) by 256x128 4-phase tiles, in ONE launch.  For the q|k|v projection with RoPE
+// (q|k = 2/3 of the columns at H = HKV): 768 tiles of 256x128 are 3 rounds of the 256 CUs; 256
+// tiles of 256x256 over q|k plus 256 tiles of 256x128 over v are 2 rounds, the 4-phase tiles
+// filling CUs as the 8-phase ones finish.  Tile order as the dual launch: each XCD takes an equal
+// contiguous share of each part, 8-phase tiles first; inside a part the usual grouped raster.
+struct MixMap {
+  DualMap d;                  // n0 / n1 = tiles per XCD of the 8-phase / 4-phase part
+  int tiles_m, tn0, tn1;      // tile grid of each part
+  int nsplit_t1;              // n_split / 128: the 4-phase part's first tile column
+};
+
+__device__ __forceinline__ void grouped_tile(int pid, int tiles_m, int tiles_n, int group, int& tm, int& tn) {
+  const int span = group * tiles_n, gid = pid / span, first = gid * group;
+  const int gsize = min(tiles_m - first, group);
+  tm = first + (pid % span) % gsize;
+  tn = (pid % span) / gsize;
+}
+
+template <bool AK, bool BKC, int EPI>
+__global__ __launch_bounds__(512) void gemm_mix_kernel(const GemmArgs a, const MixMap m) {
+  int pid, tile_m, tile_n;
+  if (dual_select(m.d, pid) == 0) {
+    grouped_tile(pid, m.tiles_m, m.tn0, 8, tile_m, tile_n);
+    gemm_8ph_tile<AK, BKC, EPI>(a, tile_m, tile_n);
+  } else {
+    grouped_tile(pid, m.tiles_m, m.tn1, 4, tile_m, tile_n);
+    gemm_4ph_tile<AK, BKC, EPI>(a, tile_m, m.nsplit_t1 + tile_n);
   }
 }
 
@@ -1387,11 +1424,55 @@ int pick_group_tile(const GemmGroup& g) {
 
 int launch_swiglu(GemmGroup& g, int a_kcontig, int b_kcontig, int epilogue, int tile, hipStream_t stream);
 
+// PICOTRON_GEMM_MIX=0 turns the mixed-tile q|k|v launch off (A/B measurement only)
+bool mix_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PICOTRON_GEMM_MIX");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
+// q|k|v + RoPE as one mixed-tile launch: the rotated columns [0, rope_cols) in 256x256 tiles, the
+// rest (v) in 256x128 tiles.  PT_EUNSUPPORTED when the shape does not split that way (the caller
+// then launches one tile shape as before).
+int launch_mix_rope(const GemmArgs& a0, hipStream_t stream) {
+  const int ns = a0.rope_cols;
+  if (ns <= 0 || ns >= a0.N || ns % 256 || (a0.N - ns) % 128) return PT_EUNSUPPORTED;
+  if (!args_fit(a0, 12) || !args_fit(a0, 13)) return PT_EUNSUPPORTED;
+  MixMap m{};
+  m.tiles_m = a0.M / 256;
+  m.tn0 = ns / 256;
+  m.tn1 = (a0.N - ns) / 128;
+  m.nsplit_t1 = ns / 128;
+  const int t0 = m.tiles_m * m.tn0, t1 = m.tiles_m * m.tn1;
+  // the two parts must each divide over the 8 XCDs; the 8-phase part at most one round of the 256
+  // CUs (the shapes this was measured on: SmolLM-1.7B's 256 + 256 tiles at T 4096)
+  if (t0 % 8 || t1 % 8 || t0 > 256) return PT_EUNSUPPORTED;
+  m.d = DualMap{t0 / 8, t1 / 8, 0};
+  GemmArgs a = a0;
+  constexpr int smem = 8 * 128 * (64 * 2 + 16);  // = the 4-phase main loop's 144 KiB
+  static_assert(smem >= 9 * 128 * BK * 2 && smem <= 160 * 1024, "LDS budget");
+  static bool attr_set = false;
+  if (!attr_set) {
+    set_smem_once(gemm_mix_kernel<true, true, EPI_ROPE>, smem);
+    attr_set = true;
+  }
+  gemm_mix_kernel<true, true, EPI_ROPE><<<t0 + t1, 512, smem, stream>>>(a, m);
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
+
 int launch_group(GemmGroup& g, int a_kcontig, int b_kcontig, int epilogue, int tile, hipStream_t stream) {
   if (epilogue == EPI_SWIGLU_FWD || epilogue == EPI_SWIGLU_BWD)
     return launch_swiglu(g, a_kcontig, b_kcontig, epilogue, tile, stream);
   // RoPE: wave tiles 64 columns wide, the phased kernels only; the 256x128 one (twice the tiles) when
   // it divides -- the q|k|v projection never fills more than a few rounds of 256x256 tiles
+  if (epilogue == EPI_ROPE && tile < 0 && a_kcontig && b_kcontig && g.nprob == 1 && mix_enabled()) {
+    const int rc = launch_mix_rope(g.p[0], stream);
+    if (rc != PT_EUNSUPPORTED) return rc;
+  }
   if (epilogue == EPI_ROPE && tile < 0) tile = args_fit(g.p[0], 13) ? 13 : 12;
   if (tile < 0) tile = pick_group_tile(g);
   if (epilogue == EPI_ROPE) {

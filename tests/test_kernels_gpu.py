@@ -326,9 +326,10 @@ def test_gemm_dual_unsupported_returns_none():
     assert not out.any()
 
 
-@pytest.mark.parametrize("nh,nkv,S", [(4, 2, 256), (8, 8, 128), (32, 32, 1024)])
+@pytest.mark.parametrize("nh,nkv,S", [(4, 2, 256), (8, 8, 128), (16, 16, 512), (32, 32, 1024)])
 def test_gemm_rope_fused(nh, nkv, S):
-    """q|k|v projection with RoPE in the epilogue == projection + rope kernel, bit for bit"""
+    """q|k|v projection with RoPE in the epilogue == projection + rope kernel, bit for bit (the last
+    two shapes take the mixed 256x256 / 256x128 launch, the first two a single tile shape)"""
     from picotron_amd import kernels as K_
     d, B = 64, 2
     T, H = B * S, 256
