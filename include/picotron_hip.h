@@ -47,6 +47,13 @@ int pt_rmsnorm_bwd_partials(int64_t rows, int cols);
 int pt_rmsnorm_bwd(const void* dy, const void* z, const void* weight, const float* rstd, const void* dres,
                    void* dx, void* dweight, float* dw_partial, int64_t rows, int64_t cols, int mode,
                    hipStream_t stream);
+/* the dweight column sums of n <= 32 pt_rmsnorm_bwd calls made with dweight = NULL (their
+ * dw_partial buffers, pt_rmsnorm_bwd_partials rows each), one launch; sinks[i] as the dweight sink
+ * bits of pt_rmsnorm_bwd's mode.  Bit-identical to passing dweight to each call.  (An
+ * implementation detail of the same LlamaRMSNorm backward: a micro-batch's norms sum their weight
+ * gradients together at the end of its backward.) */
+int pt_rmsnorm_colsum_batch(const float* const* partials, const int* nparts, void* const* dweights,
+                            const int* sinks, int n, int64_t cols, hipStream_t stream);
 
 /* ---- RoPE (rotate-half, non-interleaved) --------------------------------------------------
  * replaces picotron/model.py:136-137 (flash-attn apply_rotary_emb) and model.py:12-19

@@ -38,6 +38,7 @@ SIGNATURES = {
     "pt_adamw_step": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _vp]),
     "pt_adamw_step_multi": (_i32, [_vp, _vp, _i32, _i64, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _vp]),
     "pt_rmsnorm_bwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp]),
+    "pt_rmsnorm_colsum_batch": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _vp]),
     "pt_rope": (_i32, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _i32, _vp]),
     "pt_swiglu_fwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp]),
     "pt_swiglu_bwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp]),
@@ -121,6 +122,10 @@ def stream_ptr(device=None):
 
 def i64arr(vals):
     return (ctypes.c_int64 * len(vals))(*[int(v) for v in vals])
+
+
+def i32arr(vals):
+    return (ctypes.c_int32 * len(vals))(*[int(v) for v in vals])
 
 
 def ptrarr(vals):

@@ -222,8 +222,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(min_wa
 // Sink (flags): 0 store bf16, DW_ACC_BF16 bf16 accumulate (= autograd's grad + bf16(new)),
 // DW_ACC_F32 f32 accumulate (DataParallelBucket main_grad).
 constexpr int kCsCols = 32, kCsThreads = 1024, kCsGroups = kCsThreads / (kCsCols / 4);
-__global__ __launch_bounds__(kCsThreads) void colsum_kernel(const float* __restrict__ partial, int nparts,
-                                                            int cols, void* __restrict__ out, int sink) {
+__device__ __forceinline__ void colsum_block(const float* __restrict__ partial, int nparts, int cols,
+                                             void* __restrict__ out, int sink) {
   __shared__ float red[kCsGroups][kCsCols + 1];
   __shared__ float red2[kCsThreads / kCsCols][kCsCols + 1];
   const int t = threadIdx.x, ch = t & 7, grp = t >> 3;
@@ -270,6 +270,25 @@ __global__ __launch_bounds__(kCsThreads) void colsum_kernel(const float* __restr
       ((uint16_t*)out)[col] = f2bf(v);
     }
   }
+}
+
+__global__ __launch_bounds__(kCsThreads) void colsum_kernel(const float* __restrict__ partial, int nparts,
+                                                            int cols, void* __restrict__ out, int sink) {
+  colsum_block(partial, nparts, cols, out, sink);
+}
+
+// several norms' column sums in one launch (blockIdx.y = the norm): the backward of a micro-batch
+// defers its 2 L norms' sums to one launch at its end (picotron_amd/functional.py norm_bwd)
+constexpr int kCsBatch = 32;
+struct ColsumBatch {
+  const float* partial[kCsBatch];
+  void* out[kCsBatch];
+  int nparts[kCsBatch];
+  int sink[kCsBatch];
+};
+__global__ __launch_bounds__(kCsThreads) void colsum_batch_kernel(const ColsumBatch b, int cols) {
+  const int i = blockIdx.y;
+  colsum_block(b.partial[i], b.nparts[i], cols, b.out[i], b.sink[i]);
 }
 
 int nch_for(int cols) {
@@ -383,6 +402,28 @@ int pt_rmsnorm_bwd(const void* dy, const void* z, const void* weight, const floa
         dw_partial, grid, (int)cols, dweight, mode & (PT_DW_ACC_BF16 | PT_DW_ACC_F32));
     PT_CHECK_LAUNCH();
   }
+  return PT_OK;
+}
+
+// dweight[i] (+)= column sums of partials[i] ([nparts[i], cols] f32, from pt_rmsnorm_bwd called with
+// dweight = NULL) for n <= 32 norms of the same width, one launch; sinks[i] as pt_rmsnorm_bwd's
+// PT_DW_ACC_* bits (0 = bf16 store).  Bit-identical to the per-norm sums.
+int pt_rmsnorm_colsum_batch(const float* const* partials, const int* nparts, void* const* dweights,
+                            const int* sinks, int n, int64_t cols, hipStream_t stream) {
+  if (!partials || !nparts || !dweights || !sinks || n <= 0 || n > kCsBatch || cols <= 0 || (cols & 7))
+    return PT_EINVAL;
+  ColsumBatch b{};
+  for (int i = 0; i < n; ++i) {
+    if (!partials[i] || !dweights[i] || nparts[i] <= 0) return PT_EINVAL;
+    if (sinks[i] != 0 && sinks[i] != PT_DW_ACC_BF16 && sinks[i] != PT_DW_ACC_F32) return PT_EINVAL;
+    b.partial[i] = partials[i];
+    b.out[i] = dweights[i];
+    b.nparts[i] = nparts[i];
+    b.sink[i] = sinks[i];
+  }
+  const dim3 grid((unsigned)((cols + kCsCols - 1) / kCsCols), (unsigned)n);
+  colsum_batch_kernel<<<grid, kCsThreads, 0, stream>>>(b, (int)cols);
+  PT_CHECK_LAUNCH();
   return PT_OK;
 }
 

@@ -136,6 +136,29 @@ def dgrad_with_wgrad(dy2d, weights, wjobs, gu=None):
     return dx
 
 
+# Deferred RMSNorm weight-gradient sums: inside an autograd backward, a norm whose gradient has
+# no DataParallelBucket owner waiting on it leaves its per-block partial rows here, and one
+# pt_rmsnorm_colsum_batch launch at the end of the backward (an engine final callback) sums them
+# all into their sinks -- 2 L + 1 column-sum launches per micro-batch become one.  Norms whose
+# weights carry a _pt_grad_ready hook keep the immediate sum (their bucket's all-reduce overlaps the
+# rest of the backward).  PICOTRON_NORM_DEFER=0 turns this off (A/B only).
+_PENDING_DW = {}   # autograd graph task id -> [(partial, sink buffer, sink, stream)]
+
+
+def _norm_defer_enabled():
+    return os.environ.get("PICOTRON_NORM_DEFER", "1") != "0"
+
+
+def _flush_norm_dw(task):
+    groups = {}
+    for part, buf, sink, stream in _PENDING_DW.pop(task, []):
+        groups.setdefault((part.shape[1], part.device, stream), []).append((part, buf, sink))
+    for (_, _, stream), js in groups.items():
+        with torch.cuda.stream(stream):   # the stream the partials were produced on
+            for i in range(0, len(js), 32):
+                K.rmsnorm_colsum_batch(js[i:i + 32])
+
+
 def norm_bwd(dy2, z, weight, rstd, mode, dres=None, need_dw=True):
     """RMSNorm backward with the weight gradient summed straight into p's sink (bf16 .grad store or
     accumulate -- autograd's AccumulateGrad -- or the f32 main_grad of DataParallelBucket).  A frozen
@@ -151,6 +174,14 @@ def norm_bwd(dy2, z, weight, rstd, mode, dres=None, need_dw=True):
         buf, sink = weight.grad, 0
     else:
         buf, sink = weight.grad, K.DW_ACC_BF16
+    task = torch._C._current_graph_task_id()   # -1 outside an autograd backward
+    if getattr(weight, "_pt_grad_ready", None) is None and z.is_cuda and task != -1 and _norm_defer_enabled():
+        dx, partial = K.rmsnorm_bwd(dy2, z, weight, rstd, mode, dres=dres, defer_dw=True)
+        if task not in _PENDING_DW:
+            _PENDING_DW[task] = []
+            torch.autograd.Variable._execution_engine.queue_callback(lambda: _flush_norm_dw(task))
+        _PENDING_DW[task].append((partial, buf, sink, torch.cuda.current_stream(z.device)))
+        return dx
     dx, _ = K.rmsnorm_bwd(dy2, z, weight, rstd, mode, dres=dres, dw_out=buf, dw_sink=sink)
     _grad_ready(weight)
     return dx

@@ -58,10 +58,12 @@ def rmsnorm_fwd(x, weight, eps, mode=MODE_TRITON, residual=None):
 DW_ACC_BF16, DW_ACC_F32 = 4, 8   # pt_rmsnorm_bwd dweight sinks (include/picotron_hip.h)
 
 
-def rmsnorm_bwd(dy, z, weight, rstd, mode=MODE_TRITON, dres=None, dw_out=None, dw_sink=0):
+def rmsnorm_bwd(dy, z, weight, rstd, mode=MODE_TRITON, dres=None, dw_out=None, dw_sink=0, defer_dw=False):
     """Returns (dx, dweight).  dres (same shape as dy) is added into dx when given.
     dw_out/dw_sink: write the weight gradient into an existing buffer -- 0 store (bf16),
-    DW_ACC_BF16 accumulate into a bf16 .grad, DW_ACC_F32 accumulate into an f32 main_grad."""
+    DW_ACC_BF16 accumulate into a bf16 .grad, DW_ACC_F32 accumulate into an f32 main_grad.
+    defer_dw: no column sum; returns (dx, partial) -- the f32 per-block partial rows, to be summed
+    into the sink later by rmsnorm_colsum_batch."""
     dy = dy.contiguous()
     rows, cols = z.shape
     lib = _C.lib()
@@ -69,16 +71,36 @@ def rmsnorm_bwd(dy, z, weight, rstd, mode=MODE_TRITON, dres=None, dw_out=None, d
     _C.check(0 if nparts > 0 else nparts, "pt_rmsnorm_bwd_partials")
     partial = torch.empty(nparts, cols, dtype=torch.float32, device=z.device)
     dx = torch.empty_like(z)
-    if dw_out is None:
+    if defer_dw:
+        dw_out, dw_sink = None, 0
+    elif dw_out is None:
         dw_out, dw_sink = torch.empty(cols, dtype=BF16, device=z.device), 0
-    _req(dw_out.is_contiguous() and dw_out.numel() == cols, "dweight buffer must be contiguous [cols]")
-    _req(dw_out.dtype == (torch.float32 if dw_sink == DW_ACC_F32 else BF16), "dweight buffer dtype")
+    if dw_out is not None:
+        _req(dw_out.is_contiguous() and dw_out.numel() == cols, "dweight buffer must be contiguous [cols]")
+        _req(dw_out.dtype == (torch.float32 if dw_sink == DW_ACC_F32 else BF16), "dweight buffer dtype")
     if dres is not None:
         dres = dres.contiguous()
     rc = lib.pt_rmsnorm_bwd(_ptr(dy), _ptr(z), _ptr(weight), _ptr(rstd), _ptr(dres), _ptr(dx), _ptr(dw_out),
                             _ptr(partial), rows, cols, int(mode) | int(dw_sink), _C.stream_ptr(z.device))
     _C.check(rc, "pt_rmsnorm_bwd")
-    return dx, dw_out
+    return dx, (partial if defer_dw else dw_out)
+
+
+def rmsnorm_colsum_batch(jobs):
+    """jobs: [(partial [nparts, cols] f32, dw_out, dw_sink)], all of one width, <= 32: the deferred
+    weight-gradient sums of rmsnorm_bwd(defer_dw=True), one launch."""
+    _req(0 < len(jobs) <= 32, "rmsnorm_colsum_batch: 1..32 jobs")
+    cols = jobs[0][0].shape[1]
+    for part, out, sink in jobs:
+        _req(part.dtype == torch.float32 and part.is_contiguous() and part.shape[1] == cols, "partials [n, cols] f32")
+        _req(out.is_contiguous() and out.numel() == cols, "dweight buffer must be contiguous [cols]")
+        _req(out.dtype == (torch.float32 if sink == DW_ACC_F32 else BF16), "dweight buffer dtype")
+    rc = _C.lib().pt_rmsnorm_colsum_batch(_C.ptrarr([_ptr(p) for p, _, _ in jobs]),
+                                          _C.i32arr([p.shape[0] for p, _, _ in jobs]),
+                                          _C.ptrarr([_ptr(o) for _, o, _ in jobs]),
+                                          _C.i32arr([s for _, _, s in jobs]), len(jobs), cols,
+                                          _C.stream_ptr(jobs[0][0].device))
+    _C.check(rc, "pt_rmsnorm_colsum_batch")
 
 
 # ------------------------------------------------------------------------------- embedding

@@ -91,6 +91,55 @@ def test_rmsnorm_dweight_sinks(rows):
     assert rel_err(accf - oldf, dw.float()) < 1e-2
 
 
+def test_rmsnorm_colsum_batch_equals_per_norm():
+    """deferred weight-gradient sums (partials kept, one batched launch) == the per-norm sums, bit for
+    bit, for every sink; dx unchanged"""
+    from picotron_amd import kernels as K
+    rows, cols = 4096, 2048
+    sinks = [0, K.DW_ACC_BF16, K.DW_ACC_F32, K.DW_ACC_BF16]
+    jobs, want = [], []
+    for i, sink in enumerate(sinks):
+        x, dy = torch.randn(rows, cols).to(BF).to(DEV), torch.randn(rows, cols).to(BF).to(DEV)
+        w = (1 + 0.1 * torch.randn(cols)).to(BF).to(DEV)
+        _, rstd, _ = K.rmsnorm_fwd(x, w, 1e-5, i % 2)
+        init = torch.randn(cols, device=DEV).to(torch.float32 if sink == K.DW_ACC_F32 else BF)
+        ref = init.clone()
+        dx_ref, _ = K.rmsnorm_bwd(dy, x, w, rstd, i % 2, dw_out=ref, dw_sink=sink)
+        dx, partial = K.rmsnorm_bwd(dy, x, w, rstd, i % 2, defer_dw=True)
+        assert torch.equal(dx, dx_ref)
+        out = init.clone()
+        jobs.append((partial, out, sink))
+        want.append(ref)
+    K.rmsnorm_colsum_batch(jobs)
+    torch.cuda.synchronize()
+    for (_, out, _), ref in zip(jobs, want):
+        assert torch.equal(out, ref)
+
+
+def test_rmsnorm_deferred_dw_through_autograd(monkeypatch):
+    """a stack of norms under autograd: with the deferral (one batched column sum at the end of the
+    backward) the weight grads are bit-identical to the immediate per-norm sums"""
+    from picotron_amd import functional as FN
+    rows, cols, n = 1024, 2048, 5
+    x0 = torch.randn(rows, cols).to(BF).to(DEV)
+    ws = [torch.nn.Parameter((1 + 0.1 * torch.randn(cols)).to(BF).to(DEV)) for _ in range(n)]
+    dy = torch.randn(rows, cols).to(BF).to(DEV)
+    grads = {}
+    for defer in ("1", "0"):
+        monkeypatch.setenv("PICOTRON_NORM_DEFER", defer)
+        for w in ws:
+            w.grad = None
+        x = x0.clone().requires_grad_(True)
+        h = x
+        for w in ws:
+            h = FN.RMSNormFunction.apply(h, w, 1e-5, 0)
+        h.backward(dy)
+        assert not FN._PENDING_DW
+        grads[defer] = [w.grad.clone() for w in ws] + [x.grad.clone()]
+    for a, b in zip(grads["1"], grads["0"]):
+        assert torch.equal(a, b)
+
+
 # ------------------------------------------------------------------------------ RoPE
 @pytest.mark.parametrize("d", [64, 128])
 def test_rope_fused_qk_rows(d):

@@ -181,7 +181,8 @@ def test_ring_step_golden_g4b():
         o_f, l_f = O.ring_attention_forward(g["q1"], g["k0"], g["v0"], sc, False)
         out, lse = O.update_out_and_lse(None, None, o_c, l_c)
         out, lse = O.update_out_and_lse(out, lse, o_f, l_f)
-        tol = dict(rtol=1e-5, atol=1e-6) if tag == "f32" else dict(rtol=0, atol=0)
+        # bitwise in this container; another host's CPU GEMM can differ by an f32 ulp in an element
+        tol = dict(rtol=1e-5, atol=1e-6) if tag == "f32" else dict(rtol=4e-6, atol=1e-7)
         close(out, g["out"], **tol)
         close(lse, g["lse"], **tol)
 
