@@ -1447,8 +1447,9 @@ int launch_mix_rope(const GemmArgs& a0, hipStream_t stream) {
   m.tn1 = (a0.N - ns) / 128;
   m.nsplit_t1 = ns / 128;
   const int t0 = m.tiles_m * m.tn0, t1 = m.tiles_m * m.tn1;
-  // the two parts must each divide over the 8 XCDs; the 8-phase part at most one round of the 256
-  // CUs (the shapes this was measured on: SmolLM-1.7B's 256 + 256 tiles at T 4096)
+  // the two parts must each divide over the 8 XCDs; the 8-phase part at most one round: the gain is
+  // the round quantization (SmolLM-1.7B: 3 rounds -> 2, +0.8 % step); Llama-2-7B's 512 + 512 tiles
+  // (6 whole rounds either way) measured neutral, the CP=8 proxy's 4096 + 4096 within noise
   if (t0 % 8 || t1 % 8 || t0 > 256) return PT_EUNSUPPORTED;
   m.d = DualMap{t0 / 8, t1 / 8, 0};
   GemmArgs a = a0;
