@@ -37,7 +37,7 @@ def sources():
 # per-source code-generation flags.  attention: MFMA results in VGPRs (gfx950's unified register
 # file) instead of AGPRs -- the softmax reads every S / dP accumulator, and the AGPR form cost a
 # v_accvgpr_read per element plus registers (fwd 156 -> 124 VGPRs: 3 -> 4 waves per SIMD).
-FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-slp-vectorize"]}
+FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
 
 
 def _compile(src, obj, extra):
