@@ -1581,6 +1581,32 @@ int pt_gemm_grouped(const pt_gemm_problem* probs, int nprob, int a_kcontig, int 
   return launch_group(g, a_kcontig, b_kcontig, epilogue, tile, stream);
 }
 
+// Split-K finish: out = bf16(p0 + p1), 4 elements per thread-iteration (16-B loads, 8-B store).
+// For the long-K dX GEMMs of N = 2048 (gate|up dX, K 16384; lm_head dX, K 49152): 256x256 8-phase
+// tiles over two K halves fill the 256 CUs as one round and run ~17 % above the 256x128 4-phase
+// rate per FLOP at that K (tools/gemm_kscan.py), which pays for the f32 partials and this pass.
+__global__ __launch_bounds__(256) void splitk_sum2_kernel(const float4* __restrict__ p0, const float4* __restrict__ p1,
+                                                          uint2* __restrict__ out, int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 a = p0[i], b = p1[i];
+    uint2 w;
+    w.x = pack_bf2(a.x + b.x, a.y + b.y);
+    w.y = pack_bf2(a.z + b.z, a.w + b.w);
+    out[i] = w;
+  }
+}
+
+int pt_gemm_splitk_sum(const float* p0, const float* p1, void* out, int64_t n, hipStream_t stream) {
+  if (!p0 || !p1 || !out || n <= 0 || (n & 3)) return PT_EINVAL;
+  if (!pt_aligned16(p0) || !pt_aligned16(p1) || ((uintptr_t)out & 7)) return PT_EALIGN;
+  const int64_t n4 = n / 4;
+  int64_t grid = (n4 + 255) / 256;
+  if (grid > PT_STREAM_GRID_CAP) grid = PT_STREAM_GRID_CAP;
+  splitk_sum2_kernel<<<(int)grid, 256, 0, stream>>>((const float4*)p0, (const float4*)p1, (uint2*)out, n4);
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
+
 // Two independent groups in ONE launch of 256x256 8-phase tiles (see gemm_8ph_dual_kernel): a dX
 // group and a wgrad group of the same layer, each with its own epilogue.  PT_EUNSUPPORTED when a
 // problem does not tile by 256x256 or a group's tile count is not a multiple of 8 (the caller

@@ -634,6 +634,51 @@ def linear_dgrad_swiglu(dy2d, wd, gu):
     return dgu
 
 
+def _splitk_enabled():
+    return os.environ.get("PICOTRON_SPLITK2", "1") != "0"
+
+
+def _splitk_halves(T, Kin, ns):
+    """The two K halves of a dgrad [T, Kin] = dY [T, sum ns] . W that pays to split (None if not):
+    one round of 256x256 tiles for both halves together, at least 8192 of K per half, halves on
+    weight boundaries (2 equal weights) or through the middle of one weight."""
+    if T % 256 or Kin % 256 or 2 * (T // 256) * (Kin // 256) > 256:
+        return None
+    if len(ns) == 2 and ns[0] == ns[1]:
+        h = ns[0]
+    elif len(ns) == 1 and ns[0] % 128 == 0:
+        h = ns[0] // 2
+    else:
+        return None
+    return h if h >= 8192 and h % 64 == 0 else None
+
+
+def _linear_dgrad_splitk(dy2d, weights, h, dx):
+    """dX = bf16(dY[:, :h] . W[:h] + dY[:, h:] . W[h:]): two f32 problems on 256x256 tiles in one
+    grouped launch, then pt_gemm_splitk_sum."""
+    T, N = dy2d.shape
+    Kin = weights[0].shape[1]
+    halves = [weights[0], weights[1]] if len(weights) == 2 else [weights[0][:h], weights[0][h:]]
+    parts = [torch.empty(T, Kin, dtype=torch.float32, device=dy2d.device) for _ in range(2)]
+    probs = (_C.GemmProblem * 2)()
+    for i in range(2):
+        probs[i] = _problem(dy2d[:, i * h:], dy2d.stride(0), [halves[i]], [Kin], [0, h], 1, [parts[i]], [Kin],
+                            [0, T], T, Kin, h)
+    probe = _PROBE
+    if probe is not None:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    stream = _C.stream_ptr(dy2d.device)
+    rc = _C.lib().pt_gemm_grouped(probs, 2, 1, 0, EPI_F32, 12, stream)
+    _C.check(rc, "pt_gemm_grouped(split-K dgrad)")
+    rc = _C.lib().pt_gemm_splitk_sum(_ptr(parts[0]), _ptr(parts[1]), _ptr(dx), T * Kin, stream)
+    _C.check(rc, "pt_gemm_splitk_sum")
+    if probe is not None:
+        ev1.record()
+        probe.records.append((ev0, ev1, 2.0 * T * Kin * N, _alg_bytes(T, Kin, N, EPI_BF16)))
+    return dx
+
+
 def linear_dgrad(dy2d, weights, out=None, accumulate=False, tile=-1):
     """dX = dY . [W_0; W_1; ...]  where dY = [dY_0 | dY_1 | ...] is [T, sum N_i]."""
     _bf16_rowmajor(dy2d, "dy")
@@ -641,6 +686,10 @@ def linear_dgrad(dy2d, weights, out=None, accumulate=False, tile=-1):
     Kin = weights[0].shape[1]
     ns = [w.shape[0] for w in weights]
     _req(sum(ns) == N, "dgrad: dY width must equal the stacked weight rows")
+    if out is None and not accumulate and tile < 0 and _splitk_enabled():
+        h = _splitk_halves(T, Kin, ns)
+        if h is not None and all(w.dtype == BF16 and w.is_contiguous() for w in weights):
+            return _linear_dgrad_splitk(dy2d, weights, h, torch.empty(T, Kin, dtype=BF16, device=dy2d.device))
     dx = out if out is not None else torch.empty(T, Kin, dtype=BF16, device=dy2d.device)
     _gemm(dy2d, dy2d.stride(0), 1, weights, [Kin] * len(weights), _bounds(ns), 0, 1, [dx], [dx.stride(0)],
           [0, T], T, Kin, N, EPI_BF16_ACC if accumulate else EPI_BF16, tile)

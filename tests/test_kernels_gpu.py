@@ -375,6 +375,25 @@ def test_gemm_dual_unsupported_returns_none():
     assert not out.any()
 
 
+@pytest.mark.parametrize("T,Kin,ns", [(1024, 2048, [8192, 8192]), (512, 2048, [16384]), (4096, 2048, [8192, 8192])])
+def test_dgrad_splitk(T, Kin, ns, monkeypatch):
+    """long-K dgrad split in two K halves (f32 partials on 256x256 tiles + the sum pass) against the
+    single-pass GEMM (PICOTRON_SPLITK2=0) and an f32 reference: same result up to the f32 summation
+    order (one bf16 rounding either way)"""
+    from picotron_amd import kernels as K_
+    dy = torch.randn(T, sum(ns)).to(BF).to(DEV)
+    ws = [(torch.randn(n, Kin) / math.sqrt(sum(ns))).to(BF).to(DEV) for n in ns]
+    assert K_._splitk_halves(T, Kin, ns) is not None
+    dx = K_.linear_dgrad(dy, ws)
+    monkeypatch.setenv("PICOTRON_SPLITK2", "0")
+    ref1 = K_.linear_dgrad(dy, ws)
+    ref = (dy.float() @ torch.cat(ws).float())
+    torch.cuda.synchronize()
+    assert rel_err(dx, ref) < 4e-3
+    assert (dx.float() - ref1.float()).abs().max().item() <= 2 * ref1.float().abs().max().item() * 2 ** -8
+    assert rel_err(dx, ref1) < 4e-3
+
+
 @pytest.mark.parametrize("nh,nkv,S", [(4, 2, 256), (8, 8, 128), (16, 16, 512), (32, 32, 1024)])
 def test_gemm_rope_fused(nh, nkv, S):
     """q|k|v projection with RoPE in the epilogue == projection + rope kernel, bit for bit (the last
