@@ -203,10 +203,12 @@ int pt_gemm_grouped(const pt_gemm_problem* probs, int nprob, int a_kcontig, int 
 int pt_gemm_dual(const pt_gemm_problem* p0, int n0, int a_kcontig0, int b_kcontig0, int epilogue0,
                  const pt_gemm_problem* p1, int n1, int a_kcontig1, int b_kcontig1, int epilogue1, int order,
                  hipStream_t stream);
-/* out (bf16, n contiguous elements) = bf16(p0 + p1): the finishing pass of a dgrad split in two K
- * halves (two f32 problems of one pt_gemm_grouped launch, 256x256 tiles).  n % 4 == 0, p0 / p1
- * 16-byte and out 8-byte aligned. */
-int pt_gemm_splitk_sum(const float* p0, const float* p1, void* out, int64_t n, hipStream_t stream);
+/* out (bf16, n contiguous elements) = bf16(p0 + p1), or bf16(residual + bf16(p0 + p1)) when
+ * residual (bf16, n contiguous) is given (= the EPI_BF16_RES epilogue): the finishing pass of a GEMM
+ * split in two K halves (two f32 problems of one pt_gemm_grouped launch, 256x256 tiles).  n % 4 == 0,
+ * p0 / p1 16-byte, out / residual 8-byte aligned; residual may alias out. */
+int pt_gemm_splitk_sum(const float* p0, const float* p1, const void* residual, void* out, int64_t n,
+                       hipStream_t stream);
 
 /* ---- ring-attention merge ------------------------------------------------------------------
  * replaces picotron/context_parallel/context_parallel.py:157-187 update_out_and_lse (its non-first

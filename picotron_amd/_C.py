@@ -31,7 +31,7 @@ SIGNATURES = {
     "pt_rmsnorm_fwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _f32, _i32, _vp]),
     "pt_rmsnorm_bwd_partials": (_i32, [_i64, _i32]),
     "pt_gemm_grouped": (_i32, [ctypes.POINTER(GemmProblem), _i32, _i32, _i32, _i32, _i32, _vp]),
-    "pt_gemm_splitk_sum": (_i32, [_vp, _vp, _vp, _i64, _vp]),
+    "pt_gemm_splitk_sum": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp]),
     "pt_gemm_dual": (_i32, [ctypes.POINTER(GemmProblem), _i32, _i32, _i32, _i32, ctypes.POINTER(GemmProblem), _i32,
                             _i32, _i32, _i32, _i32, _vp]),
     "pt_embedding_fwd": (_i32, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _i64, _vp]),

@@ -1586,23 +1586,32 @@ int pt_gemm_grouped(const pt_gemm_problem* probs, int nprob, int a_kcontig, int 
 // tiles over two K halves fill the 256 CUs as one round and run ~17 % above the 256x128 4-phase
 // rate per FLOP at that K (tools/gemm_kscan.py), which pays for the f32 partials and this pass.
 __global__ __launch_bounds__(256) void splitk_sum2_kernel(const float4* __restrict__ p0, const float4* __restrict__ p1,
-                                                          uint2* __restrict__ out, int64_t n4) {
+                                                          const uint2* res, uint2* out, int64_t n4) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
     const float4 a = p0[i], b = p1[i];
+    float v[4] = {a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w};
+    if (res) {  // EPI_BF16_RES: bf16(R + bf16(acc))
+      const uint2 r = res[i];
+      const float rf[4] = {lo_bf(r.x), hi_bf(r.x), lo_bf(r.y), hi_bf(r.y)};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = rf[k] + round_bf(v[k]);
+    }
     uint2 w;
-    w.x = pack_bf2(a.x + b.x, a.y + b.y);
-    w.y = pack_bf2(a.z + b.z, a.w + b.w);
+    w.x = pack_bf2(v[0], v[1]);
+    w.y = pack_bf2(v[2], v[3]);
     out[i] = w;
   }
 }
 
-int pt_gemm_splitk_sum(const float* p0, const float* p1, void* out, int64_t n, hipStream_t stream) {
+int pt_gemm_splitk_sum(const float* p0, const float* p1, const void* residual, void* out, int64_t n,
+                       hipStream_t stream) {
   if (!p0 || !p1 || !out || n <= 0 || (n & 3)) return PT_EINVAL;
-  if (!pt_aligned16(p0) || !pt_aligned16(p1) || ((uintptr_t)out & 7)) return PT_EALIGN;
+  if (!pt_aligned16(p0) || !pt_aligned16(p1) || ((uintptr_t)out & 7) || ((uintptr_t)residual & 7)) return PT_EALIGN;
   const int64_t n4 = n / 4;
   int64_t grid = (n4 + 255) / 256;
   if (grid > PT_STREAM_GRID_CAP) grid = PT_STREAM_GRID_CAP;
-  splitk_sum2_kernel<<<(int)grid, 256, 0, stream>>>((const float4*)p0, (const float4*)p1, (uint2*)out, n4);
+  splitk_sum2_kernel<<<(int)grid, 256, 0, stream>>>((const float4*)p0, (const float4*)p1, (const uint2*)residual,
+                                                    (uint2*)out, n4);
   PT_CHECK_LAUNCH();
   return PT_OK;
 }

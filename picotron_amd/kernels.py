@@ -495,6 +495,11 @@ def linear_fwd(x2d, weights, out=None, tile=-1, residual=None):
         _bf16_rowmajor(residual, "residual")
         _req(tuple(residual.shape) == (T, N), "residual shape")
         epi, ldr = EPI_BF16_RES, residual.stride(0)
+    if out is None and tile < 0 and _splitk_enabled() and len(weights) <= 4 and \
+            (residual is None or residual.is_contiguous()):
+        h = _splitk_halves(T, N, K)
+        if h is not None:
+            return _linear_fwd_splitk(x2d, weights, h, y, residual)
     _gemm(x2d, x2d.stride(0), 1, weights, [K] * len(weights), _bounds(ns), 1, 0, [y], [y.stride(0)], [0, T],
           T, N, K, epi, tile, residual=residual, ldr=ldr)
     return y
@@ -638,45 +643,76 @@ def _splitk_enabled():
     return os.environ.get("PICOTRON_SPLITK2", "1") != "0"
 
 
-def _splitk_halves(T, Kin, ns):
-    """The two K halves of a dgrad [T, Kin] = dY [T, sum ns] . W that pays to split (None if not):
-    one round of 256x256 tiles for both halves together, at least 8192 of K per half, halves on
-    weight boundaries (2 equal weights) or through the middle of one weight."""
-    if T % 256 or Kin % 256 or 2 * (T // 256) * (Kin // 256) > 256:
-        return None
-    if len(ns) == 2 and ns[0] == ns[1]:
-        h = ns[0]
-    elif len(ns) == 1 and ns[0] % 128 == 0:
-        h = ns[0] // 2
-    else:
-        return None
-    return h if h >= 8192 and h % 64 == 0 else None
+def _splitk_min():
+    return int(os.environ.get("PICOTRON_SPLITK2_MIN", "8192"))
 
 
-def _linear_dgrad_splitk(dy2d, weights, h, dx):
-    """dX = bf16(dY[:, :h] . W[:h] + dY[:, h:] . W[h:]): two f32 problems on 256x256 tiles in one
-    grouped launch, then pt_gemm_splitk_sum."""
-    T, N = dy2d.shape
-    Kin = weights[0].shape[1]
-    halves = [weights[0], weights[1]] if len(weights) == 2 else [weights[0][:h], weights[0][h:]]
-    parts = [torch.empty(T, Kin, dtype=torch.float32, device=dy2d.device) for _ in range(2)]
-    probs = (_C.GemmProblem * 2)()
-    for i in range(2):
-        probs[i] = _problem(dy2d[:, i * h:], dy2d.stride(0), [halves[i]], [Kin], [0, h], 1, [parts[i]], [Kin],
-                            [0, T], T, Kin, h)
+def _splitk_halves(M, N, K):
+    """K of each half when C [M, N] = A [M, K] . B pays to split in two K halves (None if not): one
+    round of 256x256 tiles for both halves together and at least PICOTRON_SPLITK2_MIN (8192) of K per
+    half -- where the 256x256 8-phase rate (~17 % above the 256x128 one at long K) pays for the f32
+    partials and the sum pass."""
+    if M % 256 or N % 256 or 2 * (M // 256) * (N // 256) > 256 or K % 128:
+        return None
+    h = K // 2
+    return h if h >= _splitk_min() else None
+
+
+def _segments(sizes, lo, hi):
+    """(index, offset inside it, length) of the pieces of the concatenation of `sizes` in [lo, hi)"""
+    out, base = [], 0
+    for i, n in enumerate(sizes):
+        a, b = max(lo, base), min(hi, base + n)
+        if a < b:
+            out.append((i, a - base, b - a))
+        base += n
+    return out
+
+
+def _splitk_run(probs, b_kcontig, parts, residual, out, flops, nbytes, device):
     probe = _PROBE
     if probe is not None:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
-    stream = _C.stream_ptr(dy2d.device)
-    rc = _C.lib().pt_gemm_grouped(probs, 2, 1, 0, EPI_F32, 12, stream)
-    _C.check(rc, "pt_gemm_grouped(split-K dgrad)")
-    rc = _C.lib().pt_gemm_splitk_sum(_ptr(parts[0]), _ptr(parts[1]), _ptr(dx), T * Kin, stream)
+    stream = _C.stream_ptr(device)
+    rc = _C.lib().pt_gemm_grouped(probs, 2, 1, b_kcontig, EPI_F32, 12, stream)
+    _C.check(rc, "pt_gemm_grouped(split-K)")
+    rc = _C.lib().pt_gemm_splitk_sum(_ptr(parts[0]), _ptr(parts[1]), _ptr(residual), _ptr(out), out.numel(), stream)
     _C.check(rc, "pt_gemm_splitk_sum")
     if probe is not None:
         ev1.record()
-        probe.records.append((ev0, ev1, 2.0 * T * Kin * N, _alg_bytes(T, Kin, N, EPI_BF16)))
-    return dx
+        probe.records.append((ev0, ev1, flops, nbytes))
+    return out
+
+
+def _linear_dgrad_splitk(dy2d, weights, h, dx):
+    """dX = bf16(dY[:, :h] . W[:h] + dY[:, h:] . W[h:]) with W = [W_0; W_1; ...] (the halves may cut
+    through a weight): two f32 problems on 256x256 tiles in one grouped launch, then the sum pass."""
+    T, N = dy2d.shape
+    Kin = weights[0].shape[1]
+    ns = [w.shape[0] for w in weights]
+    parts = [torch.empty(T, Kin, dtype=torch.float32, device=dy2d.device) for _ in range(2)]
+    probs = (_C.GemmProblem * 2)()
+    for i, (lo, hi) in enumerate(((0, h), (h, N))):
+        segs = _segments(ns, lo, hi)
+        bs = [weights[j][a:a + n] for j, a, n in segs]
+        probs[i] = _problem(dy2d[:, lo:], dy2d.stride(0), bs, [Kin] * len(bs), _bounds([n for _, _, n in segs]), 1,
+                            [parts[i]], [Kin], [0, T], T, Kin, hi - lo)
+    return _splitk_run(probs, 0, parts, None, dx, 2.0 * T * Kin * N, _alg_bytes(T, Kin, N, EPI_BF16), dy2d.device)
+
+
+def _linear_fwd_splitk(x2d, weights, h, y, residual):
+    """Y = bf16(x[:, :h] . W[:, :h]^T + x[:, h:] . W[:, h:]^T) (+ residual as EPI_BF16_RES): two f32
+    problems on 256x256 tiles in one grouped launch, then the sum pass (which adds the residual)."""
+    T, K = x2d.shape
+    ns = [w.shape[0] for w in weights]
+    N = sum(ns)
+    parts = [torch.empty(T, N, dtype=torch.float32, device=x2d.device) for _ in range(2)]
+    probs = (_C.GemmProblem * 2)()
+    for i, (lo, hi) in enumerate(((0, h), (h, K))):
+        probs[i] = _problem(x2d[:, lo:], x2d.stride(0), [w[:, lo:] for w in weights], [K] * len(weights), _bounds(ns),
+                            0, [parts[i]], [N], [0, T], T, N, hi - lo)
+    return _splitk_run(probs, 1, parts, residual, y, 2.0 * T * N * K, _alg_bytes(T, N, K, EPI_BF16), x2d.device)
 
 
 def linear_dgrad(dy2d, weights, out=None, accumulate=False, tile=-1):
@@ -686,9 +722,10 @@ def linear_dgrad(dy2d, weights, out=None, accumulate=False, tile=-1):
     Kin = weights[0].shape[1]
     ns = [w.shape[0] for w in weights]
     _req(sum(ns) == N, "dgrad: dY width must equal the stacked weight rows")
-    if out is None and not accumulate and tile < 0 and _splitk_enabled():
-        h = _splitk_halves(T, Kin, ns)
-        if h is not None and all(w.dtype == BF16 and w.is_contiguous() for w in weights):
+    if out is None and not accumulate and tile < 0 and _splitk_enabled() and len(weights) <= 3:
+        h = _splitk_halves(T, Kin, N)
+        if h is not None and all(w.dtype == BF16 and w.is_contiguous() for w in weights) and \
+                all(n % 64 == 0 for n in ns):
             return _linear_dgrad_splitk(dy2d, weights, h, torch.empty(T, Kin, dtype=BF16, device=dy2d.device))
     dx = out if out is not None else torch.empty(T, Kin, dtype=BF16, device=dy2d.device)
     _gemm(dy2d, dy2d.stride(0), 1, weights, [Kin] * len(weights), _bounds(ns), 0, 1, [dx], [dx.stride(0)],

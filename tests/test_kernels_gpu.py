@@ -375,23 +375,46 @@ def test_gemm_dual_unsupported_returns_none():
     assert not out.any()
 
 
-@pytest.mark.parametrize("T,Kin,ns", [(1024, 2048, [8192, 8192]), (512, 2048, [16384]), (4096, 2048, [8192, 8192])])
-def test_dgrad_splitk(T, Kin, ns, monkeypatch):
-    """long-K dgrad split in two K halves (f32 partials on 256x256 tiles + the sum pass) against the
-    single-pass GEMM (PICOTRON_SPLITK2=0) and an f32 reference: same result up to the f32 summation
-    order (one bf16 rounding either way)"""
+@pytest.mark.parametrize("T,Kin,ns,kmin", [(1024, 2048, [8192, 8192], 8192), (512, 2048, [16384], 8192),
+                                           (4096, 2048, [8192, 8192], 8192), (4096, 2048, [2048] * 3, 1024)])
+def test_dgrad_splitk(T, Kin, ns, kmin, monkeypatch):
+    """dgrad split in two K halves (f32 partials on 256x256 tiles + the sum pass; the last shape's
+    halves cut through the middle weight, as q|k|v's) against the single pass (PICOTRON_SPLITK2=0)
+    and an f32 reference: the same up to the f32 summation order (one bf16 rounding either way)"""
     from picotron_amd import kernels as K_
+    monkeypatch.setenv("PICOTRON_SPLITK2_MIN", str(kmin))
     dy = torch.randn(T, sum(ns)).to(BF).to(DEV)
     ws = [(torch.randn(n, Kin) / math.sqrt(sum(ns))).to(BF).to(DEV) for n in ns]
-    assert K_._splitk_halves(T, Kin, ns) is not None
+    assert K_._splitk_halves(T, Kin, sum(ns)) is not None
     dx = K_.linear_dgrad(dy, ws)
     monkeypatch.setenv("PICOTRON_SPLITK2", "0")
     ref1 = K_.linear_dgrad(dy, ws)
     ref = (dy.float() @ torch.cat(ws).float())
     torch.cuda.synchronize()
     assert rel_err(dx, ref) < 4e-3
-    assert (dx.float() - ref1.float()).abs().max().item() <= 2 * ref1.float().abs().max().item() * 2 ** -8
+    assert maxabs(dx, ref1) <= 2 * ref1.float().abs().max().item() * 2 ** -8
     assert rel_err(dx, ref1) < 4e-3
+
+
+@pytest.mark.parametrize("residual", [False, True])
+def test_fwd_splitk(residual, monkeypatch):
+    """forward GEMM split in two K halves, the residual add (EPI_BF16_RES: bf16(R + bf16(acc))) in
+    the sum pass, against the single pass and an f32 reference (down_proj's shape: K 8192)"""
+    from picotron_amd import kernels as K_
+    monkeypatch.setenv("PICOTRON_SPLITK2_MIN", "4096")
+    T, K, N = 4096, 8192, 2048
+    x = torch.randn(T, K).to(BF).to(DEV)
+    w = (torch.randn(N, K) / math.sqrt(K)).to(BF).to(DEV)
+    r = torch.randn(T, N).to(BF).to(DEV) if residual else None
+    assert K_._splitk_halves(T, N, K) is not None
+    y = K_.linear_fwd(x, [w], residual=r)
+    monkeypatch.setenv("PICOTRON_SPLITK2", "0")
+    y1 = K_.linear_fwd(x, [w], residual=r)
+    ref = x.float() @ w.float().t() + (r.float() if residual else 0)
+    torch.cuda.synchronize()
+    assert rel_err(y, ref) < 4e-3
+    assert rel_err(y, y1) < 4e-3
+    assert maxabs(y, y1) <= 2 * y1.float().abs().max().item() * 2 ** -8
 
 
 @pytest.mark.parametrize("nh,nkv,S", [(4, 2, 256), (8, 8, 128), (16, 16, 512), (32, 32, 1024)])
