@@ -45,7 +45,7 @@ if ROOT not in sys.path:
 
 # HBM bytes per GEMM launch from rocprofv3 PMC passes (tools/r02_final.sh: bench.py --grad-acc 2, then
 # tools/traffic_summary.py); read for the roofline's `traffic`
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_gemm_traffic_s4.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_gemm_traffic_s7.json")
 
 
 def log(*a):
