@@ -315,7 +315,8 @@ __device__ __forceinline__ void swiglu_bwd_tail(const GemmArgs& a, const lds_u8*
 // whole 16-byte chunk of a row (the accumulator layout gives 4-byte pieces of 16 rows); the old
 // values of BOTH passes are loaded before the first store (one memory round trip per wave, was
 // one per 16-row fragment row), pass 1's loads issued once pass 0's accumulators are staged.
-template <int TM, int TN>
+// ACC = false: EPI_F32, store only (the split-K dgrad's f32 partials), the same row-chunk writes.
+template <int TM, int TN, bool ACC = true>
 __device__ __forceinline__ void f32_acc_tail(const f32x4_t (&acc)[TM / 16][TN / 16], lds_u8* st, int64_t mrow0,
                                              int ncol0, int64_t ldc, float* C, int lane) {
   constexpr int HR = TM / 2, NP = 2, FP = HR / 16, FN = TN / 16;
@@ -341,20 +342,25 @@ __device__ __forceinline__ void f32_acc_tail(const f32x4_t (&acc)[TM / 16][TN / 
             acc[p * FP + i][j];
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-private staging
   };
-  load_pass(0);
+  if (ACC) load_pass(0);
   stage_pass(0);
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int p = 1; p < NP; ++p) load_pass(p);
+  for (int p = 1; p < NP; ++p)
+    if (ACC) load_pass(p);
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     if (p > 0) stage_pass(p);
 #pragma unroll
     for (int q = 0; q < NIT; ++q) {
-      asm volatile("" : "+v"(old[p][q]));
       const f32x4_t v = *(const __attribute__((address_space(3))) f32x4_t*)(st + (q * RPI + lrow) * ROWB + ch * 16);
-      *(f32x4_t*)(cbase + (p * NIT + q) * rstep + coff) = old[p][q] + v;
+      if (ACC) {
+        asm volatile("" : "+v"(old[p][q]));
+        *(f32x4_t*)(cbase + (p * NIT + q) * rstep + coff) = old[p][q] + v;
+      } else {
+        *(f32x4_t*)(cbase + (p * NIT + q) * rstep + coff) = v;
+      }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // this pass's LDS reads done before the next staging
     __builtin_amdgcn_sched_barrier(0);
@@ -497,6 +503,12 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
     if constexpr (EPI == EPI_F32_ACC && TN == 64) {
       f32_acc_tail<TM, TN>(acc, st, mrow0, ncol0, ldc, C, lane);
       return;
+    }
+    if constexpr (EPI == EPI_F32 && TN == 64) {  // store only (the split-K partials): whole 16-B row chunks
+      if ((ldc & 3) == 0 && ((uintptr_t)C & 15) == 0) {
+        f32_acc_tail<TM, TN, false>(acc, st, mrow0, ncol0, ldc, C, lane);
+        return;
+      }
     }
     // f32 store (and accumulate for other wave tiles): one fragment row (FN x 4 values) of old
     // values loaded before any of its stores
