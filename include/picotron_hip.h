@@ -198,6 +198,8 @@ int pt_gemm_grouped(const pt_gemm_problem* probs, int nprob, int a_kcontig, int 
  * SwiGLU backward, residual = g|u), group 1 = wgrad (dY^T X; both operands MN-contiguous;
  * epilogue 0, 1 or 3).  The dX of a layer's projection beside its dW (both read only dY and saved
  * activations): the down_proj dX's HBM-bound SwiGLU-backward tail overlaps the dW's MFMA work.
+ * Group 0's epilogue: 0 (bf16), 6 (SwiGLU backward) or 2 (f32: the two K halves of a split-K dX,
+ * finished by pt_gemm_splitk_sum).
  * order: 0 group 0 first, 1 group 1 first, inside each XCD's share.
  * PT_EUNSUPPORTED when a problem does not tile by 256 x 256 or a group's tile count % 8 != 0. */
 int pt_gemm_dual(const pt_gemm_problem* p0, int n0, int a_kcontig0, int b_kcontig0, int epilogue0,

@@ -1554,6 +1554,7 @@ int launch_dual(GemmGroup& g0, int ak0, int bk0, int e0, GemmGroup& g1, int ak1,
     if (!args_fit(g1.p[i], 12)) return PT_EUNSUPPORTED;
   if (e0 == EPI_BF16) return launch_dual_e1<EPI_BF16>(g0, g1, e1, order, s);
   if (e0 == EPI_SWIGLU_BWD) return launch_dual_e1<EPI_SWIGLU_BWD>(g0, g1, e1, order, s);
+  if (e0 == EPI_F32) return launch_dual_e1<EPI_F32>(g0, g1, e1, order, s);  // split-K dX halves
   return PT_EUNSUPPORTED;
 }
 

@@ -477,6 +477,10 @@ def mlp_block_fwd(h2, wg, wu, wd, tp, residual=None):
     return m, (gu, hh)
 
 
+def _dual_gu_enabled():
+    return os.environ.get("PICOTRON_DUAL_GU", "1") != "0"
+
+
 def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True):
     gu, hh = saved
     I = wg.shape[0]
@@ -490,6 +494,11 @@ def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True):
         K.swiglu_bwd(dhh, gu[:, :I], gu[:, I:], dg=dgu[:, :I], du=dgu[:, I:])
         wgrad(dm, hh, [wd])
     dh = handle = None
+    if need_dx and tp.world_size == 1 and _dual_gu_enabled() and \
+            K._splitk_halves(dgu.shape[0], h2.shape[1], dgu.shape[1]) is not None:
+        # the split-K gate|up dX (two f32 K halves, 256 tiles) and the gate|up dW (512 tiles) in one
+        # dual launch: 3 whole rounds of the 256 CUs (no TP all-reduce to overlap at tp = 1)
+        return dgrad_with_wgrad(dgu, [wg, wu], [(dgu, h2, [wg, wu])])
     if need_dx:
         dh = K.linear_dgrad(dgu, [wg, wu])
         handle = tp.all_reduce(dh, async_op=True)

@@ -775,7 +775,20 @@ def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None):
         p0 = _problem(dy2d, dy2d.stride(0), weights, [Kin] * len(weights), _bounds(ns), 1, [dx], [dx.stride(0)],
                       [0, T], T, Kin, N)
         e0, flops, nbytes = EPI_BF16, 2.0 * T * Kin * N, _alg_bytes(T, Kin, N, EPI_BF16)
-    p0s = (_C.GemmProblem * 1)(p0)
+        h = _splitk_halves(T, Kin, N) if _splitk_enabled() else None
+        if h is not None and all(w.dtype == BF16 and w.is_contiguous() for w in weights) and \
+                all(n % 64 == 0 for n in ns):
+            # the dX as two f32 K halves (split-K, finished by the sum pass after the launch)
+            parts = [torch.empty(T, Kin, dtype=torch.float32, device=dy2d.device) for _ in range(2)]
+            p0s = (_C.GemmProblem * 2)()
+            for i, (lo, hi) in enumerate(((0, h), (h, N))):
+                segs = _segments(ns, lo, hi)
+                bs = [weights[j][a:a + n] for j, a, n in segs]
+                p0s[i] = _problem(dy2d[:, lo:], dy2d.stride(0), bs, [Kin] * len(bs), _bounds([n for _, _, n in segs]),
+                                  1, [parts[i]], [Kin], [0, T], T, Kin, hi - lo)
+            e0 = EPI_F32
+    if e0 != EPI_F32:
+        p0s = (_C.GemmProblem * 1)(p0)
     p1s = (_C.GemmProblem * len(wjobs))()
     for j, (wdy, x2d, outs) in enumerate(wjobs):
         _bf16_rowmajor(wdy, "dy")
@@ -792,11 +805,15 @@ def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None):
     if probe is not None:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
-    rc = _C.lib().pt_gemm_dual(p0s, 1, 1, 0, e0, p1s, len(wjobs), 0, 0, int(wepilogue),
+    rc = _C.lib().pt_gemm_dual(p0s, len(p0s), 1, 0, e0, p1s, len(wjobs), 0, 0, int(wepilogue),
                                _dual_order() if order is None else int(order), _C.stream_ptr(dy2d.device))
     if rc == -3:   # PT_EUNSUPPORTED: outside the dual tiling (e.g. C segments not on 256 rows)
         return None
     _C.check(rc, f"pt_gemm_dual(dX epi {e0}, {len(wjobs)} wgrads epi {wepilogue})")
+    if e0 == EPI_F32:
+        rc = _C.lib().pt_gemm_splitk_sum(_ptr(parts[0]), _ptr(parts[1]), None, _ptr(dx), dx.numel(),
+                                         _C.stream_ptr(dy2d.device))
+        _C.check(rc, "pt_gemm_splitk_sum")
     if probe is not None:
         ev1.record()
         probe.records.append((ev0, ev1, flops, nbytes))

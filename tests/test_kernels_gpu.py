@@ -396,6 +396,29 @@ def test_dgrad_splitk(T, Kin, ns, kmin, monkeypatch):
     assert rel_err(dx, ref1) < 4e-3
 
 
+@pytest.mark.parametrize("epi", [1, 3])
+def test_gemm_dual_splitk_dgrad(epi):
+    """the split-K gate|up dX (two f32 K halves) and the gate|up dW in one dual launch == the split-K
+    dX and the wgrad launched separately, bit for bit"""
+    from picotron_amd import kernels as K_
+    T, H, I = 1024, 2048, 8192
+    dgu = torch.randn(T, 2 * I).to(BF).to(DEV)
+    h2 = torch.randn(T, H).to(BF).to(DEV)
+    wg, wu = [(torch.randn(I, H) / math.sqrt(2 * I)).to(BF).to(DEV) for _ in range(2)]
+    dt = torch.float32 if epi == 3 else BF
+    init = [torch.randn(I, H).to(dt).to(DEV) for _ in range(2)]
+    outs_a, outs_b = [t.clone() for t in init], [t.clone() for t in init]
+    assert K_._splitk_halves(T, H, 2 * I) is not None
+    dx = K_.linear_dgrad_dual(dgu, [wg, wu], [(dgu, h2, outs_a)], epi)
+    assert dx is not None
+    dx_ref = K_.linear_dgrad(dgu, [wg, wu])
+    K_.linear_wgrad(dgu, h2, outs_b, epilogue=epi)
+    torch.cuda.synchronize()
+    assert torch.equal(dx, dx_ref)
+    for a, b in zip(outs_a, outs_b):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("residual", [False, True])
 def test_fwd_splitk(residual, monkeypatch):
     """forward GEMM split in two K halves, the residual add (EPI_BF16_RES: bf16(R + bf16(acc))) in
