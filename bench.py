@@ -229,12 +229,47 @@ def cfg_name(base):
     return {v[1]: v[0] for v in MODELS.values()}.get(base.get("_name"), "custom")
 
 
-def main():
-    # stdout carries exactly ONE line, the JSON result: anything else written to fd 1 (RCCL prints
-    # its version banner there when a communicator is created) is sent to stderr
-    result_out = os.fdopen(os.dup(1), "w")
-    sys.stdout.flush()
-    os.dup2(2, 1)
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(argv, nproc, port):
+    """The torchrun command line `bench.py --gpus N` starts for N > 1 when it was not itself started
+    by a launcher: one process per GPU on this node, env:// rendezvous on 127.0.0.1 -- the
+    reference's launch (train.py:2 docstring, template/base_job.slurm:64: torchrun --nproc_per_node
+    --nnodes ... train.py), with this script's own arguments passed through unchanged."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(argv, nproc):
+    """Run the N-rank job as a CHILD process (nothing in this process has touched the GPU: no exec)
+    and forward rank 0's single JSON line to stdout; everything else goes to stderr.  Returns the
+    child's exit code (non-zero also when no JSON line came back)."""
+    import subprocess
+    cmd = launcher_cmd(argv, nproc, _free_port())
+    log("launching", nproc, "ranks:", " ".join(cmd))
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
+    result = None
+    for line in p.stdout:
+        s = line.strip()
+        if s.startswith("{") and '"metric"' in s and result is None:
+            result = s
+        else:
+            sys.stderr.write(line)
+    rc = p.wait()
+    if result is not None:
+        print(result, flush=True)
+    if rc == 0 and result is None:
+        log("the ranks exited without a result line")
+        return 1
+    return rc
+
+
+def build_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -258,7 +293,23 @@ def main():
     ap.add_argument("--dp-bucket", action="store_true",
                     help="N = 1 only: run the DP path anyway (DataParallelBucket, fp32 main_grad, bucket "
                          "all-reduce over a 1-rank RCCL group) -- the per-GPU cost of N > 1 minus the links")
-    args = ap.parse_args()
+    return ap
+
+
+def main():
+    args = build_parser().parse_args()
+    proxy = bool(args.tp_proxy or args.cp_proxy)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1 and not proxy:
+        # `python bench.py --gpus N`: start the N ranks ourselves (before any GPU call in this process)
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus and not proxy:
+        raise SystemExit(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} from the launcher but --gpus "
+                         f"{args.gpus}: refusing to report a run with a different GPU count")
+    # stdout carries exactly ONE line, the JSON result: anything else written to fd 1 (RCCL prints
+    # its version banner there when a communicator is created) is sent to stderr
+    result_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -397,6 +448,8 @@ def main():
         par = "-".join(f"{k}{v}" for k, v in (("dp", dp), ("tp", tp), ("cp", cp)) if v > 1 or k == "dp")
         out = {"metric": "tokens/s/GPU and MFU, SmolLM-1.7B seq1024 at 1/2/4/8 MI355X", "value": value,
                "unit": "tokens/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ranks": dist.get_world_size() if dist.is_initialized() else 1,
+               "backend": dist.get_backend() if dist.is_initialized() else None,
                "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
                "scaling": "weak" if tp * cp == 1 else "strong",
                "vs_baseline": None, "dtype": "bf16", "data": "synthetic (seeded random tokens, random init)",

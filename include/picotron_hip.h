@@ -82,14 +82,16 @@ int pt_cross_entropy_fwd_bwd(const void* logits, int64_t logits_stride, const in
                              const float* inv_count, int64_t ignore_index, int* status, hipStream_t stream);
 /* The autograd pair (train.py:49 forward, loss.backward() at train.py:51): the forward streams the
  * logits once with an online max / sum-exp and writes row_loss and row_lse [rows] f32; the
- * backward is elementwise from the saved LSE: dlogits = (exp(x - row_lse) - onehot) * (*scale)
- * (a device scalar: grad_output / #valid), ignore_index rows -> 0.  dlogits may alias logits. */
+ * backward is elementwise from the saved LSE: dlogits = (exp(x - row_lse) - onehot) *
+ * scale[row * scale_stride] (scale_stride 0: one device scalar, grad_output / #valid for 'mean',
+ * grad_output for 'sum'; 1: a per-row f32 gradient, reduction='none'), ignore_index rows -> 0.
+ * dlogits may alias logits. */
 int pt_cross_entropy_fwd_lse(const void* logits, int64_t logits_stride, const int64_t* targets, float* row_loss,
                              float* row_lse, int64_t rows, int64_t vocab, int64_t ignore_index, int* status,
                              hipStream_t stream);
 int pt_cross_entropy_bwd_lse(const void* logits, int64_t logits_stride, const int64_t* targets, const float* row_lse,
                              void* dlogits, int64_t dlogits_stride, int64_t rows, int64_t vocab, const float* scale,
-                             int64_t ignore_index, hipStream_t stream);
+                             int64_t scale_stride, int64_t ignore_index, hipStream_t stream);
 /* The same forward from the lm_head GEMM's statistics (pt_gemm_ce_stats) instead of a second pass
  * over the logits: float2 stats[b * rows + row] = (max, sum exp(x - max)) of the row's bf16 logits
  * in column tile b < nblk (vocab / nblk columns each); only x[row, target] is read. */
@@ -99,9 +101,11 @@ int pt_cross_entropy_fwd_stats(const void* logits, int64_t logits_stride, const 
 
 /* train.py:49's reduction='mean' over the per-row losses: loss = sum(row_loss) / #(target !=
  * ignore_index) in one deterministic launch; inv_count = 1 / #valid (the backward's scale);
+ * reduce_sum != 0: reduction='sum' (loss = sum(row_loss), inv_count = 1);
  * loss_f32 / out (bf16 when out_bf16, else f32) optional. */
 int pt_cross_entropy_mean(const float* row_loss, const int64_t* targets, int64_t rows, int64_t ignore_index,
-                          float* loss_f32, float* inv_count, void* out, int out_bf16, hipStream_t stream);
+                          float* loss_f32, float* inv_count, void* out, int out_bf16, int reduce_sum,
+                          hipStream_t stream);
 
 /* ---- token embedding ----------------------------------------------------------------------
  * replaces model.py:224-225 (F.embedding + autograd's dense backward) and the masked lookup of

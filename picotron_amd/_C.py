@@ -45,7 +45,7 @@ SIGNATURES = {
     "pt_swiglu_bwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp]),
     "pt_cross_entropy_fwd_bwd": (_i32, [_vp, _i64, _vp, _vp, _i64, _vp, _i64, _i64, _f32, _vp, _i64, _vp, _vp]),
     "pt_cross_entropy_fwd_lse": (_i32, [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp]),
-    "pt_cross_entropy_bwd_lse": (_i32, [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp]),
+    "pt_cross_entropy_bwd_lse": (_i32, [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _i64, _i64, _vp]),
     "pt_gemm": (_i32, [_vp, _i64, _i32, _vpp, _i64p, _i64p, _i32, _i32, _i32, _vpp, _i64p, _i64p, _i32,
                        _i64, _i64, _i64, _i32, _vp, _i64, _i32, _vp]),
     "pt_gemm_pick_tile": (_i32, [_i64, _i64, _i64p, _i32, _i64p, _i32]),
@@ -60,7 +60,7 @@ SIGNATURES = {
     "pt_lse_merge": (_i32, [_vp, _vp, _i32, _vp, _vp, _i32, _vp, _vp, _i64, _i64, _vp]),
     "pt_gemm_ce_stats": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp]),
     "pt_cross_entropy_fwd_stats": (_i32, [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i64, _i64, _vp, _vp]),
-    "pt_cross_entropy_mean": (_i32, [_vp, _vp, _i64, _i64, _vp, _vp, _vp, _i32, _vp]),
+    "pt_cross_entropy_mean": (_i32, [_vp, _vp, _i64, _i64, _vp, _vp, _vp, _i32, _i32, _vp]),
     "pt_embedding_sort": (_i32, [_vp, _i64, _i64, _i64, _i32, _i64, _vp, _vp, _vp]),
     "pt_gemm_rope": (_i32, [_vp, _i64, _vpp, _i64p, _i64p, _i32, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _i64,
                             _i64, _i64, _i32, _vp]),

@@ -283,7 +283,7 @@ __global__ __launch_bounds__(kMeanThreads) void ce_mean_kernel(const float* __re
                                                                const int64_t* __restrict__ tgt, int64_t rows,
                                                                int64_t ignore_index, float* __restrict__ loss_f32,
                                                                float* __restrict__ inv_count, void* __restrict__ out,
-                                                               int out_bf16) {
+                                                               int out_bf16, int reduce_sum) {
   __shared__ float ssum[kMeanThreads];
   __shared__ int scnt[kMeanThreads];
   float s = 0.f;
@@ -303,8 +303,8 @@ __global__ __launch_bounds__(kMeanThreads) void ce_mean_kernel(const float* __re
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    const float inv = 1.0f / (float)scnt[0];
-    const float loss = ssum[0] * inv;
+    const float inv = reduce_sum ? 1.0f : 1.0f / (float)scnt[0];
+    const float loss = reduce_sum ? ssum[0] : ssum[0] * inv;
     inv_count[0] = inv;
     if (loss_f32) loss_f32[0] = loss;
     if (out) {
@@ -319,14 +319,14 @@ __global__ __launch_bounds__(kThreads) void ce_bwd_stream_kernel(const uint16_t*
                                                                  const float* __restrict__ row_lse,
                                                                  uint16_t* __restrict__ dl, int64_t ds, int V,
                                                                  const float* __restrict__ scale_dev,
-                                                                 int64_t ignore_index) {
+                                                                 int64_t scale_stride, int64_t ignore_index) {
   const int64_t row = blockIdx.x;
   const uint16_t* x = logits + row * ls;
   uint16_t* d = dl + row * ds;
   const int nch = V >> 3;
   const int64_t t = tgt[row];
   const float nl2 = -row_lse[row] * kLog2e;   // exp(x - lse) = exp2(x log2e - lse log2e)
-  const float g = t != ignore_index ? *scale_dev : 0.f;
+  const float g = t != ignore_index ? scale_dev[row * scale_stride] : 0.f;
   for (int c0 = threadIdx.x; c0 < nch; c0 += kThreads * kUnroll) {
     bf16x8 v[kUnroll];
 #pragma unroll
@@ -365,15 +365,16 @@ extern "C" int pt_cross_entropy_fwd_lse(const void* logits, int64_t logits_strid
 
 extern "C" int pt_cross_entropy_bwd_lse(const void* logits, int64_t logits_stride, const int64_t* targets,
                                         const float* row_lse, void* dlogits, int64_t dlogits_stride, int64_t rows,
-                                        int64_t vocab, const float* scale, int64_t ignore_index,
-                                        hipStream_t stream) {
+                                        int64_t vocab, const float* scale, int64_t scale_stride,
+                                        int64_t ignore_index, hipStream_t stream) {
   if (!logits || !targets || !row_lse || !dlogits || !scale || rows <= 0 || vocab <= 0) return PT_EINVAL;
+  if (scale_stride != 0 && scale_stride != 1) return PT_EINVAL;
   if ((vocab & 7) || (logits_stride & 7) || (dlogits_stride & 7)) return PT_EALIGN;
   if (!pt_aligned16(logits) || !pt_aligned16(dlogits)) return PT_EALIGN;
   if (rows > INT32_MAX || vocab > INT32_MAX) return PT_EUNSUPPORTED;
   ce_bwd_stream_kernel<<<(unsigned)rows, kThreads, 0, stream>>>((const uint16_t*)logits, logits_stride, targets,
                                                                row_lse, (uint16_t*)dlogits, dlogits_stride,
-                                                               (int)vocab, scale, ignore_index);
+                                                               (int)vocab, scale, scale_stride, ignore_index);
   PT_CHECK_LAUNCH();
   return PT_OK;
 }
@@ -418,13 +419,15 @@ extern "C" int pt_cross_entropy_fwd_stats(const void* logits, int64_t logits_str
   return PT_OK;
 }
 
-// loss = mean of row_loss over the rows whose target is not ignore_index; inv_count = 1 / #valid;
+// loss = mean of row_loss over the rows whose target is not ignore_index; inv_count = 1 / #valid
+// (reduce_sum: loss = the sum, inv_count = 1 -- F.cross_entropy's reduction='sum');
 // out (optional) = loss in bf16 (out_bf16) or f32.  One launch, deterministic.
 extern "C" int pt_cross_entropy_mean(const float* row_loss, const int64_t* targets, int64_t rows, int64_t ignore_index,
-                                     float* loss_f32, float* inv_count, void* out, int out_bf16, hipStream_t stream) {
+                                     float* loss_f32, float* inv_count, void* out, int out_bf16, int reduce_sum,
+                                     hipStream_t stream) {
   if (!row_loss || !targets || !inv_count || rows <= 0) return PT_EINVAL;
   ce_mean_kernel<<<1, kMeanThreads, 0, stream>>>(row_loss, targets, rows, ignore_index, loss_f32, inv_count, out,
-                                                 out_bf16);
+                                                 out_bf16, reduce_sum);
   PT_CHECK_LAUNCH();
   return PT_OK;
 }

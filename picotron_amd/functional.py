@@ -602,31 +602,44 @@ def embedding(ids, weight, vocab_lo=0, vocab_hi=None, padding_idx=None):
 
 
 class CrossEntropyFunction(torch.autograd.Function):
-    """F.cross_entropy(logits [N, V], targets [N], reduction='mean') as called at train.py:49.
-    Forward streams the logits once for the per-row loss and LSE (saved, 16 KiB at 4096 rows);
-    backward writes (exp(x - lse) - onehot) * grad / #valid elementwise in one more read + write,
-    with the incoming gradient (the reference's `/ grad_acc_steps`) taken from device memory -- no
-    host synchronisation."""
+    """F.cross_entropy(logits [N, V], targets [N]) as called at train.py:49 (reduction='mean'; 'sum'
+    and 'none' for other consumers of the logits).  Forward streams the logits once for the per-row
+    loss and LSE (saved, 16 KiB at 4096 rows) -- or takes both from the lm_head GEMM's statistics;
+    backward writes (exp(x - lse) - onehot) * scale elementwise in one more read + write, with the
+    scale (the incoming gradient, the reference's `/ grad_acc_steps`, times 1 / #valid for 'mean';
+    per row for 'none') taken from device memory -- no host synchronisation."""
 
     @staticmethod
-    def forward(ctx, logits, targets, ignore_index):
+    def forward(ctx, logits, targets, ignore_index, reduction):
         lg = _contig2d(logits)
         tg = targets.reshape(-1)
         stats = _take_ce_stats(lg)   # the lm_head GEMM's statistics of exactly these logits, if any
         odt = logits.dtype if logits.dtype in (torch.bfloat16, torch.float32) else torch.float32
         if stats is not None:
-            loss, inv_count, row_lse = K.cross_entropy_loss_lse_stats(lg, tg, stats, ignore_index, out_dtype=odt)
+            loss, inv_count, row_lse = K.cross_entropy_loss_lse_stats(lg, tg, stats, ignore_index, out_dtype=odt,
+                                                                      reduction=reduction)
         else:
-            loss, inv_count, row_lse = K.cross_entropy_loss_lse(lg, tg, ignore_index, out_dtype=odt)
-        ctx.save_for_backward(lg, tg, inv_count, row_lse)
-        ctx.ignore_index, ctx.shape = ignore_index, logits.shape
+            loss, inv_count, row_lse = K.cross_entropy_loss_lse(lg, tg, ignore_index, out_dtype=odt,
+                                                                reduction=reduction)
+        ctx.save_for_backward(lg, tg, row_lse, *([inv_count] if inv_count is not None else []))
+        ctx.ignore_index, ctx.shape, ctx.reduction = ignore_index, logits.shape, reduction
         return loss if loss.dtype == logits.dtype else loss.to(logits.dtype)
 
     @staticmethod
     def backward(ctx, g):
-        lg, tg, inv_count, row_lse = ctx.saved_tensors
-        dl = K.cross_entropy_grad_lse(lg, tg, row_lse, g.float().reshape(1) * inv_count, ctx.ignore_index)
-        return dl.view(ctx.shape), None, None
+        lg, tg, row_lse, *inv = ctx.saved_tensors
+        if ctx.reduction == "none":
+            scale = g.float().reshape(-1).contiguous()
+        elif ctx.reduction == "sum":
+            scale = g.float().reshape(1)
+        else:
+            scale = g.float().reshape(1) * inv[0]
+        dl = K.cross_entropy_grad_lse(lg, tg, row_lse, scale, ctx.ignore_index)
+        return dl.view(ctx.shape), None, None, None
+
+
+def _plain(t):
+    return t.as_subclass(torch.Tensor) if isinstance(t, (HipLogits, HipHidden)) else t
 
 
 class HipLogits(torch.Tensor):
@@ -651,15 +664,45 @@ class HipLogits(torch.Tensor):
             return func(*args, **kwargs)
 
 
-def _plain(t):
-    return t.as_subclass(torch.Tensor) if isinstance(t, HipLogits) else t
+class HipHidden(torch.Tensor):
+    """The final norm's output (model.py:269 `self.final_norm(x)`): an ordinary tensor whose
+    F.linear -- the call torch's nn.Linear.forward makes -- runs the HIP lm_head GEMM (with the CE
+    statistics epilogue) and returns HipLogits.  This keeps the lm_head and the cross-entropy on the
+    HIP path under callers that hold a plain nn.Linear final_proj: the one checkpoint.py:89-90
+    installs, called directly by PipelineParallel.forward (pipeline_parallel.py:62-63), whose
+    output then meets F.cross_entropy at pipeline_parallel.py:103,153.  Every other op returns
+    plain tensors."""
+
+    @classmethod
+    def __torch_function__(cls, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        if func is torch.nn.functional.linear:
+            return _dispatch_linear(*args, **kwargs)
+        with torch._C.DisableTorchFunctionSubclass():
+            return func(*args, **kwargs)
+
+
+def _dispatch_linear(input, weight, bias=None):
+    x, weight = _plain(input), _plain(weight)
+    y = lm_head_linear(x, weight) if bias is None else linear(x, weight) + bias
+    return as_logits(y)
+
+
+def as_hidden(t):
+    """Tag the final norm's output so an nn.Linear lm_head on it takes the HIP GEMM."""
+    return t.as_subclass(HipHidden)
 
 
 def _dispatch_cross_entropy(input, target, weight=None, size_average=None, ignore_index=-100, reduce=None,
                             reduction="mean", label_smoothing=0.0):
-    if weight is not None or size_average is not None or reduce is not None or label_smoothing != 0.0:
-        raise NotImplementedError("picotron_amd cross_entropy: class weights / label smoothing / legacy reduction "
-                                  "arguments are not on picotron's path (train.py:49)")
+    if weight is not None or size_average is not None or reduce is not None or label_smoothing != 0.0 or \
+            reduction not in ("mean", "sum", "none"):
+        # not on picotron's path (train.py:49 / pipeline_parallel.py:103,153 call the plain form): class
+        # weights, label smoothing and the legacy reduction flags are torch's own op on the same tensors
+        return torch.nn.functional.cross_entropy(_plain(input), _plain(target), weight=weight,
+                                                 size_average=size_average, ignore_index=ignore_index,
+                                                 reduce=reduce, reduction=reduction,
+                                                 label_smoothing=label_smoothing)
     return cross_entropy(_plain(input), _plain(target), reduction=reduction, ignore_index=ignore_index)
 
 
@@ -669,14 +712,16 @@ def as_logits(t):
 
 
 def cross_entropy(input, target, reduction="mean", ignore_index=-100):
-    """Drop-in for F.cross_entropy(..., reduction='mean') at the reference's two call sites:
+    """Drop-in for F.cross_entropy(input, target, reduction=..., ignore_index=...) at the reference's
+    two call sites (reduction='mean'):
       * train.py:49                     input [N, V], target [N];
       * pipeline_parallel.py:103,153    input = output.transpose(1, 2), i.e. [B, V, S] with the class
         dim 1 (a view of the [B, S, V] stage output), target [B, S].
     The [B, V, S] form is read as the [B*S, V] rows it views (no copy when the underlying [B, S, V]
-    is contiguous); the gradient flows back through the same views."""
-    if reduction != "mean":
-        raise ValueError("picotron_amd.cross_entropy implements reduction='mean' (train.py:49)")
+    is contiguous); the gradient flows back through the same views.  reduction 'sum' and 'none'
+    (per-row losses shaped like target, 0 at ignored rows) follow torch."""
+    if reduction not in ("mean", "sum", "none"):
+        raise ValueError(f"cross_entropy: reduction must be 'mean', 'sum' or 'none', got {reduction!r}")
     input, target = _plain(input), _plain(target)
     if input.dim() == 3:
         B, V, S = input.shape
@@ -684,8 +729,9 @@ def cross_entropy(input, target, reduction="mean", ignore_index=-100):
             raise ValueError(f"cross_entropy: input [B, V, S] = {tuple(input.shape)} needs target [B, S], got "
                              f"{tuple(target.shape)}")
         rows = input.transpose(1, 2).reshape(B * S, V)
-        return CrossEntropyFunction.apply(rows, target.reshape(-1), ignore_index)
+        out = CrossEntropyFunction.apply(rows, target.reshape(-1), ignore_index, reduction)
+        return out.view(B, S) if reduction == "none" else out
     if input.dim() != 2 or target.dim() != 1 or target.shape[0] != input.shape[0]:
         raise ValueError(f"cross_entropy: expected input [N, V] and target [N] (or [B, V, S] / [B, S]), got "
                          f"{tuple(input.shape)} / {tuple(target.shape)}")
-    return CrossEntropyFunction.apply(input, target, ignore_index)
+    return CrossEntropyFunction.apply(input, target, ignore_index, reduction)

@@ -301,19 +301,30 @@ def cross_entropy_loss(logits, targets, ignore_index=-100):
     return row_loss.sum() * inv_count[0], inv_count
 
 
-def _ce_mean(row_loss, targets, ignore_index, out_dtype):
-    """(mean loss over the valid rows in out_dtype, inv_count [1] f32) in one launch."""
+def _ce_mean(row_loss, targets, ignore_index, out_dtype, reduce_sum=False):
+    """(mean loss over the valid rows in out_dtype, inv_count [1] f32) in one launch
+    (reduce_sum: the sum of the row losses, inv_count 1)."""
     rows = row_loss.numel()
     _req(out_dtype in (BF16, torch.float32), "cross_entropy: loss dtype bf16 / f32")
     inv_count = torch.empty(1, dtype=torch.float32, device=row_loss.device)
     loss = torch.empty((), dtype=out_dtype, device=row_loss.device)
     rc = _C.lib().pt_cross_entropy_mean(_ptr(row_loss), _ptr(targets), rows, int(ignore_index), None, _ptr(inv_count),
-                                        _ptr(loss), int(out_dtype == BF16), _C.stream_ptr(row_loss.device))
+                                        _ptr(loss), int(out_dtype == BF16), int(bool(reduce_sum)),
+                                        _C.stream_ptr(row_loss.device))
     _C.check(rc, "pt_cross_entropy_mean")
     return loss, inv_count
 
 
-def cross_entropy_loss_lse(logits, targets, ignore_index=-100, out_dtype=torch.float32):
+def _ce_reduce(row_loss, targets, ignore_index, out_dtype, reduction):
+    """F.cross_entropy's reduction of the per-row losses (ignored rows hold 0): 'mean' / 'sum' in one
+    launch -> (loss scalar, inv_count [1]); 'none' -> (row losses in out_dtype, None)."""
+    if reduction == "none":
+        return (row_loss if out_dtype == torch.float32 else row_loss.to(out_dtype)), None
+    _req(reduction in ("mean", "sum"), f"cross_entropy: reduction {reduction!r}")
+    return _ce_mean(row_loss, targets, ignore_index, out_dtype, reduce_sum=reduction == "sum")
+
+
+def cross_entropy_loss_lse(logits, targets, ignore_index=-100, out_dtype=torch.float32, reduction="mean"):
     """Forward of the autograd pair: (mean loss f32 scalar tensor, inv_count [1] f32, row_lse [rows]
     f32) from one streaming read of the logits (online max / sum-exp)."""
     _bf16_rowmajor(logits, "logits")
@@ -326,22 +337,23 @@ def cross_entropy_loss_lse(logits, targets, ignore_index=-100, out_dtype=torch.f
                                            _ptr(row_lse), rows, vocab, int(ignore_index), _ptr(status_word(logits.device)), _C.stream_ptr(logits.device))
     _C.check(rc, "pt_cross_entropy_fwd_lse")
     # no clamp: every target ignored gives 0 * inf = nan, as F.cross_entropy's mean does (grads 0)
-    loss, inv_count = _ce_mean(row_loss, targets, ignore_index, out_dtype)
+    loss, inv_count = _ce_reduce(row_loss, targets, ignore_index, out_dtype, reduction)
     return loss, inv_count, row_lse
 
 
 def cross_entropy_grad_lse(logits, targets, row_lse, scale_dev, ignore_index=-100):
-    """dlogits = (exp(x - row_lse) - onehot) * scale_dev[0]: elementwise, no row reduction."""
+    """dlogits = (exp(x - row_lse) - onehot) * scale_dev[0] (one f32 device scalar) or
+    * scale_dev[row] (f32 [rows]: reduction='none'): elementwise, no row reduction."""
     _bf16_rowmajor(logits, "logits")
     rows, vocab = logits.shape
     targets = targets.contiguous()
-    _req(scale_dev.dtype == torch.float32 and scale_dev.numel() == 1, "scale: f32 device scalar")
+    _req(scale_dev.dtype == torch.float32 and scale_dev.numel() in (1, rows), "scale: f32 device scalar or [rows]")
     _req(row_lse.dtype == torch.float32 and row_lse.is_contiguous() and row_lse.numel() == rows, "row_lse: f32 [rows]")
     scale_dev = scale_dev.contiguous()
     dl = torch.empty(rows, vocab, dtype=BF16, device=logits.device)
     rc = _C.lib().pt_cross_entropy_bwd_lse(_ptr(logits), logits.stride(0), _ptr(targets), _ptr(row_lse), _ptr(dl),
-                                           dl.stride(0), rows, vocab, _ptr(scale_dev), int(ignore_index),
-                                           _C.stream_ptr(logits.device))
+                                           dl.stride(0), rows, vocab, _ptr(scale_dev), int(scale_dev.numel() != 1),
+                                           int(ignore_index), _C.stream_ptr(logits.device))
     _C.check(rc, "pt_cross_entropy_bwd_lse")
     return dl
 
@@ -582,7 +594,8 @@ def linear_ce_stats(x2d, weight):
     return y, stats
 
 
-def cross_entropy_loss_lse_stats(logits, targets, stats, ignore_index=-100, out_dtype=torch.float32):
+def cross_entropy_loss_lse_stats(logits, targets, stats, ignore_index=-100, out_dtype=torch.float32,
+                                 reduction="mean"):
     """cross_entropy_loss_lse from the lm_head GEMM's statistics (linear_ce_stats): same outputs,
     the logits are not streamed again (only x[row, target] is read)."""
     _bf16_rowmajor(logits, "logits")
@@ -598,7 +611,7 @@ def cross_entropy_loss_lse_stats(logits, targets, stats, ignore_index=-100, out_
                                              int(ignore_index), _ptr(status_word(logits.device)),
                                              _C.stream_ptr(logits.device))
     _C.check(rc, "pt_cross_entropy_fwd_stats")
-    loss, inv_count = _ce_mean(row_loss, targets, ignore_index, out_dtype)
+    loss, inv_count = _ce_reduce(row_loss, targets, ignore_index, out_dtype, reduction)
     return loss, inv_count, row_lse
 
 

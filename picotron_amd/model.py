@@ -12,8 +12,8 @@ The compute is different: DecoderLayer.forward is ONE autograd node (functional.
 built from hand-written HIP kernels -- fused q|k|v and gate|up GEMMs, in-place RoPE on the
 projection output, flash attention on strided views (no repeat_interleave, no transposes), the
 residual adds fused into the RMSNorm and down_proj kernels.  Attention / MLP / the norms can still
-be called on their own (each is its own Function).  Only the token embedding stays a torch op
-(F.embedding; outside the hot path).
+be called on their own (each is its own Function).  The token embedding is csrc/embedding.hip
+(masked lookup; sorted-segment backward).
 """
 import math
 import os
@@ -115,7 +115,7 @@ class TritonRMSNorm(nn.Module):
         if dropout_p != 0.0 or residual_in_fp32 or return_dropout_mask:
             raise NotImplementedError("TritonRMSNorm: dropout / fp32 residual are not on the picotron path")
         if residual is None:
-            y = FN.RMSNormFunction.apply(hidden_states, self.weight, self.eps, 0)
+            y = _tag_final(self, FN.RMSNormFunction.apply(FN._plain(hidden_states), self.weight, self.eps, 0))
             return (y, hidden_states) if prenorm else y
         y, z = FN.AddRMSNormFunction.apply(hidden_states, residual, self.weight, self.eps, 0)
         return (y, z) if prenorm else y
@@ -134,7 +134,15 @@ class LlamaRMSNorm(nn.Module):
         nn.init.ones_(self.weight)
 
     def forward(self, hidden_states):
-        return FN.RMSNormFunction.apply(hidden_states, self.weight, self.variance_epsilon, 1)
+        return _tag_final(self, FN.RMSNormFunction.apply(FN._plain(hidden_states), self.weight,
+                                                         self.variance_epsilon, 1))
+
+
+def _tag_final(norm, y):
+    """Llama's final_norm hands its output on as functional.HipHidden, so whatever module holds the
+    lm_head -- also a torch nn.Linear called directly (PipelineParallel.forward,
+    pipeline_parallel.py:62-63, after checkpoint.py:89-90) -- runs the HIP lm_head GEMM."""
+    return FN.as_hidden(y) if getattr(norm, "_pt_final_norm", False) else y
 
 
 def _norm_mode(norm):
@@ -168,6 +176,7 @@ class Linear(nn.Module):
             nn.init.uniform_(self.bias, -bound, bound)
 
     def forward(self, x):
+        x = FN._plain(x)
         if getattr(self, "_pt_lm_head", False) and self.bias is None:
             return FN.as_logits(FN.lm_head_linear(x, self.weight))
         y = FN.linear(x, self.weight)
@@ -268,7 +277,8 @@ class DecoderLayer(nn.Module):
 
 
 class Embedding(nn.Module):
-    """model.py:211-225 (torch gather; outside the decoder-layer hot path)."""
+    """model.py:211-225 on csrc/embedding.hip (lookup, and a backward that touches only the rows
+    the micro-batch uses)."""
 
     def __init__(self, num_embeddings, embedding_dim, padding_idx=None):
         super().__init__()
@@ -306,6 +316,7 @@ class Llama(nn.Module):
         self.final_proj._pt_lm_head = True
         RMSNorm = TritonRMSNorm if _flash() else LlamaRMSNorm
         self.final_norm = RMSNorm(self.hidden_size, eps=config.rms_norm_eps)
+        self.final_norm._pt_final_norm = True
         self.reset_parameters()
 
     def reset_parameters(self):
@@ -331,6 +342,7 @@ def lm_head(final_proj, x):
     build's Linear / ColumnParallelLinear call it themselves; a plain torch nn.Linear -- what
     init_model_with_materialized_weights swaps in (checkpoint.py:89-91) -- is run through
     functional.linear on its weight (+ bias) instead of torch's GEMM."""
+    x = FN._plain(x)
     if type(final_proj) is nn.Linear:
         if final_proj.bias is None:
             y = FN.lm_head_linear(x, final_proj.weight)

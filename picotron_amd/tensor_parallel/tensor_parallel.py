@@ -84,6 +84,7 @@ class ColumnParallelLinear(torch.nn.Module):
         self.weight.data = weight_list[self.tp_rank].contiguous()
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = FN._plain(x)
         if self.async_all_reduce:
             output = linear_with_async_all_reduce(x, self.weight, self.bias)
         else:

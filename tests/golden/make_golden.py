@@ -236,10 +236,102 @@ def g10m_multirank(rank, world, tp, cp, dp):
     return res
 
 
+G11_STEPS, G11_GA, G11_MBS, G11_LR = 50, 2, 2, 1e-3
+
+
+def _g11_data():
+    """[steps, dp 2, ga, mbs, seq + 1] uint8 tokens (seed 2468): a FRESH batch every step, drawn from
+    a fixed sparse bigram process (each token has 4 successors with probabilities .55 / .25 / .15 /
+    .05, about 1.1 nats of entropy) -- learnable structure, so the 50-step loss falls from ln 256 =
+    5.5 towards ~1.1 like a real run instead of memorising one batch."""
+    g = torch.Generator().manual_seed(2468)
+    V, S = G10M_CFG["vocab_size"], G10M_CFG["max_position_embeddings"]
+    succ = torch.randint(0, V, (V, 4), generator=g)
+    n = G11_STEPS * 2 * G11_GA * G11_MBS
+    choice = torch.multinomial(torch.tensor([0.55, 0.25, 0.15, 0.05]).expand(n, 4), S, replacement=True,
+                               generator=g)
+    seq = torch.empty(n, S + 1, dtype=torch.long)
+    seq[:, 0] = torch.randint(0, V, (n,), generator=g)
+    for t in range(S):
+        seq[:, t + 1] = succ[seq[:, t], choice[:, t]]
+    return seq.view(G11_STEPS, 2, G11_GA, G11_MBS, S + 1).to(torch.uint8)
+
+
+def g11_curve(rank, world, tp, cp, dp):
+    """G11: north_star's "loss curve within 1 % over 50 steps", pinned by the reference itself:
+    train.py's loop (train_step 29-55, the step loop 219-240) on gloo/CPU, fp32, FLASH_ATTEN=0, for
+    G11_STEPS AdamW steps (lr G11_LR, torch defaults), grad_acc 2, mbs 2, seq 256, a fresh bigram
+    batch every step (_g11_data), at 1 rank and at tp / cp / dp = 2.  Same model and initial weights
+    as G10m (one tp=1 init, seed 7, sharded as apply_tensor_parallel shards); DataParallelBucket only
+    for dp > 1 (train.py:194-195).  Records the logged loss per step (utils.py:93-98) and the
+    token stream (rank 0; the initial weights are G10m's: rank0.param.* of G10m_tp2.pt)."""
+    import torch.nn.functional as F
+    import picotron.process_group_manager as pgm
+    pgm.setup_process_group_manager(tp_size=tp, cp_size=cp, pp_size=1, dp_size=dp)
+    m = pgm.process_group_manager
+    from picotron import model as M
+    from picotron.context_parallel.context_parallel import apply_context_parallel
+    from picotron.data_parallel.data_parallel import DataParallelBucket
+    from picotron.tensor_parallel.tensor_parallel import apply_tensor_parallel
+    from picotron.utils import average_loss_across_dp_cp_ranks
+    cfg = types.SimpleNamespace(**G10M_CFG)
+    torch.manual_seed(7)
+    model = M.Llama(cfg)
+    full = {n: p.detach().clone() for n, p in model.named_parameters()}
+    if tp > 1:
+        model = apply_tensor_parallel(model)
+    if cp > 1:
+        model = apply_context_parallel(model)
+    for layer in model.decoder_layers:
+        layer.cos, layer.sin = layer.cos.float(), layer.sin.float()
+    with torch.no_grad():
+        for n, p in model.named_parameters():
+            p.copy_(_g10m_shard(full[n], p, m.tp_rank))
+    if dp > 1:
+        model = DataParallelBucket(model)
+    opt = torch.optim.AdamW(model.parameters(), lr=G11_LR)
+    ids = _g11_data()
+    S, V = G10M_CFG["max_position_embeddings"], G10M_CFG["vocab_size"]
+    sl = slice(m.cp_rank * S // cp, (m.cp_rank + 1) * S // cp)
+    losses = []
+    for step in range(G11_STEPS):
+        opt.zero_grad()
+        acc = 0.0
+        for i in range(G11_GA):
+            if m.cp_dp_world_size > 1:
+                model.require_backward_grad_sync = (i == G11_GA - 1)
+            t = ids[step, m.dp_rank, i].long()
+            x, y = t[:, :-1][:, sl].contiguous(), t[:, 1:][:, sl].contiguous()
+            out = model(input_ids=x)
+            loss = F.cross_entropy(out.reshape(-1, V), y.reshape(-1), reduction="mean") / G11_GA
+            loss.backward()
+            acc += loss.item()
+        losses.append(average_loss_across_dp_cp_ranks(acc, "cpu") if world > 1 else acc)
+        opt.step()
+        if hasattr(model, "reset"):
+            model.reset()
+    res = {"losses": torch.tensor(losses, dtype=torch.float64)}
+    if rank == 0:
+        res["ids"] = ids
+    return res
+
+
+def g11_all(ref):
+    import functools
+    for name, (tp, cp, dp) in (("G11_1", (1, 1, 1)), ("G11_tp2", (2, 1, 1)), ("G11_cp2", (1, 2, 1)),
+                               ("G11_dp2", (1, 1, 2))):
+        _run_dist(functools.partial(g11_curve, tp=tp, cp=cp, dp=dp), tp * cp * dp, ref, name)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", choices=["G11"], help="regenerate only these fixtures")
     args = ap.parse_args()
+    if args.only == "G11":
+        g11_all(args.ref)
+        print("wrote G11_1 G11_tp2 G11_cp2 G11_dp2")
+        return
     os.environ.update(DEVICE="cpu", LOCAL_RANK="0", FLASH_ATTEN="0")
     sys.path.insert(0, args.ref)
     _install_stubs()
@@ -371,7 +463,9 @@ def main():
     import functools
     for name, (tp, cp, dp) in (("G10m_tp2", (2, 1, 1)), ("G10m_cp2", (1, 2, 1)), ("G10m_dp2", (1, 1, 2))):
         _run_dist(functools.partial(g10m_multirank, tp=tp, cp=cp, dp=dp), 2, args.ref, name)
-    print("wrote", sorted(gold) + ["G7", "G8", "G10m_tp2", "G10m_cp2", "G10m_dp2"])
+    g11_all(args.ref)
+    print("wrote", sorted(gold) + ["G7", "G8", "G10m_tp2", "G10m_cp2", "G10m_dp2", "G11_1", "G11_tp2", "G11_cp2",
+                                   "G11_dp2"])
 
 
 if __name__ == "__main__":

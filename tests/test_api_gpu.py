@@ -192,6 +192,92 @@ def test_lm_head_swapped_for_torch_linear_stays_on_hip_gemm():
     assert torch.equal(after.detach().as_subclass(torch.Tensor), before.as_subclass(torch.Tensor))
 
 
+def _pipeline_stage_forward(model, final_norm, final_proj, input_ids):
+    """PipelineParallel.forward (pipeline_parallel.py:53-63) of a single (first and last) stage,
+    restated: embedding -> decoder layers (position_ids keyword) -> final_norm -> final_proj called
+    DIRECTLY (not through model.py:270 / Llama.forward)."""
+    x = model.embedding(input_ids)
+    for layer in model.decoder_layers:
+        x = layer(x, position_ids=None)
+    x = final_norm(x)
+    return final_proj(x)
+
+
+def test_pipeline_engine_lm_head_and_ce_stay_on_hip():
+    """checkpoint.py:89-90 installs a torch nn.Linear final_proj on the PipelineParallel wrapper and
+    pipeline_parallel.py:63 calls it directly; then F.cross_entropy(output.transpose(1, 2), target)
+    (pipeline_parallel.py:103,153).  The final norm's HipHidden output routes nn.Linear's F.linear
+    to the HIP lm_head GEMM: HipLogits bit-identical to Llama.forward's, the CE on the HIP kernel
+    (with the GEMM's statistics), and gradients equal to the Llama.forward path's."""
+    from picotron_amd import functional as FN
+    model, cfg = _tiny_llama(layers=2)
+    ids = torch.randint(0, cfg.vocab_size, (2, 129), generator=torch.Generator().manual_seed(6)).cuda()
+    inp, tgt = ids[:, :-1], ids[:, 1:]
+    ref_logits = model(inp)
+    FN.cross_entropy(ref_logits.transpose(1, 2), tgt).backward()
+    ref_grads = {n: p.grad.detach().clone() for n, p in model.named_parameters()}
+    model.zero_grad(set_to_none=True)
+
+    lin = torch.nn.Linear(cfg.hidden_size, cfg.vocab_size, bias=False, device="cuda", dtype=BF)
+    with torch.no_grad():
+        lin.weight.copy_(model.final_proj.weight)
+    gemm_calls, ce_calls = [], []
+    orig_lm, orig_ce, orig_take = FN.lm_head_linear, FN.cross_entropy, FN._take_ce_stats
+    took = []
+    FN.lm_head_linear = lambda *a, **k: (gemm_calls.append(a[1].shape), orig_lm(*a, **k))[1]
+    FN.cross_entropy = lambda *a, **k: (ce_calls.append(a[0].shape), orig_ce(*a, **k))[1]
+    FN._take_ce_stats = lambda lg: (lambda s: (took.append(s is not None), s)[1])(orig_take(lg))
+    try:
+        out = _pipeline_stage_forward(model, model.final_norm, lin, inp)
+        loss = F.cross_entropy(out.transpose(1, 2), tgt)
+        loss.backward()
+    finally:
+        FN.lm_head_linear, FN.cross_entropy, FN._take_ce_stats = orig_lm, orig_ce, orig_take
+    assert isinstance(out, FN.HipLogits) and gemm_calls == [lin.weight.shape]
+    assert len(ce_calls) == 1 and took == [True]
+    assert torch.equal(out.detach().as_subclass(torch.Tensor), ref_logits.detach().as_subclass(torch.Tensor))
+    assert torch.equal(lin.weight.grad, ref_grads["final_proj.weight"])
+    for n, p in model.named_parameters():
+        if n != "final_proj.weight":
+            assert torch.equal(p.grad, ref_grads[n]), n
+
+
+def test_cross_entropy_reductions_match_torch():
+    """Consumers of the logits other than train.py:49 (eval scripts): reduction 'sum' / 'none' run the
+    HIP kernel and match torch on the same bf16 logits (loss rel 1e-2, gradient rel 2e-2, ignored
+    rows 0); class weights / label smoothing are torch's own op."""
+    from picotron_amd import functional as FN
+    model, cfg = _tiny_llama()
+    ids = torch.randint(0, cfg.vocab_size, (2, 129), generator=torch.Generator().manual_seed(7)).cuda()
+    tgt = ids[:, 1:].clone()
+    tgt[0, :5] = -100
+    logits = model(ids[:, :-1]).detach()
+    for red in ("sum", "none"):
+        lg = logits.as_subclass(torch.Tensor).clone().requires_grad_(True)
+        ref_in = lg.detach().float().requires_grad_(True)
+        for form in ("rows", "bvs"):
+            lg.grad, ref_in.grad = None, None
+            hip_in = FN.as_logits(lg)
+            if form == "rows":
+                out = F.cross_entropy(hip_in.view(-1, cfg.vocab_size), tgt.reshape(-1), reduction=red)
+                ref = F.cross_entropy(ref_in.view(-1, cfg.vocab_size), tgt.reshape(-1), reduction=red)
+            else:
+                out = F.cross_entropy(hip_in.transpose(1, 2), tgt, reduction=red)
+                ref = F.cross_entropy(ref_in.transpose(1, 2), tgt, reduction=red)
+            assert out.shape == ref.shape and out.dtype == BF
+            assert rel(out, ref) < 1e-2, (red, form)
+            if red == "none":
+                assert (out.reshape(-1)[tgt.reshape(-1) == -100] == 0).all()
+            g = torch.rand_like(ref)
+            out.backward(g.to(BF))
+            ref.backward(g)
+            assert rel(lg.grad, ref_in.grad) < 2e-2, (red, form)
+    ls = F.cross_entropy(FN.as_logits(logits).view(-1, cfg.vocab_size), tgt.reshape(-1), label_smoothing=0.1)
+    ref = F.cross_entropy(logits.as_subclass(torch.Tensor).view(-1, cfg.vocab_size), tgt.reshape(-1),
+                          label_smoothing=0.1)
+    assert torch.equal(ls, ref)
+
+
 def test_frozen_weights_get_no_gradient():
     from picotron_amd import functional as FN
     model, cfg = _tiny_llama()

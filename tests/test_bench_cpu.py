@@ -1,0 +1,74 @@
+"""bench.py's multi-rank launch on the host (no GPU): `python bench.py --gpus N` starts the N ranks
+itself through torchrun (the reference's launch, train.py:2 / template/base_job.slurm:64), refuses a
+launcher whose WORLD_SIZE disagrees with --gpus, and forwards rank 0's one JSON line."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def test_launcher_command_line():
+    argv = ["--gpus", "8", "--steps", "5", "--warmup", "2", "--backend", "nccl"]
+    cmd = bench.launcher_cmd(argv, 8, 29611)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nnodes=1" in cmd and "--nproc-per-node=8" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and "--master-port=29611" in cmd
+    i = cmd.index(os.path.join(ROOT, "bench.py"))
+    assert cmd[i + 1:] == argv                   # the script's own arguments pass through unchanged
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(kw)
+    return env
+
+
+def test_mismatched_world_size_is_refused():
+    """torchrun with 2 ranks but --gpus 8: exit non-zero before touching the GPU."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8"], capture_output=True,
+                       text=True, env=_env(WORLD_SIZE="2", RANK="0"), timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr and r.stdout == ""
+
+
+def test_launch_forwards_one_result_line(monkeypatch, tmp_path, capsys):
+    """launch_ranks runs the job as a child and forwards only rank 0's JSON line to stdout."""
+    fake = tmp_path / "fake_ranks.py"
+    fake.write_text("import json\nprint('RCCL version banner')\n"
+                    "print(json.dumps({'metric': 'm', 'value': 1.0, 'n_gpus': 2, 'ranks': 2}))\n"
+                    "print('trailing noise')\n")
+    monkeypatch.setattr(bench, "launcher_cmd", lambda argv, n, port: [sys.executable, str(fake)])
+    assert bench.launch_ranks(["--gpus", "2"], 2) == 0
+    out = capsys.readouterr()
+    lines = out.out.strip().splitlines()
+    assert len(lines) == 1 and json.loads(lines[0])["n_gpus"] == 2
+    assert "RCCL version banner" in out.err and "trailing noise" in out.err
+
+
+def test_launch_without_result_fails(monkeypatch, tmp_path):
+    fake = tmp_path / "crash.py"
+    fake.write_text("import sys\nsys.exit(3)\n")
+    monkeypatch.setattr(bench, "launcher_cmd", lambda argv, n, port: [sys.executable, str(fake)])
+    assert bench.launch_ranks(["--gpus", "2"], 2) == 3
+    fake.write_text("print('no json')\n")
+    assert bench.launch_ranks(["--gpus", "2"], 2) == 1
+
+
+@pytest.mark.gpu
+def test_gloo_rehearsal_two_ranks_one_line():
+    """The one-GPU rehearsal of the driver's N = 2 run: both ranks on cuda:0 over gloo, DP over a
+    2-layer model; one JSON line reporting 2 GPUs and 2 ranks."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                        "--layers", "2", "--grad-acc", "2", "--steps", "1", "--warmup", "1", "--no-probe"],
+                       capture_output=True, text=True, env=_env(), timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["ranks"] == 2 and d["backend"] == "gloo"
+    assert d["config"]["parallelism"] == "dp2"

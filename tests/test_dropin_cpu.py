@@ -101,8 +101,32 @@ def test_hip_logits_route_f_cross_entropy(monkeypatch):
     assert type(lg * 1) is torch.Tensor and type(lg.view(6, 5)) is FN.HipLogits
     l1.backward()
     assert x.grad is not None and x.grad.shape == x.shape
-    with pytest.raises(NotImplementedError):
-        F.cross_entropy(lg.view(-1, 5), t.reshape(-1), label_smoothing=0.1)
+    # not on picotron's path: torch's own op on the plain tensors
+    ls = F.cross_entropy(lg.view(-1, 5), t.reshape(-1), label_smoothing=0.1)
+    assert type(ls) is torch.Tensor
+    assert torch.allclose(ls, F.cross_entropy((x * 2).detach().view(-1, 5), t.reshape(-1), label_smoothing=0.1))
+    assert len(seen) == 2
+
+
+def test_hip_hidden_routes_f_linear(monkeypatch):
+    """The final norm's output (HipHidden): torch's nn.Linear on it -- the lm_head checkpoint.py:89-90
+    installs, which PipelineParallel.forward calls directly (pipeline_parallel.py:63) -- goes to
+    functional.lm_head_linear and returns HipLogits; every other op returns plain tensors."""
+    from picotron_amd import functional as FN
+    seen = []
+
+    def fake(x, w):
+        seen.append((type(x), tuple(x.shape), tuple(w.shape)))
+        return x @ w.t()
+    monkeypatch.setattr(FN, "lm_head_linear", fake)
+    h = FN.as_hidden(torch.randn(2, 3, 8, requires_grad=True))
+    lin = torch.nn.Linear(8, 5, bias=False)
+    y = lin(h)
+    assert isinstance(y, FN.HipLogits) and seen == [(torch.Tensor, (2, 3, 8), (5, 8))]
+    assert torch.allclose(y.as_subclass(torch.Tensor), h.as_subclass(torch.Tensor) @ lin.weight.t())
+    assert type(h * 2) is torch.Tensor and type(h.view(6, 8)) is torch.Tensor
+    y.sum().backward()
+    assert lin.weight.grad is not None
 
 
 def test_cross_entropy_argument_forms():
@@ -112,7 +136,7 @@ def test_cross_entropy_argument_forms():
     with pytest.raises(ValueError):
         FN.cross_entropy(torch.zeros(4, 5), torch.zeros(4, 2, dtype=torch.long))
     with pytest.raises(ValueError):
-        FN.cross_entropy(torch.zeros(4, 5), torch.zeros(4, dtype=torch.long), reduction="sum")
+        FN.cross_entropy(torch.zeros(4, 5), torch.zeros(4, dtype=torch.long), reduction="average")
 
 
 @pytest.mark.parametrize("dims", [(2, 1, 2, 2), (1, 2, 2, 2), (2, 2, 1, 2), (1, 1, 4, 2)])

@@ -201,3 +201,44 @@ def test_g10m_fixtures_are_reference_loss_curves():
         if base is None:
             base = w
         assert w.keys() == base.keys() and all(torch.equal(w[k], base[k]) for k in w)
+
+
+def test_g11_fixtures_are_reference_50_step_curves():
+    """G11_{1,tp2,cp2,dp2}: the reference's own 50-step loss curves on a fresh bigram batch per step
+    (make_golden.g11_curve): finite, falling from ln 256 towards the data's entropy, identical on both
+    ranks, and the single-rank and tp2 curves equal to the precision of fp32 reduction order."""
+    curves = {}
+    for tag in ("1", "tp2", "cp2", "dp2"):
+        g = load(f"G11_{tag}")
+        l0 = g["rank0.losses"]
+        assert l0.numel() == 50 and torch.isfinite(l0).all()
+        assert abs(l0[0].item() - math.log(256)) < 0.3 and l0[-1].item() < 0.45 * l0[0].item()
+        if tag != "1":
+            assert torch.equal(l0, g["rank1.losses"])
+        curves[tag] = l0
+    assert (curves["tp2"] - curves["1"]).abs().max().item() < 1e-3
+
+
+def test_oracle_reproduces_g11_first_steps():
+    """The oracle's fp32 train step (llama_forward + CE / grad_acc + torch AdamW lr 1e-3) on G11_1's
+    token stream from G10m's initial weights reproduces the reference's first 3 logged losses."""
+    g = load("G11_1")
+    w = load("G10m_tp2")
+    cfg = dict(hidden_size=128, intermediate_size=256, num_attention_heads=2, num_key_value_heads=2,
+               rms_norm_eps=1e-5, vocab_size=256, num_hidden_layers=2)
+    params = {k[len("rank0.param."):]: v.clone().requires_grad_(True) for k, v in w.items()
+              if k.startswith("rank0.param.")}
+    opt = torch.optim.AdamW(list(params.values()), lr=1e-3)
+    cos, sin = O.get_cos_sin(256, 64, base=10000.0)
+    ids = g["rank0.ids"].long()
+    for step in range(3):
+        opt.zero_grad()
+        acc = 0.0
+        for i in range(2):
+            t = ids[step, 0, i]
+            lo = O.llama_forward(t[:, :-1], params, cfg, cos.float(), sin.float())
+            loss = torch.nn.functional.cross_entropy(lo.reshape(-1, 256), t[:, 1:].reshape(-1)) / 2
+            loss.backward()
+            acc += loss.item()
+        opt.step()
+        assert abs(acc - g["rank0.losses"][step].item()) < 1e-4 * abs(acc), (step, acc)
