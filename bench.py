@@ -19,8 +19,9 @@ apply_context_parallel / DataParallelBucket in train.py's order):
     config 5  --model llama2-7b --cp 8 --seq 32768 --mbs 1   (ring attention at 32k)
 One-GPU per-rank compute proxies (no collectives; what one rank of the multi-GPU run computes):
     --tp-proxy 8      the decoder stack + lm_head with TP=8 shard widths (q|k|v 3 x 256, I 1024)
-    --cp-proxy 8      Llama-2-7B at 32k, CP=8: the ring's critical rank (the last: 1 causal + 7 full
-                      4096 x 4096 d128 blocks per layer) -- attention blocks and the layer's GEMMs
+    --cp-proxy 8      Llama-2-7B at 32k, CP=8: the ring's critical rank -- the zig-zag schedule (1 causal
+                      + 7 half blocks per layer on every rank) and the reference's (the last rank: 1
+                      causal + 7 full 4096 x 4096 d128 blocks) -- attention blocks and the layer's GEMMs
 
 Rank 0 prints ONE JSON line.  `value` is whole-job tokens/s (max wall time over ranks);
 tokens/s/GPU and MFU (utils.py:42-48 formula, N counted once, 2.5 PF bf16 dense peak) ride along.
@@ -158,10 +159,16 @@ def tp_proxy(args, base, layers):
 
 
 def cp_proxy(args, base, layers):
-    """The critical rank of a CP ring (the last: it computes all C blocks) for one layer of
-    Llama-2-7B at seq = C x S_local: the layer's GEMMs + its causal diagonal block (the fused layer at
-    S_local) and C - 1 full S_local x S_local blocks (forward with the LSE merge epilogue, backward
-    from the global LSE, f32 dQ / dK / dV as the ring keeps them), fwd + bwd.  No p2p."""
+    """The critical rank of a CP ring for one layer of Llama-2-7B at seq = C x S_local: the layer's
+    GEMMs + its causal diagonal block (the fused layer at S_local) and the visiting blocks (forward
+    with the LSE merge epilogue, backward from the global LSE, f32 dQ / dK / dV as the ring keeps
+    them), fwd + bwd.  No p2p.  Two schedules:
+      reference  (context_parallel.py:30-45): the last rank computes C - 1 full S_local^2 blocks;
+      zig-zag    (the shipped one, context_parallel.zigzag_enabled): every rank computes C - 1 half
+                 blocks -- rank r: r of [S_local x S_local/2] (its queries x the first half of the
+                 keys) and C - 1 - r of [S_local/2 x S_local] -- the slowest rank sets the pace.
+    The zig-zag layout's shard exchange (q, K|V, o forward; dO, dq, dK|dV backward, over RCCL p2p)
+    is not in this 1-GPU proxy."""
     import math
     from picotron_amd import functional as FN
     from picotron_amd import kernels as K
@@ -171,6 +178,7 @@ def cp_proxy(args, base, layers):
     C = args.cp_proxy
     cfg = make_config(base, args.seq, num_hidden_layers=layers)
     S = args.seq // C
+    h = S // 2
     H, I = cfg.hidden_size, cfg.intermediate_size
     nh, nkv, d = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.hidden_size // cfg.num_attention_heads
     dev = torch.device("cuda")
@@ -204,25 +212,45 @@ def cp_proxy(args, base, layers):
 
     def block_bwd():
         K.attn_bwd(do, q, k, v, o, lse, sc, False, dq=dq, dk=dk, dv=dv, grad_f32=True, delta=delta)
+
+    def kv0_fwd():    # all S_local queries x the first half of the visiting keys
+        K.attn_fwd(q, k[:, :h], v[:, :h], sc, False, out=acc, lse=lse, merge=True)
+
+    def kv0_bwd():
+        K.attn_bwd(do, q, k[:, :h], v[:, :h], o, lse, sc, False, dq=dq, dk=dk[:, :h], dv=dv[:, :h], grad_f32=True,
+                   delta=delta)
+
+    def q1_fwd():     # the second half of the queries x all the visiting keys
+        K.attn_fwd(q[:, h:], k, v, sc, False, out=acc[:, h:], lse=lse[:, :, h:], merge=True)
+
+    def q1_bwd():
+        K.attn_bwd(do[:, h:], q[:, h:], k, v, o[:, h:], lse[:, :, h:], sc, False, dq=dq[:, h:], dk=dk, dv=dv,
+                   grad_f32=True, delta=delta[:, :, h:])
     t_layer = _events_time(layer, args.steps)
     t_f = _events_time(block_fwd, args.steps * 4)
     t_b = _events_time(block_bwd, args.steps * 4)
+    t_kv0 = _events_time(kv0_fwd, args.steps * 4) + _events_time(kv0_bwd, args.steps * 4)
+    t_q1 = _events_time(q1_fwd, args.steps * 4) + _events_time(q1_bwd, args.steps * 4)
     blk_flop = 4.0 * B * nh * S * S * d           # full block: QK^T + PV
-    t_rank = t_layer + (C - 1) * (t_f + t_b)      # per layer on the critical rank
+    t_ref = t_layer + (C - 1) * (t_f + t_b)       # reference schedule: the last rank
+    t_zz = t_layer + max(rk * t_kv0 + (C - 1 - rk) * t_q1 for rk in range(C))
     layer_flop_model = 6 * (2 * H * nh * d + 2 * H * nkv * d + 3 * H * I) + 12 * H * args.seq   # per token
-    tok_gpu = B * S / (t_rank * layers) / 1   # each rank holds S tokens; the ring's pace = critical rank
+    tok_gpu = B * S / (t_zz * layers)             # each rank holds S tokens; the ring's pace = its slowest rank
     return {"metric": f"CP={C} critical-rank compute proxy (1 GPU, no p2p)", "value": tok_gpu,
             "unit": "tokens/s/GPU (compute-only upper bound, lm_head/embedding excluded)",
             "config": {"model": cfg_name(base), "layers": layers, "micro_batch": B, "seq_len": args.seq,
-                       "S_local": S, "head_dim": d},
+                       "S_local": S, "head_dim": d, "schedule": "zig-zag (load-balanced)"},
             "layer_ms": t_layer * 1e3, "block_fwd_ms": t_f * 1e3, "block_bwd_ms": t_b * 1e3,
-            "critical_rank_layer_ms": t_rank * 1e3,
+            "half_block_kv0_ms": t_kv0 * 1e3, "half_block_q1_ms": t_q1 * 1e3,
+            "critical_rank_layer_ms": t_zz * 1e3, "reference_schedule_layer_ms": t_ref * 1e3,
+            "reference_schedule_tokens_per_s_per_gpu": B * S / (t_ref * layers),
             "mfu_upper_bound": tok_gpu * layer_flop_model * layers / MI355X_BF16_DENSE_PEAK,
             "roofline": {"bound": "mfma", "kernel": "attention block S_local x S_local d128 (fwd merge + bwd)",
                          "achieved": (blk_flop * 3.5) / (t_f + t_b) / 1e12, "peak": MI355X_BF16_DENSE_PEAK / 1e12,
                          "unit": "TFLOP/s", "frac": (blk_flop * 3.5) / (t_f + t_b) / MI355X_BF16_DENSE_PEAK,
                          "fwd_frac": blk_flop / t_f / MI355X_BF16_DENSE_PEAK,
-                         "bwd_frac": blk_flop * 2.5 / t_b / MI355X_BF16_DENSE_PEAK}}
+                         "bwd_frac": blk_flop * 2.5 / t_b / MI355X_BF16_DENSE_PEAK,
+                         "half_block_frac": (blk_flop / 2 * 3.5) / t_kv0 / MI355X_BF16_DENSE_PEAK}}
 
 
 def cfg_name(base):

@@ -230,20 +230,24 @@ int pt_lse_merge(const float* out, const void* block_out, int block_out_dtype, c
  * replaces model.py:33-37,154 flash_attn_func(causal=True) / model.py:157 SDPA, and the ring
  * blocks context_parallel.py:112-155 with update_out_and_lse (:157-187) fused (merge = 1).
  * q/k/v/o/dout/dq/dk/dv: token-major [B, S, H, D] views given as base + 3 strides
- * {batch, seq, head} (elements; d contiguous).  lse, delta: f32 [B, H, Sq].  D in {64, 128},
+ * {batch, seq, head} (elements; d contiguous).  lse, delta: f32 [B, H, Sq] whose (b, h) rows are
+ * lse_ld elements apart (0: Sq, dense; larger: the Sq rows are a slice of a longer sequence's LSE,
+ * as the zig-zag ring's half-sequence blocks use).  D in {64, 128},
  * Sq % 128 == 0, Sk % 64 == 0 (bwd: Sk % 128 == 0).  causal: key j visible to query i iff j <= i.
  * bwd rope_cos/rope_sin (may be NULL): [S, rope_stride] bf16 tables; dq and dk are then stored
  * rotated back by -theta (pt_rope inverse fused; positions = query / key index, Sq == Sk, bf16). */
 int pt_attn_fwd(const void* q, const int64_t* q_str, const void* k, const int64_t* k_str, const void* v,
                 const int64_t* v_str, void* o, const int64_t* o_str, float* lse, int64_t B, int64_t H, int64_t HKV,
-                int64_t Sq, int64_t Sk, int64_t D, float scale, int causal, int merge, hipStream_t stream);
+                int64_t Sq, int64_t Sk, int64_t D, float scale, int causal, int merge, int64_t lse_ld,
+                hipStream_t stream);
 int pt_attn_bwd_delta(const void* dout, const int64_t* do_str, const void* o, const int64_t* o_str, float* delta,
-                      int64_t B, int64_t H, int64_t Sq, int64_t D, hipStream_t stream);
+                      int64_t B, int64_t H, int64_t Sq, int64_t D, int64_t lse_ld, hipStream_t stream);
 int pt_attn_bwd(const void* q, const int64_t* q_str, const void* k, const int64_t* k_str, const void* v,
                 const int64_t* v_str, const void* dout, const int64_t* do_str, const float* lse, const float* delta,
                 void* dq, const int64_t* dq_str, void* dk, const int64_t* dk_str, void* dv, const int64_t* dv_str,
                 int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int64_t D, float scale, int causal,
-                int grad_f32, const void* rope_cos, const void* rope_sin, int64_t rope_stride, hipStream_t stream);
+                int grad_f32, const void* rope_cos, const void* rope_sin, int64_t rope_stride, int64_t lse_ld,
+                hipStream_t stream);
 /* pt_attn_bwd with the FA2 'D' = rowsum(dO * O) computed inside the dQ kernel (run first) from o
  * (bf16 [B, S, H, D] strides o_str) and written to delta_out [B, H, Sq] f32, which the dK/dV kernel
  * then reads: the separate pt_attn_bwd_delta pass disappears.  bf16 gradients only (no grad_f32). */
@@ -253,7 +257,7 @@ int pt_attn_bwd_fused_delta(const void* q, const int64_t* q_str, const void* k, 
                             const int64_t* dq_str, void* dk, const int64_t* dk_str, void* dv,
                             const int64_t* dv_str, int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk,
                             int64_t D, float scale, int causal, const void* rope_cos, const void* rope_sin,
-                            int64_t rope_stride, hipStream_t stream);
+                            int64_t rope_stride, int64_t lse_ld, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -15,16 +15,26 @@ What differs (MI355X-first):
   * the K|V shard travels as ONE contiguous [T, 2*kv*d] buffer per step (the reference sends k and
     v separately), and the host never synchronises the device between steps;
   * the token-major entry points (ring_attention_tokens*) read q/k/v straight out of the fused
-    projection output, with grouped-query heads indexed, not repeat_interleave'd (model.py:142-143).
+    projection output, with grouped-query heads indexed, not repeat_interleave'd (model.py:142-143);
+  * load-balanced causal ring (zig-zag): the reference's schedule gives rank r r + 1 blocks
+    (:30-45), so the last rank sets the pace with C blocks while rank 0 does 1.  Inside
+    RingAttentionFunc / ring_attention_tokens the shards are re-laid (one batched p2p exchange,
+    zigzag_exchange) so rank r holds global half-chunks r and 2C - 1 - r; then every step after the
+    causal diagonal is exactly half a block on every rank -- (all my queries x the first half of
+    the visiting keys) when they come from a lower rank, (my second-half queries x all the visiting
+    keys) otherwise -- and the outputs / gradients are re-laid back.  The external contract (rank r
+    holds tokens [r S, (r + 1) S), data.py:105-109, update_rope_for_context_parallel) is unchanged.
+    PICOTRON_RING_ZIGZAG=0 runs the reference's schedule instead (A/B only).
 """
 import math
 import os
+import weakref
 
 import torch
 
 from .. import kernels as K
 from .. import process_group_manager as pgm
-from .cp_communications import ContextCommunicate
+from .cp_communications import ContextCommunicate, zigzag_exchange
 
 
 def apply_context_parallel(model):
@@ -46,6 +56,8 @@ def update_rope_for_context_parallel(cos, sin):
 class HipBlocks:
     """Per-block attention on the HIP kernels (the only implementation the package ships)."""
 
+    align = 128   # the kernels tile query / key blocks of 128 rows (a zig-zag half must be a multiple)
+
     @staticmethod
     def fwd(q, k, v, scale, causal, acc, lse):
         K.attn_fwd(q, k, v, scale, causal, out=acc, lse=lse, merge=True)
@@ -64,22 +76,43 @@ def _kv_views(kv, B, S, nkv, d):
     return kv[:, :w].view(B, S, nkv, d), kv[:, w:].view(B, S, nkv, d)
 
 
-def ring_forward(q, kv, nkv, scale, is_causal, blocks=HipBlocks, comm=None):
+def zigzag_enabled(S, is_causal, blocks=HipBlocks):
+    """The load-balanced layout applies to a causal ring of C > 1 whose half shards tile."""
+    C = pgm.current().cp_world_size
+    return (is_causal and C > 1 and S % (2 * getattr(blocks, "align", 1)) == 0
+            and os.environ.get("PICOTRON_RING_ZIGZAG", "1") != "0")
+
+
+def _zz_kind(step, rank, world):
+    """Zig-zag ring, step > 0: the visiting K|V shard is rank j = rank - step's (half-chunks j and
+    2C - 1 - j).  j < rank: all my queries see its first half, none its second ('kv0');
+    j > rank: only my second half (2C - 1 - rank) sees it, all of it ('q1')."""
+    return "kv0" if (rank - step) % world < rank else "q1"
+
+
+def ring_forward(q, kv, nkv, scale, is_causal, blocks=HipBlocks, comm=None, zigzag=False):
     """RingAttentionFunc.forward (context_parallel.py:19-51) on token-major shards.
     q [B, S, nh, d] (any strides, d contiguous); kv [B*S, 2*nkv*d] contiguous (this rank's K|V).
+    zigzag: q / kv are in the zig-zag layout (zigzag_exchange) and the balanced schedule runs.
     Returns (out_f32 [B, S, nh, d], lse f32 [B, nh, S])."""
     comm = comm or ContextCommunicate("comm")
     B, S, nh, d = q.shape
     acc = torch.zeros(B, S, nh, d, dtype=torch.float32, device=q.device)
     lse = torch.full((B, nh, S), float("-inf"), dtype=torch.float32, device=q.device)
     cur = kv
+    h = S // 2
     for step in range(comm.world_size):
         nxt = None
         if step + 1 != comm.world_size:
             nxt = comm.send_recv(cur)
             comm.commit()
-        if not is_causal or step <= comm.rank:
-            k, v = _kv_views(cur, B, S, nkv, d)
+        k, v = _kv_views(cur, B, S, nkv, d)
+        if zigzag and step > 0:
+            if _zz_kind(step, comm.rank, comm.world_size) == "kv0":
+                blocks.fwd(q, k[:, :h], v[:, :h], scale, False, acc, lse)
+            else:
+                blocks.fwd(q[:, h:], k, v, scale, False, acc[:, h:], lse[:, :, h:])
+        elif zigzag or not is_causal or step <= comm.rank:
             blocks.fwd(q, k, v, scale, is_causal and step == 0, acc, lse)
         if step + 1 != comm.world_size:
             comm.wait()
@@ -87,9 +120,10 @@ def ring_forward(q, kv, nkv, scale, is_causal, blocks=HipBlocks, comm=None):
     return acc, lse
 
 
-def ring_backward(do, q, kv, o, lse, nkv, scale, is_causal, blocks=HipBlocks, kv_comm=None, d_kv_comm=None):
+def ring_backward(do, q, kv, o, lse, nkv, scale, is_causal, blocks=HipBlocks, kv_comm=None, d_kv_comm=None,
+                  zigzag=False):
     """RingAttentionFunc.backward (context_parallel.py:53-110).  Returns (dq f32 [B,S,nh,d],
-    dkv f32 [B*S, 2*nkv*d]) for this rank's own shards."""
+    dkv f32 [B*S, 2*nkv*d]) for this rank's own shards (zigzag: all in the zig-zag layout)."""
     kv_comm = kv_comm or ContextCommunicate("kv_comm")
     d_kv_comm = d_kv_comm or ContextCommunicate("d_kv_comm")
     B, S, nh, d = q.shape
@@ -108,9 +142,16 @@ def ring_backward(do, q, kv, o, lse, nkv, scale, is_causal, blocks=HipBlocks, kv
         else:  # the partial dK|dV of shard r-step, accumulated by the ranks before us
             d_kv_comm.wait()
             dkv = next_dkv
-        if step <= r or not is_causal:
-            k, v = _kv_views(cur, B, S, nkv, d)
-            dk, dv = _kv_views(dkv, B, S, nkv, d)
+        k, v = _kv_views(cur, B, S, nkv, d)
+        dk, dv = _kv_views(dkv, B, S, nkv, d)
+        h = S // 2
+        if zigzag and step > 0:
+            if _zz_kind(step, r, W) == "kv0":
+                blocks.bwd(do, q, k[:, :h], v[:, :h], o, lse, delta, scale, False, dq, dk[:, :h], dv[:, :h])
+            else:
+                blocks.bwd(do[:, h:], q[:, h:], k, v, o[:, h:], lse[:, :, h:], delta[:, :, h:], scale, False,
+                           dq[:, h:], dk, dv)
+        elif zigzag or step <= r or not is_causal:
             blocks.bwd(do, q, k, v, o, lse, delta, scale, is_causal and step == 0, dq, dk, dv)
         if step + 1 != W:
             kv_comm.wait()
@@ -122,18 +163,60 @@ def ring_backward(do, q, kv, o, lse, nkv, scale, is_causal, blocks=HipBlocks, kv
 
 
 # ---- token-major entry points used by the fused decoder layer (functional.py) ----------------
+# The zig-zag forward keeps its re-laid q / K|V / o for the backward, keyed by the returned LSE
+# (which stays in the zig-zag layout: only the ring backward reads it), so the backward exchanges
+# only dO and the gradients.
+_ZZ_SAVED = {}
+
+
+def _zz_stash(lse, tensors):
+    for key in [k for k, e in _ZZ_SAVED.items() if e[0]() is None]:
+        del _ZZ_SAVED[key]
+    _ZZ_SAVED[lse.data_ptr()] = (weakref.ref(lse), lse._version, tensors)
+
+
+def _zz_take(lse):
+    e = _ZZ_SAVED.pop(lse.data_ptr(), None)
+    if e is None or e[0]() is not lse or lse._version != e[1]:
+        return None
+    return e[2]
+
+
 def ring_attention_tokens(qkv, sh, scale, is_causal):
-    """q|k|v from the fused projection [T, q|k|v] -> (o bf16 [B,S,nh,d], lse f32)."""
+    """q|k|v from the fused projection [T, q|k|v] -> (o bf16 [B,S,nh,d], lse f32 [B,nh,S]; with the
+    zig-zag schedule the LSE is in the zig-zag layout)."""
+    B, S, T = sh.B, sh.S, sh.T
+    if zigzag_enabled(S, is_causal):
+        qz, kvz = zigzag_exchange([sh.q(qkv), qkv[:, sh.wq:].view(B, S, 2 * sh.wkv)], [1, 1], True)
+        kvz = kvz.view(T, 2 * sh.wkv)
+        acc, lse = ring_forward(qz, kvz, sh.nkv, scale, is_causal, zigzag=True)
+        oz = acc.to(torch.bfloat16)
+        (o,) = zigzag_exchange([oz], [1], False)
+        _zz_stash(lse, (qz, kvz, oz))
+        return o, lse
     kv = qkv[:, sh.wq:].contiguous()
     acc, lse = ring_forward(sh.q(qkv), kv, sh.nkv, scale, is_causal)
     return acc.to(torch.bfloat16), lse
 
 
 def ring_attention_tokens_bwd(do, qkv, o, lse, sh, scale, is_causal, dqkv):
-    kv = qkv[:, sh.wq:].contiguous()
-    dq, dkv = ring_backward(do, sh.q(qkv), kv, o, lse, sh.nkv, scale, is_causal)
-    dqkv[:, :sh.wq].copy_(dq.view(sh.T, sh.wq))
-    dqkv[:, sh.wq:].copy_(dkv)
+    B, S, T = sh.B, sh.S, sh.T
+    if zigzag_enabled(S, is_causal):
+        saved = _zz_take(lse)
+        if saved is None:   # not the forward's LSE object: re-lay q / K|V / o again
+            saved = zigzag_exchange([sh.q(qkv), qkv[:, sh.wq:].view(B, S, 2 * sh.wkv), o], [1, 1, 1], True)
+            saved[1] = saved[1].view(T, 2 * sh.wkv)
+        qz, kvz, oz = saved
+        (doz,) = zigzag_exchange([do], [1], True)
+        dq, dkv = ring_backward(doz, qz, kvz, oz, lse, sh.nkv, scale, is_causal, zigzag=True)
+        # rounded to bf16 before the way back (the same single rounding as the copy below)
+        dq, dkv = zigzag_exchange([dq.to(torch.bfloat16), dkv.to(torch.bfloat16).view(B, S, 2 * sh.wkv)], [1, 1],
+                                  False)
+    else:
+        kv = qkv[:, sh.wq:].contiguous()
+        dq, dkv = ring_backward(do, sh.q(qkv), kv, o, lse, sh.nkv, scale, is_causal)
+    dqkv[:, :sh.wq].copy_(dq.view(T, sh.wq))
+    dqkv[:, sh.wq:].copy_(dkv.view(T, 2 * sh.wkv))
 
 
 # ---- the reference's [B, H, S, D] API -------------------------------------------------------
@@ -144,28 +227,43 @@ class RingAttentionFunc(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, sm_scale, is_causal):
         B, H, S, D = q.shape
+        Hk = k.shape[1]
         qt = q.transpose(1, 2)
         kv = torch.cat([k.transpose(1, 2).reshape(B * S, -1), v.transpose(1, 2).reshape(B * S, -1)], dim=1)
-        acc, lse = ring_forward(qt, kv.contiguous(), k.shape[1], sm_scale, is_causal)
+        zz = zigzag_enabled(S, is_causal)
+        if zz:   # the balanced schedule on re-laid shards; q / K|V / out / LSE kept in that layout
+            qt, kv = zigzag_exchange([qt, kv.view(B, S, 2 * Hk * D)], [1, 1], True)
+            kv = kv.view(B * S, 2 * Hk * D)
+        acc, lse = ring_forward(qt, kv.contiguous(), Hk, sm_scale, is_causal, zigzag=zz)
         out = acc.to(q.dtype)                         # [B, S, H, D]
-        ctx.save_for_backward(q, k, v, out, lse)
-        ctx.sm_scale, ctx.is_causal = sm_scale, is_causal
+        ctx.save_for_backward(qt if zz else q, kv if zz else k, v, out, lse)
+        ctx.sm_scale, ctx.is_causal, ctx.zz, ctx.shape = sm_scale, is_causal, zz, (B, H, S, D, Hk)
+        if zz:
+            (out,) = zigzag_exchange([out], [1], False)
         return out.transpose(1, 2)
 
     @staticmethod
     def backward(ctx, dout, *args):
-        q, k, v, out, lse = ctx.saved_tensors
-        B, H, S, D = q.shape
-        Hk = k.shape[1]
-        kv = torch.cat([k.transpose(1, 2).reshape(B * S, -1), v.transpose(1, 2).reshape(B * S, -1)], dim=1)
+        a, b_, v, out, lse = ctx.saved_tensors
+        B, H, S, D, Hk = ctx.shape
         do = dout.transpose(1, 2)
         if do.stride(-1) != 1:
             do = do.contiguous()
-        dq, dkv = ring_backward(do, q.transpose(1, 2), kv.contiguous(), out, lse, Hk, ctx.sm_scale, ctx.is_causal)
+        if ctx.zz:
+            qt, kv = a, b_
+            (do,) = zigzag_exchange([do], [1], True)
+        else:
+            qt = a.transpose(1, 2)
+            kv = torch.cat([b_.transpose(1, 2).reshape(B * S, -1), v.transpose(1, 2).reshape(B * S, -1)], dim=1)
+        dq, dkv = ring_backward(do, qt, kv.contiguous(), out, lse, Hk, ctx.sm_scale, ctx.is_causal, zigzag=ctx.zz)
+        dtype = v.dtype
+        dq, dkv = dq.to(dtype), dkv.to(dtype).view(B, S, 2 * Hk * D)
+        if ctx.zz:
+            dq, dkv = zigzag_exchange([dq, dkv], [1, 1], False)
         w = Hk * D
-        dk = dkv[:, :w].view(B, S, Hk, D).transpose(1, 2).to(k.dtype)
-        dv = dkv[:, w:].view(B, S, Hk, D).transpose(1, 2).to(v.dtype)
-        return dq.transpose(1, 2).to(q.dtype), dk, dv, None, None
+        dk = dkv[:, :, :w].reshape(B, S, Hk, D).transpose(1, 2)
+        dv = dkv[:, :, w:].reshape(B, S, Hk, D).transpose(1, 2)
+        return dq.transpose(1, 2), dk, dv, None, None
 
 
 def ring_attention(q, k, v, sm_scale, is_causal):

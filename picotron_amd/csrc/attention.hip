@@ -10,7 +10,8 @@
 //   * model.py:142-143              repeat_interleave for GQA (elided: kv head = q head / group)
 //
 // Layout: q/k/v/o are token-major [B, S, H, D] strided views (d contiguous), e.g. slices of the
-// fused [T, (h + 2*hkv) * D] projection output -- no transposes, no copies.  lse is f32 [B, H, Sq].
+// fused [T, (h + 2*hkv) * D] projection output -- no transposes, no copies.  lse is f32 [B, H, Sq]
+// with rows lse_ld apart (a slice of a longer sequence's LSE: the zig-zag ring's half blocks).
 // mask: 0 = full, 1 = causal (key j visible to query i iff j <= i; Sq == Sk).
 //
 // Fragment scheme (all v_mfma_f32_32x32x16_bf16): scores are computed "key on the row",
@@ -44,9 +45,10 @@ struct AttnArgs {
   const uint16_t* k; int64_t k_sb, k_ss, k_sh;
   const uint16_t* v; int64_t v_sb, v_ss, v_sh;
   void* o; int64_t o_sb, o_ss, o_sh;            // bf16 output, or f32 accumulator when merge
-  float* lse;                                    // [B, H, Sq]
+  float* lse;                                    // [B, H, Sq] rows lse_ld apart
   const uint16_t* dout; int64_t do_sb, do_ss, do_sh;
-  const float* delta;                            // [B, H, Sq] rowsum(dO * O)
+  const float* delta;                            // [B, H, Sq] rowsum(dO * O), rows lse_ld apart
+  int64_t lse_ld;   // elements between consecutive (b, h) rows of lse / delta (Sq when dense)
   void* dq; int64_t dq_sb, dq_ss, dq_sh;
   void* dk; int64_t dk_sb, dk_ss, dk_sh;
   void* dv; int64_t dv_sb, dv_ss, dv_sh;
@@ -330,7 +332,7 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
   l = xor32_sum(l);
   const float inv_l = 1.0f / l;
   const float lse = m * kLn2 + __logf(l);
-  float* lse_p = a.lse + ((int64_t)b * a.H + h) * a.Sq + myq;
+  float* lse_p = a.lse + ((int64_t)b * a.H + h) * a.lse_ld + myq;
   if (!a.merge) {
     uint16_t* orow = (uint16_t*)a.o + b * a.o_sb + (int64_t)myq * a.o_ss + h * a.o_sh;
 #pragma unroll
@@ -395,7 +397,7 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AttnArgs a, const uint1
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc += x[j] * y[j];
     for (int off = lpr >> 1; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-    if (c == 0) a.lse[((int64_t)b * a.H + h) * a.Sq + qq] = acc;  // the delta buffer travels in the lse slot
+    if (c == 0) a.lse[((int64_t)b * a.H + h) * a.lse_ld + qq] = acc;  // the delta buffer travels in the lse slot
   }
 }
 
@@ -441,7 +443,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, i
     stage_rows<D>(a.q + b * a.q_sb + (int64_t)qt * KT * a.q_ss + hq * a.q_sh, a.q_ss, sq, wave, lane);
     stage_rows<D>(a.dout + b * a.do_sb + (int64_t)qt * KT * a.do_ss + hq * a.do_sh, a.do_ss, sq + TILE_B, wave, lane);
     if (wave == 0) {  // 64 delta floats = 256 B: one 4-byte DMA per lane
-      const int64_t ro = ((int64_t)b * a.H + hq) * a.Sq + qt * KT;
+      const int64_t ro = ((int64_t)b * a.H + hq) * a.lse_ld + qt * KT;
       lse_next = a.lse[ro + lane];
       pt_glds4(a.delta + ro, lane * 4u, (__attribute__((address_space(3))) void*)(sq + 2 * TILE_B + KT * 4));
     }
@@ -567,7 +569,7 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
     qf[ks] = ld_row_frag(qrow, ks, lane);
     dof[ks] = ld_row_frag(dorow, ks, lane);
   }
-  const int64_t ri = ((int64_t)b * a.H + h) * a.Sq + myq;
+  const int64_t ri = ((int64_t)b * a.H + h) * a.lse_ld + myq;
   const float nlse2 = -a.lse[ri] * kLog2e;
   // D of this lane's row (a.delta_w: computed here from O; its half of d in this lane, the other
   // half in lane ^ 32).  The O loads are issued now and consumed after the first K/V tile's DMA
@@ -707,7 +709,8 @@ int attn_bwd_impl(const void* q, const int64_t* q_str, const void* k, const int6
                   const float* delta, void* dq, const int64_t* dq_str, void* dk, const int64_t* dk_str, void* dv,
                   const int64_t* dv_str, int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int64_t D,
                   float scale, int causal, int grad_f32, const void* rope_cos, const void* rope_sin,
-                  int64_t rope_stride, const void* o, const int64_t* o_str, float* delta_w, hipStream_t stream);
+                  int64_t rope_stride, const void* o, const int64_t* o_str, float* delta_w, int64_t lse_ld,
+                  hipStream_t stream);
 
 }  // namespace
 
@@ -718,9 +721,12 @@ extern "C" {
 // LSE (initialise o = 0, lse = -inf); this block's result is merged in (update_out_and_lse).
 int pt_attn_fwd(const void* q, const int64_t* q_str, const void* k, const int64_t* k_str, const void* v,
                 const int64_t* v_str, void* o, const int64_t* o_str, float* lse, int64_t B, int64_t H, int64_t HKV,
-                int64_t Sq, int64_t Sk, int64_t D, float scale, int causal, int merge, hipStream_t stream) {
+                int64_t Sq, int64_t Sk, int64_t D, float scale, int causal, int merge, int64_t lse_ld,
+                hipStream_t stream) {
   if (!q || !k || !v || !o || !lse) return PT_EINVAL;
+  if (lse_ld != 0 && lse_ld < Sq) return PT_EINVAL;
   AttnArgs a{};
+  a.lse_ld = lse_ld ? lse_ld : Sq;
   a.q = (const uint16_t*)q; a.q_sb = q_str[0]; a.q_ss = q_str[1]; a.q_sh = q_str[2];
   a.k = (const uint16_t*)k; a.k_sb = k_str[0]; a.k_ss = k_str[1]; a.k_sh = k_str[2];
   a.v = (const uint16_t*)v; a.v_sb = v_str[0]; a.v_ss = v_str[1]; a.v_sh = v_str[2];
@@ -744,9 +750,11 @@ int pt_attn_fwd(const void* q, const int64_t* q_str, const void* k, const int64_
 
 // delta[b, h, q] = sum_d dO * O   (f32, [B, H, Sq])
 int pt_attn_bwd_delta(const void* dout, const int64_t* do_str, const void* o, const int64_t* o_str, float* delta,
-                      int64_t B, int64_t H, int64_t Sq, int64_t D, hipStream_t stream) {
+                      int64_t B, int64_t H, int64_t Sq, int64_t D, int64_t lse_ld, hipStream_t stream) {
   if (!dout || !o || !delta || D % 8) return PT_EINVAL;
+  if (lse_ld != 0 && lse_ld < Sq) return PT_EINVAL;
   AttnArgs a{};
+  a.lse_ld = lse_ld ? lse_ld : Sq;
   a.dout = (const uint16_t*)dout; a.do_sb = do_str[0]; a.do_ss = do_str[1]; a.do_sh = do_str[2];
   a.o_sb = o_str[0]; a.o_ss = o_str[1]; a.o_sh = o_str[2];
   a.lse = delta;
@@ -767,11 +775,12 @@ int pt_attn_bwd(const void* q, const int64_t* q_str, const void* k, const int64_
                 const int64_t* v_str, const void* dout, const int64_t* do_str, const float* lse, const float* delta,
                 void* dq, const int64_t* dq_str, void* dk, const int64_t* dk_str, void* dv, const int64_t* dv_str,
                 int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int64_t D, float scale, int causal,
-                int grad_f32, const void* rope_cos, const void* rope_sin, int64_t rope_stride, hipStream_t stream) {
+                int grad_f32, const void* rope_cos, const void* rope_sin, int64_t rope_stride, int64_t lse_ld,
+                hipStream_t stream) {
   if (!delta) return PT_EINVAL;
   return attn_bwd_impl(q, q_str, k, k_str, v, v_str, dout, do_str, lse, delta, dq, dq_str, dk, dk_str, dv, dv_str,
                        B, H, HKV, Sq, Sk, D, scale, causal, grad_f32, rope_cos, rope_sin, rope_stride, nullptr,
-                       nullptr, nullptr, stream);
+                       nullptr, nullptr, lse_ld, stream);
 }
 
 }  // extern "C"
@@ -783,8 +792,10 @@ int attn_bwd_impl(const void* q, const int64_t* q_str, const void* k, const int6
                   const float* delta, void* dq, const int64_t* dq_str, void* dk, const int64_t* dk_str, void* dv,
                   const int64_t* dv_str, int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int64_t D,
                   float scale, int causal, int grad_f32, const void* rope_cos, const void* rope_sin,
-                  int64_t rope_stride, const void* o, const int64_t* o_str, float* delta_w, hipStream_t stream) {
+                  int64_t rope_stride, const void* o, const int64_t* o_str, float* delta_w, int64_t lse_ld,
+                  hipStream_t stream) {
   if (!q || !k || !v || !dout || !lse || !dq || !dk || !dv) return PT_EINVAL;
+  if (lse_ld != 0 && lse_ld < Sq) return PT_EINVAL;
   if (rope_cos && (!rope_sin || grad_f32 || Sq != Sk || (rope_stride & 3) || !pt_aligned16(rope_cos) ||
                    !pt_aligned16(rope_sin)))
     return PT_EINVAL;
@@ -794,6 +805,7 @@ int attn_bwd_impl(const void* q, const int64_t* q_str, const void* k, const int6
   a.v = (const uint16_t*)v; a.v_sb = v_str[0]; a.v_ss = v_str[1]; a.v_sh = v_str[2];
   a.dout = (const uint16_t*)dout; a.do_sb = do_str[0]; a.do_ss = do_str[1]; a.do_sh = do_str[2];
   a.lse = (float*)lse; a.delta = delta;
+  a.lse_ld = lse_ld ? lse_ld : Sq;
   a.dq = dq; a.dq_sb = dq_str[0]; a.dq_ss = dq_str[1]; a.dq_sh = dq_str[2];
   a.dk = dk; a.dk_sb = dk_str[0]; a.dk_ss = dk_str[1]; a.dk_sh = dk_str[2];
   a.dv = dv; a.dv_sb = dv_str[0]; a.dv_ss = dv_str[1]; a.dv_sh = dv_str[2];
@@ -847,12 +859,12 @@ int pt_attn_bwd_fused_delta(const void* q, const int64_t* q_str, const void* k, 
                             const int64_t* dq_str, void* dk, const int64_t* dk_str, void* dv,
                             const int64_t* dv_str, int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk,
                             int64_t D, float scale, int causal, const void* rope_cos, const void* rope_sin,
-                            int64_t rope_stride, hipStream_t stream) {
+                            int64_t rope_stride, int64_t lse_ld, hipStream_t stream) {
   if (!o || !delta_out || !o_str) return PT_EINVAL;
   if (!pt_aligned16(o) || (o_str[0] & 7) || (o_str[1] & 7) || (o_str[2] & 7)) return PT_EALIGN;
   return attn_bwd_impl(q, q_str, k, k_str, v, v_str, dout, do_str, lse, nullptr, dq, dq_str, dk, dk_str, dv,
                        dv_str, B, H, HKV, Sq, Sk, D, scale, causal, 0, rope_cos, rope_sin, rope_stride, o, o_str,
-                       delta_out, stream);
+                       delta_out, lse_ld, stream);
 }
 
 }  // extern "C"

@@ -872,28 +872,41 @@ def _str3(t):
     return _C.i64arr([t.stride(0), t.stride(1), t.stride(2)])
 
 
+def _lse_ld(t, B, H, Sq, name="lse"):
+    """Row stride of an f32 [B, H, Sq] LSE / delta tensor: dense, or the Sq-column slice of a longer
+    [B, H, S] one (the zig-zag ring's half blocks); the kernels index (b, h) rows lse_ld apart."""
+    _req(t.dtype == torch.float32 and tuple(t.shape) == (B, H, Sq) and t.stride(2) == 1
+         and t.stride(1) >= Sq and (B == 1 or t.stride(0) == H * t.stride(1)) and (H == 1 or t.stride(1) > 0),
+         f"{name} must be f32 [B, H, Sq] with unit column stride and (b, h) rows evenly spaced")
+    return t.stride(1) if H > 1 else (t.stride(0) if B > 1 else Sq)
+
+
 def attn_fwd(q, k, v, scale, causal, out=None, lse=None, merge=False):
     """q [B,Sq,H,D], k/v [B,Sk,Hkv,D] (token-major views).  Returns (out, lse[B,H,Sq] f32).
-    merge=True: `out` is an f32 accumulator and `lse` the running LSE; this block is merged in."""
+    merge=True: `out` is an f32 accumulator and `lse` the running LSE; this block is merged in.
+    lse may be the Sq-column slice of a longer [B, H, S] LSE (rows evenly spaced)."""
     B, Sq, H, D = q.shape
     Sk, HKV = k.shape[1], k.shape[2]
     if out is None:
         out = torch.empty(B, Sq, H, D, dtype=BF16, device=q.device)
     if lse is None:
         lse = torch.empty(B, H, Sq, dtype=torch.float32, device=q.device)
-    _req(lse.is_contiguous() and lse.shape == (B, H, Sq), "lse must be contiguous [B, H, Sq] f32")
+    ld = _lse_ld(lse, B, H, Sq)
     rc = _C.lib().pt_attn_fwd(_ptr(q), _str3(q), _ptr(k), _str3(k), _ptr(v), _str3(v), _ptr(out), _str3(out),
                               _ptr(lse), B, H, HKV, Sq, Sk, D, float(scale), int(bool(causal)), int(bool(merge)),
-                              _C.stream_ptr(q.device))
+                              ld, _C.stream_ptr(q.device))
     _C.check(rc, "pt_attn_fwd")
     return out, lse
 
 
-def attn_delta(dout, out):
-    """delta[b, h, q] = sum_d dO * O  (f32 [B, H, Sq]) for the backward (FA2 'D')."""
+def attn_delta(dout, out, delta=None):
+    """delta[b, h, q] = sum_d dO * O  (f32 [B, H, Sq]) for the backward (FA2 'D'); into `delta` (a
+    dense or row-strided [B, H, Sq] f32 tensor) when given."""
     B, Sq, H, D = out.shape
-    delta = torch.empty(B, H, Sq, dtype=torch.float32, device=out.device)
-    rc = _C.lib().pt_attn_bwd_delta(_ptr(dout), _str3(dout), _ptr(out), _str3(out), _ptr(delta), B, H, Sq, D,
+    if delta is None:
+        delta = torch.empty(B, H, Sq, dtype=torch.float32, device=out.device)
+    ld = _lse_ld(delta, B, H, Sq, "delta")
+    rc = _C.lib().pt_attn_bwd_delta(_ptr(dout), _str3(dout), _ptr(out), _str3(out), _ptr(delta), B, H, Sq, D, ld,
                                     _C.stream_ptr(out.device))
     _C.check(rc, "pt_attn_bwd_delta")
     return delta
@@ -908,7 +921,11 @@ def attn_bwd(dout, q, k, v, out, lse, scale, causal, dq=None, dk=None, dv=None, 
     lib = _C.lib()
     fuse_delta = delta is None and not grad_f32 and out.dtype == BF16 and os.environ.get("PICOTRON_FUSE_DELTA", "1") != "0"
     if delta is None and not fuse_delta:
-        delta = attn_delta(dout, out)
+        ld0 = _lse_ld(lse, B, H, Sq)
+        delta = attn_delta(dout, out, torch.empty(B, H, ld0, dtype=torch.float32, device=q.device)[:, :, :Sq]
+                           if ld0 != Sq else None)
+    if delta is not None:
+        _req(_lse_ld(delta, B, H, Sq, "delta") == _lse_ld(lse, B, H, Sq), "attn_bwd: delta and lse rows must share a stride")
     gdt = torch.float32 if grad_f32 else BF16
     if dq is None:
         dq = (torch.zeros if grad_f32 else torch.empty)(B, Sq, H, D, dtype=gdt, device=q.device)
@@ -924,18 +941,21 @@ def attn_bwd(dout, q, k, v, out, lse, scale, causal, dq=None, dk=None, dv=None, 
              "attn_bwd rope tables: bf16 [S, d]")
         _req(rc_sin.stride(0) == rc_cos.stride(0), "attn_bwd rope tables share a stride")
         rstride = rc_cos.stride(0)
+    ld = _lse_ld(lse, B, H, Sq)
     if fuse_delta:   # D = rowsum(dO * O) inside the dQ kernel (no separate pass)
         _req(out.shape == q.shape, "attn_bwd: out must be [B, Sq, H, D]")
+        _req(ld == Sq, "attn_bwd: the fused-delta form takes a dense lse")
         delta = torch.empty(B, H, Sq, dtype=torch.float32, device=q.device)
         rc = lib.pt_attn_bwd_fused_delta(_ptr(q), _str3(q), _ptr(k), _str3(k), _ptr(v), _str3(v), _ptr(out), _str3(out),
                                          _ptr(dout), _str3(dout), _ptr(lse), _ptr(delta), _ptr(dq), _str3(dq), _ptr(dk),
                                          _str3(dk), _ptr(dv), _str3(dv), B, H, HKV, Sq, Sk, D, float(scale),
-                                         int(bool(causal)), _ptr(rc_cos), _ptr(rc_sin), rstride, _C.stream_ptr(q.device))
+                                         int(bool(causal)), _ptr(rc_cos), _ptr(rc_sin), rstride, ld,
+                                         _C.stream_ptr(q.device))
         _C.check(rc, "pt_attn_bwd_fused_delta")
         return dq, dk, dv, delta
     rc = lib.pt_attn_bwd(_ptr(q), _str3(q), _ptr(k), _str3(k), _ptr(v), _str3(v), _ptr(dout), _str3(dout),
                          _ptr(lse), _ptr(delta), _ptr(dq), _str3(dq), _ptr(dk), _str3(dk), _ptr(dv), _str3(dv),
                          B, H, HKV, Sq, Sk, D, float(scale), int(bool(causal)), int(bool(grad_f32)),
-                         _ptr(rc_cos), _ptr(rc_sin), rstride, _C.stream_ptr(q.device))
+                         _ptr(rc_cos), _ptr(rc_sin), rstride, ld, _C.stream_ptr(q.device))
     _C.check(rc, "pt_attn_bwd")
     return dq, dk, dv, delta

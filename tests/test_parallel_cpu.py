@@ -188,10 +188,10 @@ class OracleBlocks:
         dq_, dk_, dv_ = O.ring_attention_backward(do.float().transpose(1, 2), q.float().transpose(1, 2),
                                                   OracleBlocks._expand(k, nh), OracleBlocks._expand(v, nh),
                                                   o.float().transpose(1, 2), lse, scale, causal)
-        B, S, _, d = q.shape
+        B, Sk, _, d = k.shape
         dq += dq_.transpose(1, 2)
-        dk += dk_.view(B, nkv, nh // nkv, S, d).sum(2).transpose(1, 2)
-        dv += dv_.view(B, nkv, nh // nkv, S, d).sum(2).transpose(1, 2)
+        dk += dk_.view(B, nkv, nh // nkv, Sk, d).sum(2).transpose(1, 2)
+        dv += dv_.view(B, nkv, nh // nkv, Sk, d).sum(2).transpose(1, 2)
 
 
 def _ring(rank, world, nh, nkv):
@@ -229,6 +229,77 @@ def _ring(rank, world, nh, nkv):
 @pytest.mark.parametrize("world,nh,nkv", [(2, 2, 2), (4, 4, 2)])
 def test_ring_attention_schedule_matches_full_attention(world, nh, nkv):
     _dist.run(_ring, world, nh, nkv)
+
+
+class CountingBlocks(OracleBlocks):
+    """OracleBlocks that also record the causal work (visible query-key pairs) of every call."""
+    work = []
+
+    @staticmethod
+    def fwd(q, k, v, scale, causal, acc, lse):
+        Sq, Sk = q.shape[1], k.shape[1]
+        CountingBlocks.work.append(Sq * (Sq + 1) // 2 if causal else Sq * Sk)
+        OracleBlocks.fwd(q, k, v, scale, causal, acc, lse)
+
+
+def _ring_zigzag(rank, world, nh, nkv):
+    """The load-balanced (zig-zag) ring: shards re-laid by zigzag_exchange, the balanced schedule,
+    outputs / gradients re-laid back -- equal to full causal attention over the whole sequence on
+    the reference's contiguous chunks, and every rank does the same causal work (the reference's
+    schedule: rank r does r + 1 blocks)."""
+    from oracle import picotron_oracle as O
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.context_parallel import context_parallel as CP
+    from picotron_amd.context_parallel.cp_communications import zigzag_exchange
+    pgm.setup_process_group_manager(tp_size=1, cp_size=world, pp_size=1, dp_size=1)
+    B, S, d = 2, 8, 16
+    g = torch.Generator().manual_seed(7)
+    q = torch.randn(B, world * S, nh, d, generator=g)
+    k = torch.randn(B, world * S, nkv, d, generator=g)
+    v = torch.randn(B, world * S, nkv, d, generator=g)
+    do = torch.randn(B, world * S, nh, d, generator=g)
+    sl = slice(rank * S, (rank + 1) * S)
+    scale = 1 / math.sqrt(d)
+    kv = torch.cat([k[:, sl].reshape(B, S, -1), v[:, sl].reshape(B, S, -1)], dim=2)
+    # the exchange is a permutation: there and back is the identity
+    back = zigzag_exchange(zigzag_exchange([q[:, sl], kv], [1, 1], True), [1, 1], False)
+    assert torch.equal(back[0], q[:, sl]) and torch.equal(back[1], kv)
+    qz, kvz = zigzag_exchange([q[:, sl], kv], [1, 1], True)
+    # rank r holds global half-chunks r and 2 world - 1 - r
+    h = S // 2
+    assert torch.equal(qz[:, :h], q[:, rank * h:(rank + 1) * h])
+    assert torch.equal(qz[:, h:], q[:, (2 * world - 1 - rank) * h:(2 * world - rank) * h])
+    kvz = kvz.reshape(B * S, -1)
+    CountingBlocks.work = []
+    acc, lse = CP.ring_forward(qz, kvz, nkv, scale, True, blocks=CountingBlocks, zigzag=True)
+    work = torch.tensor([float(sum(CountingBlocks.work))])
+    allw = [torch.zeros(1) for _ in range(world)]
+    dist.all_gather(allw, work)
+    assert len({w.item() for w in allw}) == 1, allw         # balanced
+    assert work.item() == S * (S + 1) // 2 + (world - 1) * S * S // 2
+    (o,) = zigzag_exchange([acc], [1], False)
+    (lse_c,) = zigzag_exchange([lse], [2], False)
+    qr = q.transpose(1, 2).requires_grad_(True)
+    kr = k.transpose(1, 2).repeat_interleave(nh // nkv, 1).detach().requires_grad_(True)
+    vr = v.transpose(1, 2).repeat_interleave(nh // nkv, 1).detach().requires_grad_(True)
+    o_ref, lse_ref = O.attention_lse(qr, kr, vr, scale, True)
+    torch.testing.assert_close(o, o_ref.transpose(1, 2)[:, sl].detach(), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(lse_c, lse_ref[:, :, sl].detach(), rtol=1e-5, atol=1e-5)
+    (o_ref * do.transpose(1, 2)).sum().backward()
+    (doz,) = zigzag_exchange([do[:, sl]], [1], True)
+    dq, dkv = CP.ring_backward(doz, qz, kvz, acc, lse, nkv, scale, True, blocks=OracleBlocks, zigzag=True)
+    dq, dkv = zigzag_exchange([dq, dkv.view(B, S, -1)], [1, 1], False)
+    torch.testing.assert_close(dq, qr.grad.transpose(1, 2)[:, sl], rtol=1e-4, atol=1e-5)
+    dk_ref = kr.grad.view(B, nkv, nh // nkv, world * S, d).sum(2).transpose(1, 2)[:, sl]
+    dv_ref = vr.grad.view(B, nkv, nh // nkv, world * S, d).sum(2).transpose(1, 2)[:, sl]
+    w = nkv * d
+    torch.testing.assert_close(dkv[:, :, :w].reshape(B, S, nkv, d), dk_ref, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(dkv[:, :, w:].reshape(B, S, nkv, d), dv_ref, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("world,nh,nkv", [(2, 2, 2), (3, 2, 1), (4, 4, 2)])
+def test_zigzag_ring_is_balanced_and_exact(world, nh, nkv):
+    _dist.run(_ring_zigzag, world, nh, nkv)
 
 
 # ----------------------------------------------------------------------------- PP p2p

@@ -38,7 +38,7 @@ def _shard(full, local, rank):
     return full.narrow(d, rank * n, n)
 
 
-def _setup(tp, cp):
+def _setup(tp, cp, seq=256):
     import types
     os.environ["FLASH_ATTEN"] = "1"
     torch.cuda.set_device(0)
@@ -48,7 +48,8 @@ def _setup(tp, cp):
     from picotron_amd.model import Llama
     from picotron_amd.tensor_parallel.tensor_parallel import apply_tensor_parallel
     m = pgm.setup_process_group_manager(tp_size=tp, cp_size=cp, pp_size=1, dp_size=1)
-    cfg = types.SimpleNamespace(**CFG)
+    c = dict(CFG, max_position_embeddings=seq)
+    cfg = types.SimpleNamespace(**c)
     full = {k: v.to(torch.bfloat16) for k, v in O.init_params(dict(CFG), seed=7).items()}
     with torch.device("cuda"):
         model = Llama(cfg)
@@ -63,20 +64,22 @@ def _setup(tp, cp):
         for n, p in names.items():
             p.copy_(_shard(full[n], p, m.tp_rank))
     g = torch.Generator().manual_seed(11)
-    ids = torch.randint(0, CFG["vocab_size"], (2, CFG["max_position_embeddings"] + 1), generator=g)
+    ids = torch.randint(0, CFG["vocab_size"], (2, seq + 1), generator=g)
     # the oracle on the full model, fp32 from the same bf16 weights
     pf = {k: v.float().requires_grad_(True) for k, v in full.items()}
-    cos, sin = O.get_cos_sin(CFG["max_position_embeddings"], 64, base=CFG["rope_theta"])
+    cos, sin = O.get_cos_sin(seq, 64, base=CFG["rope_theta"])
     lo = O.llama_forward(ids[:, :-1], pf, dict(CFG), cos.float(), sin.float(), norm=O.rmsnorm_flash_semantics)
     loss_r = F.cross_entropy(lo.reshape(-1, CFG["vocab_size"]), ids[:, 1:].reshape(-1))
     loss_r.backward()
     return m, model, names, pf, ids, lo, loss_r
 
 
-def _llama(rank, world, tp, cp):
+def _llama(rank, world, tp, cp, seq=256, zigzag=False):
     from picotron_amd import functional as FN
-    m, model, names, pf, ids, lo, loss_r = _setup(tp, cp)
-    s = CFG["max_position_embeddings"] // cp
+    from picotron_amd.context_parallel.context_parallel import zigzag_enabled
+    m, model, names, pf, ids, lo, loss_r = _setup(tp, cp, seq)
+    s = seq // cp
+    assert zigzag_enabled(s, True) == zigzag   # which ring schedule this case exercises
     sl = slice(m.cp_rank * s, (m.cp_rank + 1) * s)                # data.py:105-109: contiguous chunks
     x, t = ids[:, :-1][:, sl].contiguous(), ids[:, 1:][:, sl].contiguous()
     logits = model(x.cuda())
@@ -109,6 +112,46 @@ def test_context_parallel_llama_cp2():
 
 def test_tp2_cp2_llama():
     _dist.run(_llama, 4, 2, 2, device="cuda")
+
+
+@pytest.mark.parametrize("tp,cp,seq", [(1, 2, 512), (1, 4, 1024), (2, 2, 512)])
+def test_zigzag_ring_llama(tp, cp, seq):
+    """The load-balanced (zig-zag) causal ring (S_local = 256: its half shards tile the kernels):
+    full Llama forward + backward at cp2 / cp4 / tp2.cp2 against the oracle on the whole sequence,
+    the reference's contiguous token chunks in and out."""
+    _dist.run(_llama, tp * cp, tp, cp, seq, True, device="cuda")
+
+
+def _ring_api(rank, world):
+    """ring_attention (context_parallel.py:14-15, RingAttentionFunc [B, H, S, D], GQA-expanded k/v
+    as model.py:142-143 passes them) with the zig-zag schedule: out and dq / dk / dv of this rank's
+    contiguous chunk against the oracle's full causal attention (fp32 from the same bf16 inputs)."""
+    import math
+    torch.cuda.set_device(0)
+    from oracle import picotron_oracle as O
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.context_parallel import context_parallel as CP
+    pgm.setup_process_group_manager(tp_size=1, cp_size=world, pp_size=1, dp_size=1)
+    B, H, S, D = 1, 4, 256, 128
+    g = torch.Generator().manual_seed(5)
+    q, k, v, do = (torch.randn(B, H, world * S, D, generator=g).to(torch.bfloat16) for _ in range(4))
+    sl = slice(rank * S, (rank + 1) * S)
+    assert CP.zigzag_enabled(S, True)
+    ql, kl, vl = (t[:, :, sl].cuda().requires_grad_(True) for t in (q, k, v))
+    out = CP.ring_attention(ql, kl, vl, 1 / math.sqrt(D), True)
+    out.backward(do[:, :, sl].cuda())
+    qr, kr, vr = (t.float().requires_grad_(True) for t in (q, k, v))
+    o_ref, _ = O.attention_lse(qr, kr, vr, 1 / math.sqrt(D), True)
+    o_ref.backward(do.float())
+    assert out.dtype == torch.bfloat16 and out.shape == ql.shape
+    assert _rel(out, o_ref[:, :, sl]) < TOL
+    for got, ref in ((ql.grad, qr.grad), (kl.grad, kr.grad), (vl.grad, vr.grad)):
+        assert _rel(got, ref[:, :, sl]) < TOL
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ring_attention_api_zigzag(world):
+    _dist.run(_ring_api, world, device="cuda")
 
 
 def _dp_llama(rank, world, tp):

@@ -1,0 +1,145 @@
+#!/bin/bash
+# One parameterised driver for the GPU-box sessions (replaces the round-2 one-off lease scripts).
+# Run from the repo root ON THE BOX (through gpurun):   bash tools/gpu.sh <tag> <step>[,<step>...] [k=v ...]
+#
+# steps (run in the order given; the first failure ends the call -- no retries on the GPU):
+#   suite        pytest -m gpu (whole suite; TESTS=... to narrow), then smoke()
+#   bench        bench.py N=1 (BENCH_RUNS=2 lines), default arguments
+#   prof         rocprofv3 --kernel-trace --stats of bench.py --steps 2 (kernel table -> profiles via tools/prof_summary.py)
+#   pmc          GEMM/all-kernel HBM traffic: separate FETCH_SIZE and WRITE_SIZE passes over bench.py --grad-acc 2
+#   pmcx         extra counter sets over bench.py --grad-acc 1 (SQ busy/VALU/MFMA, TCC hit/miss/EA reads)
+#   configs      Llama-2-7B 1-GPU bench, TP=8 proxy, CP=8 proxy
+#   gloo2        bench.py --gpus 2 --backend gloo rehearsal (2 ranks on cuda:0)
+#   dp           bench.py --dp-bucket fp32 / bf16 vs plain (the per-GPU DP cost)
+#   attn         tools/attn_bench.py d64 and d128 (OLD=<lib> for an in-process A/B)
+#   pmcattn      attention PMC passes (ATTN_ARGS="--B 1 --S 4096 --H 32 --D 128" for d128)
+#   norm         tools/norm_bench.py (OLD=<lib> for an A/B)
+#   envab        whole-step A/B of two env settings: A="X=0" B="X=1" ROUNDS=3
+#   libab        whole-step A/B of library builds swapped in place: LIBS=a.so,b.so ROUNDS=2
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+T=$1; STEPS=$2; shift 2
+for kv in "$@"; do export "$kv"; done
+LIB=picotron_amd/lib/libpicotron_hip.so
+O=gpurun_out/$T
+
+jline() {  # print a bench JSON line's headline fields
+  python -c "import json,sys; d=json.load(open('$1')); r=d.get('roofline') or {}; print('$2', round(d['value']), round(d.get('ms_per_step', d.get('ms_per_microbatch', 0)),1), round(d.get('mfu', d.get('mfu_upper_bound', 0)) or 0,4), round(r.get('frac', 0) or 0,3))"
+}
+
+step_suite() {
+  timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 300 --timeout-method thread > $O.pytest.log 2>&1 || { echo pytest failed; grep -E "Error|FAILED|assert" $O.pytest.log | head -30; return 1; }
+  tail -1 $O.pytest.log
+  timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O.smoke.log 2>&1 || { echo smoke failed; tail $O.smoke.log; return 1; }
+  tail -1 $O.smoke.log
+}
+
+step_bench() {
+  for i in $(seq 1 ${BENCH_RUNS:-1}); do
+    timeout -k 10 300 python -u bench.py $BENCH_ARGS > $O.bench$i.json 2> $O.bench$i.err || { echo bench failed; tail $O.bench$i.err; return 1; }
+    jline $O.bench$i.json bench
+  done
+}
+
+step_prof() {
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O.prof -o k -- python -u bench.py --steps 2 --warmup 1 --cpu-tokens 0 > $O.prof.log 2>&1 || { echo prof failed; tail $O.prof.log; return 1; }
+  gzip -f $O.prof/k_kernel_trace.csv
+  python tools/prof_summary.py --trace $O.prof/k_kernel_trace.csv.gz --steps 3 > $O.kernels.md || true
+}
+
+step_pmc() {
+  timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O.pmc1 -o f -- python -u bench.py --steps 1 --warmup 0 --grad-acc 2 --cpu-tokens 0 --no-probe > $O.pmc1.log 2>&1 || { echo pmc1 failed; return 1; }
+  timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O.pmc2 -o w -- python -u bench.py --steps 1 --warmup 0 --grad-acc 2 --cpu-tokens 0 --no-probe > $O.pmc2.log 2>&1 || { echo pmc2 failed; return 1; }
+  python tools/traffic_summary.py $O.pmc1/f_counter_collection.csv $O.pmc2/w_counter_collection.csv $O.gemm_traffic.json
+}
+
+step_pmcx() {
+  local i=0
+  for C in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES" \
+           "SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE" \
+           "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" ${PMCX_EXTRA}; do
+    i=$((i+1))
+    timeout -s KILL 150 rocprofv3 --pmc $C --output-format csv -d $O.pmcx$i -o c -- python -u bench.py --steps 1 --warmup 0 --grad-acc 1 --cpu-tokens 0 --no-probe > $O.pmcx$i.log 2>&1 || { echo "pmcx $i failed"; tail -3 $O.pmcx$i.log; return 1; }
+  done
+}
+
+step_configs() {
+  timeout -k 10 400 python -u bench.py --model llama2-7b --grad-acc 8 --steps 2 --warmup 1 --cpu-tokens 0 > $O.llama.json 2> $O.llama.err || { echo llama failed; tail $O.llama.err; return 1; }
+  jline $O.llama.json llama2-7b
+  timeout -k 10 200 python -u bench.py --tp-proxy 8 --steps 3 > $O.tpproxy.json 2> $O.tpproxy.err || { echo tpproxy failed; tail $O.tpproxy.err; return 1; }
+  jline $O.tpproxy.json tp8-proxy
+  timeout -k 10 300 python -u bench.py --cp-proxy 8 --model llama2-7b --seq 32768 --mbs 1 --steps 3 $CP_ARGS > $O.cpproxy.json 2> $O.cpproxy.err || { echo cpproxy failed; tail $O.cpproxy.err; return 1; }
+  python -c "import json; d=json.load(open('$O.cpproxy.json')); print('cp8 proxy', round(d['value']), round(d['critical_rank_layer_ms'],2), round(d['roofline']['fwd_frac'],3), round(d['roofline']['bwd_frac'],3))"
+}
+
+step_gloo2() {
+  timeout -k 10 400 python -u bench.py --gpus 2 --backend gloo --steps 1 --warmup 1 --grad-acc 4 > $O.gloo2.json 2> $O.gloo2.err || { echo gloo2 failed; tail -20 $O.gloo2.err; return 1; }
+  [ $(wc -l < $O.gloo2.json) = 1 ] || { echo "gloo2: stdout is not one line"; return 1; }
+  python -c "import json; d=json.load(open('$O.gloo2.json')); print('gloo2', d['n_gpus'], d['ranks'], d['backend'], d['config']['parallelism'], round(d['value']))"
+}
+
+step_dp() {
+  for gt in fp32 bf16; do
+    timeout -k 10 300 python -u bench.py --dp-bucket --grad-type $gt --steps 3 --cpu-tokens 0 > $O.dp_$gt.json 2>/dev/null || { echo dp $gt failed; return 1; }
+    jline $O.dp_$gt.json dp-bucket-$gt
+  done
+  timeout -k 10 300 python -u bench.py --steps 3 --cpu-tokens 0 > $O.plain.json 2>/dev/null || { echo plain failed; return 1; }
+  jline $O.plain.json plain
+}
+
+step_attn() {
+  local old=${OLD:+--old $OLD}
+  timeout -k 10 200 python -u tools/attn_bench.py --rounds ${ROUNDS:-4} $old > $O.attn_d64.log 2>&1 || { echo attn d64 failed; tail -30 $O.attn_d64.log; return 1; }
+  cat $O.attn_d64.log
+  timeout -k 10 200 python -u tools/attn_bench.py --rounds ${ROUNDS:-4} --B 1 --S 4096 --D 128 $old > $O.attn_d128.log 2>&1 || { echo attn d128 failed; tail -30 $O.attn_d128.log; return 1; }
+  cat $O.attn_d128.log
+}
+
+step_pmcattn() {
+  local i=0
+  for C in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES" \
+           "SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE"; do
+    i=$((i+1))
+    timeout -s KILL 90 rocprofv3 --pmc $C --output-format csv --kernel-include-regex attn -d $O.pmca$i -o a -- python -u tools/attn_bench.py --reps 5 $ATTN_ARGS > $O.pmca$i.log 2>&1 || { echo "pmcattn $i failed"; tail -3 $O.pmca$i.log; return 1; }
+  done
+}
+
+step_norm() {
+  timeout -k 10 120 python -u tools/norm_bench.py ${OLD:+--old $OLD} > $O.norm.log 2>&1 || { echo norm failed; tail $O.norm.log; return 1; }
+  grep -v "^$" $O.norm.log | tail -8
+}
+
+step_envab() {
+  for i in $(seq 1 ${ROUNDS:-3}); do
+    for v in A B; do
+      if [ $v = A ]; then E=$A; else E=$B; fi
+      env $E timeout -k 10 300 python -u bench.py --cpu-tokens 0 --steps 3 $BENCH_ARGS > $O.$v$i.json 2>/dev/null || { echo "bench $E failed"; return 1; }
+      jline $O.$v$i.json "$E"
+    done
+  done
+}
+
+step_libab() {
+  IFS=, read -ra L <<< "$LIBS"
+  for f in "${L[@]}"; do [ -f "$f" ] || { echo "missing $f on the box"; return 1; }; done
+  [ $(md5sum "${L[@]}" | cut -d' ' -f1 | sort -u | wc -l) -eq ${#L[@]} ] || { echo "identical builds in $LIBS"; return 1; }
+  cp $LIB $O.orig.so
+  for i in $(seq 1 ${ROUNDS:-2}); do
+    for f in "${L[@]}"; do
+      cp "$f" $LIB || return 1
+      n=$(basename $f .so)
+      timeout -k 10 300 python -u bench.py --cpu-tokens 0 --steps 3 $BENCH_ARGS > $O.${n}_$i.json 2>/dev/null || { echo "bench $n failed"; cp $O.orig.so $LIB; return 1; }
+      jline $O.${n}_$i.json $n
+    done
+  done
+  cp $O.orig.so $LIB && rm -f $O.orig.so
+}
+
+IFS=, read -ra S <<< "$STEPS"
+for s in "${S[@]}"; do
+  echo "== $s"
+  step_$s || exit 1
+done
+find gpurun_out -name "*.db" -delete
+echo done
