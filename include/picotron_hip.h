@@ -177,7 +177,10 @@ int pt_gemm_ce_stats(const void* A, int64_t lda, const void* W, int64_t ldw, voi
                      int64_t block, int64_t M, int64_t N, int64_t K, hipStream_t stream);
 /* Grouped GEMM: nprob (<= 4) independent problems in ONE launch, each described like pt_gemm's
  * arguments, sharing layouts (a_kcontig, b_kcontig), epilogue and tile (-1 = auto over the
- * group).  Used where one problem alone would leave CUs idle (dW of q|k|v + dW of o_proj). */
+ * group).  Used where one problem alone would leave CUs idle (dW of q|k|v + dW of o_proj).
+ * ksplit > 1 (epilogue 2 only): the problem runs as ksplit K-slices of K / ksplit (a multiple of 64)
+ * whose f32 partials land kpart_stride elements apart from C (slice s at C + s kpart_stride) -- for
+ * the few-tile TP-shard GEMMs (24-128 tiles on 256 CUs); pt_gemm_splitk_reduce finishes them. */
 typedef struct {
   const void* A;
   int64_t lda;
@@ -193,6 +196,8 @@ typedef struct {
   int64_t M, N, K;
   const void* residual;
   int64_t ldr;
+  int ksplit;              /* 0 / 1: not split */
+  int64_t kpart_stride;    /* elements between two slices' f32 partials */
 } pt_gemm_problem;
 int pt_gemm_grouped(const pt_gemm_problem* probs, int nprob, int a_kcontig, int b_kcontig, int epilogue, int tile,
                     hipStream_t stream);
@@ -200,11 +205,12 @@ int pt_gemm_grouped(const pt_gemm_problem* probs, int nprob, int a_kcontig, int 
 /* Two independent groups in ONE launch of 256x256 tiles, each with its own layouts and epilogue:
  * group 0 = dX (A = dY [M, K] K-contiguous, B = W [K, N] N-contiguous; epilogue 0 or 6 = the
  * SwiGLU backward, residual = g|u), group 1 = wgrad (dY^T X; both operands MN-contiguous;
- * epilogue 0, 1 or 3).  The dX of a layer's projection beside its dW (both read only dY and saved
+ * epilogue 0, 1 or 3; or 2 with ksplit problems: a split-K dW's f32 slices, pt_gemm_splitk_reduce).  The dX of a layer's projection beside its dW (both read only dY and saved
  * activations): the down_proj dX's HBM-bound SwiGLU-backward tail overlaps the dW's MFMA work.
  * Group 0's epilogue: 0 (bf16), 6 (SwiGLU backward) or 2 (f32: the two K halves of a split-K dX,
  * finished by pt_gemm_splitk_sum).
- * order: 0 group 0 first, 1 group 1 first, inside each XCD's share.
+ * order: 0 group 0 first, 1 group 1 first, inside each XCD's share; 2 staggered (even XCDs group 0 first,
+ * odd XCDs group 1 first).
  * PT_EUNSUPPORTED when a problem does not tile by 256 x 256 or a group's tile count % 8 != 0. */
 int pt_gemm_dual(const pt_gemm_problem* p0, int n0, int a_kcontig0, int b_kcontig0, int epilogue0,
                  const pt_gemm_problem* p1, int n1, int a_kcontig1, int b_kcontig1, int epilogue1, int order,
@@ -215,6 +221,13 @@ int pt_gemm_dual(const pt_gemm_problem* p0, int n0, int a_kcontig0, int b_kconti
  * p0 / p1 16-byte, out / residual 8-byte aligned; residual may alias out. */
 int pt_gemm_splitk_sum(const float* p0, const float* p1, const void* residual, void* out, int64_t n,
                        hipStream_t stream);
+/* Split-K finish for nparts f32 partials [nparts][M][N] (ld N, part_stride >= M N elements apart):
+ * the sum in part order through `mode` = the GEMM epilogue it completes -- 0 bf16 store, 1 bf16
+ * accumulate, 2 f32 store, 3 f32 accumulate (main_grad), 4 bf16 residual (residual [M, N], ld ldr)
+ * -- into nc (<= 4) row segments of C (c_bounds, NULL = one), each with its own ld.  N % 4 == 0. */
+int pt_gemm_splitk_reduce(const float* parts, int nparts, int64_t part_stride, int64_t M, int64_t N, void* const* C,
+                          const int64_t* ldc, const int64_t* c_bounds, int nc, int mode, const void* residual,
+                          int64_t ldr, hipStream_t stream);
 
 /* ---- ring-attention merge ------------------------------------------------------------------
  * replaces picotron/context_parallel/context_parallel.py:157-187 update_out_and_lse (its non-first

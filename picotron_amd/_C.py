@@ -23,7 +23,8 @@ class GemmProblem(ctypes.Structure):
     """pt_gemm_problem (include/picotron_hip.h)."""
     _fields_ = [("A", _vp), ("lda", _i64), ("B", _vp * 4), ("ldb", _i64 * 4), ("b_bounds", _i64 * 5), ("nb", _i32),
                 ("b_seg_dim", _i32), ("C", _vp * 4), ("ldc", _i64 * 4), ("c_bounds", _i64 * 5), ("nc", _i32),
-                ("M", _i64), ("N", _i64), ("K", _i64), ("residual", _vp), ("ldr", _i64)]
+                ("M", _i64), ("N", _i64), ("K", _i64), ("residual", _vp), ("ldr", _i64), ("ksplit", _i32),
+                ("kpart_stride", _i64)]
 
 
 # name -> (restype, argtypes); mirrors include/picotron_hip.h one to one
@@ -32,6 +33,7 @@ SIGNATURES = {
     "pt_rmsnorm_bwd_partials": (_i32, [_i64, _i32]),
     "pt_gemm_grouped": (_i32, [ctypes.POINTER(GemmProblem), _i32, _i32, _i32, _i32, _i32, _vp]),
     "pt_gemm_splitk_sum": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp]),
+    "pt_gemm_splitk_reduce": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _i32, _i32, _vp, _i64, _vp]),
     "pt_gemm_dual": (_i32, [ctypes.POINTER(GemmProblem), _i32, _i32, _i32, _i32, ctypes.POINTER(GemmProblem), _i32,
                             _i32, _i32, _i32, _i32, _vp]),
     "pt_embedding_fwd": (_i32, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _i64, _vp]),

@@ -102,6 +102,10 @@ struct GemmArgs {
   int M, N, K;
   int tiles_m, tiles_n;
   int group_m;
+  // split-K: the launch computes ksplit K-slices of K / ksplit each (EPI_F32 only); slice s writes
+  // its f32 partial at C + s * kpart_stride (pt_gemm_splitk_reduce sums them into the real sink)
+  int ksplit;
+  int64_t kpart_stride;
 };
 
 // swizzles (chunk = 16 bytes); see tools/lds_swizzle_search.py
@@ -193,14 +197,19 @@ struct GemmGroup {
 // output (A and B panels shared through that XCD's L2): 8 for 256x256 tiles, 4 for 256x128
 // (32 tiles = 1024 x 1024 elements either way)
 // tile id pid_all (already in XCD order) of group g -> its problem and (tile_m, tile_n)
+// (split-K: the K-slice is the outermost index of a problem's tiles, so an XCD's consecutive tiles
+// share one slice's A / B panels)
 __device__ __forceinline__ const GemmArgs& select_problem_pid(const GemmGroup& g, int pid_all, int& tile_m,
-                                                              int& tile_n) {
+                                                              int& tile_n, int& kslice) {
   int pi = 0;
 #pragma unroll
   for (int i = 1; i < kMaxProb; ++i)
     if (i < g.nprob && pid_all >= g.start[i]) pi = i;
   const GemmArgs& a = g.p[pi];
-  const int pid = pid_all - g.start[pi];
+  int pid = pid_all - g.start[pi];
+  const int per_slice = a.tiles_m * a.tiles_n;
+  kslice = a.ksplit > 1 ? pid / per_slice : 0;
+  pid -= kslice * per_slice;
   const int GROUP = a.group_m;
   const int group_span = GROUP * a.tiles_n;
   const int gid = pid / group_span;
@@ -211,11 +220,15 @@ __device__ __forceinline__ const GemmArgs& select_problem_pid(const GemmGroup& g
   return a;
 }
 
-__device__ __forceinline__ const GemmArgs& select_problem(const GemmGroup& g, int& tile_m, int& tile_n,
+__device__ __forceinline__ const GemmArgs& select_problem(const GemmGroup& g, int& tile_m, int& tile_n, int& kslice,
                                                           int bid = -1, int nwg = -1) {
   const int pid_all = bid < 0 ? xcd_remap(blockIdx.x, gridDim.x) : xcd_remap(bid, nwg);
-  return select_problem_pid(g, pid_all, tile_m, tile_n);
+  return select_problem_pid(g, pid_all, tile_m, tile_n, kslice);
 }
+
+// K range of split-K slice ks: first element, and the slice's K-tile count
+__device__ __forceinline__ int kslice_begin(const GemmArgs& a, int ks) { return a.ksplit > 1 ? ks * (a.K / a.ksplit) : 0; }
+__device__ __forceinline__ int kslice_tiles(const GemmArgs& a) { return (a.ksplit > 1 ? a.K / a.ksplit : a.K) / BK; }
 
 // Write the wave's TM x TN accumulator tile (FM x FN 16x16 fragments) at output (m0 + wm*TM,
 // n0 + wn*TN).  `st` is this wave's private LDS staging area (TM * (2*TN + 16) bytes).
@@ -369,7 +382,8 @@ __device__ __forceinline__ void f32_acc_tail(const f32x4_t (&acc)[TM / 16][TN / 
 
 template <int TM, int TN, int EPI>
 __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)[TM / 16][TN / 16], lds_u8* st,
-                                         int m0, int n0, int wm, int wn, int lane, float2* xs_wave = nullptr) {
+                                         int m0, int n0, int wm, int wn, int lane, float2* xs_wave = nullptr,
+                                         int64_t c_off = 0) {
   constexpr int FM = TM / 16, FN = TN / 16;
   const int cs = find_seg(a.cseg, a.ncseg, m0);
   const int64_t ldc = a.ldc[cs];
@@ -499,7 +513,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
       }
     }
   } else {
-    float* C = (float*)a.C[cs];
+    float* C = (float*)a.C[cs] + c_off;   // c_off: this split-K slice's partial (EPI_F32)
     if constexpr (EPI == EPI_F32_ACC && TN == 64) {
       f32_acc_tail<TM, TN>(acc, st, mrow0, ncol0, ldc, C, lane);
       return;
@@ -690,7 +704,7 @@ __device__ __forceinline__ void glds16_asm(const uint16_t* base, uint32_t voff_e
 
 // one 256x256 output tile (tile_m, tile_n) of problem `a` by the whole 512-thread workgroup
 template <bool AK, bool BKC, int EPI>
-__device__ __forceinline__ void gemm_8ph_tile(const GemmArgs& a, const int tile_m, const int tile_n) {
+__device__ __forceinline__ void gemm_8ph_tile(const GemmArgs& a, const int tile_m, const int tile_n, const int ks = 0) {
   constexpr int TM = 128, TN = 64, FM = 8, FN = 4;
   constexpr int HALF = 128 * BK * 2;          // 16 KiB
   constexpr int BUF = 4 * HALF;               // At, Bl, Br, Ab
@@ -723,12 +737,13 @@ __device__ __forceinline__ void gemm_8ph_tile(const GemmArgs& a, const int tile_
       vB[1][it] = himg_voff<BKC, 32>(i, lane, ldb, 32);
     }
   }
-  const uint16_t* Ab0 = AK ? a.A + (int64_t)m0 * lda : a.A + m0;
+  const int kb = kslice_begin(a, ks);        // this split-K slice's first k (0 unsplit)
+  const uint16_t* Ab0 = AK ? a.A + (int64_t)m0 * lda + kb : a.A + m0 + (int64_t)kb * lda;
   auto a_ptr = [&](int t) { return AK ? Ab0 + t * BK : Ab0 + (int64_t)t * BK * lda; };
-  auto b_ptr = [&](int t) { return bimg_ptr(bi, BKC, t * BK); };
+  auto b_ptr = [&](int t) { return bimg_ptr(bi, BKC, kb + t * BK); };
   // paired: rows tile_n * 128 .. +127 of W_gate (Bl) and W_up (Br), K-contiguous
   auto pair_ptr = [&](int t, int which) {
-    return (which ? pairB1 : pairB0) + (int64_t)tile_n * 128 * ldb + t * BK;
+    return (which ? pairB1 : pairB0) + (int64_t)tile_n * 128 * ldb + kb + t * BK;
   };
   // half image h (0 At, 1 Bl, 2 Br, 3 Ab) of K-tile t into buffer buf
   auto stage = [&](int t, int buf, int h) {
@@ -749,7 +764,7 @@ __device__ __forceinline__ void gemm_8ph_tile(const GemmArgs& a, const int tile_
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = a.K / BK;
+  const int nk = kslice_tiles(a);
   stage(0, 0, 0); stage(0, 0, 1); stage(0, 0, 2); stage(0, 0, 3);
   if (nk > 1) {
     stage(1, 1, 0); stage(1, 1, 1); stage(1, 1, 2);
@@ -845,7 +860,8 @@ __device__ __forceinline__ void gemm_8ph_tile(const GemmArgs& a, const int tile_
   } else {
     // EPI_CE_STATS: per-wave row statistics beside the 8 staging areas (launch_8ph sizes the LDS)
     float2* xs = (float2*)(smem + 8 * (TM * (TN * 2 + 16)));
-    epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane, xs + wave * TM);
+    epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane, xs + wave * TM,
+                          (int64_t)ks * a.kpart_stride);
     if constexpr (EPI == EPI_CE_STATS) {
       __syncthreads();
       if (wn == 0) ce_stats_merge<4, TM, TN>(a, xs, m0, n0, wm, lane);
@@ -855,9 +871,9 @@ __device__ __forceinline__ void gemm_8ph_tile(const GemmArgs& a, const int tile_
 
 template <bool AK, bool BKC, int EPI>
 __global__ __launch_bounds__(512) void gemm_8ph_kernel(const GemmGroup g) {
-  int tile_m, tile_n;
-  const GemmArgs& a = select_problem(g, tile_m, tile_n);
-  gemm_8ph_tile<AK, BKC, EPI>(a, tile_m, tile_n);
+  int tile_m, tile_n, ks;
+  const GemmArgs& a = select_problem(g, tile_m, tile_n, ks);
+  gemm_8ph_tile<AK, BKC, EPI>(a, tile_m, tile_n, ks);
 }
 
 // ---------------------------------------------------------------------------- dual launch
@@ -875,11 +891,16 @@ struct DualMap {
   int n0, n1, order;
 };
 
+// order 2 (staggered): even XCDs run their group-0 tiles first, odd XCDs their group-1 tiles first,
+// so the dX tiles' HBM-bound SwiGLU-backward tails of half the chip overlap the other half's dW
+// main loops instead of all 256 CUs reaching them together (each XCD still works on one GEMM at a
+// time: its L2 grouping is kept)
 __device__ __forceinline__ int dual_select(const DualMap& m, int& pid) {
   const int bid = blockIdx.x, xcd = bid & 7, li = bid >> 3;
-  const int nfirst = m.order == 0 ? m.n0 : m.n1;
+  const int ord = m.order == 2 ? (xcd & 1) : m.order;
+  const int nfirst = ord == 0 ? m.n0 : m.n1;
   const bool first = li < nfirst;
-  const int which = (m.order == 0) ? !first : first;
+  const int which = (ord == 0) ? !first : first;
   const int local = first ? li : li - nfirst;
   pid = xcd * (which ? m.n1 : m.n0) + local;
   return which;
@@ -887,13 +908,13 @@ __device__ __forceinline__ int dual_select(const DualMap& m, int& pid) {
 
 template <bool AK0, bool BKC0, int EPI0, bool AK1, bool BKC1, int EPI1>
 __global__ __launch_bounds__(512) void gemm_8ph_dual_kernel(const GemmGroup g0, const GemmGroup g1, const DualMap m) {
-  int pid, tile_m, tile_n;
+  int pid, tile_m, tile_n, ks;
   if (dual_select(m, pid) == 0) {
-    const GemmArgs& a = select_problem_pid(g0, pid, tile_m, tile_n);
-    gemm_8ph_tile<AK0, BKC0, EPI0>(a, tile_m, tile_n);
+    const GemmArgs& a = select_problem_pid(g0, pid, tile_m, tile_n, ks);
+    gemm_8ph_tile<AK0, BKC0, EPI0>(a, tile_m, tile_n, ks);
   } else {
-    const GemmArgs& a = select_problem_pid(g1, pid, tile_m, tile_n);
-    gemm_8ph_tile<AK1, BKC1, EPI1>(a, tile_m, tile_n);
+    const GemmArgs& a = select_problem_pid(g1, pid, tile_m, tile_n, ks);
+    gemm_8ph_tile<AK1, BKC1, EPI1>(a, tile_m, tile_n, ks);
   }
 }
 
@@ -911,7 +932,7 @@ __global__ __launch_bounds__(512) void gemm_8ph_dual_kernel(const GemmGroup g0, 
 // (At in phase 1, B and Ab in phase 2), and the one wait per K-tile (phase 2, vmcnt(6)) retires
 // K-tile t+1 with t+2 in flight -- every DMA has >= 1.5 K-tiles to land.
 template <bool AK, bool BKC, int EPI>
-__device__ __forceinline__ void gemm_4ph_tile(const GemmArgs& a, const int tile_m, const int tile_n) {
+__device__ __forceinline__ void gemm_4ph_tile(const GemmArgs& a, const int tile_m, const int tile_n, const int ks = 0) {
   constexpr int TM = 64, TN = 64, FM = 4, FN = 4;
   constexpr int IMG = 128 * BK * 2;           // 16 KiB
   constexpr int BUF = 3 * IMG;                // At, B, Ab
@@ -933,9 +954,10 @@ __device__ __forceinline__ void gemm_4ph_tile(const GemmArgs& a, const int tile_
     vA[1][it] = himg_voff<AK, 32>(i, lane, lda, 32);
     vB[it] = himg_voff<BKC, 128>(i, lane, ldb, 0);
   }
-  const uint16_t* Ab0 = AK ? a.A + (int64_t)m0 * lda : a.A + m0;
+  const int kb = kslice_begin(a, ks);
+  const uint16_t* Ab0 = AK ? a.A + (int64_t)m0 * lda + kb : a.A + m0 + (int64_t)kb * lda;
   auto a_ptr = [&](int t) { return AK ? Ab0 + t * BK : Ab0 + (int64_t)t * BK * lda; };
-  auto b_ptr = [&](int t) { return bimg_ptr(bi, BKC, t * BK); };
+  auto b_ptr = [&](int t) { return bimg_ptr(bi, BKC, kb + t * BK); };
   // image h (0 At, 1 B, 2 Ab) of K-tile t into buffer buf
   // DMA instruction `it` (of 2 per wave) of image h (0 At, 1 B, 2 Ab) of K-tile t into buffer buf
   auto stage1 = [&](int t, int buf, int h, int it) {
@@ -955,7 +977,7 @@ __device__ __forceinline__ void gemm_4ph_tile(const GemmArgs& a, const int tile_
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = a.K / BK;
+  const int nk = kslice_tiles(a);
   stage(0, 0, 0); stage(0, 0, 1); stage(0, 0, 2);
   if (nk > 1) {
     stage(1, 1, 0); stage(1, 1, 1); stage(1, 1, 2);
@@ -1035,7 +1057,8 @@ __device__ __forceinline__ void gemm_4ph_tile(const GemmArgs& a, const int tile_
   if (!late) bar();
   __syncthreads();
   float2* xs = (float2*)(smem + 8 * (TM * (TN * 2 + 16)));  // EPI_CE_STATS row statistics
-  epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane, xs + wave * TM);
+  epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane, xs + wave * TM,
+                        (int64_t)ks * a.kpart_stride);
   if constexpr (EPI == EPI_CE_STATS) {
     __syncthreads();
     if (wn == 0) ce_stats_merge<2, TM, TN>(a, xs, m0, n0, wm, lane);
@@ -1044,9 +1067,9 @@ __device__ __forceinline__ void gemm_4ph_tile(const GemmArgs& a, const int tile_
 
 template <bool AK, bool BKC, int EPI>
 __global__ __launch_bounds__(512) void gemm_4ph_kernel(const GemmGroup g) {
-  int tile_m, tile_n;
-  const GemmArgs& a = select_problem(g, tile_m, tile_n);
-  gemm_4ph_tile<AK, BKC, EPI>(a, tile_m, tile_n);
+  int tile_m, tile_n, ks;
+  const GemmArgs& a = select_problem(g, tile_m, tile_n, ks);
+  gemm_4ph_tile<AK, BKC, EPI>(a, tile_m, tile_n, ks);
 }
 
 // ------------------------------------------------------------------- mixed-tile launch (q|k|v)
@@ -1094,10 +1117,11 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const GemmGroup g) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  int tile_m, tile_n;
-  const GemmArgs& a = select_problem(g, tile_m, tile_n);
+  int tile_m, tile_n, ks;
+  const GemmArgs& a = select_problem(g, tile_m, tile_n, ks);
   const int m0 = tile_m * BM, n0 = tile_n * BN;
-  const uint16_t* Abase = AK ? a.A + (int64_t)m0 * a.lda : a.A + m0;
+  const int kb = kslice_begin(a, ks);
+  const uint16_t* Abase = AK ? a.A + (int64_t)m0 * a.lda + kb : a.A + m0 + (int64_t)kb * a.lda;
 
   f32x4_t acc[FM][FN];
 #pragma unroll
@@ -1113,10 +1137,10 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const GemmGroup g) {
     lds_u8* sb = sa + A_BYTES;
     const uint16_t* ga = AK ? Abase + k0 : Abase + (int64_t)k0 * lda;
     stage_tile<BM, AK, NT>(ga, lda, sa, tid);
-    stage_tile<BN, BKC, NT>(bimg_ptr(bi, BKC, k0), bi.ld, sb, tid);
+    stage_tile<BN, BKC, NT>(bimg_ptr(bi, BKC, kb + k0), bi.ld, sb, tid);
   };
 
-  const int nk = a.K / BK;
+  const int nk = kslice_tiles(a);
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1170,7 +1194,8 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const GemmGroup g) {
       __builtin_amdgcn_s_barrier();
     }
   }
-  epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane);
+  epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane, nullptr,
+                        (int64_t)ks * a.kpart_stride);
 }
 
 // ================================================================================== launch
@@ -1198,7 +1223,7 @@ inline int group_tiles(GemmGroup& g, int bm, int bn) {
     g.p[i].tiles_n = g.p[i].N / bn;
     g.p[i].group_m = gm;
     g.start[i] = n;
-    n += g.p[i].tiles_m * g.p[i].tiles_n;
+    n += g.p[i].tiles_m * g.p[i].tiles_n * (g.p[i].ksplit > 1 ? g.p[i].ksplit : 1);
   }
   for (int i = g.nprob; i <= kMaxProb; ++i) g.start[i] = n;
   return n;
@@ -1240,7 +1265,7 @@ int launch_8ph(GemmGroup g, hipStream_t stream) {
 
 template <bool AK0, bool BKC0, int EPI0, bool AK1, bool BKC1, int EPI1>
 int launch_dual_t(GemmGroup g0, GemmGroup g1, int order, hipStream_t stream) {
-  const int t0 = group_tiles(g0, 256, 256), t1 = group_tiles(g1, 256, 256);
+  const int t0 = group_tiles(g0, 256, 256), t1 = group_tiles(g1, 256, 256);  // (x ksplit)
   if (t0 % 8 || t1 % 8) return PT_EUNSUPPORTED;  // equal per-XCD shares of both groups
   const DualMap m{t0 / 8, t1 / 8, order};
   constexpr int smem = 8 * 128 * (64 * 2 + 16);  // epilogue staging (> the 128 KiB main loop)
@@ -1310,6 +1335,20 @@ int launch_epi(const GemmGroup& a, int a_kcontig, int b_kcontig, int tile, hipSt
 }  // namespace
 
 namespace {
+
+// split-K fields of a grouped problem: ksplit slices of K / ksplit (a multiple of BK) written as f32
+// partials kpart_stride elements apart (EPI_F32 only).
+int fill_split(GemmArgs& a, const pt_gemm_problem& q, int epilogue) {
+  a.ksplit = q.ksplit > 1 ? q.ksplit : 1;
+  a.kpart_stride = q.kpart_stride;
+  if (a.ksplit == 1) return PT_OK;
+  if (epilogue != EPI_F32 || q.kpart_stride <= 0 || a.ksplit > 64) return PT_EINVAL;
+  if (a.K % (a.ksplit * BK)) return PT_EUNSUPPORTED;
+  if (a.bdim == 1)  // a K-tile never straddles a K-segment boundary (segments are BK multiples)
+    for (int i = 0; i <= a.nbseg; ++i)
+      if (a.bseg[i] % BK) return PT_EUNSUPPORTED;
+  return PT_OK;
+}
 
 // Validate one problem and fill its kernel arguments.  Returns PT_OK or a PT_E* code.
 int fill_args(GemmArgs& a, const void* A, int64_t lda, const void* const* B, const int64_t* ldb,
@@ -1412,7 +1451,8 @@ int pick_group_tile(const GemmGroup& g) {
   };
   auto ntiles = [&](int t) {
     int64_t tiles = 0;
-    for (int i = 0; i < g.nprob; ++i) tiles += (int64_t)(g.p[i].M / kTileBM[t]) * (g.p[i].N / kTileBN[t]);
+    for (int i = 0; i < g.nprob; ++i)
+      tiles += (int64_t)(g.p[i].M / kTileBM[t]) * (g.p[i].N / kTileBN[t]) * (g.p[i].ksplit > 1 ? g.p[i].ksplit : 1);
     return tiles;
   };
   auto fill = [&](int t) {
@@ -1539,13 +1579,14 @@ int launch_dual_e1(GemmGroup& g0, GemmGroup& g1, int e1, int order, hipStream_t 
     case EPI_BF16: return launch_dual_t<true, false, EPI0, false, false, EPI_BF16>(g0, g1, order, s);
     case EPI_BF16_ACC: return launch_dual_t<true, false, EPI0, false, false, EPI_BF16_ACC>(g0, g1, order, s);
     case EPI_F32_ACC: return launch_dual_t<true, false, EPI0, false, false, EPI_F32_ACC>(g0, g1, order, s);
+    case EPI_F32: return launch_dual_t<true, false, EPI0, false, false, EPI_F32>(g0, g1, order, s);  // split-K dW
     default: return PT_EUNSUPPORTED;
   }
 }
 
 int launch_dual(GemmGroup& g0, int ak0, int bk0, int e0, GemmGroup& g1, int ak1, int bk1, int e1, int order,
                 hipStream_t s) {
-  if (!ak0 || bk0 || ak1 || bk1 || order < 0 || order > 1) return PT_EUNSUPPORTED;
+  if (!ak0 || bk0 || ak1 || bk1 || order < 0 || order > 2) return PT_EUNSUPPORTED;
   for (int i = 0; i < g0.nprob; ++i) {
     if (!args_fit(g0.p[i], 12)) return PT_EUNSUPPORTED;
     if (e0 == EPI_SWIGLU_BWD && (g0.p[i].ncseg != 1 || g0.p[i].bdim != 0 || g0.p[i].nbseg != 1)) return PT_EUNSUPPORTED;
@@ -1587,11 +1628,113 @@ int pt_gemm_grouped(const pt_gemm_problem* probs, int nprob, int a_kcontig, int 
   g.nprob = nprob;
   for (int i = 0; i < nprob; ++i) {
     const pt_gemm_problem& q = probs[i];
-    const int rc = fill_args(g.p[i], q.A, q.lda, q.B, q.ldb, q.b_bounds, q.nb, q.b_seg_dim, q.C, q.ldc, q.c_bounds,
-                             q.nc, q.M, q.N, q.K, epilogue, q.residual, q.ldr);
+    int rc = fill_args(g.p[i], q.A, q.lda, q.B, q.ldb, q.b_bounds, q.nb, q.b_seg_dim, q.C, q.ldc, q.c_bounds,
+                       q.nc, q.M, q.N, q.K, epilogue, q.residual, q.ldr);
+    if (!rc) rc = fill_split(g.p[i], q, epilogue);
     if (rc) return rc;
   }
   return launch_group(g, a_kcontig, b_kcontig, epilogue, tile, stream);
+}
+
+}  // extern "C"
+
+namespace {
+
+// Split-K finish for nparts f32 partials [nparts][M][N] (ld N, part stride M N): out = the sum in
+// part order (deterministic), through the sink's epilogue -- 0 bf16 store, 1 bf16 accumulate
+// (bf16(C + bf16(sum)), the wgrad's .grad accumulation), 2 f32 store, 3 f32 accumulate (main_grad),
+// 4 bf16 residual (bf16(R + bf16(sum))) -- into up to 4 row segments of C (c_bounds), each with its
+// own pointer and leading dimension.  4 columns per thread-iteration (16-B partial loads).
+struct ReduceArgs {
+  const float* parts;
+  int nparts;
+  int64_t M, N, part_stride;
+  void* C[4];
+  int64_t ldc[4];
+  int64_t cseg[5];
+  int nc;
+  const uint16_t* R;
+  int64_t ldr;
+};
+
+template <int MODE>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const ReduceArgs r) {
+  const int64_t n4 = r.N / 4, total = r.M * n4;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t row = i / n4, c4 = i - row * n4;
+    const float* p = r.parts + row * r.N + c4 * 4;
+    float4 acc = *(const float4*)p;
+    for (int k = 1; k < r.nparts; ++k) {
+      const float4 v = *(const float4*)(p + k * r.part_stride);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    int seg = 0;
+#pragma unroll
+    for (int j = 1; j < 4; ++j)
+      if (j < r.nc && row >= r.cseg[j]) seg = j;
+    const int64_t off = (row - r.cseg[seg]) * r.ldc[seg] + c4 * 4;
+    const float v[4] = {acc.x, acc.y, acc.z, acc.w};
+    if (MODE == EPI_F32 || MODE == EPI_F32_ACC) {
+      float4* o = (float4*)((float*)r.C[seg] + off);
+      float4 w = make_float4(v[0], v[1], v[2], v[3]);
+      if (MODE == EPI_F32_ACC) {
+        const float4 old = *o;
+        w.x += old.x; w.y += old.y; w.z += old.z; w.w += old.w;
+      }
+      *o = w;
+    } else {
+      uint2* o = (uint2*)((uint16_t*)r.C[seg] + off);
+      float f[4] = {v[0], v[1], v[2], v[3]};
+      if (MODE == EPI_BF16_ACC || MODE == EPI_BF16_RES) {
+        const uint2 old = MODE == EPI_BF16_ACC ? *o : *(const uint2*)(r.R + row * r.ldr + c4 * 4);
+        const float of[4] = {lo_bf(old.x), hi_bf(old.x), lo_bf(old.y), hi_bf(old.y)};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) f[e] = of[e] + round_bf(f[e]);
+      }
+      uint2 w;
+      w.x = pack_bf2(f[0], f[1]);
+      w.y = pack_bf2(f[2], f[3]);
+      *o = w;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int pt_gemm_splitk_reduce(const float* parts, int nparts, int64_t part_stride, int64_t M, int64_t N, void* const* C,
+                          const int64_t* ldc, const int64_t* c_bounds, int nc, int mode, const void* residual,
+                          int64_t ldr, hipStream_t stream) {
+  if (!parts || nparts < 1 || M <= 0 || N <= 0 || (N & 3) || !C || nc < 1 || nc > 4) return PT_EINVAL;
+  if (part_stride < M * N || !pt_aligned16(parts) || (part_stride & 3)) return PT_EALIGN;
+  if (mode == EPI_BF16_RES && (!residual || ((uintptr_t)residual & 7) || (ldr & 3))) return PT_EINVAL;
+  ReduceArgs r{};
+  r.parts = parts; r.nparts = nparts; r.M = M; r.N = N; r.part_stride = part_stride;
+  r.nc = nc;
+  for (int i = 0; i <= nc; ++i) r.cseg[i] = c_bounds ? c_bounds[i] : (i == 0 ? 0 : M);
+  if (r.cseg[0] != 0 || r.cseg[nc] != M) return PT_EINVAL;
+  const int esz = (mode == EPI_F32 || mode == EPI_F32_ACC) ? 4 : 2;
+  for (int i = 0; i < nc; ++i) {
+    if (!C[i] || ((uintptr_t)C[i] & (esz * 4 - 1)) || (ldc[i] & 3)) return PT_EALIGN;
+    r.C[i] = C[i];
+    r.ldc[i] = ldc[i];
+  }
+  r.R = (const uint16_t*)residual;
+  r.ldr = ldr;
+  const int64_t total = M * (N / 4);
+  int64_t grid = (total + 255) / 256;
+  if (grid > PT_STREAM_GRID_CAP) grid = PT_STREAM_GRID_CAP;
+  switch (mode) {
+    case EPI_BF16: splitk_reduce_kernel<EPI_BF16><<<(int)grid, 256, 0, stream>>>(r); break;
+    case EPI_BF16_ACC: splitk_reduce_kernel<EPI_BF16_ACC><<<(int)grid, 256, 0, stream>>>(r); break;
+    case EPI_F32: splitk_reduce_kernel<EPI_F32><<<(int)grid, 256, 0, stream>>>(r); break;
+    case EPI_F32_ACC: splitk_reduce_kernel<EPI_F32_ACC><<<(int)grid, 256, 0, stream>>>(r); break;
+    case EPI_BF16_RES: splitk_reduce_kernel<EPI_BF16_RES><<<(int)grid, 256, 0, stream>>>(r); break;
+    default: return PT_EINVAL;
+  }
+  PT_CHECK_LAUNCH();
+  return PT_OK;
 }
 
 // Split-K finish: out = bf16(p0 + p1), 4 elements per thread-iteration (16-B loads, 8-B store).
@@ -1644,8 +1787,9 @@ int pt_gemm_dual(const pt_gemm_problem* p0, int n0, int a_kcontig0, int b_kconti
     g[k].nprob = ns[k];
     for (int i = 0; i < ns[k]; ++i) {
       const pt_gemm_problem& q = ps[k][i];
-      const int rc = fill_args(g[k].p[i], q.A, q.lda, q.B, q.ldb, q.b_bounds, q.nb, q.b_seg_dim, q.C, q.ldc,
-                               q.c_bounds, q.nc, q.M, q.N, q.K, es[k], q.residual, q.ldr);
+      int rc = fill_args(g[k].p[i], q.A, q.lda, q.B, q.ldb, q.b_bounds, q.nb, q.b_seg_dim, q.C, q.ldc,
+                         q.c_bounds, q.nc, q.M, q.N, q.K, es[k], q.residual, q.ldr);
+      if (!rc) rc = fill_split(g[k].p[i], q, es[k]);
       if (rc) return rc;
     }
   }

@@ -464,9 +464,78 @@ def _problem(A, lda, Bs, ldbs, b_bounds, b_seg_dim, Cs, ldcs, c_bounds, M, N, K)
     return pr
 
 
+def _ksplit_enabled():
+    return os.environ.get("PICOTRON_KSPLIT", "1") != "0"
+
+
+def wgrad_ksplit(mnks, extra_tiles=0):
+    """K-slices for a group of wgrad problems [(M, N, K)] (K = the token count) that leaves CUs idle:
+    the TP-shard weight gradients (TP = 8 at SmolLM-1.7B: q|k|v dW 24 + o_proj dW 8 tiles of 256x256,
+    down_proj dW 32, gate|up dW 64, on 256 CUs) run as ksplit slices of K / ksplit -- the largest
+    power of two keeping every slice >= 512 deep and the launch within one round of the 256 CUs
+    (2 ... 16) -- into f32 partials that pt_gemm_splitk_reduce sums into the sink.  1 = unsplit:
+    shapes that already fill half the CUs, or do not tile by 256.  extra_tiles: tiles of other
+    problems sharing the launch (a dual launch's dX), counted in the round."""
+    if not _ksplit_enabled() or any(m % 256 or n % 256 for m, n, _ in mnks):
+        return 1
+    tiles = sum((m // 256) * (n // 256) for m, n, _ in mnks)
+    if tiles >= 128:
+        return 1
+    s = 1
+    while s < 16 and tiles * s * 2 + extra_tiles <= 256 and \
+            all(k % (s * 2 * 64) == 0 and k // (s * 2) >= 512 for _, _, k in mnks):
+        s *= 2
+    return s
+
+
+def _wgrad_ksplit_run(jobs, epilogue, s):
+    """The wgrad jobs [(dy2d, x2d, outs)] as s-way split-K problems of ONE grouped launch (f32
+    partials in one workspace), then one reduce pass per job into its outs through `epilogue`."""
+    dev = jobs[0][0].device
+    sizes = [dy.shape[1] * x.shape[1] for dy, x, _ in jobs]
+    ws = torch.empty(s * sum(sizes), dtype=torch.float32, device=dev)
+    probs = (_C.GemmProblem * len(jobs))()
+    flops = nbytes = 0.0
+    base = 0
+    views = []
+    for j, (dy2d, x2d, outs) in enumerate(jobs):
+        T, N = dy2d.shape
+        Kin = x2d.shape[1]
+        part = ws[base:base + s * N * Kin]
+        views.append(part)
+        pr = _problem(dy2d, dy2d.stride(0), [x2d], [x2d.stride(0)], [0, Kin], 0, [part], [Kin], [0, N], N, Kin, T)
+        pr.ksplit, pr.kpart_stride = s, N * Kin
+        probs[j] = pr
+        base += s * N * Kin
+        flops += 2.0 * N * Kin * T
+        nbytes += _alg_bytes(N, Kin, T, epilogue)
+    probe = _PROBE
+    if probe is not None:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    stream = _C.stream_ptr(dev)
+    rc = _C.lib().pt_gemm_grouped(probs, len(jobs), 0, 0, EPI_F32, -1, stream)
+    _C.check(rc, f"pt_gemm_grouped({len(jobs)} problems, split-K {s})")
+    for (dy2d, x2d, outs), part in zip(jobs, views):
+        N, Kin = dy2d.shape[1], x2d.shape[1]
+        ns = [o.shape[0] for o in outs]
+        rc = _C.lib().pt_gemm_splitk_reduce(_ptr(part), s, N * Kin, N, Kin, _C.ptrarr([_ptr(o) for o in outs]),
+                                            _C.i64arr([o.stride(0) for o in outs]), _C.i64arr(_bounds(ns)), len(outs),
+                                            int(epilogue), None, 0, stream)
+        _C.check(rc, "pt_gemm_splitk_reduce")
+    if probe is not None:
+        ev1.record()
+        probe.records.append((ev0, ev1, flops, nbytes))
+
+
 def linear_wgrad_grouped(jobs, epilogue=EPI_BF16, tile=-1):
     """Several wgrad GEMMs (dW_i = dY_i^T X for each job (dy2d, x2d, outs)) in ONE launch
-    (pt_gemm_grouped): e.g. dW of q|k|v (192 tiles) + dW of o_proj (64 tiles) fill 256 CUs."""
+    (pt_gemm_grouped): e.g. dW of q|k|v (192 tiles) + dW of o_proj (64 tiles) fill 256 CUs.  A group
+    that would leave most CUs idle (TP shards) runs split-K (wgrad_ksplit)."""
+    if tile < 0 and epilogue in (EPI_BF16, EPI_BF16_ACC, EPI_F32_ACC):
+        s = wgrad_ksplit([(dy.shape[1], x.shape[1], dy.shape[0]) for dy, x, _ in jobs])
+        if s > 1 and all(o.stride(1) == 1 and o.stride(0) % 4 == 0 for _, _, outs in jobs for o in outs):
+            return _wgrad_ksplit_run(jobs, epilogue, s)
     probs = (_C.GemmProblem * len(jobs))()
     flops = nbytes = 0.0
     for j, (dy2d, x2d, outs) in enumerate(jobs):
@@ -803,6 +872,11 @@ def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None):
     if e0 != EPI_F32:
         p0s = (_C.GemmProblem * 1)(p0)
     p1s = (_C.GemmProblem * len(wjobs))()
+    # the TP shards' few-tile dW as split-K slices beside the dX tiles (f32 partials, reduced below)
+    dx_tiles = sum(p.M // 256 * (p.N // 256) for p in p0s)
+    ws = wgrad_ksplit([(dy.shape[1], x.shape[1], dy.shape[0]) for dy, x, _ in wjobs], extra_tiles=dx_tiles) \
+        if wepilogue in (EPI_BF16, EPI_BF16_ACC, EPI_F32_ACC) else 1
+    wparts = []
     for j, (wdy, x2d, outs) in enumerate(wjobs):
         _bf16_rowmajor(wdy, "dy")
         _bf16_rowmajor(x2d, "x")
@@ -810,19 +884,33 @@ def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None):
         Kin = x2d.shape[1]
         ns = [o.shape[0] for o in outs]
         _req(sum(ns) == Nw and x2d.shape[0] == Tw, "wgrad: output rows must cover dY's width")
-        p1s[j] = _problem(wdy, wdy.stride(0), [x2d], [x2d.stride(0)], [0, Kin], 0, outs, [o.stride(0) for o in outs],
-                          _bounds(ns), Nw, Kin, Tw)
+        if ws > 1:
+            part = torch.empty(ws * Nw * Kin, dtype=torch.float32, device=dy2d.device)
+            wparts.append(part)
+            p1s[j] = _problem(wdy, wdy.stride(0), [x2d], [x2d.stride(0)], [0, Kin], 0, [part], [Kin], [0, Nw], Nw,
+                              Kin, Tw)
+            p1s[j].ksplit, p1s[j].kpart_stride = ws, Nw * Kin
+        else:
+            p1s[j] = _problem(wdy, wdy.stride(0), [x2d], [x2d.stride(0)], [0, Kin], 0, outs,
+                              [o.stride(0) for o in outs], _bounds(ns), Nw, Kin, Tw)
         flops += 2.0 * Nw * Kin * Tw
         nbytes += _alg_bytes(Nw, Kin, Tw, wepilogue)
     probe = _PROBE
     if probe is not None:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
-    rc = _C.lib().pt_gemm_dual(p0s, len(p0s), 1, 0, e0, p1s, len(wjobs), 0, 0, int(wepilogue),
+    rc = _C.lib().pt_gemm_dual(p0s, len(p0s), 1, 0, e0, p1s, len(wjobs), 0, 0, EPI_F32 if ws > 1 else int(wepilogue),
                                _dual_order() if order is None else int(order), _C.stream_ptr(dy2d.device))
     if rc == -3:   # PT_EUNSUPPORTED: outside the dual tiling (e.g. C segments not on 256 rows)
         return None
-    _C.check(rc, f"pt_gemm_dual(dX epi {e0}, {len(wjobs)} wgrads epi {wepilogue})")
+    _C.check(rc, f"pt_gemm_dual(dX epi {e0}, {len(wjobs)} wgrads epi {wepilogue}, split {ws})")
+    for (wdy, x2d, outs), part in zip(wjobs, wparts):
+        Nw, Kin = wdy.shape[1], x2d.shape[1]
+        ns = [o.shape[0] for o in outs]
+        rc = _C.lib().pt_gemm_splitk_reduce(_ptr(part), ws, Nw * Kin, Nw, Kin, _C.ptrarr([_ptr(o) for o in outs]),
+                                            _C.i64arr([o.stride(0) for o in outs]), _C.i64arr(_bounds(ns)), len(outs),
+                                            int(wepilogue), None, 0, _C.stream_ptr(dy2d.device))
+        _C.check(rc, "pt_gemm_splitk_reduce")
     if e0 == EPI_F32:
         rc = _C.lib().pt_gemm_splitk_sum(_ptr(parts[0]), _ptr(parts[1]), None, _ptr(dx), dx.numel(),
                                          _C.stream_ptr(dy2d.device))
@@ -841,6 +929,10 @@ def linear_wgrad(dy2d, x2d, outs, epilogue=EPI_BF16, tile=-1):
     Kin = x2d.shape[1]
     ns = [o.shape[0] for o in outs]
     _req(sum(ns) == N, "wgrad: output rows must cover dY's width")
+    if tile < 0 and epilogue in (EPI_BF16, EPI_BF16_ACC, EPI_F32_ACC) and wgrad_ksplit([(N, Kin, T)]) > 1 and \
+            all(o.stride(1) == 1 and o.stride(0) % 4 == 0 for o in outs):
+        _wgrad_ksplit_run([(dy2d, x2d, outs)], epilogue, wgrad_ksplit([(N, Kin, T)]))
+        return outs
     _gemm(dy2d, dy2d.stride(0), 0, [x2d], [x2d.stride(0)], [0, Kin], 0, 0, outs, [o.stride(0) for o in outs],
           _bounds(ns), N, Kin, T, epilogue, tile)
     return outs

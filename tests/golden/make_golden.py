@@ -257,9 +257,11 @@ def _g11_data():
     return seq.view(G11_STEPS, 2, G11_GA, G11_MBS, S + 1).to(torch.uint8)
 
 
-def g11_curve(rank, world, tp, cp, dp):
+def g11_curve(rank, world, tp, cp, dp, dtype=torch.bfloat16):
     """G11: north_star's "loss curve within 1 % over 50 steps", pinned by the reference itself:
-    train.py's loop (train_step 29-55, the step loop 219-240) on gloo/CPU, fp32, FLASH_ATTEN=0, for
+    train.py's loop (train_step 29-55, the step loop 219-240) on gloo/CPU, FLASH_ATTEN=0, in the
+    reference's GPU training precision (train.py:76,190: the model and so AdamW's states in bf16,
+    cos/sin in bf16 as get_cos_sin makes them; G11f32_*: the same run in fp32), for
     G11_STEPS AdamW steps (lr G11_LR, torch defaults), grad_acc 2, mbs 2, seq 256, a fresh bigram
     batch every step (_g11_data), at 1 rank and at tp / cp / dp = 2.  Same model and initial weights
     as G10m (one tp=1 init, seed 7, sharded as apply_tensor_parallel shards); DataParallelBucket only
@@ -275,6 +277,7 @@ def g11_curve(rank, world, tp, cp, dp):
     from picotron.tensor_parallel.tensor_parallel import apply_tensor_parallel
     from picotron.utils import average_loss_across_dp_cp_ranks
     cfg = types.SimpleNamespace(**G10M_CFG)
+    torch.set_num_threads(max(1, 8 // world))
     torch.manual_seed(7)
     model = M.Llama(cfg)
     full = {n: p.detach().clone() for n, p in model.named_parameters()}
@@ -283,10 +286,11 @@ def g11_curve(rank, world, tp, cp, dp):
     if cp > 1:
         model = apply_context_parallel(model)
     for layer in model.decoder_layers:
-        layer.cos, layer.sin = layer.cos.float(), layer.sin.float()
+        layer.cos, layer.sin = layer.cos.to(dtype), layer.sin.to(dtype)
     with torch.no_grad():
         for n, p in model.named_parameters():
             p.copy_(_g10m_shard(full[n], p, m.tp_rank))
+    model = model.to(dtype)            # train.py:190
     if dp > 1:
         model = DataParallelBucket(model)
     opt = torch.optim.AdamW(model.parameters(), lr=G11_LR)
@@ -316,21 +320,23 @@ def g11_curve(rank, world, tp, cp, dp):
     return res
 
 
-def g11_all(ref):
+def g11_all(ref, dtypes=("bf16", "f32")):
     import functools
-    for name, (tp, cp, dp) in (("G11_1", (1, 1, 1)), ("G11_tp2", (2, 1, 1)), ("G11_cp2", (1, 2, 1)),
-                               ("G11_dp2", (1, 1, 2))):
-        _run_dist(functools.partial(g11_curve, tp=tp, cp=cp, dp=dp), tp * cp * dp, ref, name)
+    for tag in dtypes:
+        dt = torch.bfloat16 if tag == "bf16" else torch.float32
+        for name, (tp, cp, dp) in (("1", (1, 1, 1)), ("tp2", (2, 1, 1)), ("cp2", (1, 2, 1)), ("dp2", (1, 1, 2))):
+            _run_dist(functools.partial(g11_curve, tp=tp, cp=cp, dp=dp, dtype=dt), tp * cp * dp, ref,
+                      f"G11_{name}" if tag == "bf16" else f"G11f32_{name}")
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
-    ap.add_argument("--only", choices=["G11"], help="regenerate only these fixtures")
+    ap.add_argument("--only", choices=["G11", "G11bf16"], help="regenerate only these fixtures")
     args = ap.parse_args()
-    if args.only == "G11":
-        g11_all(args.ref)
-        print("wrote G11_1 G11_tp2 G11_cp2 G11_dp2")
+    if args.only:
+        g11_all(args.ref, ("bf16",) if args.only == "G11bf16" else ("bf16", "f32"))
+        print("wrote G11 fixtures")
         return
     os.environ.update(DEVICE="cpu", LOCAL_RANK="0", FLASH_ATTEN="0")
     sys.path.insert(0, args.ref)
@@ -464,8 +470,7 @@ def main():
     for name, (tp, cp, dp) in (("G10m_tp2", (2, 1, 1)), ("G10m_cp2", (1, 2, 1)), ("G10m_dp2", (1, 1, 2))):
         _run_dist(functools.partial(g10m_multirank, tp=tp, cp=cp, dp=dp), 2, args.ref, name)
     g11_all(args.ref)
-    print("wrote", sorted(gold) + ["G7", "G8", "G10m_tp2", "G10m_cp2", "G10m_dp2", "G11_1", "G11_tp2", "G11_cp2",
-                                   "G11_dp2"])
+    print("wrote", sorted(gold) + ["G7", "G8", "G10m_tp2", "G10m_cp2", "G10m_dp2", "G11_*", "G11f32_*"])
 
 
 if __name__ == "__main__":

@@ -297,6 +297,92 @@ def test_gemm_grouped_wgrad(epi):
     assert rel_err(outs[0], full[:H] + base) < 1e-2
 
 
+@pytest.mark.parametrize("epi", [0, 1, 3])
+def test_wgrad_ksplit_tp8_shapes(epi, monkeypatch):
+    """The TP = 8 shard weight gradients (SmolLM-1.7B: q|k|v dW [768, 2048] + o_proj dW [2048, 256]
+    in one group, 32 tiles; down_proj dW [2048, 1024], 32 tiles) as split-K slices (f32 partials +
+    pt_gemm_splitk_reduce into the bf16 store / bf16 accumulate / f32 accumulate sinks) against the
+    unsplit launch (PICOTRON_KSPLIT=0) and an f32 reference: equal up to the f32 summation order."""
+    from picotron_amd import kernels as K_
+    T, H, q, o_in, I = 4096, 2048, 256, 256, 1024
+    dqkv, h = torch.randn(T, 3 * q).to(BF).to(DEV), torch.randn(T, H).to(BF).to(DEV)
+    da, o = torch.randn(T, H).to(BF).to(DEV), torch.randn(T, o_in).to(BF).to(DEV)
+    dm, hh = torch.randn(T, H).to(BF).to(DEV), torch.randn(T, I).to(BF).to(DEV)
+    assert K_.wgrad_ksplit([(3 * q, H, T), (H, o_in, T)]) == 8
+    assert K_.wgrad_ksplit([(H, I, T)]) == 8 and K_.wgrad_ksplit([(2 * I, H, T)]) == 4
+    dt = torch.float32 if epi == 3 else BF
+    init = [torch.randn(n, k).to(dt).to(DEV) for n, k in ((q, H), (q, H), (q, H), (H, o_in), (H, I))]
+    outs, refs = [t.clone() for t in init], [t.clone() for t in init]
+    K_.linear_wgrad_grouped([(dqkv, h, outs[:3]), (da, o, outs[3:4])], epilogue=epi)
+    K_.linear_wgrad(dm, hh, outs[4:], epilogue=epi)
+    monkeypatch.setenv("PICOTRON_KSPLIT", "0")
+    K_.linear_wgrad_grouped([(dqkv, h, refs[:3]), (da, o, refs[3:4])], epilogue=epi)
+    K_.linear_wgrad(dm, hh, refs[4:], epilogue=epi)
+    torch.cuda.synchronize()
+    full = [dqkv[:, :q].t().float() @ h.float(), dqkv[:, q:2 * q].t().float() @ h.float(),
+            dqkv[:, 2 * q:].t().float() @ h.float(), da.t().float() @ o.float(), dm.t().float() @ hh.float()]
+    for a, b, f, i0 in zip(outs, refs, full, init):
+        want = f + (i0.float() if epi else 0)
+        assert rel_err(a, want) < 4e-3 and rel_err(b, want) < 4e-3
+        assert maxabs(a, b) <= 2 * b.float().abs().max().item() * (2 ** -8 if dt == BF else 2 ** -20)
+
+
+@pytest.mark.parametrize("epi", [1, 3])
+def test_gemm_dual_with_ksplit_wgrad(epi, monkeypatch):
+    """TP = 8 down_proj backward: the SwiGLU-backward dX (64 tiles) beside the split-K down_proj dW
+    (32 tiles x 4 slices: one round with the dX tiles; f32 partials + reduce) in one dual launch == the unsplit dual launch up to
+    the dW's f32 summation order; the dX bit for bit."""
+    from picotron_amd import kernels as K_
+    T, H, I = 4096, 2048, 1024
+    dm = torch.randn(T, H).to(BF).to(DEV)
+    wd = (torch.randn(H, I) / math.sqrt(I)).to(BF).to(DEV)
+    gu = torch.randn(T, 2 * I).to(BF).to(DEV)
+    hh = torch.randn(T, I).to(BF).to(DEV)
+    dt = torch.float32 if epi == 3 else BF
+    init = torch.randn(H, I).to(dt).to(DEV)
+    out_a, out_b = init.clone(), init.clone()
+    dx_a = K_.linear_dgrad_dual(dm, [wd], [(dm, hh, [out_a])], epi, gu=gu)
+    monkeypatch.setenv("PICOTRON_KSPLIT", "0")
+    dx_b = K_.linear_dgrad_dual(dm, [wd], [(dm, hh, [out_b])], epi, gu=gu)
+    torch.cuda.synchronize()
+    assert dx_a is not None and dx_b is not None and torch.equal(dx_a, dx_b)
+    want = dm.t().float() @ hh.float() + init.float()
+    assert rel_err(out_a, want) < 4e-3
+    assert maxabs(out_a, out_b) <= 2 * out_b.float().abs().max().item() * (2 ** -8 if dt == BF else 2 ** -20)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4])
+def test_splitk_reduce_modes(mode):
+    """pt_gemm_splitk_reduce: the sum of the partials in part order through each sink epilogue,
+    into two row segments with their own leading dimensions."""
+    from picotron_amd import _C, kernels as K_
+    parts = torch.randn(3, 512, 256, device=DEV)
+    total = parts[0] + parts[1] + parts[2]
+    f32 = mode in (2, 3)
+    dt = torch.float32 if f32 else BF
+    seg = [torch.randn(384, 264, device=DEV).to(dt)[:, :256], torch.randn(128, 256, device=DEV).to(dt)]
+    init = [t.clone() for t in seg]
+    res = torch.randn(512, 256, device=DEV).to(BF)
+    rc = _C.lib().pt_gemm_splitk_reduce(K_._ptr(parts), 3, 512 * 256, 512, 256, _C.ptrarr([K_._ptr(t) for t in seg]),
+                                        _C.i64arr([t.stride(0) for t in seg]), _C.i64arr([0, 384, 512]), 2, mode,
+                                        K_._ptr(res) if mode == 4 else None, 256, _C.stream_ptr(torch.device(DEV)))
+    assert rc == 0
+    torch.cuda.synchronize()
+    got = torch.cat([seg[0], seg[1]]).float()
+    old = torch.cat(init).float()
+    if mode == 0:
+        want = total.to(BF).float()
+    elif mode == 1:
+        want = (old + total.to(BF).float()).to(BF).float()
+    elif mode == 2:
+        want = total
+    elif mode == 3:
+        want = old + total
+    else:
+        want = (res.float() + total.to(BF).float()).to(BF).float()
+    assert torch.equal(got, want)
+
+
 @pytest.mark.parametrize("T,H,I", [(256, 256, 128), (512, 512, 1024), (1024, 256, 384)])
 def test_gemm_swiglu_fused(T, H, I):
     """gate|up GEMM with SwiGLU in the epilogue == GEMM + swiglu kernel, bit for bit; and the down
@@ -324,12 +410,14 @@ def test_gemm_swiglu_fused(T, H, I):
 
 @pytest.mark.parametrize("swiglu", [True, False])
 @pytest.mark.parametrize("epi", [0, 1, 3])
-@pytest.mark.parametrize("order", [0, 1])
-def test_gemm_dual_equals_separate(swiglu, epi, order):
+@pytest.mark.parametrize("order", [0, 1, 2])
+def test_gemm_dual_equals_separate(swiglu, epi, order, monkeypatch):
     """pt_gemm_dual (a dX group and a wgrad group in one launch, every dispatch order) == the two
     groups as separate 256x256 launches, bit for bit: the down_proj dX with the SwiGLU backward
-    beside its dW, and a K-segmented q|k|v dX beside the q|k|v + o_proj dWs"""
+    beside its dW, and a K-segmented q|k|v dX beside the q|k|v + o_proj dWs (unsplit dW: the split-K
+    dW beside a dX is test_gemm_dual_with_ksplit_wgrad)"""
     from picotron_amd import kernels as K_
+    monkeypatch.setenv("PICOTRON_KSPLIT", "0")
     T, H = 1024, 512
     dt = torch.float32 if epi == 3 else BF
     if swiglu:
