@@ -821,7 +821,10 @@ def dual_enabled():
 
 
 def _dual_order():
-    return int(os.environ.get("PICOTRON_DUAL_ORDER", "0"))
+    """0: dX tiles first in every XCD, 1: dW first, 2 (default): staggered -- even XCDs dX first, odd XCDs
+    dW first, so half the chip is in the dX tiles' HBM-bound SwiGLU-backward tail at a time (+0.8 %
+    on the step, profiles/r03/dual_order_ab.txt)."""
+    return int(os.environ.get("PICOTRON_DUAL_ORDER", "2"))
 
 
 def dual_fits(dgrad_mn, wgrad_mns):

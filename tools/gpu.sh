@@ -14,6 +14,9 @@
 #   attn         tools/attn_bench.py d64 and d128 (OLD=<lib> for an in-process A/B)
 #   pmcattn      attention PMC passes (ATTN_ARGS="--B 1 --S 4096 --H 32 --D 128" for d128)
 #   norm         tools/norm_bench.py (OLD=<lib> for an A/B)
+#   tpprof       rocprofv3 kernel trace of the TP=8 proxy (PROXY="--tp-proxy 8" or "--cp-proxy 8 --model ...")
+#   counters     rocprofv3 -L: the counters this box's gfx950 exposes (e.g. for HBM vs Infinity-Cache reads)
+#   mall         TCC_EA0_RDREQ vs TCC_EA0_RDREQ_DRAM on a cold and a warm (Infinity-Cache) read (tools/mall_probe.py)
 #   envab        whole-step A/B of two env settings: A="X=0" B="X=1" ROUNDS=3
 #   libab        whole-step A/B of library builds swapped in place: LIBS=a.so,b.so ROUNDS=2
 set -o pipefail
@@ -108,6 +111,30 @@ step_pmcattn() {
 step_norm() {
   timeout -k 10 120 python -u tools/norm_bench.py ${OLD:+--old $OLD} > $O.norm.log 2>&1 || { echo norm failed; tail $O.norm.log; return 1; }
   grep -v "^$" $O.norm.log | tail -8
+}
+
+step_tpprof() {
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O.tpprof -o k -- python -u bench.py ${PROXY:---tp-proxy 8} --steps 3 > $O.tpprof.log 2>&1 || { echo tpprof failed; tail $O.tpprof.log; return 1; }
+  gzip -f $O.tpprof/k_kernel_trace.csv
+  tail -1 $O.tpprof.log
+}
+
+step_counters() {
+  timeout -k 10 120 rocprofv3 -L > $O.counters.txt 2>&1 || { echo counters failed; tail $O.counters.txt; return 1; }
+  grep -ciE "TCC_EA|MALL|DRAM|HBM" $O.counters.txt || true
+}
+
+step_mall() {
+  timeout -s KILL 60 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum --kernel-include-regex reduce --output-format csv -d $O.mall -o m -- python -u tools/mall_probe.py > $O.mall.log 2>&1 || { echo mall failed; tail -3 $O.mall.log; return 1; }
+  python - "$O.mall/m_counter_collection.csv" <<'PY'
+import csv, sys, collections
+rows = list(csv.DictReader(open(sys.argv[1])))
+per = collections.defaultdict(dict)
+for r in rows:
+    per[int(r["Dispatch_Id"])][r["Counter_Name"]] = float(r["Counter_Value"])
+for d in sorted(per):
+    print(d, {k: int(v) for k, v in sorted(per[d].items())})
+PY
 }
 
 step_envab() {
