@@ -44,9 +44,9 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
-# HBM bytes per GEMM launch from rocprofv3 PMC passes (tools/r02_final.sh: bench.py --grad-acc 2, then
+# HBM bytes per GEMM launch from rocprofv3 PMC passes (tools/gpu.sh counters: bench.py --grad-acc 2, then
 # tools/traffic_summary.py); read for the roofline's `traffic`
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_gemm_traffic_s7.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03", "gemm_traffic_r03g.json")
 
 
 def log(*a):

@@ -72,7 +72,8 @@ SIGNATURES = {
 ERRORS = {-1: "PT_EINVAL (bad size or null pointer)", -2: "PT_EALIGN (misaligned pointer/stride)",
           -3: "PT_EUNSUPPORTED (shape outside the kernel's tiling)"}
 
-_lib = None
+_lib = None          # the product library (LIB_PATH), used by every op
+_alt_libs = {}       # other builds loaded for A/B tools, one entry per path; never become _lib
 
 
 class HipKernelError(RuntimeError):
@@ -81,10 +82,15 @@ class HipKernelError(RuntimeError):
 
 def load_library(path=LIB_PATH, strict=True):
     """dlopen the kernel library and bind every symbol; does not touch the GPU.  strict=False (A/B
-    runs against another build) skips symbols that build does not export."""
+    runs against another build) skips symbols that build does not export.  Only LIB_PATH becomes
+    the library the ops call; another path is cached under its own name and returned."""
     global _lib
-    if _lib is not None and path == LIB_PATH:
+    path = os.path.abspath(path)
+    is_main = path == os.path.abspath(LIB_PATH)
+    if is_main and _lib is not None:
         return _lib
+    if not is_main and path in _alt_libs:
+        return _alt_libs[path]
     if not os.path.exists(path):
         raise HipKernelError(f"picotron_amd HIP library not built: {path} (run python -m picotron_amd.build)")
     import torch  # noqa: F401  -- its HIP runtime must be the one our SONAME binds to
@@ -95,8 +101,19 @@ def load_library(path=LIB_PATH, strict=True):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    _lib = lib
+    if is_main:
+        _lib = lib
+    else:
+        _alt_libs[path] = lib
     return lib
+
+
+def use_library(path):
+    """A/B tools only: make another build the library every op calls, explicitly (and say so)."""
+    global _lib
+    _lib = load_library(path, strict=False)
+    print(f"[picotron_amd] ops now call {os.path.abspath(path)}", flush=True)
+    return _lib
 
 
 def lib():

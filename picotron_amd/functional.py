@@ -142,18 +142,36 @@ def dgrad_with_wgrad(dy2d, weights, wjobs, gu=None):
 # all into their sinks -- 2 L + 1 column-sum launches per micro-batch become one.  Norms whose
 # weights carry a _pt_grad_ready hook keep the immediate sum (their bucket's all-reduce overlaps the
 # rest of the backward).  PICOTRON_NORM_DEFER=0 turns this off (A/B only).
-_PENDING_DW = {}   # autograd graph task id -> [(partial, sink buffer, sink, stream)]
+_PENDING_DW = {}   # autograd graph task id -> [(partial, weight, stream)]
 
 
 def _norm_defer_enabled():
     return os.environ.get("PICOTRON_NORM_DEFER", "1") != "0"
 
 
+def _norm_dw_sink(weight):
+    """The weight gradient's sink as AccumulateGrad would treat it now: (buffer, epilogue)."""
+    mg = getattr(weight, "main_grad", None)
+    if mg is not None:
+        return mg, (K.DW_ACC_F32 if mg.dtype == torch.float32 else K.DW_ACC_BF16)
+    if weight.grad is None:
+        weight.grad = torch.empty_like(weight)
+        return weight.grad, 0
+    return weight.grad, K.DW_ACC_BF16
+
+
 def _flush_norm_dw(task):
-    groups = {}
-    for part, buf, sink, stream in _PENDING_DW.pop(task, []):
-        groups.setdefault((part.shape[1], part.device, stream), []).append((part, buf, sink))
-    for (_, _, stream), js in groups.items():
+    """Sum every pending partial into its sink.  Sinks are resolved here, in backward order, so a
+    .grad is only created (and stored into) once its sum is launched; a weight used by several
+    norms of one backward gets a store and then accumulates, and jobs that share a sink go into
+    separate, stream-ordered launches (generation g = the g-th job on that sink)."""
+    groups, seen = {}, {}
+    for part, weight, stream in _PENDING_DW.pop(task, []):
+        buf, sink = _norm_dw_sink(weight)
+        gen = seen.get(buf.data_ptr(), 0)
+        seen[buf.data_ptr()] = gen + 1
+        groups.setdefault((gen, part.shape[1], part.device, stream), []).append((part, buf, sink))
+    for (_, _, _, stream), js in sorted(groups.items(), key=lambda kv: kv[0][0]):
         with torch.cuda.stream(stream):   # the stream the partials were produced on
             for i in range(0, len(js), 32):
                 K.rmsnorm_colsum_batch(js[i:i + 32])
@@ -166,22 +184,15 @@ def norm_bwd(dy2, z, weight, rstd, mode, dres=None, need_dw=True):
     if not (need_dw and weight.requires_grad):
         dx, _ = K.rmsnorm_bwd(dy2, z, weight, rstd, mode, dres=dres)
         return dx
-    mg = getattr(weight, "main_grad", None)
-    if mg is not None:
-        buf, sink = mg, (K.DW_ACC_F32 if mg.dtype == torch.float32 else K.DW_ACC_BF16)
-    elif weight.grad is None:
-        weight.grad = torch.empty_like(weight)
-        buf, sink = weight.grad, 0
-    else:
-        buf, sink = weight.grad, K.DW_ACC_BF16
     task = torch._C._current_graph_task_id()   # -1 outside an autograd backward
     if getattr(weight, "_pt_grad_ready", None) is None and z.is_cuda and task != -1 and _norm_defer_enabled():
         dx, partial = K.rmsnorm_bwd(dy2, z, weight, rstd, mode, dres=dres, defer_dw=True)
         if task not in _PENDING_DW:
             _PENDING_DW[task] = []
             torch.autograd.Variable._execution_engine.queue_callback(lambda: _flush_norm_dw(task))
-        _PENDING_DW[task].append((partial, buf, sink, torch.cuda.current_stream(z.device)))
+        _PENDING_DW[task].append((partial, weight, torch.cuda.current_stream(z.device)))
         return dx
+    buf, sink = _norm_dw_sink(weight)
     dx, _ = K.rmsnorm_bwd(dy2, z, weight, rstd, mode, dres=dres, dw_out=buf, dw_sink=sink)
     _grad_ready(weight)
     return dx

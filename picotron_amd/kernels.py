@@ -168,7 +168,9 @@ _ADAM_DESC = {}
 def adamw_step_multi(items, decay, w1, beta2, c2, bc2_sqrt, eps, step_size):
     """One launch of the fused AdamW update over a list of bf16 (param, grad, exp_avg, exp_avg_sq)
     tuples (pt_adamw_step_multi).  The device descriptor table is cached per pointer set (the
-    tensors of a model stay put across steps; a re-allocated gradient makes a new table)."""
+    tensors of a model stay put across steps; a re-allocated gradient makes a new table).  A new
+    table is staged in pinned host memory and copied on the current stream without a host sync
+    (the caching host allocator keeps the staging buffer alive until that copy has run)."""
     for p, g, m, v in items:
         for t in (p, g, m, v):
             _req(t.dtype == BF16 and t.is_contiguous() and t.numel() == p.numel() and t.data_ptr() % 16 == 0,
@@ -177,11 +179,12 @@ def adamw_step_multi(items, decay, w1, beta2, c2, bc2_sqrt, eps, step_size):
     ent = _ADAM_DESC.get(key)
     if ent is None:
         dev = items[0][0].device
-        desc = torch.tensor([list(k) for k in key], dtype=torch.int64).to(dev, non_blocking=False)
         chunks = [0]
         for k in key:
             chunks.append(chunks[-1] + (k[4] + 7) // 8)
-        ent = (desc, torch.tensor(chunks, dtype=torch.int64).to(dev), chunks[-1])
+        desc_h = torch.tensor([list(k) for k in key], dtype=torch.int64).pin_memory()
+        chunk_h = torch.tensor(chunks, dtype=torch.int64).pin_memory()
+        ent = (desc_h.to(dev, non_blocking=True), chunk_h.to(dev, non_blocking=True), chunks[-1])
         if len(_ADAM_DESC) > 64:
             _ADAM_DESC.clear()
         _ADAM_DESC[key] = ent
@@ -238,11 +241,34 @@ def _dev_index(device):
 
 def status_word(device):
     """The per-device int32 status word data-validating kernels OR their error bits into."""
+    _status_poll(device)   # an error an earlier launch posted raises before the next launch
     w = _STATUS.get(_dev_index(device))
     if w is None:
         w = torch.zeros(1, dtype=torch.int32, device=torch.device("cuda", _dev_index(device)))
         _STATUS[_dev_index(device)] = w
     return w
+
+
+_STATUS_HOST = {}   # device index -> pinned int32 mirror of the status word (async D2H copies)
+
+
+def _status_posted(device):
+    """After a validating launch: copy the status word into its pinned host mirror on the same
+    stream, without a host sync.  The next validating call reads the mirror (see _status_poll), so a
+    bad target raises one call later even on the drop-in path, whose train.py never calls
+    check_device_status -- as torch's own asynchronous device-side assert surfaces at a later op."""
+    i = _dev_index(device)
+    h = _STATUS_HOST.get(i)
+    if h is None:
+        h = _STATUS_HOST[i] = torch.zeros(1, dtype=torch.int32).pin_memory()
+    h.copy_(status_word(device), non_blocking=True)
+
+
+def _status_poll(device):
+    """Raise if a copy that has already landed in the pinned mirror carries an error bit."""
+    h = _STATUS_HOST.get(_dev_index(device))
+    if h is not None and int(h[0]):
+        check_device_status(device)
 
 
 def device_status(device=None, reset=True):
@@ -253,6 +279,9 @@ def device_status(device=None, reset=True):
     v = int(w.item())
     if reset and v:
         w.zero_()
+        h = _STATUS_HOST.get(_dev_index(device))
+        if h is not None:
+            h.zero_()   # every copy into it was enqueued before the item() sync above
     return v
 
 
@@ -283,6 +312,7 @@ def cross_entropy_fwd_bwd(logits, targets, scale=1.0, ignore_index=-100, inplace
                                            dlogits.stride(0), _ptr(row_loss), rows, vocab, float(scale),
                                            _ptr(inv_count), int(ignore_index), _ptr(status_word(logits.device)), _C.stream_ptr(logits.device))
     _C.check(rc, "pt_cross_entropy_fwd_bwd")
+    _status_posted(logits.device)
     loss = row_loss.sum() * inv_count[0]
     return loss, dlogits, inv_count
 
@@ -298,6 +328,7 @@ def cross_entropy_loss(logits, targets, ignore_index=-100):
     rc = _C.lib().pt_cross_entropy_fwd_bwd(_ptr(logits), logits.stride(0), _ptr(targets), None, 0, _ptr(row_loss),
                                            rows, vocab, 1.0, None, int(ignore_index), _ptr(status_word(logits.device)), _C.stream_ptr(logits.device))
     _C.check(rc, "pt_cross_entropy_fwd_bwd(loss)")
+    _status_posted(logits.device)
     return row_loss.sum() * inv_count[0], inv_count
 
 
@@ -336,6 +367,7 @@ def cross_entropy_loss_lse(logits, targets, ignore_index=-100, out_dtype=torch.f
     rc = _C.lib().pt_cross_entropy_fwd_lse(_ptr(logits), logits.stride(0), _ptr(targets), _ptr(row_loss),
                                            _ptr(row_lse), rows, vocab, int(ignore_index), _ptr(status_word(logits.device)), _C.stream_ptr(logits.device))
     _C.check(rc, "pt_cross_entropy_fwd_lse")
+    _status_posted(logits.device)
     # no clamp: every target ignored gives 0 * inf = nan, as F.cross_entropy's mean does (grads 0)
     loss, inv_count = _ce_reduce(row_loss, targets, ignore_index, out_dtype, reduction)
     return loss, inv_count, row_lse
@@ -371,6 +403,7 @@ def cross_entropy_grad(logits, targets, scale_dev, ignore_index=-100):
                                            _ptr(row_loss), rows, vocab, 1.0, _ptr(scale_dev), int(ignore_index),
                                            _ptr(status_word(logits.device)), _C.stream_ptr(logits.device))
     _C.check(rc, "pt_cross_entropy_fwd_bwd(grad)")
+    _status_posted(logits.device)
     return dl
 
 
@@ -680,6 +713,7 @@ def cross_entropy_loss_lse_stats(logits, targets, stats, ignore_index=-100, out_
                                              int(ignore_index), _ptr(status_word(logits.device)),
                                              _C.stream_ptr(logits.device))
     _C.check(rc, "pt_cross_entropy_fwd_stats")
+    _status_posted(logits.device)
     loss, inv_count = _ce_reduce(row_loss, targets, ignore_index, out_dtype, reduction)
     return loss, inv_count, row_lse
 

@@ -170,6 +170,24 @@ def test_cross_entropy_bad_target_is_an_error():
         K.check_device_status(torch.device("cuda"))
 
 
+def test_cross_entropy_bad_target_raises_at_next_call_without_check():
+    """The drop-in path (the reference's train.py) never calls check_device_status: the status word's
+    pinned mirror makes the next cross_entropy call raise once the bad call's copy has landed."""
+    from picotron_amd import functional as FN
+    from picotron_amd import kernels as K
+    from picotron_amd._C import HipKernelError
+    K.device_status(torch.device("cuda"))
+    lg = torch.randn(16, 1000, device="cuda").to(BF)
+    tgt = torch.randint(0, 1000, (16,), device="cuda")
+    bad = tgt.clone()
+    bad[2] = 4000
+    assert math.isnan(FN.cross_entropy(lg, bad).float().item())   # .item(): the host syncs, as train.py's print
+    with pytest.raises(HipKernelError, match="outside"):
+        FN.cross_entropy(lg, tgt)
+    assert not math.isnan(FN.cross_entropy(lg, tgt).float().item())   # reported once, then cleared
+    K.check_device_status(torch.device("cuda"))
+
+
 def test_lm_head_swapped_for_torch_linear_stays_on_hip_gemm():
     """checkpoint.py:89-91 replaces final_proj by a torch nn.Linear; Llama.forward still runs it on
     the MFMA GEMM (bit-identical logits to the build's own Linear with the same weight)."""

@@ -77,7 +77,7 @@ def main():
     ap.add_argument("--brief", action="store_true", help="one short line per shape")
     args = ap.parse_args()
     if args.lib:
-        K._C.load_library(os.path.abspath(args.lib))
+        K._C.use_library(os.path.abspath(args.lib))
     tiles = [int(t) for t in args.tiles.split(",")]
     out = []
     for name, M, N, Kd, ak, bk in SHAPES:
@@ -129,7 +129,7 @@ def one(shape, tile, reps):
 
 if __name__ == "__main__":
     if os.environ.get("PT_LIB"):   # A/B: load another build of the library (before any launch)
-        K._C.load_library(os.path.abspath(os.environ["PT_LIB"]), strict=False)
+        K._C.use_library(os.path.abspath(os.environ["PT_LIB"]))
     if len(sys.argv) > 1 and sys.argv[1] == "one":
         one(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]) if len(sys.argv) > 4 else 5)
     else:
