@@ -49,7 +49,11 @@ def _compile(src, obj, extra):
     return obj
 
 
-def build(force=False, verbose=True, extra=()):
+def build(force=False, verbose=True, extra=(), out=None):
+    """out: another library path (A/B and diagnostic builds with `extra` flags; always rebuilt)."""
+    if out is not None:
+        force = True
+    lib_path = out or LIB
     os.makedirs(LIBDIR, exist_ok=True)
     srcs = sources()
     hdrs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
@@ -58,23 +62,27 @@ def build(force=False, verbose=True, extra=()):
         if verbose:
             print(f"[picotron_amd.build] up to date: {LIB}")
         return LIB
-    objdir = os.path.join(LIBDIR, "obj")
+    objdir = os.path.join(LIBDIR, "obj" if out is None else "obj_alt")
     os.makedirs(objdir, exist_ok=True)
     objs = [os.path.join(objdir, os.path.basename(s)[:-4] + ".o") for s in srcs]
     jobs = min(len(srcs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16)
     with concurrent.futures.ThreadPoolExecutor(jobs) as ex:
         list(ex.map(lambda so: _compile(so[0], so[1], list(extra)), zip(srcs, objs)))
     tl = _torch_lib_dir()
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs + \
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib_path + ".tmp"] + objs + \
           [f"-L{tl}", f"-Wl,-rpath,{tl}", "-lamdhip64"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
-    os.replace(LIB + ".tmp", LIB)
+    os.replace(lib_path + ".tmp", lib_path)
     if verbose:
-        print(f"[picotron_amd.build] built {LIB} from {len(srcs)} sources")
-    return LIB
+        print(f"[picotron_amd.build] built {lib_path} from {len(srcs)} sources")
+    return lib_path
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    # python -m picotron_amd.build [--force] [--out PATH -DFLAG ...]  (--out: an A/B or diagnostic build)
+    args = sys.argv[1:]
+    out = args[args.index("--out") + 1] if "--out" in args else None
+    flags = [a for a in args if a.startswith("-D")]
+    build(force="--force" in args, extra=flags, out=os.path.abspath(out) if out else None)

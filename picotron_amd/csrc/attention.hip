@@ -65,6 +65,11 @@ struct AttnArgs {
   // causal load balance: each workgroup runs block x and block (n - 1 - x) one after the other,
   // so every workgroup gets the same number of tiles whatever CU slot it lands in
   int pair;
+  // dK/dV wave-pair kernel: which waves are score waves (0: waves 0-3, 1: even waves)
+  int role_even;
+  int prio;    // dK/dV pair kernel: raise the score wave's priority over its MFMA cluster
+  unsigned long long* stamps;  // diagnostic builds only (-DPT_STAMP): per-step s_memtime of workgroups 0-7
+  int ablate;  // diagnostic builds only (-DPT_ABLATE): bits skip parts of the dK/dV pair kernel
   // bwd: when set, the dQ kernel (launched first) computes D = rowsum(dO * O) of its own rows from
   // O (a.o, bf16) and writes it here for the dK/dV kernel -- no separate delta pass
   float* delta_w;
@@ -136,7 +141,13 @@ __device__ __forceinline__ int crow(int r, int lane) { return (r & 3) + 8 * (r >
 // K/V (or Q/dO) tiles -- over 8 different L2s.  Remap so each XCD gets a contiguous range of
 // (block, head, batch) ids, blocks of one head adjacent: a head's tiles are fetched into one L2
 // and re-read from there (a head's K+V at S 1024, d 64 is 256 KiB; an XCD's L2 is 4 MiB).
-__device__ __forceinline__ void attn_coords(int& x, int& y, int& z) {
+__device__ __forceinline__ void attn_coords(const AttnArgs& a, int& x, int& y, int& z) {
+#ifdef PT_ABLATE
+  if (a.ablate & 16) {  // diagnostic: the dispatcher's own order
+    x = blockIdx.x; y = blockIdx.y; z = blockIdx.z;
+    return;
+  }
+#endif
   const int nx = gridDim.x, ny = gridDim.y, nwg = nx * ny * gridDim.z;
   const int id = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
   const int xcd = id & 7, q = nwg >> 3, r = nwg & 7;
@@ -365,7 +376,7 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
 template <int D, int NWK>
 __global__ __launch_bounds__(NWK * 64) void attn_fwd_kernel(AttnArgs a) {
   int bx, hh, b;
-  attn_coords(bx, hh, b);
+  attn_coords(a, bx, hh, b);
   for (int pass = 0; pass <= a.pair; ++pass) {  // one inlined body: no register growth
     if (pass) __syncthreads();
     attn_fwd_block<D, NWK>(a, pass ? a.Sq / (NWK * 32) - 1 - bx : bx, hh, b);
@@ -539,10 +550,255 @@ template <int D>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(D == 64 ? 2 : 1)))
 void attn_bwd_dkdv_kernel(AttnArgs a) {
   int bx, hh, b;
-  attn_coords(bx, hh, b);
+  attn_coords(a, bx, hh, b);
   for (int pass = 0; pass <= a.pair; ++pass) {  // one inlined body: no register growth
     if (pass) __syncthreads();
     attn_bwd_dkdv_block<D>(a, pass ? a.Sk / (NW * 32) - 1 - bx : bx, hh, b);
+  }
+}
+
+// ================================================================ dK / dV, split over wave pairs
+// The same products as attn_bwd_dkdv_block, divided between the two waves of a pair so that one
+// SIMD holds a VALU-heavy and an MFMA-only wave side by side (8-wave workgroups; 128 keys = 4
+// pairs x 32; waves w and w + 4 share a SIMD).  Wave p < 4 ("score wave") keeps K and V of the
+// pair's keys in registers and runs S = Q K^T, dP = dO V^T, P = exp2(S c2 - lse log2e),
+// dS = P (dP - delta); it hands P and dS, already rounded to bf16 in the MFMA B-operand layout, to
+// wave p + 4 ("accumulator wave") through LDS; wave p + 4 keeps dV^T and dK^T and runs
+// dV^T += dO^T P, dK^T += Q^T dS one step behind.  A step is half a Q/dO tile (32 queries); a
+// tile is read in steps 2t .. 2t + 2.  Staging is a 3-deep ring: the DMA of tile t + 2 is issued
+// in step 2t + 1 and waited for (counted vmcnt: the younger tile's pieces stay in flight) at the
+// end of step 2t + 3, so a tile has three steps to arrive -- the workgroups of one XCD walk the
+// same Q/dO tiles together, and each tile's first touch is an HBM miss all of them wait on.
+// Each wave executes the same number of barriers (one per step) on its own branch.  The MFMA
+// operands and their order per accumulator are those of attn_bwd_dkdv_block: dK and dV are
+// bit-identical.
+constexpr int kXchB = 4 * 2 * 2 * 1024;  // one step's P|dS hand-off: 4 pairs x 2 k-steps x 2 kinds x 1 KiB
+#ifdef PT_STAMP
+constexpr int kStampSteps = 136;
+constexpr int kStampB = 8 * 2 * kStampSteps * 8;
+#else
+constexpr int kStampB = 0;
+#endif
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else static_assert(N == 0, "vm_wait: add the count");
+}
+
+template <int D>
+__device__ __forceinline__ void attn_bwd_dkdv_pair_block(const AttnArgs& a, int bx, int hk, int b) {
+  constexpr int DT = D / 32, KS = D / 16;
+  constexpr int TILE_B = KT * D * 2;
+  constexpr int STAGE_B = 2 * TILE_B + 2 * KT * 4;  // Q tile, dO tile, lse [64], delta [64]
+  constexpr int NSTG = 3;
+  // LDS-DMA pieces one tile's staging issues per wave (the lse and delta rows: wave 0)
+  constexpr int OPS = 2 * (KT * D * 2 / 1024) / 8, OPS0 = OPS + 2;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+  lds_u8* smem = (lds_u8*)smem_raw;
+  lds_u8* xch = smem + NSTG * STAGE_B;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool score = a.role_even ? (wave & 1) == 0 : wave < 4;
+  const int pr = a.role_even ? wave >> 1 : wave & 3;
+  const int k0 = bx * 128 + pr * 32;
+  const int mykey = k0 + (lane & 31);
+  const int group = a.H / a.HKV;
+  const float c2 = a.scale * kLog2e;
+
+  const int qt_begin = a.causal ? (bx * 128) / KT : 0;
+  const int nq = a.Sq / KT - qt_begin;  // q tiles per query head
+  const int n_tiles = nq * group;
+  const int n_steps = 2 * n_tiles;
+
+  // staging: tile t = (query head hk * group + t / nq, q tile qt_begin + t % nq), counters advanced
+  // per staged tile (no divisions in the loop)
+  int st_hq = hk * group, st_qt = qt_begin, st_buf = 0;
+  auto stage_next = [&]() {
+    lds_u8* sq = smem + st_buf * STAGE_B;
+    stage_rows<D, 8>(a.q + b * a.q_sb + (int64_t)st_qt * KT * a.q_ss + st_hq * a.q_sh, a.q_ss, sq, wave, lane);
+    stage_rows<D, 8>(a.dout + b * a.do_sb + (int64_t)st_qt * KT * a.do_ss + st_hq * a.do_sh, a.do_ss, sq + TILE_B,
+                     wave, lane);
+    if (wave == 0) {
+      const int64_t ro = ((int64_t)b * a.H + st_hq) * a.lse_ld + st_qt * KT;
+      pt_glds4(a.lse + ro, lane * 4u, (__attribute__((address_space(3))) void*)(sq + 2 * TILE_B));
+      pt_glds4(a.delta + ro, lane * 4u, (__attribute__((address_space(3))) void*)(sq + 2 * TILE_B + KT * 4));
+    }
+    if (++st_qt == qt_begin + nq) { st_qt = qt_begin; ++st_hq; }
+    if (++st_buf == NSTG) st_buf = 0;
+  };
+  // wait for every staged tile but the youngest one (when `keep`), then the barrier
+  auto wait_keep = [&](bool keep) {
+    if (keep) {
+      if (wave == 0) vm_wait<OPS0>(); else vm_wait<OPS>();
+    } else {
+      vm_wait<0>();
+    }
+  };
+  // step j (odd, j = 2t + 1) issues tile t + 2; its end waits for tile t + 1 (used from step 2t + 2)
+  auto issue = [&](int j) { return (j & 1) && (j >> 1) + 2 < n_tiles; };
+#ifdef PT_STAMP
+  // per wave and step: (start, arrival at the end-of-step wait) in LDS past the hand-off buffers
+  unsigned long long* stl = (unsigned long long*)(xch + 2 * kXchB) + wave * 2 * kStampSteps;
+  const int wg_lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  auto stamp = [&](int j, int w) {
+    if (lane == 0 && j < kStampSteps) stl[2 * j + w] = __builtin_amdgcn_s_memtime();
+  };
+#else
+  auto stamp = [&](int, int) {};
+#endif
+  auto end_step = [&](int j) {
+    stamp(j, 1);
+    if (j & 1) wait_keep(issue(j));
+    __syncthreads();
+  };
+
+  if (n_tiles > 0) stage_next();
+  if (n_tiles > 1) stage_next();
+  // the q tile of the step this wave works on (A: step j, B: step j - 1), advanced every second step
+  int qt = qt_begin;
+  if (score) {
+    const uint16_t* krow = a.k + b * a.k_sb + (int64_t)mykey * a.k_ss + hk * a.k_sh;
+    const uint16_t* vrow = a.v + b * a.v_sb + (int64_t)mykey * a.v_ss + hk * a.v_sh;
+    bf16x8_t kf[KS], vf[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      kf[ks] = ld_row_frag(krow, ks, lane);
+      vf[ks] = ld_row_frag(vrow, ks, lane);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler: K / V and tiles 0, 1
+    __syncthreads();
+    int buf = 0;
+    for (int j = 0; j <= n_steps; ++j) {
+      stamp(j, 0);
+      if (issue(j)) stage_next();
+      const int qh = j & 1;
+      const int qs = qt * KT + 32 * qh;
+      // causal: every query of the half tile precedes the pair's keys (wave-uniform; the partner
+      // wave skips the same step)
+      if (j < n_steps && !(a.causal && qs + 31 < k0)) {
+        const lds_u8* sq = smem + buf * STAGE_B;
+        const lds_u8* sdo = sq + TILE_B;
+        const float* sl = (const float*)(sq + 2 * TILE_B);
+        const float* sdel = sl + KT;
+        f32x16_t s = zero16(), dp = zero16();
+        // the score wave's MFMAs go first on the SIMD (its softmax then runs beside the partner's
+        // MFMAs instead of after them)
+        if (a.prio) __builtin_amdgcn_s_setprio(1);
+#ifdef PT_ABLATE
+        if (!(a.ablate & 4))
+#endif
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          s = mfma(rd_row<D>(sq, 32 * qh, ks, lane), kf[ks], s);
+          dp = mfma(rd_row<D>(sdo, 32 * qh, ks, lane), vf[ks], dp);
+        }
+        if (a.prio) __builtin_amdgcn_s_setprio(0);
+        if (a.causal && (qs < k0 + 31)) {  // diagonal: query row crow(r) sees my key iff >= thr
+          const int thr = mykey - qs - 4 * (lane >> 5);
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if ((r & 3) + 8 * (r >> 2) < thr) s[r] = -INFINITY;
+        }
+#ifdef PT_ABLATE
+        if (!(a.ablate & 2))
+#endif
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qi = 32 * qh + crow(r, lane);
+          const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -(sl[qi] * kLog2e)));
+          s[r] = p;
+          dp[r] = p * (dp[r] - sdel[qi]);
+        }
+        lds_u8* x = xch + (j & 1) * kXchB + pr * 4096 + lane * 16;
+#ifdef PT_ABLATE
+        if (!(a.ablate & 8))
+#endif
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          *(__attribute__((address_space(3))) bf16x8_t*)(x + st * 2048) = acc_as_b(s, st);
+          *(__attribute__((address_space(3))) bf16x8_t*)(x + st * 2048 + 1024) = acc_as_b(dp, st);
+        }
+      }
+      if (qh) {
+        if (++qt == qt_begin + nq) qt = qt_begin;
+        if (++buf == NSTG) buf = 0;
+      }
+      end_step(j);
+    }
+  } else {
+    f32x16_t dk[DT], dv[DT];
+#pragma unroll
+    for (int i = 0; i < DT; ++i) { dk[i] = zero16(); dv[i] = zero16(); }
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __syncthreads();
+    int buf = 0;
+    for (int j = 0; j <= n_steps; ++j) {
+      stamp(j, 0);
+      if (issue(j)) stage_next();
+      const int h = j - 1, qh = h & 1;
+      if (j > 0 && !(a.causal && qt * KT + 32 * qh + 31 < k0)) {
+        const lds_u8* sq = smem + buf * STAGE_B;
+        const lds_u8* sdo = sq + TILE_B;
+        const lds_u8* x = xch + (h & 1) * kXchB + pr * 4096 + lane * 16;
+#ifdef PT_ABLATE
+        if (!(a.ablate & 1))
+#endif
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const bf16x8_t pb = *(const __attribute__((address_space(3))) bf16x8_t*)(x + st * 2048);
+          const bf16x8_t db = *(const __attribute__((address_space(3))) bf16x8_t*)(x + st * 2048 + 1024);
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            dv[dt] = mfma(rd_tr<D>(sdo, 2 * qh + st, dt, lane), pb, dv[dt]);
+            dk[dt] = mfma(rd_tr<D>(sq, 2 * qh + st, dt, lane), db, dk[dt]);
+          }
+        }
+      }
+      if (j > 0 && qh) {
+        if (++qt == qt_begin + nq) qt = qt_begin;
+        if (++buf == NSTG) buf = 0;
+      }
+      end_step(j);
+    }
+    if (!a.grad_f32) {
+      uint16_t* dkr = (uint16_t*)a.dk + b * a.dk_sb + (int64_t)mykey * a.dk_ss + hk * a.dk_sh;
+      uint16_t* dvr = (uint16_t*)a.dv + b * a.dv_sb + (int64_t)mykey * a.dv_ss + hk * a.dv_sh;
+      if (a.rope_cos) {
+        store_T_bf16_unrope<DT>(dkr, dk, a.scale, a.rope_cos + (int64_t)mykey * a.rope_ld,
+                                a.rope_sin + (int64_t)mykey * a.rope_ld, lane);
+      } else {
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) store_T_bf16(dkr, dt, dk[dt], a.scale, lane);
+      }
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) store_T_bf16(dvr, dt, dv[dt], 1.0f, lane);
+    } else {
+      float* dkr = (float*)a.dk + b * a.dk_sb + (int64_t)mykey * a.dk_ss + hk * a.dk_sh;
+      float* dvr = (float*)a.dv + b * a.dv_sb + (int64_t)mykey * a.dv_ss + hk * a.dv_sh;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        accum_T_f32(dkr, dt, dk[dt], a.scale, lane);
+        accum_T_f32(dvr, dt, dv[dt], 1.0f, lane);
+      }
+    }
+  }
+#ifdef PT_STAMP
+  if (a.stamps && wg_lin < 8)
+    for (int i = lane; i < 2 * kStampSteps; i += 64)
+      a.stamps[((int64_t)wg_lin * 8 + wave) * 2 * kStampSteps + i] = stl[i];
+#endif
+}
+
+template <int D>
+__global__ __launch_bounds__(8 * 64) void attn_bwd_dkdv_pair_kernel(AttnArgs a) {
+  int bx, hh, b;
+  attn_coords(a, bx, hh, b);
+  for (int pass = 0; pass <= a.pair; ++pass) {
+    if (pass) __syncthreads();
+    attn_bwd_dkdv_pair_block<D>(a, pass ? a.Sk / 128 - 1 - bx : bx, hh, b);
   }
 }
 
@@ -674,7 +930,7 @@ template <int D>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(D == 128 ? 2 : 1)))
 void attn_bwd_dq_kernel(AttnArgs a) {
   int bx, hh, b;
-  attn_coords(bx, hh, b);
+  attn_coords(a, bx, hh, b);
   for (int pass = 0; pass <= a.pair; ++pass) {  // one inlined body: no register growth
     if (pass) __syncthreads();
     attn_bwd_dq_block<D>(a, pass ? nqb_of(a) - 1 - bx : bx, hh, b);
@@ -694,6 +950,17 @@ bool pair_enabled() {
     v = (e && e[0] == '0') ? 0 : 1;
   }
   return v == 1;
+}
+
+// dK/dV kernel form per head dim: bit 0 = d64, bit 1 = d128 use the wave-pair split
+// (PICOTRON_ATTN_SPLIT, read per launch while it is being measured; default both)
+int split_mask() {
+  const char* e = getenv("PICOTRON_ATTN_SPLIT");
+  return e ? atoi(e) : 2;
+}
+int role_even() {
+  const char* e = getenv("PICOTRON_ATTN_ROLE_EVEN");
+  return e ? atoi(e) : 0;
 }
 
 int check_common(const AttnArgs& a, int D) {
@@ -825,23 +1092,43 @@ int attn_bwd_impl(const void* q, const int64_t* q_str, const void* k, const int6
   a.pair = causal && nqb % 2 == 0 && nkb % 2 == 0 && pair_enabled();
   const dim3 gq((unsigned)(a.pair ? nqb / 2 : nqb), (unsigned)H, (unsigned)B);
   const dim3 gk((unsigned)(a.pair ? nkb / 2 : nkb), (unsigned)HKV, (unsigned)B);
+  const int smem_pair = 3 * (2 * KT * (int)D * 2 + 2 * KT * 4) + 2 * kXchB + kStampB;
+  const bool split = (split_mask() >> (D == 64 ? 0 : 1)) & 1;
+  a.role_even = role_even();
+  a.prio = getenv("PICOTRON_ATTN_PRIO") ? atoi(getenv("PICOTRON_ATTN_PRIO")) : 1;
+#ifdef PT_STAMP
+  a.stamps = getenv("PICOTRON_ATTN_STAMPS") ? (unsigned long long*)strtoull(getenv("PICOTRON_ATTN_STAMPS"), nullptr, 10) : nullptr;
+#endif
+#ifdef PT_ABLATE
+  a.ablate = getenv("PICOTRON_ATTN_ABLATE") ? atoi(getenv("PICOTRON_ATTN_ABLATE")) : 0;
+#endif
   // dQ first: with delta_w set it produces the D the dK/dV kernel reads (same stream, in order)
   if (D == 64) {
-    set_smem(attn_bwd_dkdv_kernel<64>, smem_q);
     set_smem(attn_bwd_dq_kernel<64>, smem_kv);
     attn_bwd_dq_kernel<64><<<gq, NW * 64, smem_kv, stream>>>(a);
     PT_CHECK_LAUNCH();
     a.delta = a.delta_w ? a.delta_w : a.delta;
     a.delta_w = nullptr;
-    attn_bwd_dkdv_kernel<64><<<gk, NW * 64, smem_q, stream>>>(a);
+    if (split) {
+      set_smem(attn_bwd_dkdv_pair_kernel<64>, smem_pair);
+      attn_bwd_dkdv_pair_kernel<64><<<gk, 8 * 64, smem_pair, stream>>>(a);
+    } else {
+      set_smem(attn_bwd_dkdv_kernel<64>, smem_q);
+      attn_bwd_dkdv_kernel<64><<<gk, NW * 64, smem_q, stream>>>(a);
+    }
   } else {
-    set_smem(attn_bwd_dkdv_kernel<128>, smem_q);
     set_smem(attn_bwd_dq_kernel<128>, smem_kv);
     attn_bwd_dq_kernel<128><<<gq, NW * 64, smem_kv, stream>>>(a);
     PT_CHECK_LAUNCH();
     a.delta = a.delta_w ? a.delta_w : a.delta;
     a.delta_w = nullptr;
-    attn_bwd_dkdv_kernel<128><<<gk, NW * 64, smem_q, stream>>>(a);
+    if (split) {
+      set_smem(attn_bwd_dkdv_pair_kernel<128>, smem_pair);
+      attn_bwd_dkdv_pair_kernel<128><<<gk, 8 * 64, smem_pair, stream>>>(a);
+    } else {
+      set_smem(attn_bwd_dkdv_kernel<128>, smem_q);
+      attn_bwd_dkdv_kernel<128><<<gk, NW * 64, smem_q, stream>>>(a);
+    }
   }
   PT_CHECK_LAUNCH();
   return PT_OK;

@@ -661,6 +661,37 @@ def test_attention_fwd_bwd(B, S, H, HKV, D, causal):
     assert rel_err(dv, dv_ref) < 2e-2
 
 
+@pytest.mark.parametrize("B,S,H,HKV,D,causal,f32,rope", [
+    (2, 1024, 4, 4, 64, True, False, True), (1, 512, 4, 2, 64, True, False, False),
+    (1, 384, 2, 1, 64, True, False, False), (1, 512, 2, 2, 128, True, False, True),
+    (1, 1024, 4, 2, 128, False, True, False), (2, 256, 2, 2, 64, False, True, False),
+    (1, 2048, 2, 2, 128, True, False, False)])
+def test_attention_dkdv_wave_pair_split_is_bit_identical(monkeypatch, B, S, H, HKV, D, causal, f32, rope):
+    """The dK/dV kernel split over wave pairs (score wave -> P|dS hand-off -> accumulator wave) runs
+    the same MFMA operands in the same order as the one-wave kernel: dq, dk, dv bit-identical
+    (causal pairing on and off, GQA, d 64 / 128, f32 ring accumulators, fused RoPE backward)."""
+    from picotron_amd import kernels as K_
+    q, k, v = _qkv(B, S, H, HKV, D)
+    scale = 1 / math.sqrt(D)
+    o, lse = K_.attn_fwd(q, k, v, scale, causal)
+    do = torch.randn(o.shape).to(BF).to(DEV)
+    rp = None
+    if rope:
+        rp = tuple(t.to(DEV) for t in O.get_cos_sin(S, D, base=10000.0))
+    outs = []
+    for mask in ("0", "3"):
+        monkeypatch.setenv("PICOTRON_ATTN_SPLIT", mask)
+        if f32:
+            g = [torch.full((B, S, n, D), 0.25, device=DEV) for n in (H, HKV, HKV)]
+            K_.attn_bwd(do, q, k, v, o, lse, scale, causal, dq=g[0], dk=g[1], dv=g[2], grad_f32=True)
+        else:
+            g = K_.attn_bwd(do, q, k, v, o, lse, scale, causal, rope=rp)[:3]
+        torch.cuda.synchronize()
+        outs.append([t.clone() for t in g])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_attention_ring_merge_matches_full():
     """Two key blocks merged by the fused update_out_and_lse epilogue == attention over both
     (context_parallel.py:157-187), and the backward with the global LSE sums to the full grads."""

@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--H", type=int, default=32)
     ap.add_argument("--D", type=int, default=64)
     ap.add_argument("--old", default="")
+    ap.add_argument("--full", action="store_true",
+                    help="the CP ring's visiting block: no causal mask, f32 dq/dk/dv accumulators (grad_f32)")
     ap.add_argument("--rounds", type=int, default=2, help="interleaved rounds; medians are printed at the end")
     a = ap.parse_args()
     B, S, H, D = a.B, a.S, a.H, a.D
@@ -62,7 +64,10 @@ def main():
     q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
     do = torch.randn(B, S, H, D, device="cuda", generator=g).to(torch.bfloat16)
     scale = D ** -0.5
-    unit = 2.0 * B * H * S * S * D / 2
+    causal = not a.full
+    unit = 2.0 * B * H * S * S * D / (2 if causal else 1)
+    if a.full:
+        acc = [torch.zeros(B, S, H, D, device="cuda") for _ in range(3)]
     libs = {"new": _C.load_library()}
     for i, path in enumerate(x for x in a.old.split(",") if x):   # comma-separated: old, old1, old2 ...
         libs["old" if i == 0 else f"old{i}"] = _C.load_library(os.path.abspath(path), strict=False)
@@ -73,15 +78,29 @@ def main():
         order = order[rnd % len(order):] + order[:rnd % len(order)]   # rotate who goes first
         for name, lib in order:
             _C._lib = lib
-            o, lse = K.attn_fwd(q, k, v, scale, True)
+            o, lse = K.attn_fwd(q, k, v, scale, causal)
             delta = K.attn_delta(do, o)
-            dq, dk, dv, _ = K.attn_bwd(do, q, k, v, o, lse, scale, True, delta=delta)
+            if a.full:
+                for t in acc:
+                    t.zero_()
+                K.attn_bwd(do, q, k, v, o, lse, scale, False, dq=acc[0], dk=acc[1], dv=acc[2], grad_f32=True,
+                           delta=delta)
+                dq, dk, dv = acc
+
+                def bwd():
+                    K.attn_bwd(do, q, k, v, o, lse, scale, False, dq=acc[0], dk=acc[1], dv=acc[2], grad_f32=True,
+                               delta=delta)
+            else:
+                dq, dk, dv, _ = K.attn_bwd(do, q, k, v, o, lse, scale, True, delta=delta)
+
+                def bwd():
+                    K.attn_bwd(do, q, k, v, o, lse, scale, True, delta=delta)
             outs[name] = [t.clone() for t in (o, lse, dq, dk, dv)]
-            t_fwd = graph_us(lambda: K.attn_fwd(q, k, v, scale, True, out=o, lse=lse), a.reps)
-            t_bwd = graph_us(lambda: K.attn_bwd(do, q, k, v, o, lse, scale, True, delta=delta), a.reps)
+            t_fwd = graph_us(lambda: K.attn_fwd(q, k, v, scale, causal, out=o, lse=lse), a.reps)
+            t_bwd = graph_us(bwd, a.reps)
             med[name]["fwd"].append(t_fwd)
             med[name]["bwd"].append(t_bwd)
-            print(json.dumps({"lib": f"{name}:r{rnd}", "B": B, "S": S, "H": H, "D": D,
+            print(json.dumps({"lib": f"{name}:r{rnd}", "B": B, "S": S, "H": H, "D": D, "causal": causal,
                               "fwd_us": round(t_fwd, 1), "fwd_tflops": round(2 * unit / t_fwd / 1e6, 1),
                               "bwd_us": round(t_bwd, 1), "bwd_tflops": round(5 * unit / t_bwd / 1e6, 1),
                               "bwd_kernel_flop_tflops": round(7 * unit / t_bwd / 1e6, 1)}), flush=True)
