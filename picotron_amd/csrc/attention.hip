@@ -32,6 +32,15 @@ typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 
+// the d64 forward: a batch of LDS operand reads stays ahead of the MFMAs that consume it (no
+// scheduling across; 34.3 vs 34.9 us at the SmolLM layer shape; at d128 and in the backward kernels
+// the compiler's own interleave measured equal or faster).  -DPT_NO_BATCH: that interleave (A/B)
+#ifdef PT_NO_BATCH
+#define PT_BATCH_BARRIER(D) ((void)0)
+#else
+#define PT_BATCH_BARRIER(D) do { if constexpr ((D) == 64) __builtin_amdgcn_sched_barrier(0); } while (0)
+#endif
+
 namespace {
 
 constexpr float kLog2e = 1.4426950408889634f;
@@ -281,11 +290,19 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
     if (a.causal && kv0 > q0 + 31) return;  // wave-uniform: skip tiles fully above the diagonal
     {
       f32x16_t s[2];
+      // the tile's K operands in one batch of LDS reads ahead of the MFMAs (left to itself the
+      // compiler re-uses one register pair and waits out the LDS latency every MFMA or two)
+      bf16x8_t ka[2][KS];
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) ka[kh][ks] = rd_row<D>(sk, 32 * kh, ks, lane);
+      PT_BATCH_BARRIER(D);
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh) {
         s[kh] = zero16();
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) s[kh] = mfma(rd_row<D>(sk, 32 * kh, ks, lane), qf[ks], s[kh]);
+        for (int ks = 0; ks < KS; ++ks) s[kh] = mfma(ka[kh][ks], qf[ks], s[kh]);
       }
       // causal mask, diagonal tiles only: key row 32 kh + crow(r) visible iff <= thr
       if (a.causal && (kv0 + KT - 1 > q0)) {
@@ -324,10 +341,19 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
           l += p;
         }
 #pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        const bf16x8_t pb = acc_as_b(s[st >> 1], st & 1);
+      for (int half = 0; half < 2; ++half) {  // V operands of two k-steps per batch
+        bf16x8_t va[2][DT];
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt) o[dt] = mfma(rd_tr<D>(sv, st, dt, lane), pb, o[dt]);
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) va[u][dt] = rd_tr<D>(sv, 2 * half + u, dt, lane);
+        PT_BATCH_BARRIER(D);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const bf16x8_t pb = acc_as_b(s[half], u);
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) o[dt] = mfma(va[u][dt], pb, o[dt]);
+        }
       }
     }
   };
@@ -574,8 +600,8 @@ void attn_bwd_dkdv_kernel(AttnArgs a) {
 // bit-identical.
 constexpr int kXchB = 4 * 2 * 2 * 1024;  // one step's P|dS hand-off: 4 pairs x 2 k-steps x 2 kinds x 1 KiB
 #ifdef PT_STAMP
-constexpr int kStampSteps = 136;
-constexpr int kStampB = 8 * 2 * kStampSteps * 8;
+constexpr int kStampSteps = 72;
+constexpr int kStampB = 8 * 4 * kStampSteps * 8;
 #else
 constexpr int kStampB = 0;
 #endif
@@ -641,16 +667,16 @@ __device__ __forceinline__ void attn_bwd_dkdv_pair_block(const AttnArgs& a, int 
   auto issue = [&](int j) { return (j & 1) && (j >> 1) + 2 < n_tiles; };
 #ifdef PT_STAMP
   // per wave and step: (start, arrival at the end-of-step wait) in LDS past the hand-off buffers
-  unsigned long long* stl = (unsigned long long*)(xch + 2 * kXchB) + wave * 2 * kStampSteps;
+  unsigned long long* stl = (unsigned long long*)(xch + 2 * kXchB) + wave * 4 * kStampSteps;
   const int wg_lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
   auto stamp = [&](int j, int w) {
-    if (lane == 0 && j < kStampSteps) stl[2 * j + w] = __builtin_amdgcn_s_memtime();
+    if (lane == 0 && j < kStampSteps) stl[4 * j + w] = __builtin_amdgcn_s_memtime();
   };
 #else
   auto stamp = [&](int, int) {};
 #endif
   auto end_step = [&](int j) {
-    stamp(j, 1);
+    stamp(j, 3);
     if (j & 1) wait_keep(issue(j));
     __syncthreads();
   };
@@ -683,6 +709,19 @@ __device__ __forceinline__ void attn_bwd_dkdv_pair_block(const AttnArgs& a, int 
         const lds_u8* sdo = sq + TILE_B;
         const float* sl = (const float*)(sq + 2 * TILE_B);
         const float* sdel = sl + KT;
+        // every LDS operand of the step is read up front (the compiler otherwise re-uses one register
+        // pair and waits out the LDS latency every two MFMAs), then the MFMA chains
+        bf16x8_t qa[KS], da[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          qa[ks] = rd_row<D>(sq, 32 * qh, ks, lane);
+          da[ks] = rd_row<D>(sdo, 32 * qh, ks, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#ifdef PT_STAMP
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        stamp(j, 1);
+#endif
         f32x16_t s = zero16(), dp = zero16();
         // the score wave's MFMAs go first on the SIMD (its softmax then runs beside the partner's
         // MFMAs instead of after them)
@@ -692,10 +731,22 @@ __device__ __forceinline__ void attn_bwd_dkdv_pair_block(const AttnArgs& a, int 
 #endif
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-          s = mfma(rd_row<D>(sq, 32 * qh, ks, lane), kf[ks], s);
-          dp = mfma(rd_row<D>(sdo, 32 * qh, ks, lane), vf[ks], dp);
+          s = mfma(qa[ks], kf[ks], s);
+          dp = mfma(da[ks], vf[ks], dp);
         }
         if (a.prio) __builtin_amdgcn_s_setprio(0);
+#ifdef PT_STAMP
+        asm volatile("" ::"v"(s[15]), "v"(dp[15]));
+        stamp(j, 2);
+#endif
+        // the row constants, read while the MFMAs run
+        float lr[16], dr[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qi = 32 * qh + crow(r, lane);
+          lr[r] = sl[qi];
+          dr[r] = sdel[qi];
+        }
         if (a.causal && (qs < k0 + 31)) {  // diagonal: query row crow(r) sees my key iff >= thr
           const int thr = mykey - qs - 4 * (lane >> 5);
 #pragma unroll
@@ -707,10 +758,9 @@ __device__ __forceinline__ void attn_bwd_dkdv_pair_block(const AttnArgs& a, int 
 #endif
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int qi = 32 * qh + crow(r, lane);
-          const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -(sl[qi] * kLog2e)));
+          const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -(lr[r] * kLog2e)));
           s[r] = p;
-          dp[r] = p * (dp[r] - sdel[qi]);
+          dp[r] = p * (dp[r] - dr[r]);
         }
         lds_u8* x = xch + (j & 1) * kXchB + pr * 4096 + lane * 16;
 #ifdef PT_ABLATE
@@ -746,15 +796,37 @@ __device__ __forceinline__ void attn_bwd_dkdv_pair_block(const AttnArgs& a, int 
 #ifdef PT_ABLATE
         if (!(a.ablate & 1))
 #endif
+        {
+          // each k-step's LDS operands are read in one batch (the compiler otherwise re-uses one
+          // register pair and waits out the LDS latency every two MFMAs): k-step 1's batch is
+          // issued behind k-step 0's MFMAs
 #pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          const bf16x8_t pb = *(const __attribute__((address_space(3))) bf16x8_t*)(x + st * 2048);
-          const bf16x8_t db = *(const __attribute__((address_space(3))) bf16x8_t*)(x + st * 2048 + 1024);
+          for (int st = 0; st < 2; ++st) {
+            bf16x8_t ta[DT], tq[DT];
+            const bf16x8_t pb = *(const __attribute__((address_space(3))) bf16x8_t*)(x + st * 2048);
+            const bf16x8_t db = *(const __attribute__((address_space(3))) bf16x8_t*)(x + st * 2048 + 1024);
 #pragma unroll
-          for (int dt = 0; dt < DT; ++dt) {
-            dv[dt] = mfma(rd_tr<D>(sdo, 2 * qh + st, dt, lane), pb, dv[dt]);
-            dk[dt] = mfma(rd_tr<D>(sq, 2 * qh + st, dt, lane), db, dk[dt]);
+            for (int dt = 0; dt < DT; ++dt) {
+              ta[dt] = rd_tr<D>(sdo, 2 * qh + st, dt, lane);
+              tq[dt] = rd_tr<D>(sq, 2 * qh + st, dt, lane);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#ifdef PT_STAMP
+            if (st == 0) {
+              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+              stamp(j, 1);
+            }
+#endif
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) {
+              dv[dt] = mfma(ta[dt], pb, dv[dt]);
+              dk[dt] = mfma(tq[dt], db, dk[dt]);
+            }
           }
+#ifdef PT_STAMP
+          asm volatile("" ::"v"(dv[DT - 1][15]), "v"(dk[DT - 1][15]));
+          stamp(j, 2);
+#endif
         }
       }
       if (j > 0 && qh) {
@@ -787,8 +859,8 @@ __device__ __forceinline__ void attn_bwd_dkdv_pair_block(const AttnArgs& a, int 
   }
 #ifdef PT_STAMP
   if (a.stamps && wg_lin < 8)
-    for (int i = lane; i < 2 * kStampSteps; i += 64)
-      a.stamps[((int64_t)wg_lin * 8 + wave) * 2 * kStampSteps + i] = stl[i];
+    for (int i = lane; i < 4 * kStampSteps; i += 64)
+      a.stamps[((int64_t)wg_lin * 8 + wave) * 4 * kStampSteps + i] = stl[i];
 #endif
 }
 

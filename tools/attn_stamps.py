@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from picotron_amd import _C  # noqa: E402
 from picotron_amd import kernels as K  # noqa: E402
 
-STEPS = 136
+STEPS = 72
 
 
 def main():
@@ -32,30 +32,31 @@ def main():
     o, lse = K.attn_fwd(q, k, v, D ** -0.5, False)
     delta = K.attn_delta(do, o)
     acc = [torch.zeros(B, S, H, D, device="cuda") for _ in range(3)]
-    st = torch.zeros(8, 8, STEPS, 2, dtype=torch.int64, device="cuda")
+    st = torch.zeros(8, 8, STEPS, 4, dtype=torch.int64, device="cuda")
     os.environ["PICOTRON_ATTN_STAMPS"] = str(st.data_ptr())
     os.environ["PICOTRON_ATTN_SPLIT"] = "3"
     for _ in range(3):
         K.attn_bwd(do, q, k, v, o, lse, D ** -0.5, False, dq=acc[0], dk=acc[1], dv=acc[2], grad_f32=True, delta=delta)
     torch.cuda.synchronize()
     t = st.cpu()
-    nsteps = S // 64 * 2 + 1
+    nsteps = min(S // 64 * 2 + 1, STEPS)
+    import statistics
     for role, waves in (("score", range(0, 4)), ("accum", range(4, 8))):
-        work, wait = [], []
+        ph = {"lds operands": [], "mfma": [], "rest of work": [], "barrier wait": []}
         for wg in range(8):
             for w in waves:
-                for j in range(1, min(nsteps, STEPS) - 1):
-                    s0, arr, s1 = t[wg, w, j, 0].item(), t[wg, w, j, 1].item(), t[wg, w, j + 1, 0].item()
-                    work.append(arr - s0)
-                    wait.append(s1 - arr)
-        work.sort(), wait.sort()
-        med = lambda x: x[len(x) // 2]
-        print(f"{role}: work median {med(work)} p90 {work[int(len(work) * .9)]}  wait median {med(wait)} "
-              f"p90 {wait[int(len(wait) * .9)]} (cycles per step)")
-    odd = [t[0, 0, j + 1, 0].item() - t[0, 0, j, 0].item() for j in range(1, nsteps - 2, 2)]
-    even = [t[0, 0, j + 1, 0].item() - t[0, 0, j, 0].item() for j in range(2, nsteps - 2, 2)]
-    odd.sort(), even.sort()
-    print("step length wg0 wave0: odd (issue + wait) median", odd[len(odd) // 2], " even median", even[len(even) // 2])
+                for j in range(2, nsteps - 2):
+                    s0, s1, s2, s3 = (t[wg, w, j, i].item() for i in range(4))
+                    nxt = t[wg, w, j + 1, 0].item()
+                    if s1 == 0 or s2 == 0:
+                        continue
+                    ph["lds operands"].append(s1 - s0)
+                    ph["mfma"].append(s2 - s1)
+                    ph["rest of work"].append(s3 - s2)
+                    ph["barrier wait"].append(nxt - s3)
+        print(role, {k: int(statistics.median(v)) for k, v in ph.items() if v}, "(median cycles per step)")
+    steps = [t[0, 0, j + 1, 0].item() - t[0, 0, j, 0].item() for j in range(2, nsteps - 2)]
+    print("step length wg0 wave0 median", int(statistics.median(steps)))
 
 
 if __name__ == "__main__":
