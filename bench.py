@@ -15,7 +15,7 @@ The other BASELINE configs through the same step (process grid from
 setup_process_group_manager(tp, cp, 1, N / (tp cp)), train.py:95-100; apply_tensor_parallel /
 apply_context_parallel / DataParallelBucket in train.py's order):
     config 3  --tp 8                                  (SmolLM-1.7B TP=8 over xGMI, strong scaling)
-    config 4  --model llama2-7b --tp 2 (--gpus 4: dp2 tp2; PP is the reference's engine, not here)
+    config 4  --model llama2-7b --tp 2 --pp 2 --gpus 8  (dp2 tp2 pp2, 1F1B: pipeline_parallel/pipeline_parallel.py)
     config 5  --model llama2-7b --cp 8 --seq 32768 --mbs 1   (ring attention at 32k)
 One-GPU per-rank compute proxies (no collectives; what one rank of the multi-GPU run computes):
     --tp-proxy 8      the decoder stack + lm_head with TP=8 shard widths (q|k|v 3 x 256, I 1024)
@@ -155,7 +155,8 @@ def tp_proxy(args, base, layers):
             "roofline": {"bound": "mfma", "kernel": "gemm (every GEMM launch of one micro-batch)", "achieved": ach,
                          "peak": MI355X_BF16_DENSE_PEAK / 1e12, "unit": "TFLOP/s",
                          "frac": ach / (MI355X_BF16_DENSE_PEAK / 1e12), "launches": s["launches"],
-                         "gemm_share": s["total_ms"] * 1e-3 / t}}
+                         "gemm_share": s["total_ms"] * 1e-3 / t},
+            "gemm_by_launch": {k: {"launches": v[0], "ms": v[1], "tflops": v[2]} for k, v in probe.by_label().items()}}
 
 
 def cp_proxy(args, base, layers):
@@ -306,6 +307,8 @@ def build_parser():
     ap.add_argument("--layers", type=int, default=0, help="decoder layers (0 = the config's: 15 / 32)")
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (N GPUs = dp x tp x cp)")
     ap.add_argument("--cp", type=int, default=1, help="context-parallel (ring attention) degree")
+    ap.add_argument("--pp", type=int, default=1, help="pipeline-parallel degree (N GPUs = dp x tp x cp x pp)")
+    ap.add_argument("--pp-engine", choices=["1f1b", "afab"], default="1f1b", help="pipeline schedule (train.py:222-225)")
     ap.add_argument("--tp-proxy", type=int, default=0, help="1 GPU: one TP rank's compute at this degree")
     ap.add_argument("--cp-proxy", type=int, default=0, help="1 GPU: the CP ring's critical rank at this degree")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
@@ -380,21 +383,24 @@ def main():
         out = tp_proxy(args, base, layers) if args.tp_proxy else cp_proxy(args, base, layers)
         print(json.dumps(out), file=result_out, flush=True)
         return
-    tp, cp = args.tp, args.cp
-    if world % (tp * cp):
-        raise SystemExit(f"--gpus {world} is not a multiple of tp {tp} x cp {cp}")
-    dp = world // (tp * cp)
-    m = setup_process_group_manager(tp_size=tp, cp_size=cp, pp_size=1, dp_size=dp)
+    tp, cp, pp = args.tp, args.cp, args.pp
+    if world % (tp * cp * pp):
+        raise SystemExit(f"--gpus {world} is not a multiple of tp {tp} x cp {cp} x pp {pp}")
+    dp = world // (tp * cp * pp)
+    m = setup_process_group_manager(tp_size=tp, cp_size=cp, pp_size=pp, dp_size=dp)
     torch.manual_seed(42)
     cfg = make_config({k: v for k, v in base.items() if k != "_name"}, args.seq, num_hidden_layers=layers)
     t0 = time.time()
     with torch.device(device):
-        model = Llama(cfg)            # train.py:174-186 order: build, TP swap, (PP), CP, dtype, DP wrap
+        model = Llama(cfg)            # train.py:174-186 order: build, TP swap, PP, CP, dtype, DP wrap
         if tp > 1:
             apply_tensor_parallel(model)
+        num_params = count_params(model)   # the whole model (before a pipeline stage keeps its slice)
+        if pp > 1:
+            from picotron_amd.pipeline_parallel.pipeline_parallel import PipelineParallel
+            model = PipelineParallel(model, cfg)
     apply_context_parallel(model)
     model.to(torch.bfloat16)
-    num_params = count_params(model)
     if m.cp_dp_world_size > 1 or force_dp:
         model = DataParallelBucket(model, bucket_cap_mb=args.bucket_mb,
                                    grad_type=torch.bfloat16 if args.grad_type == "bf16" else torch.float32)
@@ -411,8 +417,19 @@ def main():
         # on all ~550 GEMM launches of a step costs ~5 % of the step on ROCm
         K._PROBE = probe if (probe is not None and i == probe_mb) else None
 
+    if pp > 1:
+        from picotron_amd.pipeline_parallel import pipeline_parallel as PPE
+        pp_step = PPE.train_step_pipeline_1f1b if args.pp_engine == "1f1b" else PPE.train_step_pipeline_afab
+        shapes = (args.mbs, args.seq // cp, cfg.hidden_size)
+
     def step():
         optimizer.zero_grad()
+        if pp > 1:   # train.py:222-225 (the GEMM probe samples micro-batches of train_step only)
+            loss = pp_step(model, loader, shapes, device, torch.bfloat16)
+            if hasattr(model, "reset"):
+                model.reset()
+            optimizer.step()
+            return loss
         loss = train_step(model, loader, device, on_microbatch=sample)
         optimizer.step()
         if hasattr(model, "reset"):
@@ -429,7 +446,7 @@ def main():
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     losses = []
-    probe = K.GemmProbe() if not args.no_probe else None
+    probe = K.GemmProbe() if not (args.no_probe or pp > 1) else None
     for i in range(args.steps):
         losses.append(step())
         log(f"step {i}: loss {losses[-1]:.4f}")
@@ -443,7 +460,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
 
-    tokens = dp * args.grad_acc * args.mbs * args.seq * args.steps    # tp / cp ranks share their tokens
+    tokens = dp * args.grad_acc * args.mbs * args.seq * args.steps    # tp / cp / pp ranks share their tokens
+    if pp > 1 and losses:   # the loss lives on the last stage: report it from rank 0 too
+        lt = torch.tensor([losses[-1]], dtype=torch.float64, device=device)
+        dist.all_reduce(lt, op=dist.ReduceOp.SUM, group=m.pp_group)
+        losses[-1] = lt.item()
     value = tokens / elapsed
     per_gpu = value / world
     fpt = flops_per_token(num_params, cfg)
@@ -473,13 +494,15 @@ def main():
         cpu = cpu_baseline(cfg, args.cpu_tokens)
 
     if rank == 0:
-        par = "-".join(f"{k}{v}" for k, v in (("dp", dp), ("tp", tp), ("cp", cp)) if v > 1 or k == "dp")
+        par = "-".join(f"{k}{v}" for k, v in (("dp", dp), ("tp", tp), ("cp", cp), ("pp", pp)) if v > 1 or k == "dp")
+        if pp > 1:
+            par += f"-{args.pp_engine}"
         out = {"metric": "tokens/s/GPU and MFU, SmolLM-1.7B seq1024 at 1/2/4/8 MI355X", "value": value,
                "unit": "tokens/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ranks": dist.get_world_size() if dist.is_initialized() else 1,
                "backend": dist.get_backend() if dist.is_initialized() else None,
                "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-               "scaling": "weak" if tp * cp == 1 else "strong",
+               "scaling": "weak" if tp * cp * pp == 1 else "strong",
                "vs_baseline": None, "dtype": "bf16", "data": "synthetic (seeded random tokens, random init)",
                "tokens_per_s_per_gpu": per_gpu, "mfu": mfu, "flops_per_token": fpt, "num_params": num_params,
                "final_loss": losses[-1] if losses else None,

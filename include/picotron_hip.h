@@ -47,6 +47,13 @@ int pt_rmsnorm_bwd_partials(int64_t rows, int cols);
 int pt_rmsnorm_bwd(const void* dy, const void* z, const void* weight, const float* rstd, const void* dres,
                    void* dx, void* dweight, float* dw_partial, int64_t rows, int64_t cols, int mode,
                    hipStream_t stream);
+/* pt_rmsnorm_bwd with dy given as the two f32 K halves of a split-K dX GEMM (pt_gemm_dual / pt_gemm
+ * with EPI_F32 partials: contiguous [rows, cols]): dy = bf16(dy_p0 + dy_p1) is formed in the kernel,
+ * bit-identical to pt_gemm_splitk_sum followed by pt_rmsnorm_bwd without writing and re-reading dy.
+ * (The post_attention_layernorm backward behind the gate|up dX, model.py:206-208.) */
+int pt_rmsnorm_bwd_splitk(const float* dy_p0, const float* dy_p1, const void* z, const void* weight,
+                          const float* rstd, const void* dres, void* dx, void* dweight, float* dw_partial,
+                          int64_t rows, int64_t cols, int mode, hipStream_t stream);
 /* the dweight column sums of n <= 32 pt_rmsnorm_bwd calls made with dweight = NULL (their
  * dw_partial buffers, pt_rmsnorm_bwd_partials rows each), one launch; sinks[i] as the dweight sink
  * bits of pt_rmsnorm_bwd's mode.  Bit-identical to passing dweight to each call.  (An

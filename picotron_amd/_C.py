@@ -42,6 +42,7 @@ SIGNATURES = {
     "pt_adamw_step_multi": (_i32, [_vp, _vp, _i32, _i64, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _vp]),
     "pt_rmsnorm_bwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp]),
     "pt_rmsnorm_colsum_batch": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _vp]),
+    "pt_rmsnorm_bwd_splitk": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp]),
     "pt_rope": (_i32, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _i32, _vp]),
     "pt_swiglu_fwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp]),
     "pt_swiglu_bwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp]),

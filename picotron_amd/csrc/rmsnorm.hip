@@ -121,11 +121,30 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(min_wa
 // dx = dz (+ dres when the residual branch gradient is fused in)
 // dw partial per block: sum over this block's rows of dy * xh (mode 1: dy * bf16(xh)), the block's
 // waves combined through LDS in a fixed order -> one partial row per block (deterministic).
-template <int NCH, int WPB>
+// SPLIT: dy arrives as the two f32 K halves of a split-K dX GEMM (gemm.hip splitk_sum2_kernel's
+// inputs) and is formed here as bf16(p0 + p1) -- the sum pass's own rounding -- so the bf16 dy is
+// never written and re-read (dy_p1 = the second half; dy = the first, as float)
+template <int NCH>
+__device__ __forceinline__ void load_split_row(const float* __restrict__ p0, const float* __restrict__ p1, int lane,
+                                               int nchunk, bf16x8 (&v)[NCH]) {
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int c = lane + i * PT_WAVE;
+    if (c < nchunk) {
+      const float4 a0 = *(const float4*)(p0 + c * 8), a1 = *(const float4*)(p0 + c * 8 + 4);
+      const float4 b0 = *(const float4*)(p1 + c * 8), b1 = *(const float4*)(p1 + c * 8 + 4);
+      float f[8] = {a0.x + b0.x, a0.y + b0.y, a0.z + b0.z, a0.w + b0.w,
+                    a1.x + b1.x, a1.y + b1.y, a1.z + b1.z, a1.w + b1.w};
+      v[i] = pack8(f);
+    }
+  }
+}
+
+template <int NCH, int WPB, bool SPLIT = false>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(min_waves<NCH>()))) void rmsnorm_bwd_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ z, const uint16_t* __restrict__ w,
     const float* __restrict__ rstd_in, const uint16_t* __restrict__ dres, uint16_t* __restrict__ dx,
-    float* __restrict__ dw_partial, int64_t rows, int cols, int mode) {
+    float* __restrict__ dw_partial, int64_t rows, int cols, int mode, const float* __restrict__ dy_p1 = nullptr) {
   extern __shared__ float red[];  // [WPB][cols]
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -147,7 +166,10 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(min_wa
   for (; row < rows; row += stride) {
     bf16x8 zc[NCH], dc[NCH], rc[NCH];
     load_row<NCH>(z + row * cols, lane, nchunk, zc);
-    load_row<NCH>(dy + row * cols, lane, nchunk, dc);
+    if constexpr (SPLIT)
+      load_split_row<NCH>((const float*)dy + row * cols, dy_p1 + row * cols, lane, nchunk, dc);
+    else
+      load_row<NCH>(dy + row * cols, lane, nchunk, dc);
     if (dres) load_row<NCH>(dres + row * cols, lane, nchunk, rc);
     const float rstd = rstd_in[row];
     float dot = 0.f;
@@ -315,22 +337,23 @@ void launch_fwd(int wpb, int grid, hipStream_t s, const uint16_t* X, const uint1
   else rmsnorm_fwd_kernel<NCH, 4><<<grid, 256, 0, s>>>(X, R, W, Y, Z, rstd, rows, cols, eps, mode);
 }
 
-template <int NCH>
+template <int NCH, bool SPLIT = false>
 void launch_bwd(int wpb, int grid, hipStream_t s, const uint16_t* DY, const uint16_t* Z, const uint16_t* W,
-                const float* rstd, const uint16_t* DR, uint16_t* DX, float* part, int64_t rows, int cols, int mode) {
+                const float* rstd, const uint16_t* DR, uint16_t* DX, float* part, int64_t rows, int cols, int mode,
+                const float* P1 = nullptr) {
   const size_t lds = (size_t)wpb * cols * sizeof(float);
   if (wpb == 16) {
     static bool attr = false;
     if (!attr) {
-      (void)hipFuncSetAttribute((const void*)rmsnorm_bwd_kernel<NCH, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024);
+      (void)hipFuncSetAttribute((const void*)rmsnorm_bwd_kernel<NCH, 16, SPLIT>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr = true;
     }
-    rmsnorm_bwd_kernel<NCH, 16><<<grid, 1024, lds, s>>>(DY, Z, W, rstd, DR, DX, part, rows, cols, mode);
+    rmsnorm_bwd_kernel<NCH, 16, SPLIT><<<grid, 1024, lds, s>>>(DY, Z, W, rstd, DR, DX, part, rows, cols, mode, P1);
   } else if (wpb == 8) {
-    rmsnorm_bwd_kernel<NCH, 8><<<grid, 512, lds, s>>>(DY, Z, W, rstd, DR, DX, part, rows, cols, mode);
+    rmsnorm_bwd_kernel<NCH, 8, SPLIT><<<grid, 512, lds, s>>>(DY, Z, W, rstd, DR, DX, part, rows, cols, mode, P1);
   } else {
-    rmsnorm_bwd_kernel<NCH, 4><<<grid, 256, lds, s>>>(DY, Z, W, rstd, DR, DX, part, rows, cols, mode);
+    rmsnorm_bwd_kernel<NCH, 4, SPLIT><<<grid, 256, lds, s>>>(DY, Z, W, rstd, DR, DX, part, rows, cols, mode, P1);
   }
 }
 
@@ -394,6 +417,45 @@ int pt_rmsnorm_bwd(const void* dy, const void* z, const void* weight, const floa
     case 2: launch_bwd<2>(wpb, grid, stream, DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
     case 4: launch_bwd<4>(wpb, grid, stream, DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
     case 8: launch_bwd<8>(wpb, grid, stream, DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
+    default: return PT_EUNSUPPORTED;
+  }
+  PT_CHECK_LAUNCH();
+  if (dweight) {
+    colsum_kernel<<<(int)((cols + kCsCols - 1) / kCsCols), kCsThreads, 0, stream>>>(
+        dw_partial, grid, (int)cols, dweight, mode & (PT_DW_ACC_BF16 | PT_DW_ACC_F32));
+    PT_CHECK_LAUNCH();
+  }
+  return PT_OK;
+}
+
+// pt_rmsnorm_bwd with dy = bf16(dy_p0 + dy_p1): the two f32 K halves [rows, cols] (contiguous) of a
+// split-K dX GEMM, summed here instead of by pt_gemm_splitk_sum (bit-identical to that sum followed
+// by pt_rmsnorm_bwd)
+int pt_rmsnorm_bwd_splitk(const float* dy_p0, const float* dy_p1, const void* z, const void* weight,
+                          const float* rstd, const void* dres, void* dx, void* dweight, float* dw_partial,
+                          int64_t rows, int64_t cols, int mode, hipStream_t stream) {
+  if (!dy_p0 || !dy_p1 || !z || !weight || !rstd || !dx || !dw_partial || rows <= 0 || cols <= 0 || (cols & 7))
+    return PT_EINVAL;
+  if (!pt_aligned16(dy_p0) || !pt_aligned16(dy_p1) || !pt_aligned16(z) || !pt_aligned16(dx) ||
+      (dres && !pt_aligned16(dres)))
+    return PT_EALIGN;
+  const int nch = nch_for((int)cols);
+  if (nch < 0) return PT_EUNSUPPORTED;
+  const int nmode = mode & 3;
+  if (nmode > 1 || (mode & PT_DW_ACC_BF16 && mode & PT_DW_ACC_F32)) return PT_EINVAL;
+  const NormCfg& c = norm_cfg();
+  const int wpb = bwd_wpb(nch, c);
+  const int grid = grid_for(rows, wpb, c.bwd_bpc);
+  const auto* P0 = (const uint16_t*)dy_p0;  // reinterpreted as float inside the SPLIT kernel
+  const auto* Z = (const uint16_t*)z;
+  const auto* W = (const uint16_t*)weight;
+  const auto* DR = (const uint16_t*)dres;
+  auto* DX = (uint16_t*)dx;
+  switch (nch) {
+    case 1: launch_bwd<1, true>(wpb, grid, stream, P0, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode, dy_p1); break;
+    case 2: launch_bwd<2, true>(wpb, grid, stream, P0, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode, dy_p1); break;
+    case 4: launch_bwd<4, true>(wpb, grid, stream, P0, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode, dy_p1); break;
+    case 8: launch_bwd<8, true>(wpb, grid, stream, P0, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode, dy_p1); break;
     default: return PT_EUNSUPPORTED;
   }
   PT_CHECK_LAUNCH();

@@ -102,7 +102,7 @@ def wgrad_group(jobs):
             _grad_ready(p)
 
 
-def dgrad_with_wgrad(dy2d, weights, wjobs, gu=None):
+def dgrad_with_wgrad(dy2d, weights, wjobs, gu=None, keep_parts=False):
     """dX = dY . [W_0; ...] (with gu: the down_proj dX's SwiGLU backward, dg|du) AND the wgrads
     wjobs [(dy2d, x2d, params)] of the same layer in ONE launch (K.linear_dgrad_dual) when the
     shapes tile for it and every sink takes one epilogue; otherwise the separate launches.
@@ -116,7 +116,7 @@ def dgrad_with_wgrad(dy2d, weights, wjobs, gu=None):
         if len(epis) == 1:
             epi = epis.pop()
             wk = [(dy, x, [t for t, _ in tg]) for (dy, x, _), tg in zip(wjobs, targets)]
-            dx = K.linear_dgrad_dual(dy2d, weights, wk, epi, gu=gu)
+            dx = K.linear_dgrad_dual(dy2d, weights, wk, epi, gu=gu, keep_parts=keep_parts)
             if dx is None:   # not tileable after all: the same sinks, separate launches
                 dx = K.linear_dgrad_swiglu(dy2d, weights[0], gu) if gu is not None else K.linear_dgrad(dy2d, weights)
                 K.linear_wgrad_grouped(wk, epilogue=epi)
@@ -477,7 +477,7 @@ class AttentionFunction(torch.autograd.Function):
 def mlp_block_fwd(h2, wg, wu, wd, tp, residual=None):
     """h2 [T,H] -> down(silu(gate) * up) (+ residual, entering the tp sum once, from tp rank 0)."""
     I = wg.shape[0]
-    if _fuse() and K.swiglu_fusable(h2.shape[0], I):   # SwiGLU in the gate|up GEMM's epilogue
+    if _fuse() and K.swiglu_fuse_pays(h2.shape[0], I):   # SwiGLU in the gate|up GEMM's epilogue
         gu, hh = K.linear_swiglu_fwd(h2, wg, wu)
     else:
         gu = K.linear_fwd(h2, [wg, wu])
@@ -492,10 +492,12 @@ def _dual_gu_enabled():
     return os.environ.get("PICOTRON_DUAL_GU", "1") != "0"
 
 
-def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True):
+def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True, keep_parts=False):
+    """keep_parts: the gate|up dX may come back as K.SplitKParts (its split-K halves unsummed) for a
+    following rmsnorm backward to sum."""
     gu, hh = saved
     I = wg.shape[0]
-    if _fuse() and K.swiglu_fusable(dm.shape[0], I, backward=True):   # SwiGLU bwd in the down dX epilogue
+    if _fuse() and K.swiglu_fuse_pays(dm.shape[0], I, backward=True):   # SwiGLU bwd in the down dX epilogue
         # ... in one launch with the down_proj dW: the epilogue's HBM-bound g|u / dg|du tail
         # overlaps the dW's MFMA work (K.linear_dgrad_dual)
         dgu = dgrad_with_wgrad(dm, [wd], [(dm, hh, [wd])], gu=gu)
@@ -509,7 +511,7 @@ def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True):
             K._splitk_halves(dgu.shape[0], h2.shape[1], dgu.shape[1]) is not None:
         # the split-K gate|up dX (two f32 K halves, 256 tiles) and the gate|up dW (512 tiles) in one
         # dual launch: 3 whole rounds of the 256 CUs (no TP all-reduce to overlap at tp = 1)
-        return dgrad_with_wgrad(dgu, [wg, wu], [(dgu, h2, [wg, wu])])
+        return dgrad_with_wgrad(dgu, [wg, wu], [(dgu, h2, [wg, wu])], keep_parts=keep_parts)
     if need_dx:
         dh = K.linear_dgrad(dgu, [wg, wu])
         handle = tp.all_reduce(dh, async_op=True)
@@ -570,7 +572,8 @@ class DecoderLayerFunction(torch.autograd.Function):
         sh, mode = ctx.sh, ctx.mode
         tp = TPContext.current()
         dout2 = _contig2d(dout)
-        dh2 = mlp_block_bwd(dout2, h2, (gu, hh), wg, wu, wd, tp)
+        # the gate|up dX's split-K halves go straight into the norm backward (summed there)
+        dh2 = mlp_block_bwd(dout2, h2, (gu, hh), wg, wu, wd, tp, keep_parts=K.norm_splitk_enabled())
         dz = norm_bwd(dh2, z, w2, rstd2, mode, dres=dout2)
         dh1 = attn_block_bwd(dz, h1, (qkv, o, lse), wq, wk, wv, wo, cos, sin, sh, tp)
         dx = norm_bwd(dh1, x2, w1, rstd1, mode, dres=dz)   # (norm_bwd skips dW of frozen weights)

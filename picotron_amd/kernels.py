@@ -8,6 +8,7 @@ validates with asserts (e.g. picotron/model.py:95-96, tensor_parallel.py:81,151,
 import math
 
 import os
+import sys
 
 import torch
 
@@ -58,13 +59,32 @@ def rmsnorm_fwd(x, weight, eps, mode=MODE_TRITON, residual=None):
 DW_ACC_BF16, DW_ACC_F32 = 4, 8   # pt_rmsnorm_bwd dweight sinks (include/picotron_hip.h)
 
 
+class SplitKParts:
+    """A split-K dX GEMM's result before its sum pass: two f32 K halves [rows, cols] whose
+    bf16(p0 + p1) is the dX (linear_dgrad_dual(keep_parts=True)).  rmsnorm_bwd takes it as its dy
+    and sums in the norm kernel; anything else calls .sum() for the bf16 tensor."""
+
+    def __init__(self, p0, p1):
+        self.p0, self.p1 = p0, p1
+        self.shape, self.device = p0.shape, p0.device
+
+    def sum(self):
+        out = torch.empty(self.shape, dtype=BF16, device=self.device)
+        rc = _C.lib().pt_gemm_splitk_sum(_ptr(self.p0), _ptr(self.p1), None, _ptr(out), out.numel(),
+                                         _C.stream_ptr(self.device))
+        _C.check(rc, "pt_gemm_splitk_sum")
+        return out
+
+
 def rmsnorm_bwd(dy, z, weight, rstd, mode=MODE_TRITON, dres=None, dw_out=None, dw_sink=0, defer_dw=False):
     """Returns (dx, dweight).  dres (same shape as dy) is added into dx when given.
     dw_out/dw_sink: write the weight gradient into an existing buffer -- 0 store (bf16),
     DW_ACC_BF16 accumulate into a bf16 .grad, DW_ACC_F32 accumulate into an f32 main_grad.
     defer_dw: no column sum; returns (dx, partial) -- the f32 per-block partial rows, to be summed
-    into the sink later by rmsnorm_colsum_batch."""
-    dy = dy.contiguous()
+    into the sink later by rmsnorm_colsum_batch.  dy may be a SplitKParts (summed in the kernel)."""
+    split = isinstance(dy, SplitKParts)
+    if not split:
+        dy = dy.contiguous()
     rows, cols = z.shape
     lib = _C.lib()
     nparts = lib.pt_rmsnorm_bwd_partials(rows, cols)
@@ -80,9 +100,16 @@ def rmsnorm_bwd(dy, z, weight, rstd, mode=MODE_TRITON, dres=None, dw_out=None, d
         _req(dw_out.dtype == (torch.float32 if dw_sink == DW_ACC_F32 else BF16), "dweight buffer dtype")
     if dres is not None:
         dres = dres.contiguous()
-    rc = lib.pt_rmsnorm_bwd(_ptr(dy), _ptr(z), _ptr(weight), _ptr(rstd), _ptr(dres), _ptr(dx), _ptr(dw_out),
-                            _ptr(partial), rows, cols, int(mode) | int(dw_sink), _C.stream_ptr(z.device))
-    _C.check(rc, "pt_rmsnorm_bwd")
+    if split:
+        _req(dy.p0.is_contiguous() and dy.p1.is_contiguous() and tuple(dy.shape) == (rows, cols), "split dy parts")
+        rc = lib.pt_rmsnorm_bwd_splitk(_ptr(dy.p0), _ptr(dy.p1), _ptr(z), _ptr(weight), _ptr(rstd), _ptr(dres), _ptr(dx),
+                                       _ptr(dw_out), _ptr(partial), rows, cols, int(mode) | int(dw_sink),
+                                       _C.stream_ptr(z.device))
+        _C.check(rc, "pt_rmsnorm_bwd_splitk")
+    else:
+        rc = lib.pt_rmsnorm_bwd(_ptr(dy), _ptr(z), _ptr(weight), _ptr(rstd), _ptr(dres), _ptr(dx), _ptr(dw_out),
+                                _ptr(partial), rows, cols, int(mode) | int(dw_sink), _C.stream_ptr(z.device))
+        _C.check(rc, "pt_rmsnorm_bwd")
     return dx, (partial if defer_dw else dw_out)
 
 
@@ -437,6 +464,16 @@ class GemmProbe:
                 "avg_ms": sum(ms) / max(n, 1), "avg_flop": sum(flops) / max(n, 1),
                 "avg_alg_bytes": sum(byts) / max(n, 1)}
 
+    def by_label(self):
+        """{label: (launches, total ms, TF/s)} -- which GEMM shapes / launch kinds take the time."""
+        torch.cuda.synchronize()
+        out = {}
+        for r in self.records:
+            n, t, f = out.get(r[4], (0, 0.0, 0.0))
+            out[r[4]] = (n + 1, t + r[0].elapsed_time(r[1]), f + r[2])
+        return {k: (n, round(t, 4), round(f / (t * 1e-3) / 1e12, 1)) for k, (n, t, f) in
+                sorted(out.items(), key=lambda kv: -kv[1][1])}
+
 
 def _alg_bytes(M, N, K, epilogue):
     """Algorithmic HBM bytes of one GEMM launch: A and B read once, C written once (read too when
@@ -470,7 +507,8 @@ def _gemm(A, lda, a_kcontig, Bs, ldbs, b_bounds, b_kcontig, b_seg_dim, Cs, ldcs,
     _C.check(rc, f"pt_gemm(M={M}, N={N}, K={K}, a_k={a_kcontig}, b_k={b_kcontig}, epi={epilogue})")
     if probe is not None:
         ev1.record()
-        probe.records.append((ev0, ev1, 2.0 * M * N * K, _alg_bytes(M, N, K, epilogue)))
+        probe.records.append((ev0, ev1, 2.0 * M * N * K, _alg_bytes(M, N, K, epilogue),
+                              f"gemm {M}x{N}x{K} e{epilogue} t{tile}"))
 
 
 def _bounds(sizes):
@@ -558,7 +596,7 @@ def _wgrad_ksplit_run(jobs, epilogue, s):
         _C.check(rc, "pt_gemm_splitk_reduce")
     if probe is not None:
         ev1.record()
-        probe.records.append((ev0, ev1, flops, nbytes))
+        probe.records.append((ev0, ev1, flops, nbytes, sys._getframe().f_code.co_name))
 
 
 def linear_wgrad_grouped(jobs, epilogue=EPI_BF16, tile=-1):
@@ -590,7 +628,7 @@ def linear_wgrad_grouped(jobs, epilogue=EPI_BF16, tile=-1):
     _C.check(rc, f"pt_gemm_grouped({len(jobs)} problems, epi={epilogue})")
     if probe is not None:
         ev1.record()
-        probe.records.append((ev0, ev1, flops, nbytes))
+        probe.records.append((ev0, ev1, flops, nbytes, sys._getframe().f_code.co_name))
 
 
 def linear_fwd(x2d, weights, out=None, tile=-1, residual=None):
@@ -629,6 +667,10 @@ def rope_fusable(T, head_dim, seq_len, widths=()):
     return head_dim == 64 and T % 256 == 0 and T % seq_len == 0 and all(w % 128 == 0 for w in widths)
 
 
+# fewer 256x256 tiles than this: q|k|v + RoPE as a plain GEMM + rope kernel (PICOTRON_ROPE_FUSE_MIN_TILES)
+_ROPE_FUSE_MIN_TILES = int(os.environ.get("PICOTRON_ROPE_FUSE_MIN_TILES", "96"))
+
+
 def linear_fwd_rope(x2d, weights, cos, sin, seq_len, rot_heads, head_dim):
     """Y = x . [W_0; ...]^T with the first rot_heads heads of every row rotated by RoPE in the GEMM
     epilogue (model.py:124-126 + 136-137: the q|k|v projection, then apply_rotary_emb on q and k)."""
@@ -641,6 +683,12 @@ def linear_fwd_rope(x2d, weights, cos, sin, seq_len, rot_heads, head_dim):
     _req(cos.shape[0] >= seq_len and rope_fusable(T, head_dim, seq_len), "linear_fwd_rope: shape")
     ns = [w.shape[0] for w in weights]
     N = sum(ns)
+    if (T // 256) * (N // 256) < _ROPE_FUSE_MIN_TILES:
+        # a TP shard's q|k|v (TP = 8: N 768, 48 tiles of 256x256 on 256 CUs): the phased kernels
+        # the RoPE epilogue needs would leave most CUs idle; the plain GEMM picks a smaller tile and
+        # csrc/rope.hip rotates q|k after it (bit-identical to the fused epilogue)
+        y = linear_fwd(x2d, weights)
+        return rope_(y, rot_heads, head_dim, cos, sin, seq_len)
     y = torch.empty(T, N, dtype=BF16, device=x2d.device)
     probe = _PROBE
     if probe is not None:
@@ -652,7 +700,7 @@ def linear_fwd_rope(x2d, weights, cos, sin, seq_len, rot_heads, head_dim):
     _C.check(rc, "pt_gemm_rope")
     if probe is not None:
         ev1.record()
-        probe.records.append((ev0, ev1, 2.0 * T * N * K, _alg_bytes(T, N, K, EPI_BF16)))
+        probe.records.append((ev0, ev1, 2.0 * T * N * K, _alg_bytes(T, N, K, EPI_BF16), sys._getframe().f_code.co_name))
     return y
 
 
@@ -692,7 +740,7 @@ def linear_ce_stats(x2d, weight):
     _C.check(rc, "pt_gemm_ce_stats")
     if probe is not None:
         ev1.record()
-        probe.records.append((ev0, ev1, 2.0 * T * V * K, _alg_bytes(T, V, K, EPI_BF16)))
+        probe.records.append((ev0, ev1, 2.0 * T * V * K, _alg_bytes(T, V, K, EPI_BF16), sys._getframe().f_code.co_name))
     return y, stats
 
 
@@ -721,6 +769,20 @@ def cross_entropy_loss_lse_stats(logits, targets, stats, ignore_index=-100, out_
 def swiglu_fusable(T, I, backward=False):
     """Shapes the SwiGLU-fused projections tile (8-phase kernel: T % 256, I % 128 (fwd) / 256 (bwd))."""
     return T % 256 == 0 and I % (256 if backward else 128) == 0
+
+
+# fewer 256-row x (128 fwd / 256 bwd)-column tiles than this: the SwiGLU runs as its own kernel
+# beside a plain GEMM (whose auto tile fills the CUs) -- a TP shard's I (TP = 8: 1024; 128 tiles
+# on 256 CUs); bit-identical either way.  The backward keeps its fused dual launch at every width
+# (TP = 8 proxy: 8.95 vs 9.08 ms per micro-batch split).  PICOTRON_SWIGLU_FUSE_MIN_TILES / _BWD_MIN_TILES.
+_SWIGLU_FUSE_MIN_TILES = int(os.environ.get("PICOTRON_SWIGLU_FUSE_MIN_TILES", "192"))
+_SWIGLU_BWD_MIN_TILES = int(os.environ.get("PICOTRON_SWIGLU_BWD_MIN_TILES", "0"))
+
+
+def swiglu_fuse_pays(T, I, backward=False):
+    """swiglu_fusable and enough tiles that the fused (8-phase 256x256) launch fills the CUs."""
+    tiles = (T // 256) * (I // (256 if backward else 128))
+    return swiglu_fusable(T, I, backward) and tiles >= (_SWIGLU_BWD_MIN_TILES if backward else _SWIGLU_FUSE_MIN_TILES)
 
 
 def linear_swiglu_fwd(x2d, wg, wu):
@@ -797,7 +859,7 @@ def _splitk_run(probs, b_kcontig, parts, residual, out, flops, nbytes, device):
     _C.check(rc, "pt_gemm_splitk_sum")
     if probe is not None:
         ev1.record()
-        probe.records.append((ev0, ev1, flops, nbytes))
+        probe.records.append((ev0, ev1, flops, nbytes, sys._getframe().f_code.co_name))
     return out
 
 
@@ -869,7 +931,13 @@ def dual_fits(dgrad_mn, wgrad_mns):
     return ok([dgrad_mn]) and ok(wgrad_mns)
 
 
-def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None):
+def norm_splitk_enabled():
+    """The post-attention norm backward takes the gate|up dX's split-K halves directly
+    (PICOTRON_NORM_SPLITK=0: the sum pass + the plain norm backward, A/B only)."""
+    return os.environ.get("PICOTRON_NORM_SPLITK", "1") != "0"
+
+
+def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None, keep_parts=False):
     """dX = dY . [W_0; ...] (or, with gu, the SwiGLU backward dg|du of the down_proj dX:
     linear_dgrad_swiglu) AND the wgrads wjobs [(dy2d, x2d, outs)] (linear_wgrad, epilogue
     wepilogue) in ONE launch (pt_gemm_dual).  Returns dX / dg|du, or None (nothing launched) when
@@ -949,12 +1017,15 @@ def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None):
                                             int(wepilogue), None, 0, _C.stream_ptr(dy2d.device))
         _C.check(rc, "pt_gemm_splitk_reduce")
     if e0 == EPI_F32:
-        rc = _C.lib().pt_gemm_splitk_sum(_ptr(parts[0]), _ptr(parts[1]), None, _ptr(dx), dx.numel(),
-                                         _C.stream_ptr(dy2d.device))
-        _C.check(rc, "pt_gemm_splitk_sum")
+        if keep_parts:   # the consumer (rmsnorm_bwd) sums the halves
+            dx = SplitKParts(parts[0], parts[1])
+        else:
+            rc = _C.lib().pt_gemm_splitk_sum(_ptr(parts[0]), _ptr(parts[1]), None, _ptr(dx), dx.numel(),
+                                             _C.stream_ptr(dy2d.device))
+            _C.check(rc, "pt_gemm_splitk_sum")
     if probe is not None:
         ev1.record()
-        probe.records.append((ev0, ev1, flops, nbytes))
+        probe.records.append((ev0, ev1, flops, nbytes, sys._getframe().f_code.co_name))
     return dx
 
 

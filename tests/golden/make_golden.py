@@ -236,6 +236,56 @@ def g10m_multirank(rank, world, tp, cp, dp):
     return res
 
 
+def g10m_pipeline(rank, world, engine):
+    """G10m at pp = world (BASELINE config 4's composition): the reference's PipelineParallel stages
+    (pipeline_parallel.py:8-75) trained by its own 1F1B / AFAB step (:77-214) on gloo/CPU, fp32,
+    FLASH_ATTEN=0, from the same full weights (seed 7) re-applied after the stage re-draws its
+    parameters, the G10m batch every step, G10M_STEPS AdamW steps at lr 1e-2.  Records the last
+    stage's logged loss per step (the engine's loss: each micro-batch's mean CE, not divided by
+    grad_acc) and the full initial weights (rank 0)."""
+    import picotron.process_group_manager as pgm
+    pgm.setup_process_group_manager(tp_size=1, cp_size=1, pp_size=world, dp_size=1)
+    m = pgm.process_group_manager
+    from picotron import model as M
+    from picotron.pipeline_parallel import pipeline_parallel as PP
+    cfg = types.SimpleNamespace(**G10M_CFG)
+    torch.manual_seed(7)
+    full_model = M.Llama(cfg)
+    full = {n: p.detach().clone() for n, p in full_model.named_parameters()}
+    model = PP.PipelineParallel(full_model, cfg)
+    for layer in model.decoder_layers.values():
+        layer.cos, layer.sin = layer.cos.float(), layer.sin.float()
+    with torch.no_grad():
+        for n, p in model.named_parameters():
+            p.copy_(full[n])
+    opt = torch.optim.AdamW(model.parameters(), lr=G10M_LR)
+    ids = _g10m_data()
+    S = G10M_CFG["max_position_embeddings"]
+    step_fn = PP.train_step_pipeline_1f1b if engine == "1f1b" else PP.train_step_pipeline_afab
+
+    class Loader:
+        grad_acc_steps = G10M_GA
+
+        def __init__(self, step):
+            self.step, self.i = step, 0
+
+        def __next__(self):
+            t = ids[self.step, 0, self.i]
+            self.i += 1
+            return {"input_ids": t[:, :-1], "target_ids": t[:, 1:],
+                    "position_ids": torch.arange(S).expand(G10M_MBS, S), "hidden_states": None}
+    losses = []
+    for step in range(G10M_STEPS):
+        opt.zero_grad()
+        loss = step_fn(model, Loader(step), (G10M_MBS, S, G10M_CFG["hidden_size"]), "cpu", torch.float32)
+        losses.append(loss if m.pp_is_last_stage else 0.0)
+        opt.step()
+    res = {"losses": torch.tensor(losses, dtype=torch.float64)}
+    if rank == 0:
+        res.update({f"param.{n}": v for n, v in full.items()})
+    return res
+
+
 G11_STEPS, G11_GA, G11_MBS, G11_LR = 50, 2, 2, 1e-3
 
 
@@ -320,6 +370,12 @@ def g11_curve(rank, world, tp, cp, dp, dtype=torch.bfloat16):
     return res
 
 
+def g10m_pp_all(ref):
+    import functools
+    _run_dist(functools.partial(g10m_pipeline, engine="1f1b"), 2, ref, "G10m_pp2")
+    _run_dist(functools.partial(g10m_pipeline, engine="afab"), 2, ref, "G10m_pp2afab")
+
+
 def g11_all(ref, dtypes=("bf16", "f32")):
     import functools
     for tag in dtypes:
@@ -332,8 +388,12 @@ def g11_all(ref, dtypes=("bf16", "f32")):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
-    ap.add_argument("--only", choices=["G11", "G11bf16"], help="regenerate only these fixtures")
+    ap.add_argument("--only", choices=["G11", "G11bf16", "G10m_pp"], help="regenerate only these fixtures")
     args = ap.parse_args()
+    if args.only == "G10m_pp":
+        g10m_pp_all(args.ref)
+        print("wrote G10m_pp fixtures")
+        return
     if args.only:
         g11_all(args.ref, ("bf16",) if args.only == "G11bf16" else ("bf16", "f32"))
         print("wrote G11 fixtures")
@@ -469,8 +529,9 @@ def main():
     import functools
     for name, (tp, cp, dp) in (("G10m_tp2", (2, 1, 1)), ("G10m_cp2", (1, 2, 1)), ("G10m_dp2", (1, 1, 2))):
         _run_dist(functools.partial(g10m_multirank, tp=tp, cp=cp, dp=dp), 2, args.ref, name)
+    g10m_pp_all(args.ref)
     g11_all(args.ref)
-    print("wrote", sorted(gold) + ["G7", "G8", "G10m_tp2", "G10m_cp2", "G10m_dp2", "G11_*", "G11f32_*"])
+    print("wrote", sorted(gold) + ["G7", "G8", "G10m_tp2", "G10m_cp2", "G10m_dp2", "G10m_pp2*", "G11_*", "G11f32_*"])
 
 
 if __name__ == "__main__":

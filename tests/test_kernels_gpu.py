@@ -49,6 +49,22 @@ def test_rmsnorm_fwd_bwd(rows, cols, mode):
     assert rel_err(dw, wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("rows,cols,mode", [(4096, 2048, 0), (300, 2048, 1), (256, 512, 0), (64, 4096, 0)])
+def test_rmsnorm_bwd_from_splitk_parts(rows, cols, mode):
+    """dy given as two f32 split-K halves (pt_rmsnorm_bwd_splitk) == their bf16 sum pass followed
+    by the plain backward, bit for bit (dx with the residual gradient, dweight)."""
+    from picotron_amd import kernels as K
+    z = torch.randn(rows, cols).to(BF).to(DEV)
+    w = (1 + 0.1 * torch.randn(cols)).to(BF).to(DEV)
+    dres = torch.randn(rows, cols).to(BF).to(DEV)
+    parts = K.SplitKParts(torch.randn(rows, cols, device=DEV), torch.randn(rows, cols, device=DEV))
+    _, rstd, _ = K.rmsnorm_fwd(z, w, 1e-5, mode)
+    dx1, dw1 = K.rmsnorm_bwd(parts, z, w, rstd, mode, dres=dres)
+    dx2, dw2 = K.rmsnorm_bwd(parts.sum(), z, w, rstd, mode, dres=dres)
+    torch.cuda.synchronize()
+    assert torch.equal(dx1, dx2) and torch.equal(dw1, dw2)
+
+
 def test_rmsnorm_fused_residual():
     from picotron_amd import kernels as K
     rows, cols = 256, 2048
@@ -408,6 +424,30 @@ def test_gemm_swiglu_fused(T, H, I):
     assert torch.equal(dgu[:, I:], du)
 
 
+def test_mlp_block_split_swiglu_equals_fused(monkeypatch):
+    """Below the tile thresholds (a TP = 8 shard) the MLP runs its SwiGLU forward / backward as
+    separate kernels beside plain GEMMs: output, dX and all three dW bit-identical to the fused
+    epilogues."""
+    from picotron_amd import functional as FN
+    from picotron_amd import kernels as K_
+    T, H, I = 1024, 256, 512
+    x = torch.randn(T, H).to(BF).to(DEV)
+    ws = [(torch.randn(o, i) / math.sqrt(i)).to(BF).to(DEV) for o, i in ((I, H), (I, H), (H, I))]
+    dm = torch.randn(T, H).to(BF).to(DEV)
+    outs = []
+    for thr in (0, 1 << 30):
+        monkeypatch.setattr(K_, "_SWIGLU_FUSE_MIN_TILES", thr)
+        monkeypatch.setattr(K_, "_SWIGLU_BWD_MIN_TILES", thr)
+        wl = [w.clone().requires_grad_(True) for w in ws]
+        tp = FN.TPContext()
+        m, saved = FN.mlp_block_fwd(x, *wl, tp)
+        dx = FN.mlp_block_bwd(dm, x, saved, *wl, tp)
+        torch.cuda.synchronize()
+        outs.append([m.clone(), dx.clone()] + [w.grad.clone() for w in wl])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("swiglu", [True, False])
 @pytest.mark.parametrize("epi", [0, 1, 3])
 @pytest.mark.parametrize("order", [0, 1, 2])
@@ -528,11 +568,14 @@ def test_fwd_splitk(residual, monkeypatch):
     assert maxabs(y, y1) <= 2 * y1.float().abs().max().item() * 2 ** -8
 
 
-@pytest.mark.parametrize("nh,nkv,S", [(4, 2, 256), (8, 8, 128), (16, 16, 512), (32, 32, 1024)])
-def test_gemm_rope_fused(nh, nkv, S):
-    """q|k|v projection with RoPE in the epilogue == projection + rope kernel, bit for bit (the last
-    two shapes take the mixed 256x256 / 256x128 launch, the first two a single tile shape)"""
+@pytest.mark.parametrize("nh,nkv,S,fuse", [(4, 2, 256, True), (8, 8, 128, True), (16, 16, 512, True),
+                                            (32, 32, 1024, True), (4, 4, 2048, False)])
+def test_gemm_rope_fused(monkeypatch, nh, nkv, S, fuse):
+    """q|k|v projection with RoPE in the epilogue == projection + rope kernel, bit for bit (the
+    third and fourth shapes take the mixed 256x256 / 256x128 launch, the first two a single tile
+    shape; fuse=False: a TP-shard width below the fusion threshold, plain GEMM + rope kernel)"""
     from picotron_amd import kernels as K_
+    monkeypatch.setattr(K_, "_ROPE_FUSE_MIN_TILES", 0 if fuse else 96)
     d, B = 64, 2
     T, H = B * S, 256
     x = torch.randn(T, H).to(BF).to(DEV)

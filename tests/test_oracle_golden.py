@@ -247,3 +247,33 @@ def test_oracle_reproduces_g11_first_steps():
             acc += loss.item()
         opt.step()
         assert abs(acc - g["rank0.losses"][step].item()) < 1e-4 * abs(acc), (step, acc)
+
+
+def test_oracle_reproduces_g10m_pp2_pipeline_curve():
+    """G10m_pp2 / G10m_pp2afab: the reference's PipelineParallel at pp 2 (1F1B and AFAB: the same
+    curve, 5.71 -> 3.04) from G10m's initial weights.  The oracle restating the engine's loss -- each
+    micro-batch's mean CE, NOT divided by grad_acc (pipeline_parallel.py:103,153), gradients summed
+    over the micro-batches, torch AdamW lr 1e-2 -- reproduces all 4 logged losses."""
+    a, b = load("G10m_pp2"), load("G10m_pp2afab")
+    assert torch.equal(a["rank1.losses"], b["rank1.losses"]) and not a["rank0.losses"].any()
+    w = load("G10m_tp2")
+    assert all(torch.equal(a[k], w[k]) for k in a if k.startswith("rank0.param."))
+    cfg = dict(hidden_size=128, intermediate_size=256, num_attention_heads=2, num_key_value_heads=2,
+               rms_norm_eps=1e-5, vocab_size=256, num_hidden_layers=2)
+    params = {k[len("rank0.param."):]: v.clone().requires_grad_(True) for k, v in a.items()
+              if k.startswith("rank0.param.")}
+    opt = torch.optim.AdamW(list(params.values()), lr=1e-2)
+    cos, sin = O.get_cos_sin(256, 64, base=10000.0)
+    gen = torch.Generator().manual_seed(1234)      # make_golden._g10m_data: one batch, every step
+    ids = torch.randint(0, 256, (1, 2, 2, 2, 257), generator=gen)[0, 0]
+    for step in range(4):
+        opt.zero_grad()
+        acc = 0.0
+        for i in range(2):
+            lo = O.llama_forward(ids[i][:, :-1], params, cfg, cos.float(), sin.float())
+            loss = torch.nn.functional.cross_entropy(lo.transpose(1, 2), ids[i][:, 1:])
+            loss.backward()
+            acc += loss.item() / 2
+        opt.step()
+        ref = a["rank1.losses"][step].item()
+        assert abs(acc - ref) < 1e-4 * abs(ref), (step, acc, ref)

@@ -352,3 +352,168 @@ def _pp_p2p(rank, world):
 @pytest.mark.parametrize("world", [2, 3])
 def test_pp_p2p(world):
     _dist.run(_pp_p2p, world)
+
+
+# ------------------------------------------------------------------------ pipeline engine
+def _ref_order_1f1b(pp, rank, n):
+    """The reference's 1F1B action order (pipeline_parallel.py:139-214), restated: warmup forwards,
+    then (F, B) pairs, then the remaining backwards."""
+    w = min(pp - rank - 1, n)
+    out = [("F", i) for i in range(w)]
+    for k in range(n - w):
+        out += [("F", w + k), ("B", k)]
+    return out + [("B", n - w + j) for j in range(w)]
+
+
+@pytest.mark.parametrize("pp,n", [(2, 1), (2, 4), (3, 2), (4, 8), (4, 3)])
+def test_pipeline_schedule_order_and_transfers(pp, n):
+    """Every stage runs each micro-batch forward once and backward once, in the reference's 1F1B
+    order; and replaying all stages' transfers (plain sends / receives, and the paired exchanges
+    that the steady state batches) through blocking point-to-point channels terminates -- no stage
+    waits on a transfer its neighbour never makes (the deadlock the pairing avoids)."""
+    from picotron_amd.pipeline_parallel.pipeline_parallel import pipeline_schedule
+    scheds = [pipeline_schedule("1f1b", pp, r, n) for r in range(pp)]
+    for r, s in enumerate(scheds):
+        assert [(op, i) for op, i, _, _ in s] == _ref_order_1f1b(pp, r, n)
+    afab = pipeline_schedule("afab", pp, 0, n)
+    assert [(op, i) for op, i, _, _ in afab] == [("F", i) for i in range(n)] + [("B", i) for i in range(n)]
+    # expand every stage's actions into primitive transfer events in execution order
+    ev = []
+    for r, s in enumerate(scheds):
+        e = []
+        for op, i, recv, send in s:
+            if recv == "fwd" and r > 0:
+                e.append(("recv", r - 1, "act"))
+            if recv == "bwd" and r < pp - 1:
+                e.append(("recv", r + 1, "grad"))
+            if send == "fwd" and r < pp - 1:
+                e.append(("send", r + 1, "act"))
+            if send == "bwd" and r > 0:
+                e.append(("send", r - 1, "grad"))
+            if send == "fwd+bwd" and r < pp - 1:
+                e.append(("xchg", r + 1, "act", "grad"))
+            if send == "bwd+fwd" and r > 0:
+                e.append(("xchg", r - 1, "grad", "act"))
+        ev.append(e)
+    # rendezvous semantics: a send meets the peer's recv (or the peer's exchange that receives it);
+    # an exchange completes when the peer posts the complementary exchange or a matching plain op
+    pos = [0] * pp
+    sent = {}       # (src, dst, kind) -> count delivered and not yet consumed
+    progress = True
+    while progress:
+        progress = False
+        for r in range(pp):
+            while pos[r] < len(ev[r]):
+                e = ev[r][pos[r]]
+                if e[0] == "send":                       # buffered send (the batch_isend_irecv post)
+                    sent[(r, e[1], e[2])] = sent.get((r, e[1], e[2]), 0) + 1
+                elif e[0] == "recv":
+                    key = (e[1], r, e[2])
+                    if not sent.get(key):
+                        break
+                    sent[key] -= 1
+                else:                                    # exchange: post the send, then wait for the recv
+                    _, peer, out_kind, in_kind = e[:4]
+                    if len(e) == 4:
+                        sent[(r, peer, out_kind)] = sent.get((r, peer, out_kind), 0) + 1
+                        ev[r][pos[r]] = e + ("posted",)
+                    key = (peer, r, in_kind)
+                    if not sent.get(key):
+                        break
+                    sent[key] -= 1
+                pos[r] += 1
+                progress = True
+    assert pos == [len(e) for e in ev], f"stuck at {pos} of {[len(e) for e in ev]}"
+    assert not any(sent.values())
+
+
+class _TinyLayer(torch.nn.Module):
+    """A decoder-layer stand-in with the submodules PipelineParallel.reset_parameters walks."""
+
+    def __init__(self, h):
+        super().__init__()
+        self.input_layernorm = torch.nn.LayerNorm(h)
+        self.attention = torch.nn.Linear(h, h)
+        self.post_attention_layernorm = torch.nn.LayerNorm(h)
+        self.mlp = torch.nn.Linear(h, h)
+
+    def forward(self, x, position_ids=None):
+        x = x + self.attention(self.input_layernorm(x))
+        return x + torch.tanh(self.mlp(self.post_attention_layernorm(x)))
+
+
+class _TinyModel(torch.nn.Module):
+    def __init__(self, v, h, layers):
+        super().__init__()
+        self.embedding = torch.nn.Embedding(v, h)
+        self.decoder_layers = torch.nn.ModuleList([_TinyLayer(h) for _ in range(layers)])
+        self.final_norm = torch.nn.LayerNorm(h)
+        self.final_proj = torch.nn.Linear(h, v)
+
+
+def _pp_engine(rank, world, kind, dp):
+    import types
+    import torch.nn.functional as F
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.data_parallel.data_parallel import DataParallelBucket
+    from picotron_amd.pipeline_parallel.pipeline_parallel import (PipelineParallel, train_step_pipeline_1f1b,
+                                                                  train_step_pipeline_afab)
+    pp = world // dp
+    m = pgm.setup_process_group_manager(tp_size=1, cp_size=1, pp_size=pp, dp_size=dp)
+    V, H, L, mbs, S, ga = 32, 16, 5, 2, 8, 4
+    torch.manual_seed(0)
+    full = _TinyModel(V, H, L)
+    ref = {k: v.detach().clone() for k, v in full.state_dict().items()}
+    stage = PipelineParallel(full, types.SimpleNamespace(num_hidden_layers=L))   # re-draws its parameters
+    with torch.no_grad():
+        for n, p in stage.named_parameters():
+            p.copy_(ref[n])
+    model = DataParallelBucket(stage) if dp > 1 else stage   # train.py:194-195
+    g = torch.Generator().manual_seed(3)
+    toks = torch.randint(0, V, (dp, ga, mbs, S + 1), generator=g)
+
+    class Loader:
+        grad_acc_steps = ga
+
+        def __init__(self):
+            self.i = 0
+
+        def __next__(self):
+            t = toks[m.dp_rank, self.i]
+            self.i += 1
+            return {"input_ids": t[:, :-1], "target_ids": t[:, 1:], "position_ids": torch.arange(S).expand(mbs, S),
+                    "hidden_states": None}
+    step = train_step_pipeline_1f1b if kind == "1f1b" else train_step_pipeline_afab
+    loss = step(model, Loader(), (mbs, S, H), torch.device("cpu"), torch.float32)
+    # single-process reference: the same micro-batches through the unsplit model (mean CE per
+    # micro-batch, not divided by grad_acc -- pipeline_parallel.py:103,153), dp ranks averaged
+    torch.manual_seed(0)
+    whole = _TinyModel(V, H, L)
+    whole.load_state_dict(ref)
+    losses = []
+    for r in range(dp):
+        for i in range(ga):
+            t = toks[r, i]
+            x = whole.embedding(t[:, :-1])
+            for lay in whole.decoder_layers:
+                x = lay(x)
+            out = whole.final_proj(whole.final_norm(x))
+            lo = F.cross_entropy(out.transpose(1, 2), t[:, 1:])
+            (lo / dp).backward()
+            if r == m.dp_rank:
+                losses.append(lo.item())
+    if m.pp_is_last_stage:
+        assert abs(loss - sum(losses) / ga) < 1e-5
+    else:
+        assert loss == 0.0
+    wref = dict(whole.named_parameters())
+    for n, p in stage.named_parameters():
+        assert torch.allclose(p.grad, wref[n].grad, rtol=1e-4, atol=1e-5), n
+
+
+@pytest.mark.parametrize("kind,world,dp", [("1f1b", 2, 1), ("afab", 2, 1), ("1f1b", 3, 1), ("1f1b", 4, 2)])
+def test_pipeline_engine_matches_unsplit_model(kind, world, dp):
+    """PipelineParallel + the 1F1B / AFAB steps over gloo (pp 2-3, and pp2 x dp2 under
+    DataParallelBucket, whose all-reduce only the stage's last backward triggers): the last stage's logging loss is the mean micro-batch loss and every
+    stage's gradients equal the unsplit model's on the same micro-batches."""
+    _dist.run(_pp_engine, world, kind, dp)

@@ -210,3 +210,59 @@ def test_data_parallel_bucket_dp2():
 
 def test_data_parallel_bucket_dp2_tp2():
     _dist.run(_dp_llama, 4, 2, device="cuda")
+
+
+# --------------------------------------------------------------------------- pipeline parallel
+def _pp_llama(rank, world, kind):
+    """BASELINE config 4's pipeline composition on the HIP path: PipelineParallel stages of the HIP
+    Llama (embedding / decoder layers / final_norm + lm_head as the reference splits them) driven by
+    the 1F1B or AFAB step over p2p; the lm_head's HipLogits meet F.cross_entropy(logits.transpose(1, 2))
+    (pipeline_parallel.py:103,153), i.e. the HIP cross-entropy.  Against the oracle on the full model:
+    the last stage's logging loss and every stage's gradients (summed over the micro-batches: the
+    engine's loss is each micro-batch's mean, not divided by grad_acc)."""
+    import types
+    os.environ["FLASH_ATTEN"] = "1"
+    torch.cuda.set_device(0)
+    from oracle import picotron_oracle as O
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.model import Llama
+    from picotron_amd.pipeline_parallel.pipeline_parallel import (PipelineParallel, train_step_pipeline_1f1b,
+                                                                  train_step_pipeline_afab)
+    from picotron_amd.train import SyntheticMicroBatchDataLoader
+    m = pgm.setup_process_group_manager(tp_size=1, cp_size=1, pp_size=world, dp_size=1)
+    seq, mbs, ga = 256, 2, 3
+    cfg = types.SimpleNamespace(**dict(CFG, num_hidden_layers=3, max_position_embeddings=seq))
+    full = {k: v.to(torch.bfloat16) for k, v in O.init_params(dict(CFG, num_hidden_layers=3), seed=7).items()}
+    with torch.device("cuda"):
+        model = PipelineParallel(Llama(cfg), cfg)
+    model.to(torch.bfloat16)
+    names = dict(model.named_parameters())
+    assert set(names) <= set(full)
+    with torch.no_grad():
+        for n, p in names.items():
+            p.copy_(full[n])
+    loader = SyntheticMicroBatchDataLoader(mbs, seq, ga, CFG["vocab_size"], torch.device("cuda"), seed=1234)
+    step = train_step_pipeline_1f1b if kind == "1f1b" else train_step_pipeline_afab
+    loss = step(model, loader, (mbs, seq, CFG["hidden_size"]), torch.device("cuda"), torch.bfloat16)
+    torch.cuda.synchronize()
+    pf = {k: v.float().requires_grad_(True) for k, v in full.items()}
+    cos, sin = O.get_cos_sin(seq, 64, base=CFG["rope_theta"])
+    losses = []
+    for i in range(ga):
+        x, t = loader._inputs[i].cpu(), loader._targets[i].cpu()
+        lo = O.llama_forward(x, pf, dict(CFG, num_hidden_layers=3), cos.float(), sin.float(),
+                             norm=O.rmsnorm_flash_semantics)
+        li = F.cross_entropy(lo.transpose(1, 2), t)
+        li.backward()
+        losses.append(li.item())
+    if m.pp_is_last_stage:
+        ref = sum(losses) / ga
+        assert abs(loss - ref) < TOL * abs(ref), (loss, ref)
+    for n, p in names.items():
+        assert p.grad is not None, n
+        assert _rel(p.grad, pf[n].grad) < TOL, n
+
+
+@pytest.mark.parametrize("kind,world", [("1f1b", 2), ("afab", 2), ("1f1b", 3)])
+def test_pipeline_parallel_llama(kind, world):
+    _dist.run(_pp_llama, world, kind, device="cuda")

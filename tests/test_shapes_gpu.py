@@ -50,6 +50,36 @@ def _weights(H, I, nh, nkv, d, seed):
             "mlp.gate_proj.weight": u(I, H), "mlp.up_proj.weight": u(I, H), "mlp.down_proj.weight": u(H, I)}
 
 
+def _layer_grads(B, S, H, I, nh, nkv, d, seed=0):
+    """(y, dx, every weight grad) of one DecoderLayerFunction fwd + bwd at these dims (GPU)."""
+    from picotron_amd import functional as FN
+    from picotron_amd import process_group_manager as pgm
+    pgm.setup_process_group_manager(1, 1, 1, 1)
+    w = _weights(H, I, nh, nkv, d, seed)
+    dev = torch.device("cuda")
+    params = {k: torch.nn.Parameter(v.to(dev)) for k, v in w.items()}
+    cos, sin = O.get_cos_sin(S, d, base=10000.0)
+    g = torch.Generator().manual_seed(seed + 1)
+    x = torch.randn(B, S, H, generator=g).to(BF).to(dev).requires_grad_(True)
+    dy = torch.randn(B, S, H, generator=g).to(BF).to(dev)
+    y = FN.DecoderLayerFunction.apply(x, *[params[n] for n in NAMES], cos.to(dev), sin.to(dev), 1e-5, 0, nh, nkv, d)
+    y.backward(dy)
+    torch.cuda.synchronize()
+    return [y.detach(), x.grad] + [params[n].grad for n in NAMES]
+
+
+def test_smollm_layer_norm_from_splitk_halves_is_bit_identical(monkeypatch):
+    """At config 2's shape the gate|up dX is split-K (K 16384): its two f32 halves go straight into
+    the post-attention norm backward (pt_rmsnorm_bwd_splitk) -- every output bit-identical to the
+    sum pass + plain norm backward (PICOTRON_NORM_SPLITK=0)."""
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("PICOTRON_NORM_SPLITK", v)
+        outs.append(_layer_grads(B=4, S=1024, H=2048, I=8192, nh=32, nkv=32, d=64, seed=11))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def _layer_parity(B, S, H, I, nh, nkv, d, seed=0, main_grad=False):
     """One decoder layer (model.py:204-209) fwd + bwd through functional.DecoderLayerFunction (the
     node model.DecoderLayer runs) at these dims vs the oracle.  main_grad: every weight carries an

@@ -24,6 +24,17 @@ SHAPES = [
     ("wgrad.o", H, H, T, 0, 0), ("wgrad.qkv", 3 * H, H, T, 0, 0), ("wgrad.gate_up", 2 * I, H, T, 0, 0),
     ("wgrad.down", H, I, T, 0, 0), ("wgrad.lm_head", V, H, T, 0, 0),
 ]
+def tp_shapes(tp):
+    """The TP shard shapes of the same layer (ColumnParallel q|k|v, gate|up: N / tp; RowParallel o, down:
+    K / tp) -- the TP=8 proxy's GEMMs."""
+    q, i = 3 * H // tp, I // tp
+    return [("tp.fwd.qkv", T, q, H, 1, 1), ("tp.fwd.o", T, H, H // tp, 1, 1), ("tp.fwd.gate_up", T, 2 * i, H, 1, 1),
+            ("tp.fwd.down", T, H, i, 1, 1), ("tp.dgrad.o", T, H // tp, H, 1, 0), ("tp.dgrad.qkv", T, H, q, 1, 0),
+            ("tp.dgrad.gate_up", T, H, 2 * i, 1, 0), ("tp.dgrad.down", T, i, H, 1, 0),
+            ("tp.wgrad.o", H, H // tp, T, 0, 0), ("tp.wgrad.qkv", q, H, T, 0, 0), ("tp.wgrad.gate_up", 2 * i, H, T, 0, 0),
+            ("tp.wgrad.down", H, i, T, 0, 0)]
+
+
 TILES = {0: (256, 256), 1: (256, 128), 2: (128, 128), 3: (64, 64), 4: (256, 256), 5: (256, 128), 6: (256, 256), 7: (256, 128), 8: (256, 256), 9: (128, 128), 10: (256, 256), 11: (256, 256), 12: (256, 256), 13: (256, 128)}
 
 
@@ -75,7 +86,11 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--lib", default="", help="load this libpicotron_hip.so instead (A/B runs)")
     ap.add_argument("--brief", action="store_true", help="one short line per shape")
+    ap.add_argument("--tp", type=int, default=0, help="the TP shard shapes at this degree instead")
     args = ap.parse_args()
+    global SHAPES
+    if args.tp:
+        SHAPES = tp_shapes(args.tp)
     if args.lib:
         K._C.use_library(os.path.abspath(args.lib))
     tiles = [int(t) for t in args.tiles.split(",")]

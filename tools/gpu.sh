@@ -10,6 +10,7 @@
 #   pmcx         extra counter sets over bench.py --grad-acc 1 (SQ busy/VALU/MFMA, TCC hit/miss/EA reads)
 #   configs      Llama-2-7B 1-GPU bench, TP=8 proxy, CP=8 proxy
 #   gloo2        bench.py --gpus 2 --backend gloo rehearsal (2 ranks on cuda:0)
+#   pp2          bench.py --gpus 2 --pp 2 --backend gloo rehearsal of the pipeline engine (config 4's 1F1B)
 #   dp           bench.py --dp-bucket fp32 / bf16 vs plain (the per-GPU DP cost)
 #   attn         tools/attn_bench.py d64 and d128 (OLD=<lib> for an in-process A/B)
 #   pmcattn      attention PMC passes (ATTN_ARGS="--B 1 --S 4096 --H 32 --D 128" for d128)
@@ -80,6 +81,12 @@ step_gloo2() {
   timeout -k 10 400 python -u bench.py --gpus 2 --backend gloo --steps 1 --warmup 1 --grad-acc 4 > $O.gloo2.json 2> $O.gloo2.err || { echo gloo2 failed; tail -20 $O.gloo2.err; return 1; }
   [ $(wc -l < $O.gloo2.json) = 1 ] || { echo "gloo2: stdout is not one line"; return 1; }
   python -c "import json; d=json.load(open('$O.gloo2.json')); print('gloo2', d['n_gpus'], d['ranks'], d['backend'], d['config']['parallelism'], round(d['value']))"
+}
+
+step_pp2() {
+  timeout -k 10 400 python -u bench.py --gpus 2 --pp 2 --backend gloo --steps 1 --warmup 1 --grad-acc 4 --cpu-tokens 0 ${PP_ARGS} > $O.pp2.json 2> $O.pp2.err || { echo pp2 failed; tail -20 $O.pp2.err; return 1; }
+  [ $(wc -l < $O.pp2.json) = 1 ] || { echo "pp2: stdout is not one line"; return 1; }
+  python -c "import json; d=json.load(open('$O.pp2.json')); print('pp2', d['n_gpus'], d['ranks'], d['backend'], d['config']['parallelism'], round(d['value']), d['final_loss'])"
 }
 
 step_dp() {
