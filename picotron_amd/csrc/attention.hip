@@ -191,14 +191,25 @@ __device__ __forceinline__ f32x16_t mfma(const bf16x8_t& a, const bf16x8_t& b, c
 
 // store a 32(d) x 32(row) C-layout tile transposed into row-major memory: lane owns row
 // (lane & 31), d = 32 dt + crow(r); 4 consecutive d per 8-byte store
+// Widened (guide T21): the 4-column chunks of lanes l and l ^ 32 sit side by side in the row, so
+// for each pair of groups (g4, g4 + 1) one v_permlane32_swap per dword (vdst = the g4 chunk, src =
+// the g4 + 1 chunk: lanes 32-63 of vdst trade with lanes 0-31 of src) leaves the lower lanes
+// [own g4 | upper's g4] and the upper lanes [lower's g4 + 1 | own g4 + 1]: 8 consecutive columns per
+// lane, one 16-byte store instead of two 8-byte ones (the epilogue tail is store-issue-bound).  The
+// stored values are those of the 8-byte form.
 __device__ __forceinline__ void store_T_bf16(uint16_t* row_ptr, int dt, const f32x16_t& x, float mul, int lane) {
 #pragma unroll
-  for (int g4 = 0; g4 < 4; ++g4) {
-    const int d = 32 * dt + 8 * g4 + 4 * (lane >> 5);
-    uint2 w;
-    w.x = pack_bf2(x[4 * g4 + 0] * mul, x[4 * g4 + 1] * mul);
-    w.y = pack_bf2(x[4 * g4 + 2] * mul, x[4 * g4 + 3] * mul);
-    *(uint2*)(row_ptr + d) = w;
+  for (int gp = 0; gp < 4; gp += 2) {
+    uint32_t a[2], b[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const uint32_t c0 = pack_bf2(x[4 * gp + 2 * u] * mul, x[4 * gp + 2 * u + 1] * mul);
+      const uint32_t c1 = pack_bf2(x[4 * gp + 4 + 2 * u] * mul, x[4 * gp + 4 + 2 * u + 1] * mul);
+      const auto r = __builtin_amdgcn_permlane32_swap(c0, c1, false, false);
+      a[u] = r[0];
+      b[u] = r[1];
+    }
+    *(uint4*)(row_ptr + 32 * dt + 8 * gp + (lane >= 32 ? 8 : 0)) = make_uint4(a[0], a[1], b[0], b[1]);
   }
 }
 // store_T_bf16 of all DT tiles of one row with the inverse RoPE rotation applied to the bf16
@@ -207,6 +218,7 @@ template <int DT>
 __device__ __forceinline__ void store_T_bf16_unrope(uint16_t* row_ptr, const f32x16_t (&x)[DT], float mul,
                                                     const uint16_t* cos_row, const uint16_t* sin_row, int lane) {
   constexpr int HD = DT / 2;  // (d, d + 32 HD) pairs sit in tiles dt and dt + HD
+  uint32_t e1[2], e2[2];      // the even group's packed chunks, waiting for the odd one
 #pragma unroll
   for (int dt = 0; dt < HD; ++dt)
 #pragma unroll
@@ -223,11 +235,24 @@ __device__ __forceinline__ void store_T_bf16_unrope(uint16_t* row_ptr, const f32
         o1[e] = fmaf(g1, c[e], -(g2 * sj));
         o2[e] = fmaf(g2, c[e], g1 * sj);
       }
-      uint2 w1, w2;
-      w1.x = pack_bf2(o1[0], o1[1]); w1.y = pack_bf2(o1[2], o1[3]);
-      w2.x = pack_bf2(o2[0], o2[1]); w2.y = pack_bf2(o2[2], o2[3]);
-      *(uint2*)(row_ptr + d) = w1;
-      *(uint2*)(row_ptr + d + 32 * HD) = w2;
+      uint32_t p1[2] = {pack_bf2(o1[0], o1[1]), pack_bf2(o1[2], o1[3])};
+      uint32_t p2[2] = {pack_bf2(o2[0], o2[1]), pack_bf2(o2[2], o2[3])};
+      if ((g4 & 1) == 0) {   // hold group g4's chunks; the odd group completes the pair (store_T_bf16)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) { e1[u] = p1[u]; e2[u] = p2[u]; }
+        continue;
+      }
+      uint32_t a1[2], b1[2], a2[2], b2[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const auto r1 = __builtin_amdgcn_permlane32_swap(e1[u], p1[u], false, false);
+        const auto r2 = __builtin_amdgcn_permlane32_swap(e2[u], p2[u], false, false);
+        a1[u] = r1[0]; b1[u] = r1[1];
+        a2[u] = r2[0]; b2[u] = r2[1];
+      }
+      const int dw = 32 * dt + 8 * (g4 - 1) + (lane >= 32 ? 8 : 0);
+      *(uint4*)(row_ptr + dw) = make_uint4(a1[0], a1[1], b1[0], b1[1]);
+      *(uint4*)(row_ptr + dw + 32 * HD) = make_uint4(a2[0], a2[1], b2[0], b2[1]);
     }
 }
 
@@ -241,6 +266,43 @@ __device__ __forceinline__ void accum_T_f32(float* row_ptr, int dt, const f32x16
     *(float4*)(row_ptr + d) = o;
   }
 }
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else static_assert(N == 0, "vm_wait: add the count");
+}
+
+// K/V (Q/dO) staging ring of NS LDS stages: tile t lives in stage t % NS and its LDS-DMA pieces (OPS
+// per wave) are issued NS - 1 tiles ahead; before tile t + 1 is read, every piece older than the
+// `younger` tiles issued after it must have landed.  Attention workgroups of one XCD walk the same
+// K/V tiles in step, so a tile's first touch is an HBM miss they all wait on: with one tile of
+// look-ahead that latency was most of the d64 kernels' time (the forward's DMA / barrier skeleton
+// alone: 21 of 37 us).
+template <int OPS, int NS>
+__device__ __forceinline__ void ring_wait(int younger) {
+  if constexpr (NS >= 4) {
+    if (younger >= 2) { vm_wait<2 * OPS>(); return; }
+  }
+  if constexpr (NS >= 3) {
+    if (younger >= 1) { vm_wait<OPS>(); return; }
+  }
+  vm_wait<0>();
+}
+
+// ring depth per kernel and head dim (LDS: a d64 K|V stage is 16 KiB, d128 32 KiB).  Measured
+// (tools/attn_bench.py, in-process A/B): d64 forward 4 stages 36.0 -> 35.1 us with the widened stores
+// (ring alone -2 %); the d128 forward slower with 3 (138.5 vs 145.8 us), so it keeps 2.
+template <int D, int NWK>
+constexpr int fwd_stages() { return D == 64 ? 4 : 2; }
+template <int D>
+constexpr int dq_stages() { return D == 64 ? 4 : 2; }
 
 // ============================================================================ forward
 // NWK waves per workgroup (32 query rows each): 4, or 8 at d 128 (the K/V tiles staged once for
@@ -275,12 +337,14 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
   for (int i = 0; i < DT; ++i) o[i] = zero16();
   float m = -INFINITY, l = 0.f;
 
+  constexpr int NS = fwd_stages<D, NWK>(), OPS = 2 * (KT * D * 2 / 1024) / NWK;
   auto stage = [&](int kt, int buf) {
     lds_u8* sk = smem + buf * 2 * TILE_B;
     stage_rows<D, NWK>(kbase + (int64_t)kt * KT * a.k_ss, a.k_ss, sk, wave, lane);
     stage_rows<D, NWK>(vbase + (int64_t)kt * KT * a.v_ss, a.v_ss, sk + TILE_B, wave, lane);
   };
-  stage(0, 0);
+  const int pre = nkt < NS - 1 ? nkt : NS - 1;
+  for (int t = 0; t < pre; ++t) stage(t, t);
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler: its own fragment loads are done
   __syncthreads();
 
@@ -288,6 +352,9 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
   auto tile = [&](const lds_u8* sk, int kv0) {
     const lds_u8* sv = sk + TILE_B;
     if (a.causal && kv0 > q0 + 31) return;  // wave-uniform: skip tiles fully above the diagonal
+#ifdef PT_ABLATE
+    if (a.ablate & 64) return;  // diagnostic: the forward's DMA / barrier skeleton alone
+#endif
     {
       f32x16_t s[2];
       // the tile's K operands in one batch of LDS reads ahead of the MFMAs (left to itself the
@@ -358,11 +425,15 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
     }
   };
 
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nkt) stage(kt + 1, buf ^ 1);
+  for (int kt = 0, buf = 0, sbuf = pre % NS; kt < nkt; ++kt) {
+    if (kt + NS - 1 < nkt) {  // into the stage tile kt - 1 used (every wave passed its barrier)
+      stage(kt + NS - 1, sbuf);
+      if (++sbuf == NS) sbuf = 0;
+    }
     tile(smem + buf * 2 * TILE_B, kt * KT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (++buf == NS) buf = 0;
+    const int issued = kt + NS - 1 < nkt ? kt + NS - 1 : nkt - 1;   // the last tile issued so far
+    ring_wait<OPS, NS>(issued - (kt + 1));
     __syncthreads();
   }
 
@@ -491,6 +562,9 @@ __device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, i
 
   // one (query head, q tile) step
   auto tile = [&](const lds_u8* sq, int qt) {
+#ifdef PT_ABLATE
+    if (a.ablate & 128) return;  // diagnostic: the one-wave dK/dV kernel's DMA / barrier skeleton alone
+#endif
     const lds_u8* sdo = sq + TILE_B;
     const float* sl2 = (const float*)(sq + 2 * TILE_B);
     const float* sdel = sl2 + KT;
@@ -606,14 +680,6 @@ constexpr int kStampB = 8 * 4 * kStampSteps * 8;
 constexpr int kStampB = 0;
 #endif
 
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else static_assert(N == 0, "vm_wait: add the count");
-}
 
 template <int D>
 __device__ __forceinline__ void attn_bwd_dkdv_pair_block(const AttnArgs& a, int bx, int hk, int b) {
@@ -921,12 +987,14 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
 #pragma unroll
   for (int i = 0; i < DT; ++i) dq[i] = zero16();
 
+  constexpr int NS = dq_stages<D>(), OPS = 2 * (KT * D * 2 / 1024) / NW;
   auto stage = [&](int kt, int buf) {
     lds_u8* sk = smem + buf * 2 * TILE_B;
     stage_rows<D>(kbase + (int64_t)kt * KT * a.k_ss, a.k_ss, sk, wave, lane);
     stage_rows<D>(vbase + (int64_t)kt * KT * a.v_ss, a.v_ss, sk + TILE_B, wave, lane);
   };
-  stage(0, 0);
+  const int pre = nkt < NS - 1 ? nkt : NS - 1;
+  for (int t = 0; t < pre; ++t) stage(t, t);
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler: its own fragment loads are done
   if (a.delta_w) {
     float part = 0.f;
@@ -943,6 +1011,9 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
   auto tile = [&](const lds_u8* sk, int kv0) {
     const lds_u8* sv = sk + TILE_B;
     if (a.causal && kv0 > q0 + 31) return;  // wave-uniform: every key of the tile is after my queries
+#ifdef PT_ABLATE
+    if (a.ablate & 32) return;  // diagnostic: the dQ kernel's DMA / barrier skeleton alone
+#endif
     // each 32-key half's dS feeds its two dQ k-steps right away: one dS tile live, not two
     // (16 VGPRs: d128's dQ kernel fits 2 waves per SIMD)
 #pragma unroll
@@ -974,11 +1045,15 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
     }
   };
 
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nkt) stage(kt + 1, buf ^ 1);
+  for (int kt = 0, buf = 0, sbuf = pre % NS; kt < nkt; ++kt) {   // the forward's ring (ring_wait)
+    if (kt + NS - 1 < nkt) {
+      stage(kt + NS - 1, sbuf);
+      if (++sbuf == NS) sbuf = 0;
+    }
     tile(smem + buf * 2 * TILE_B, kt * KT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (++buf == NS) buf = 0;
+    const int issued = kt + NS - 1 < nkt ? kt + NS - 1 : nkt - 1;
+    ring_wait<OPS, NS>(issued - (kt + 1));
     __syncthreads();
   }
 
@@ -1073,16 +1148,29 @@ int pt_attn_fwd(const void* q, const int64_t* q_str, const void* k, const int64_
   a.lse = lse;
   a.B = (int)B; a.H = (int)H; a.HKV = (int)HKV; a.Sq = (int)Sq; a.Sk = (int)Sk;
   a.scale = scale; a.causal = causal; a.merge = merge;
+#ifdef PT_ABLATE
+  a.ablate = getenv("PICOTRON_ATTN_ABLATE") ? atoi(getenv("PICOTRON_ATTN_ABLATE")) : 0;
+#endif
   int rc = check_common(a, (int)D);
   if (rc) return rc;
   const int nwk = (D == 128 && Sq % (8 * 32) == 0) ? 8 : NW;
   const int nqb = (int)(Sq / (nwk * 32));
   a.pair = causal && nqb % 2 == 0 && pair_enabled();
   const dim3 grid((unsigned)(a.pair ? nqb / 2 : nqb), (unsigned)H, (unsigned)B);
-  const int smem = 2 * 2 * KT * (int)D * 2;
-  if (D == 64) { set_smem(attn_fwd_kernel<64, NW>, smem); attn_fwd_kernel<64, NW><<<grid, NW * 64, smem, stream>>>(a); }
-  else if (nwk == 8) { set_smem(attn_fwd_kernel<128, 8>, smem); attn_fwd_kernel<128, 8><<<grid, 8 * 64, smem, stream>>>(a); }
-  else { set_smem(attn_fwd_kernel<128, NW>, smem); attn_fwd_kernel<128, NW><<<grid, NW * 64, smem, stream>>>(a); }
+  const int stage_b = 2 * KT * (int)D * 2;
+  if (D == 64) {
+    const int smem = fwd_stages<64, NW>() * stage_b;
+    set_smem(attn_fwd_kernel<64, NW>, smem);
+    attn_fwd_kernel<64, NW><<<grid, NW * 64, smem, stream>>>(a);
+  } else if (nwk == 8) {
+    const int smem = fwd_stages<128, 8>() * stage_b;
+    set_smem(attn_fwd_kernel<128, 8>, smem);
+    attn_fwd_kernel<128, 8><<<grid, 8 * 64, smem, stream>>>(a);
+  } else {
+    const int smem = fwd_stages<128, NW>() * stage_b;
+    set_smem(attn_fwd_kernel<128, NW>, smem);
+    attn_fwd_kernel<128, NW><<<grid, NW * 64, smem, stream>>>(a);
+  }
   PT_CHECK_LAUNCH();
   return PT_OK;
 }
@@ -1158,7 +1246,7 @@ int attn_bwd_impl(const void* q, const int64_t* q_str, const void* k, const int6
   int rc = check_common(a, (int)D);
   if (rc) return rc;
   if (Sk % (NW * 32)) return PT_EUNSUPPORTED;
-  const int smem_kv = 2 * 2 * KT * (int)D * 2;
+  const int smem_kv = (D == 64 ? dq_stages<64>() : dq_stages<128>()) * 2 * KT * (int)D * 2;
   const int smem_q = 2 * (2 * KT * (int)D * 2 + 2 * KT * 4);
   const int nqb = (int)(Sq / (NW * 32)), nkb = (int)(Sk / (NW * 32));
   a.pair = causal && nqb % 2 == 0 && nkb % 2 == 0 && pair_enabled();
