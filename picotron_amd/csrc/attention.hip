@@ -425,7 +425,12 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
     }
   };
 
-  for (int kt = 0, buf = 0, sbuf = pre % NS; kt < nkt; ++kt) {
+#ifdef PT_ABLATE
+  const int nkt_run = (a.ablate & 256) ? 0 : nkt;   // diagnostic: prologue + epilogue only
+#else
+  const int nkt_run = nkt;
+#endif
+  for (int kt = 0, buf = 0, sbuf = pre % NS; kt < nkt_run; ++kt) {
     if (kt + NS - 1 < nkt) {  // into the stage tile kt - 1 used (every wave passed its barrier)
       stage(kt + NS - 1, sbuf);
       if (++sbuf == NS) sbuf = 0;
@@ -441,6 +446,9 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
   const float inv_l = 1.0f / l;
   const float lse = m * kLn2 + __logf(l);
   float* lse_p = a.lse + ((int64_t)b * a.H + h) * a.lse_ld + myq;
+#ifdef PT_ABLATE
+  if (a.ablate & 512) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); return; }   // diagnostic: no epilogue
+#endif
   if (!a.merge) {
     uint16_t* orow = (uint16_t*)a.o + b * a.o_sb + (int64_t)myq * a.o_ss + h * a.o_sh;
 #pragma unroll
