@@ -102,7 +102,7 @@ def wgrad_group(jobs):
             _grad_ready(p)
 
 
-def dgrad_with_wgrad(dy2d, weights, wjobs, gu=None, keep_parts=False):
+def dgrad_with_wgrad(dy2d, weights, wjobs, gu=None, keep_parts=False, split_min=None):
     """dX = dY . [W_0; ...] (with gu: the down_proj dX's SwiGLU backward, dg|du) AND the wgrads
     wjobs [(dy2d, x2d, params)] of the same layer in ONE launch (K.linear_dgrad_dual) when the
     shapes tile for it and every sink takes one epilogue; otherwise the separate launches.
@@ -116,7 +116,7 @@ def dgrad_with_wgrad(dy2d, weights, wjobs, gu=None, keep_parts=False):
         if len(epis) == 1:
             epi = epis.pop()
             wk = [(dy, x, [t for t, _ in tg]) for (dy, x, _), tg in zip(wjobs, targets)]
-            dx = K.linear_dgrad_dual(dy2d, weights, wk, epi, gu=gu, keep_parts=keep_parts)
+            dx = K.linear_dgrad_dual(dy2d, weights, wk, epi, gu=gu, keep_parts=keep_parts, split_min=split_min)
             if dx is None:   # not tileable after all: the same sinks, separate launches
                 dx = K.linear_dgrad_swiglu(dy2d, weights[0], gu) if gu is not None else K.linear_dgrad(dy2d, weights)
                 K.linear_wgrad_grouped(wk, epilogue=epi)
@@ -432,11 +432,24 @@ def attn_block_fwd(h2, wq, wk, wv, wo, cos, sin, sh, tp):
     return a, (qkv, o, lse)
 
 
-def attn_block_bwd(da, h2, saved, wq, wk, wv, wo, cos, sin, sh, tp, need_dx=True):
+def _dual_qkv_enabled():
+    return os.environ.get("PICOTRON_DUAL_QKV", "1") != "0"
+
+
+def attn_block_bwd(da, h2, saved, wq, wk, wv, wo, cos, sin, sh, tp, need_dx=True, keep_parts=False):
+    """keep_parts: the q|k|v dX may come back as K.SplitKParts (two f32 K halves) for a following
+    rmsnorm backward to sum."""
     qkv, o, lse = saved
     scale = 1.0 / math.sqrt(sh.d)
     do2 = K.linear_dgrad(da, [wo])
     dqkv = attention_core_bwd(do2.view(sh.B, sh.S, sh.nh, sh.d), qkv, o, lse, sh, cos, sin, scale)
+    if need_dx and keep_parts and tp.world_size == 1 and _dual_qkv_enabled():
+        # tp = 1 (no all-reduce to overlap): the q|k|v dX as two split-K halves (128 + 128 tiles of
+        # 256x256, summed by the input norm's backward) in ONE launch with the q|k|v and o_proj dW
+        # (192 + 64 tiles): 512 tiles = 2 whole rounds of the 256 CUs instead of a 128-tile dX launch
+        # and a 256-tile dW launch
+        return dgrad_with_wgrad(dqkv, [wq, wk, wv], [(dqkv, h2, [wq, wk, wv]), (da, o.view(sh.T, sh.wq), [wo])],
+                                keep_parts=True, split_min=1024)
     dh = handle = None
     if need_dx:
         dh = K.linear_dgrad(dqkv, [wq, wk, wv])
@@ -575,7 +588,7 @@ class DecoderLayerFunction(torch.autograd.Function):
         # the gate|up dX's split-K halves go straight into the norm backward (summed there)
         dh2 = mlp_block_bwd(dout2, h2, (gu, hh), wg, wu, wd, tp, keep_parts=K.norm_splitk_enabled())
         dz = norm_bwd(dh2, z, w2, rstd2, mode, dres=dout2)
-        dh1 = attn_block_bwd(dz, h1, (qkv, o, lse), wq, wk, wv, wo, cos, sin, sh, tp)
+        dh1 = attn_block_bwd(dz, h1, (qkv, o, lse), wq, wk, wv, wo, cos, sin, sh, tp, keep_parts=K.norm_splitk_enabled())
         dx = norm_bwd(dh1, x2, w1, rstd1, mode, dres=dz)   # (norm_bwd skips dW of frozen weights)
         return (dx.view(sh.B, sh.S, -1),) + (None,) * 16
 

@@ -825,15 +825,16 @@ def _splitk_min():
     return int(os.environ.get("PICOTRON_SPLITK2_MIN", "8192"))
 
 
-def _splitk_halves(M, N, K):
+def _splitk_halves(M, N, K, min_half=None):
     """K of each half when C [M, N] = A [M, K] . B pays to split in two K halves (None if not): one
     round of 256x256 tiles for both halves together and at least PICOTRON_SPLITK2_MIN (8192) of K per
     half -- where the 256x256 8-phase rate (~17 % above the 256x128 one at long K) pays for the f32
-    partials and the sum pass."""
+    partials and the sum pass.  min_half overrides that floor (a caller whose halves share a launch
+    with other work and whose consumer sums them)."""
     if M % 256 or N % 256 or 2 * (M // 256) * (N // 256) > 256 or K % 128:
         return None
     h = K // 2
-    return h if h >= _splitk_min() else None
+    return h if h >= (_splitk_min() if min_half is None else min_half) else None
 
 
 def _segments(sizes, lo, hi):
@@ -937,7 +938,7 @@ def norm_splitk_enabled():
     return os.environ.get("PICOTRON_NORM_SPLITK", "1") != "0"
 
 
-def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None, keep_parts=False):
+def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None, keep_parts=False, split_min=None):
     """dX = dY . [W_0; ...] (or, with gu, the SwiGLU backward dg|du of the down_proj dX:
     linear_dgrad_swiglu) AND the wgrads wjobs [(dy2d, x2d, outs)] (linear_wgrad, epilogue
     wepilogue) in ONE launch (pt_gemm_dual).  Returns dX / dg|du, or None (nothing launched) when
@@ -962,7 +963,7 @@ def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None, keep
         p0 = _problem(dy2d, dy2d.stride(0), weights, [Kin] * len(weights), _bounds(ns), 1, [dx], [dx.stride(0)],
                       [0, T], T, Kin, N)
         e0, flops, nbytes = EPI_BF16, 2.0 * T * Kin * N, _alg_bytes(T, Kin, N, EPI_BF16)
-        h = _splitk_halves(T, Kin, N) if _splitk_enabled() else None
+        h = _splitk_halves(T, Kin, N, split_min) if _splitk_enabled() else None
         if h is not None and all(w.dtype == BF16 and w.is_contiguous() for w in weights) and \
                 all(n % 64 == 0 for n in ns):
             # the dX as two f32 K halves (split-K, finished by the sum pass after the launch)

@@ -71,13 +71,35 @@ def _layer_grads(B, S, H, I, nh, nkv, d, seed=0):
 def test_smollm_layer_norm_from_splitk_halves_is_bit_identical(monkeypatch):
     """At config 2's shape the gate|up dX is split-K (K 16384): its two f32 halves go straight into
     the post-attention norm backward (pt_rmsnorm_bwd_splitk) -- every output bit-identical to the
-    sum pass + plain norm backward (PICOTRON_NORM_SPLITK=0)."""
+    sum pass + plain norm backward (PICOTRON_NORM_SPLITK=0).  The q|k|v dX stays one GEMM here
+    (PICOTRON_DUAL_QKV=0; its split form is the next test)."""
+    monkeypatch.setenv("PICOTRON_DUAL_QKV", "0")
     outs = []
     for v in ("0", "1"):
         monkeypatch.setenv("PICOTRON_NORM_SPLITK", v)
         outs.append(_layer_grads(B=4, S=1024, H=2048, I=8192, nh=32, nkv=32, d=64, seed=11))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_smollm_layer_qkv_dx_split_beside_dw(monkeypatch):
+    """tp = 1: the q|k|v dX as two split-K halves (summed by the input norm's backward) in one launch
+    with the q|k|v and o_proj dW.  The dW tiles run the same 8-phase kernel over the same K order as
+    the grouped dW launch: those gradients, the forward and everything upstream of the q|k|v dX are
+    bit-identical; dX and the input norm's weight gradient differ only by the f32 split-K order
+    (norm-relative 1e-3 here, far inside the 2e-2 tolerance)."""
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("PICOTRON_DUAL_QKV", v)
+        outs.append(_layer_grads(B=4, S=1024, H=2048, I=8192, nh=32, nkv=32, d=64, seed=11))
+    (y0, dx0, *g0), (y1, dx1, *g1) = outs
+    assert torch.equal(y0, y1)
+    for n, a, b in zip(NAMES, g0, g1):
+        if n == "input_layernorm.weight":
+            assert rel(b, a) < 1e-3, n
+        else:
+            assert torch.equal(a, b), n
+    assert rel(dx1, dx0) < 1e-3
 
 
 def _layer_parity(B, S, H, I, nh, nkv, d, seed=0, main_grad=False):
