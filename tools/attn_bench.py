@@ -54,6 +54,9 @@ def main():
     ap.add_argument("--H", type=int, default=32)
     ap.add_argument("--D", type=int, default=64)
     ap.add_argument("--old", default="")
+    ap.add_argument("--model-path", action="store_true",
+                    help="causal: time the backward as the layer calls it (delta inside, no precomputed delta)")
+    ap.add_argument("--env-ab", default="", help="VAR: also time the new library with VAR=0 (an env switch A/B)")
     ap.add_argument("--full", action="store_true",
                     help="the CP ring's visiting block: no causal mask, f32 dq/dk/dv accumulators (grad_f32)")
     ap.add_argument("--rounds", type=int, default=2, help="interleaved rounds; medians are printed at the end")
@@ -71,6 +74,10 @@ def main():
     libs = {"new": _C.load_library()}
     for i, path in enumerate(x for x in a.old.split(",") if x):   # comma-separated: old, old1, old2 ...
         libs["old" if i == 0 else f"old{i}"] = _C.load_library(os.path.abspath(path), strict=False)
+    envs = {name: {} for name in libs}
+    if a.env_ab:   # the new library once more, with the switch off ("old" in the comparison below)
+        libs["old" if "old" not in libs else "new_" + a.env_ab + "0"] = libs["new"]
+        envs[list(libs)[-1]] = {a.env_ab: "0"}
     outs = {}
     med = {name: {"fwd": [], "bwd": []} for name in libs}
     for rnd in range(a.rounds):
@@ -78,6 +85,9 @@ def main():
         order = order[rnd % len(order):] + order[:rnd % len(order)]   # rotate who goes first
         for name, lib in order:
             _C._lib = lib
+            for var in {v for e in envs.values() for v in e}:
+                os.environ.pop(var, None)
+            os.environ.update(envs[name])
             o, lse = K.attn_fwd(q, k, v, scale, causal)
             delta = K.attn_delta(do, o)
             if a.full:
@@ -91,10 +101,11 @@ def main():
                     K.attn_bwd(do, q, k, v, o, lse, scale, False, dq=acc[0], dk=acc[1], dv=acc[2], grad_f32=True,
                                delta=delta)
             else:
-                dq, dk, dv, _ = K.attn_bwd(do, q, k, v, o, lse, scale, True, delta=delta)
+                dl = None if a.model_path else delta
+                dq, dk, dv, _ = K.attn_bwd(do, q, k, v, o, lse, scale, True, delta=dl)
 
                 def bwd():
-                    K.attn_bwd(do, q, k, v, o, lse, scale, True, delta=delta)
+                    K.attn_bwd(do, q, k, v, o, lse, scale, True, delta=dl)
             outs[name] = [t.clone() for t in (o, lse, dq, dk, dv)]
             t_fwd = graph_us(lambda: K.attn_fwd(q, k, v, scale, causal, out=o, lse=lse), a.reps)
             t_bwd = graph_us(bwd, a.reps)

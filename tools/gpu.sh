@@ -12,7 +12,7 @@
 #   gloo2        bench.py --gpus 2 --backend gloo rehearsal (2 ranks on cuda:0)
 #   pp2          bench.py --gpus 2 --pp 2 --backend gloo rehearsal of the pipeline engine (config 4's 1F1B)
 #   dp           bench.py --dp-bucket fp32 / bf16 vs plain (the per-GPU DP cost)
-#   attn         tools/attn_bench.py d64 and d128 (OLD=<lib> for an in-process A/B)
+#   attn         tools/attn_bench.py d64 and d128 (OLD=<lib> for an in-process A/B; ATTN64_ARGS for the d64 run)
 #   pmcattn      attention PMC passes (ATTN_ARGS="--B 1 --S 4096 --H 32 --D 128" for d128)
 #   norm         tools/norm_bench.py (OLD=<lib> for an A/B)
 #   tpprof       rocprofv3 kernel trace of the TP=8 proxy (PROXY="--tp-proxy 8" or "--cp-proxy 8 --model ...")
@@ -100,7 +100,7 @@ step_dp() {
 
 step_attn() {
   local old=${OLD:+--old $OLD}
-  timeout -k 10 200 python -u tools/attn_bench.py --rounds ${ROUNDS:-4} $old > $O.attn_d64.log 2>&1 || { echo attn d64 failed; tail -30 $O.attn_d64.log; return 1; }
+  timeout -k 10 200 python -u tools/attn_bench.py --rounds ${ROUNDS:-4} $old ${ATTN64_ARGS} > $O.attn_d64.log 2>&1 || { echo attn d64 failed; tail -30 $O.attn_d64.log; return 1; }
   cat $O.attn_d64.log
   timeout -k 10 200 python -u tools/attn_bench.py --rounds ${ROUNDS:-4} --B 1 --S 4096 --D 128 $old > $O.attn_d128.log 2>&1 || { echo attn d128 failed; tail -30 $O.attn_d128.log; return 1; }
   cat $O.attn_d128.log
