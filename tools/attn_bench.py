@@ -56,7 +56,7 @@ def main():
     ap.add_argument("--old", default="")
     ap.add_argument("--model-path", action="store_true",
                     help="causal: time the backward as the layer calls it (delta inside, no precomputed delta)")
-    ap.add_argument("--env-ab", default="", help="VAR: also time the new library with VAR=0 (an env switch A/B)")
+    ap.add_argument("--env-ab", default="", help="VAR: time the new library with VAR=1 and with VAR=0 (an env A/B)")
     ap.add_argument("--full", action="store_true",
                     help="the CP ring's visiting block: no causal mask, f32 dq/dk/dv accumulators (grad_f32)")
     ap.add_argument("--rounds", type=int, default=2, help="interleaved rounds; medians are printed at the end")
@@ -75,7 +75,8 @@ def main():
     for i, path in enumerate(x for x in a.old.split(",") if x):   # comma-separated: old, old1, old2 ...
         libs["old" if i == 0 else f"old{i}"] = _C.load_library(os.path.abspath(path), strict=False)
     envs = {name: {} for name in libs}
-    if a.env_ab:   # the new library once more, with the switch off ("old" in the comparison below)
+    if a.env_ab:   # the new library with VAR=1 ("new") and once more with VAR=0 ("old" in the comparison)
+        envs["new"] = {a.env_ab: "1"}
         libs["old" if "old" not in libs else "new_" + a.env_ab + "0"] = libs["new"]
         envs[list(libs)[-1]] = {a.env_ab: "0"}
     outs = {}
