@@ -278,19 +278,6 @@ int pt_attn_bwd_fused_delta(const void* q, const int64_t* q_str, const void* k, 
                             const int64_t* dv_str, int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk,
                             int64_t D, float scale, int causal, const void* rope_cos, const void* rope_sin,
                             int64_t rope_stride, int64_t lse_ld, hipStream_t stream);
-/* pt_attn_bwd_fused_delta's head-dim-64 form through dS (same reference interface,
- * model.py:33-37 flash_attn_func backward): D = rowsum(dO * O) by the delta pass into delta_out, the
- * dK/dV kernel also stores bf16 dS^T into the caller's workspace ds_ws ([B, H, Sk, Sq] bf16,
- * ds_ws_elems >= B*H*Sk*Sq; causal: only blocks at or below the diagonal are written and read), and
- * the dQ kernel forms dQ = scale * dS K from it instead of recomputing S, P and dP.  D = 64 only
- * (PT_EUNSUPPORTED otherwise); bf16 gradients. */
-int pt_attn_bwd_ds(const void* q, const int64_t* q_str, const void* k, const int64_t* k_str, const void* v,
-                   const int64_t* v_str, const void* o, const int64_t* o_str, const void* dout,
-                   const int64_t* do_str, const float* lse, float* delta_out, void* dq, const int64_t* dq_str,
-                   void* dk, const int64_t* dk_str, void* dv, const int64_t* dv_str, int64_t B, int64_t H,
-                   int64_t HKV, int64_t Sq, int64_t Sk, int64_t D, float scale, int causal, const void* rope_cos,
-                   const void* rope_sin, int64_t rope_stride, int64_t lse_ld, void* ds_ws, int64_t ds_ws_elems,
-                   hipStream_t stream);
 
 #ifdef __cplusplus
 }

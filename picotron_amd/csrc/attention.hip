@@ -82,11 +82,6 @@ struct AttnArgs {
   // bwd: when set, the dQ kernel (launched first) computes D = rowsum(dO * O) of its own rows from
   // O (a.o, bf16) and writes it here for the dK/dV kernel -- no separate delta pass
   float* delta_w;
-  // bwd, dS form (d64): the dK/dV kernel stores bf16 dS^T here ([B, H, Sk, Sq]: plane ds_sbh elements
-  // per (batch, query head), rows = keys ds_sk apart) and the dQ kernel reads it instead of
-  // recomputing S, P and dP
-  uint16_t* ds;
-  int64_t ds_sbh, ds_sk;
 };
 
 template <int D>
@@ -574,7 +569,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, i
   };
 
   // one (query head, q tile) step
-  auto tile = [&](const lds_u8* sq, int hq, int qt) {
+  auto tile = [&](const lds_u8* sq, int qt) {
 #ifdef PT_ABLATE
     if (a.ablate & 128) return;  // diagnostic: the one-wave dK/dV kernel's DMA / barrier skeleton alone
 #endif
@@ -605,8 +600,6 @@ __device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, i
         s[r] = p;                             // P
         dp[r] = p * (dp[r] - sdel[qi]);       // dS
       }
-      if (a.ds)   // dS^T row of my key, the half tile's 32 queries (store_T_bf16's row-per-lane form)
-        store_T_bf16(a.ds + ((int64_t)b * a.H + hq) * a.ds_sbh + (int64_t)mykey * a.ds_sk + qs, 0, dp, 1.0f, lane);
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
         const bf16x8_t pb = acc_as_b(s, st), db = acc_as_b(dp, st);
@@ -631,7 +624,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, i
     if (++nxt_t == nq) { nxt_t = 0; ++nxt_h; }
     if (it + 1 < n_iter) stage(nxt_h, qt_begin + nxt_t, buf ^ 1);
     const lds_u8* sq = smem + buf * STAGE_B;
-    tile(sq, cur_h, qt_begin + cur_t);
+    tile(sq, qt_begin + cur_t);
     cur_h = nxt_h; cur_t = nxt_t;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (it + 1 < n_iter) put_lse(buf ^ 1);
@@ -1099,94 +1092,6 @@ void attn_bwd_dq_kernel(AttnArgs a) {
   }
 }
 
-// ============================================================================ dQ from dS
-// dQ = scale * dS K from the dS^T the dK/dV kernel stored (a.ds): no S / P / dP recomputation.  A
-// step stages one K tile [64 keys x D] and the workgroup's dS^T tile [64 keys x 128 queries] (rows
-// 256 B: the d128 swizzle); each wave runs dQ^T [D x 32] += K^T dS^T over the tile's four 16-key
-// steps, both operands by transposed LDS reads, in the dQ kernel's key order.  Causal: a 32-key half
-// that lies wholly after the wave's queries was never written (the dK/dV kernel skips that block) and
-// is skipped here as well.
-template <int D>
-__device__ __forceinline__ void attn_bwd_dq_ds_block(const AttnArgs& a, int bx, int h, int b) {
-  constexpr int DT = D / 32;
-  constexpr int TILE_K = KT * D * 2, TILE_S = KT * NW * 32 * 2, STAGE_B = TILE_K + TILE_S;
-  constexpr int NS = 3, OPS = (TILE_K + TILE_S) / 1024 / NW;
-  static_assert(NW * 32 == 128, "the dS^T tile is staged as 128 columns (the d128 image)");
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
-  lds_u8* smem = (lds_u8*)smem_raw;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int nqb = a.Sq / (NW * 32);
-  const int qb = a.causal ? nqb - 1 - bx : bx;
-  const int hk = h / (a.H / a.HKV);
-  const int qb0 = qb * NW * 32;
-  const int q0 = qb0 + wave * 32;
-  const int myq = q0 + (lane & 31);
-
-  const uint16_t* kbase = a.k + b * a.k_sb + hk * a.k_sh;
-  const uint16_t* dsb = a.ds + ((int64_t)b * a.H + h) * a.ds_sbh + qb0;
-  const int kv_end = a.causal ? qb0 + NW * 32 : a.Sk;
-  const int nkt = kv_end / KT;
-  f32x16_t dq[DT];
-#pragma unroll
-  for (int i = 0; i < DT; ++i) dq[i] = zero16();
-
-  auto stage = [&](int kt, int buf) {
-    lds_u8* sk = smem + buf * STAGE_B;
-    stage_rows<D>(kbase + (int64_t)kt * KT * a.k_ss, a.k_ss, sk, wave, lane);
-    stage_rows<128>(dsb + (int64_t)kt * KT * a.ds_sk, a.ds_sk, sk + TILE_K, wave, lane);
-  };
-  const int pre = nkt < NS - 1 ? nkt : NS - 1;
-  for (int t = 0; t < pre; ++t) stage(t, t);
-  vm_wait<0>();
-  __syncthreads();
-
-  auto tile = [&](const lds_u8* sk, int kv0) {
-    const lds_u8* sds = sk + TILE_K;
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      if (a.causal && kv0 + 32 * hh > q0 + 31) continue;  // wave-uniform: never written
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int st = 2 * hh + u;
-        const bf16x8_t db = rd_tr<128>(sds, st, wave, lane);
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) dq[dt] = mfma(rd_tr<D>(sk, st, dt, lane), db, dq[dt]);
-      }
-    }
-  };
-
-  for (int kt = 0, buf = 0, sbuf = pre % NS; kt < nkt; ++kt) {
-    if (kt + NS - 1 < nkt) {
-      stage(kt + NS - 1, sbuf);
-      if (++sbuf == NS) sbuf = 0;
-    }
-    tile(smem + buf * STAGE_B, kt * KT);
-    if (++buf == NS) buf = 0;
-    const int issued = kt + NS - 1 < nkt ? kt + NS - 1 : nkt - 1;
-    ring_wait<OPS, NS>(issued - (kt + 1));
-    __syncthreads();
-  }
-
-  uint16_t* dqr = (uint16_t*)a.dq + b * a.dq_sb + (int64_t)myq * a.dq_ss + h * a.dq_sh;
-  if (a.rope_cos) {
-    store_T_bf16_unrope<DT>(dqr, dq, a.scale, a.rope_cos + (int64_t)myq * a.rope_ld,
-                            a.rope_sin + (int64_t)myq * a.rope_ld, lane);
-  } else {
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) store_T_bf16(dqr, dt, dq[dt], a.scale, lane);
-  }
-}
-
-template <int D>
-__global__ __launch_bounds__(NW * 64) void attn_bwd_dq_ds_kernel(AttnArgs a) {
-  int bx, hh, b;
-  attn_coords(a, bx, hh, b);
-  for (int pass = 0; pass <= a.pair; ++pass) {
-    if (pass) __syncthreads();
-    attn_bwd_dq_ds_block<D>(a, pass ? nqb_of(a) - 1 - bx : bx, hh, b);
-  }
-}
-
 template <typename K>
 void set_smem(K kern, int bytes) {
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
@@ -1227,7 +1132,7 @@ int attn_bwd_impl(const void* q, const int64_t* q_str, const void* k, const int6
                   const int64_t* dv_str, int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int64_t D,
                   float scale, int causal, int grad_f32, const void* rope_cos, const void* rope_sin,
                   int64_t rope_stride, const void* o, const int64_t* o_str, float* delta_w, int64_t lse_ld,
-                  hipStream_t stream, uint16_t* ds = nullptr);
+                  hipStream_t stream);
 
 }  // namespace
 
@@ -1323,7 +1228,7 @@ int attn_bwd_impl(const void* q, const int64_t* q_str, const void* k, const int6
                   const int64_t* dv_str, int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int64_t D,
                   float scale, int causal, int grad_f32, const void* rope_cos, const void* rope_sin,
                   int64_t rope_stride, const void* o, const int64_t* o_str, float* delta_w, int64_t lse_ld,
-                  hipStream_t stream, uint16_t* ds) {
+                  hipStream_t stream) {
   if (!q || !k || !v || !dout || !lse || !dq || !dk || !dv) return PT_EINVAL;
   if (lse_ld != 0 && lse_ld < Sq) return PT_EINVAL;
   if (rope_cos && (!rope_sin || grad_f32 || Sq != Sk || (rope_stride & 3) || !pt_aligned16(rope_cos) ||
@@ -1365,20 +1270,6 @@ int attn_bwd_impl(const void* q, const int64_t* q_str, const void* k, const int6
 #ifdef PT_ABLATE
   a.ablate = getenv("PICOTRON_ATTN_ABLATE") ? atoi(getenv("PICOTRON_ATTN_ABLATE")) : 0;
 #endif
-  if (ds) {   // dS form (d64, bf16 grads, delta given): dK/dV storing dS^T, then dQ from it
-    if (D != 64 || grad_f32 || !delta || delta_w) return PT_EINVAL;
-    a.ds = ds;
-    a.ds_sk = Sq;
-    a.ds_sbh = Sk * Sq;
-    set_smem(attn_bwd_dkdv_kernel<64>, smem_q);
-    attn_bwd_dkdv_kernel<64><<<gk, NW * 64, smem_q, stream>>>(a);
-    PT_CHECK_LAUNCH();
-    const int smem_ds = 3 * (KT * 64 * 2 + KT * NW * 32 * 2);
-    set_smem(attn_bwd_dq_ds_kernel<64>, smem_ds);
-    attn_bwd_dq_ds_kernel<64><<<gq, NW * 64, smem_ds, stream>>>(a);
-    PT_CHECK_LAUNCH();
-    return PT_OK;
-  }
   // dQ first: with delta_w set it produces the D the dK/dV kernel reads (same stream, in order)
   if (D == 64) {
     set_smem(attn_bwd_dq_kernel<64>, smem_kv);
@@ -1429,29 +1320,6 @@ int pt_attn_bwd_fused_delta(const void* q, const int64_t* q_str, const void* k, 
   return attn_bwd_impl(q, q_str, k, k_str, v, v_str, dout, do_str, lse, nullptr, dq, dq_str, dk, dk_str, dv,
                        dv_str, B, H, HKV, Sq, Sk, D, scale, causal, 0, rope_cos, rope_sin, rope_stride, o, o_str,
                        delta_out, lse_ld, stream);
-}
-
-
-// pt_attn_bwd_fused_delta through dS (d64): D = rowsum(dO * O) by the delta pass into delta_out, the
-// dK/dV kernel also stores bf16 dS^T into ds_ws ([B, H, Sk, Sq] bf16, ds_ws_elems >= B H Sk Sq; with a
-// causal mask only the blocks at or below the diagonal are written and read), and the dQ kernel forms
-// dQ = scale dS K from it instead of recomputing S, P and dP
-int pt_attn_bwd_ds(const void* q, const int64_t* q_str, const void* k, const int64_t* k_str, const void* v,
-                   const int64_t* v_str, const void* o, const int64_t* o_str, const void* dout,
-                   const int64_t* do_str, const float* lse, float* delta_out, void* dq, const int64_t* dq_str,
-                   void* dk, const int64_t* dk_str, void* dv, const int64_t* dv_str, int64_t B, int64_t H,
-                   int64_t HKV, int64_t Sq, int64_t Sk, int64_t D, float scale, int causal, const void* rope_cos,
-                   const void* rope_sin, int64_t rope_stride, int64_t lse_ld, void* ds_ws, int64_t ds_ws_elems,
-                   hipStream_t stream) {
-  if (D != 64) return PT_EUNSUPPORTED;
-  if (!o || !delta_out || !o_str || !ds_ws || B <= 0 || H <= 0 || Sq <= 0 || Sk <= 0) return PT_EINVAL;
-  if (ds_ws_elems < B * H * Sk * Sq) return PT_EINVAL;
-  if (!pt_aligned16(ds_ws) || Sq % 8) return PT_EALIGN;
-  const int rc = pt_attn_bwd_delta(dout, do_str, o, o_str, delta_out, B, H, Sq, D, lse_ld, stream);
-  if (rc) return rc;
-  return attn_bwd_impl(q, q_str, k, k_str, v, v_str, dout, do_str, lse, delta_out, dq, dq_str, dk, dk_str, dv,
-                       dv_str, B, H, HKV, Sq, Sk, D, scale, causal, 0, rope_cos, rope_sin, rope_stride, nullptr,
-                       nullptr, nullptr, lse_ld, stream, (uint16_t*)ds_ws);
 }
 
 }  // extern "C"

@@ -1113,12 +1113,6 @@ def attn_delta(dout, out, delta=None):
     return delta
 
 
-def attn_ds_enabled():
-    """The d64 backward through dS (pt_attn_bwd_ds) when PICOTRON_ATTN_DS=1; default: the recomputing
-    dQ kernel."""
-    return os.environ.get("PICOTRON_ATTN_DS", "0") != "0"
-
-
 def attn_bwd(dout, q, k, v, out, lse, scale, causal, dq=None, dk=None, dv=None, grad_f32=False, delta=None,
              rope=None):
     """rope = (cos, sin) [S, d] bf16 tables: dq / dk are stored rotated back by -theta (the RoPE
@@ -1149,17 +1143,6 @@ def attn_bwd(dout, q, k, v, out, lse, scale, causal, dq=None, dk=None, dv=None, 
         _req(rc_sin.stride(0) == rc_cos.stride(0), "attn_bwd rope tables share a stride")
         rstride = rc_cos.stride(0)
     ld = _lse_ld(lse, B, H, Sq)
-    if fuse_delta and D == 64 and attn_ds_enabled():
-        # d64: dK/dV store dS^T, dQ = scale dS K from it (no second S / P / dP); the delta pass first
-        _req(out.shape == q.shape, "attn_bwd: out must be [B, Sq, H, D]")
-        delta = torch.empty(B, H, ld, dtype=torch.float32, device=q.device)[:, :, :Sq]
-        ws = torch.empty(B * H * Sk * Sq, dtype=BF16, device=q.device)
-        rc = lib.pt_attn_bwd_ds(_ptr(q), _str3(q), _ptr(k), _str3(k), _ptr(v), _str3(v), _ptr(out), _str3(out),
-                                _ptr(dout), _str3(dout), _ptr(lse), _ptr(delta), _ptr(dq), _str3(dq), _ptr(dk),
-                                _str3(dk), _ptr(dv), _str3(dv), B, H, HKV, Sq, Sk, D, float(scale), int(bool(causal)),
-                                _ptr(rc_cos), _ptr(rc_sin), rstride, ld, _ptr(ws), ws.numel(), _C.stream_ptr(q.device))
-        _C.check(rc, "pt_attn_bwd_ds")
-        return dq, dk, dv, delta
     if fuse_delta:   # D = rowsum(dO * O) inside the dQ kernel (no separate pass)
         _req(out.shape == q.shape, "attn_bwd: out must be [B, Sq, H, D]")
         _req(ld == Sq, "attn_bwd: the fused-delta form takes a dense lse")

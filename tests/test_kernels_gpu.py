@@ -735,33 +735,6 @@ def test_attention_dkdv_wave_pair_split_is_bit_identical(monkeypatch, B, S, H, H
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("B,S,H,HKV,causal,rope", [
-    (4, 1024, 4, 4, True, True), (1, 512, 4, 2, True, False), (2, 384, 2, 1, True, False),
-    (1, 512, 2, 2, False, False), (2, 256, 4, 4, False, True)])
-def test_attention_bwd_through_ds_matches_recompute(monkeypatch, B, S, H, HKV, causal, rope):
-    """d64 backward through dS (the dK/dV kernel stores bf16 dS^T, dQ = scale dS K from it) against
-    the recomputing dQ kernel: dV bit-identical (it does not depend on delta), dQ / dK within the
-    rounding of delta's two summation orders and of the shared bf16 dS; both against the fp32
-    reference of the same inputs."""
-    from picotron_amd import kernels as K_
-    D = 64
-    q, k, v = _qkv(B, S, H, HKV, D)
-    scale = 1 / math.sqrt(D)
-    o, lse = K_.attn_fwd(q, k, v, scale, causal)
-    do = torch.randn(o.shape).to(BF).to(DEV)
-    rp = tuple(t.to(DEV) for t in O.get_cos_sin(S, D, base=10000.0)) if rope else None
-    outs = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("PICOTRON_ATTN_DS", flag)
-        g = K_.attn_bwd(do, q, k, v, o, lse, scale, causal, rope=rp)[:3]
-        torch.cuda.synchronize()
-        outs.append([t.clone() for t in g])
-    (dq0, dk0, dv0), (dq1, dk1, dv1) = outs
-    assert torch.equal(dv0, dv1)
-    assert rel_err(dq1, dq0) < 5e-3 and rel_err(dk1, dk0) < 5e-3
-    assert torch.isfinite(dq1).all() and torch.isfinite(dk1).all()
-
-
 def test_attention_ring_merge_matches_full():
     """Two key blocks merged by the fused update_out_and_lse epilogue == attention over both
     (context_parallel.py:157-187), and the backward with the global LSE sums to the full grads."""
