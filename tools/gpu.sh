@@ -18,7 +18,7 @@
 #   tpprof       rocprofv3 kernel trace of the TP=8 proxy (PROXY="--tp-proxy 8" or "--cp-proxy 8 --model ...")
 #   counters     rocprofv3 -L: the counters this box's gfx950 exposes (e.g. for HBM vs Infinity-Cache reads)
 #   mall         TCC_EA0_RDREQ vs TCC_EA0_RDREQ_DRAM on a cold and a warm (Infinity-Cache) read (tools/mall_probe.py)
-#   envab        whole-step A/B of two env settings: A="X=0" B="X=1" ROUNDS=3
+#   envab        whole-step A/B of two (or three: C=...) env settings: A="X=0" B="X=1" ROUNDS=3
 #   libab        whole-step A/B of library builds swapped in place: LIBS=a.so,b.so ROUNDS=2
 set -o pipefail
 export TMPDIR=/tmp
@@ -146,8 +146,8 @@ PY
 
 step_envab() {
   for i in $(seq 1 ${ROUNDS:-3}); do
-    for v in A B; do
-      if [ $v = A ]; then E=$A; else E=$B; fi
+    for v in A B ${C:+C}; do
+      if [ $v = A ]; then E=$A; elif [ $v = B ]; then E=$B; else E=$C; fi
       env $E timeout -k 10 300 python -u bench.py --cpu-tokens 0 --steps 3 $BENCH_ARGS > $O.$v$i.json 2>/dev/null || { echo "bench $E failed"; return 1; }
       jline $O.$v$i.json "$E"
     done
