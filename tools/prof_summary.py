@@ -57,6 +57,12 @@ def main():
             hbm = f"{(p[0] / p[1] + p[2] / p[3]) / 1e6:.1f}"
         print(f"| `{k[0]}` | {k[1]} | {len(v)} | {sum(v) / 1e6:.1f} | {sum(v) / total * 100:.1f}% | "
               f"{sum(v) / len(v) / 1e3:.1f} | {hbm} |")
+    # the bench line's roofline kernel is "every GEMM launch": its average, to set beside
+    # roofline.avg_launch_ms (bench.py times one steady-state micro-batch per step with HIP events)
+    g = [d for k, v in groups.items() if k[0].startswith("void gemm_") for d in v]
+    if g:
+        print(f"\nAll GEMM launches (`gemm_*` kernels): {len(g)} launches, {sum(g) / 1e6:.1f} ms, "
+              f"average {sum(g) / len(g) / 1e3:.1f} us per launch, {sum(g) / total * 100:.1f}% of kernel time")
 
 
 if __name__ == "__main__":
