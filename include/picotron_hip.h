@@ -279,6 +279,18 @@ int pt_attn_bwd_fused_delta(const void* q, const int64_t* q_str, const void* k, 
                             int64_t D, float scale, int causal, const void* rope_cos, const void* rope_sin,
                             int64_t rope_stride, int64_t lse_ld, hipStream_t stream);
 
+/* ---- measurement variants ------------------------------------------------------------------
+ * Not a reference interface: selects between kernel forms with identical results, for A/B runs and
+ * the bit-identity tests.  The library reads no environment; the host sets these (picotron_amd/
+ * switches.py reads PICOTRON_<NAME> once at import and pushes them here).  Names and defaults:
+ *   "attn_pair"     1   causal attention: pair query/key blocks (i, n-1-i) per workgroup
+ *   "attn_split"    2   dK/dV kernel form per head dim: bit 0 = d64, bit 1 = d128 use the wave pair
+ *   "gemm_group_m" -1   GEMM tile-row grouping for L2 reuse (-1 = the built-in per-tile choice)
+ *   "gemm_mix"      1   q|k|v + RoPE GEMM as one mixed 256x256 / 256x128 launch
+ * Returns PT_EINVAL for an unknown name.  pt_get_variant returns the value (or PT_EINVAL). */
+int pt_set_variant(const char* name, int value);
+int pt_get_variant(const char* name);
+
 #ifdef __cplusplus
 }
 #endif

@@ -66,6 +66,8 @@ SIGNATURES = {
     "pt_cross_entropy_fwd_stats": (_i32, [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i64, _i64, _vp, _vp]),
     "pt_cross_entropy_mean": (_i32, [_vp, _vp, _i64, _i64, _vp, _vp, _vp, _i32, _i32, _vp]),
     "pt_embedding_sort": (_i32, [_vp, _i64, _i64, _i64, _i32, _i64, _vp, _vp, _vp]),
+    "pt_set_variant": (_i32, [ctypes.c_char_p, _i32]),
+    "pt_get_variant": (_i32, [ctypes.c_char_p]),
     "pt_gemm_rope": (_i32, [_vp, _i64, _vpp, _i64p, _i64p, _i32, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _i64,
                             _i64, _i64, _i32, _vp]),
 }
@@ -103,6 +105,8 @@ def load_library(path=LIB_PATH, strict=True):
         fn.restype = res
         fn.argtypes = args
     if is_main:
+        from .switches import apply_native
+        apply_native(lib)
         _lib = lib
     else:
         _alt_libs[path] = lib

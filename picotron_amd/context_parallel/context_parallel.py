@@ -34,6 +34,7 @@ import torch
 
 from .. import kernels as K
 from .. import process_group_manager as pgm
+from ..switches import S
 from .cp_communications import ContextCommunicate, zigzag_exchange
 
 
@@ -80,7 +81,7 @@ def zigzag_enabled(S, is_causal, blocks=HipBlocks):
     """The load-balanced layout applies to a causal ring of C > 1 whose half shards tile."""
     C = pgm.current().cp_world_size
     return (is_causal and C > 1 and S % (2 * getattr(blocks, "align", 1)) == 0
-            and os.environ.get("PICOTRON_RING_ZIGZAG", "1") != "0")
+            and S.ring_zigzag != 0)
 
 
 def _zz_kind(step, rank, world):

@@ -34,12 +34,8 @@ typedef __attribute__((address_space(3))) uint8_t lds_u8;
 
 // the d64 forward: a batch of LDS operand reads stays ahead of the MFMAs that consume it (no
 // scheduling across; 34.3 vs 34.9 us at the SmolLM layer shape; at d128 and in the backward kernels
-// the compiler's own interleave measured equal or faster).  -DPT_NO_BATCH: that interleave (A/B)
-#ifdef PT_NO_BATCH
-#define PT_BATCH_BARRIER(D) ((void)0)
-#else
+// the compiler's own interleave measured equal or faster).
 #define PT_BATCH_BARRIER(D) do { if constexpr ((D) == 64) __builtin_amdgcn_sched_barrier(0); } while (0)
-#endif
 
 namespace {
 
@@ -74,11 +70,6 @@ struct AttnArgs {
   // causal load balance: each workgroup runs block x and block (n - 1 - x) one after the other,
   // so every workgroup gets the same number of tiles whatever CU slot it lands in
   int pair;
-  // dK/dV wave-pair kernel: which waves are score waves (0: waves 0-3, 1: even waves)
-  int role_even;
-  int prio;    // dK/dV pair kernel: raise the score wave's priority over its MFMA cluster
-  unsigned long long* stamps;  // diagnostic builds only (-DPT_STAMP): per-step s_memtime of workgroups 0-7
-  int ablate;  // diagnostic builds only (-DPT_ABLATE): bits skip parts of the dK/dV pair kernel
   // bwd: when set, the dQ kernel (launched first) computes D = rowsum(dO * O) of its own rows from
   // O (a.o, bf16) and writes it here for the dK/dV kernel -- no separate delta pass
   float* delta_w;
@@ -151,12 +142,6 @@ __device__ __forceinline__ int crow(int r, int lane) { return (r & 3) + 8 * (r >
 // (block, head, batch) ids, blocks of one head adjacent: a head's tiles are fetched into one L2
 // and re-read from there (a head's K+V at S 1024, d 64 is 256 KiB; an XCD's L2 is 4 MiB).
 __device__ __forceinline__ void attn_coords(const AttnArgs& a, int& x, int& y, int& z) {
-#ifdef PT_ABLATE
-  if (a.ablate & 16) {  // diagnostic: the dispatcher's own order
-    x = blockIdx.x; y = blockIdx.y; z = blockIdx.z;
-    return;
-  }
-#endif
   const int nx = gridDim.x, ny = gridDim.y, nwg = nx * ny * gridDim.z;
   const int id = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
   const int xcd = id & 7, q = nwg >> 3, r = nwg & 7;
@@ -352,9 +337,6 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
   auto tile = [&](const lds_u8* sk, int kv0) {
     const lds_u8* sv = sk + TILE_B;
     if (a.causal && kv0 > q0 + 31) return;  // wave-uniform: skip tiles fully above the diagonal
-#ifdef PT_ABLATE
-    if (a.ablate & 64) return;  // diagnostic: the forward's DMA / barrier skeleton alone
-#endif
     {
       f32x16_t s[2];
       // the tile's K operands in one batch of LDS reads ahead of the MFMAs (left to itself the
@@ -425,11 +407,7 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
     }
   };
 
-#ifdef PT_ABLATE
-  const int nkt_run = (a.ablate & 256) ? 0 : nkt;   // diagnostic: prologue + epilogue only
-#else
   const int nkt_run = nkt;
-#endif
   for (int kt = 0, buf = 0, sbuf = pre % NS; kt < nkt_run; ++kt) {
     if (kt + NS - 1 < nkt) {  // into the stage tile kt - 1 used (every wave passed its barrier)
       stage(kt + NS - 1, sbuf);
@@ -446,9 +424,6 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
   const float inv_l = 1.0f / l;
   const float lse = m * kLn2 + __logf(l);
   float* lse_p = a.lse + ((int64_t)b * a.H + h) * a.lse_ld + myq;
-#ifdef PT_ABLATE
-  if (a.ablate & 512) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); return; }   // diagnostic: no epilogue
-#endif
   if (!a.merge) {
     uint16_t* orow = (uint16_t*)a.o + b * a.o_sb + (int64_t)myq * a.o_ss + h * a.o_sh;
 #pragma unroll
@@ -570,9 +545,6 @@ __device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, i
 
   // one (query head, q tile) step
   auto tile = [&](const lds_u8* sq, int qt) {
-#ifdef PT_ABLATE
-    if (a.ablate & 128) return;  // diagnostic: the one-wave dK/dV kernel's DMA / barrier skeleton alone
-#endif
     const lds_u8* sdo = sq + TILE_B;
     const float* sl2 = (const float*)(sq + 2 * TILE_B);
     const float* sdel = sl2 + KT;
@@ -681,12 +653,7 @@ void attn_bwd_dkdv_kernel(AttnArgs a) {
 // operands and their order per accumulator are those of attn_bwd_dkdv_block: dK and dV are
 // bit-identical.
 constexpr int kXchB = 4 * 2 * 2 * 1024;  // one step's P|dS hand-off: 4 pairs x 2 k-steps x 2 kinds x 1 KiB
-#ifdef PT_STAMP
-constexpr int kStampSteps = 72;
-constexpr int kStampB = 8 * 4 * kStampSteps * 8;
-#else
 constexpr int kStampB = 0;
-#endif
 
 
 template <int D>
@@ -701,8 +668,8 @@ __device__ __forceinline__ void attn_bwd_dkdv_pair_block(const AttnArgs& a, int 
   lds_u8* smem = (lds_u8*)smem_raw;
   lds_u8* xch = smem + NSTG * STAGE_B;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool score = a.role_even ? (wave & 1) == 0 : wave < 4;
-  const int pr = a.role_even ? wave >> 1 : wave & 3;
+  const bool score = wave < 4;
+  const int pr = wave & 3;
   const int k0 = bx * 128 + pr * 32;
   const int mykey = k0 + (lane & 31);
   const int group = a.H / a.HKV;
@@ -739,16 +706,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_pair_block(const AttnArgs& a, int 
   };
   // step j (odd, j = 2t + 1) issues tile t + 2; its end waits for tile t + 1 (used from step 2t + 2)
   auto issue = [&](int j) { return (j & 1) && (j >> 1) + 2 < n_tiles; };
-#ifdef PT_STAMP
-  // per wave and step: (start, arrival at the end-of-step wait) in LDS past the hand-off buffers
-  unsigned long long* stl = (unsigned long long*)(xch + 2 * kXchB) + wave * 4 * kStampSteps;
-  const int wg_lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-  auto stamp = [&](int j, int w) {
-    if (lane == 0 && j < kStampSteps) stl[4 * j + w] = __builtin_amdgcn_s_memtime();
-  };
-#else
   auto stamp = [&](int, int) {};
-#endif
   auto end_step = [&](int j) {
     stamp(j, 3);
     if (j & 1) wait_keep(issue(j));
@@ -792,27 +750,16 @@ __device__ __forceinline__ void attn_bwd_dkdv_pair_block(const AttnArgs& a, int 
           da[ks] = rd_row<D>(sdo, 32 * qh, ks, lane);
         }
         __builtin_amdgcn_sched_barrier(0);
-#ifdef PT_STAMP
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        stamp(j, 1);
-#endif
         f32x16_t s = zero16(), dp = zero16();
         // the score wave's MFMAs go first on the SIMD (its softmax then runs beside the partner's
         // MFMAs instead of after them)
-        if (a.prio) __builtin_amdgcn_s_setprio(1);
-#ifdef PT_ABLATE
-        if (!(a.ablate & 4))
-#endif
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           s = mfma(qa[ks], kf[ks], s);
           dp = mfma(da[ks], vf[ks], dp);
         }
-        if (a.prio) __builtin_amdgcn_s_setprio(0);
-#ifdef PT_STAMP
-        asm volatile("" ::"v"(s[15]), "v"(dp[15]));
-        stamp(j, 2);
-#endif
+        __builtin_amdgcn_s_setprio(0);
         // the row constants, read while the MFMAs run
         float lr[16], dr[16];
 #pragma unroll
@@ -827,9 +774,6 @@ __device__ __forceinline__ void attn_bwd_dkdv_pair_block(const AttnArgs& a, int 
           for (int r = 0; r < 16; ++r)
             if ((r & 3) + 8 * (r >> 2) < thr) s[r] = -INFINITY;
         }
-#ifdef PT_ABLATE
-        if (!(a.ablate & 2))
-#endif
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -(lr[r] * kLog2e)));
@@ -837,9 +781,6 @@ __device__ __forceinline__ void attn_bwd_dkdv_pair_block(const AttnArgs& a, int 
           dp[r] = p * (dp[r] - dr[r]);
         }
         lds_u8* x = xch + (j & 1) * kXchB + pr * 4096 + lane * 16;
-#ifdef PT_ABLATE
-        if (!(a.ablate & 8))
-#endif
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
           *(__attribute__((address_space(3))) bf16x8_t*)(x + st * 2048) = acc_as_b(s, st);
@@ -867,9 +808,6 @@ __device__ __forceinline__ void attn_bwd_dkdv_pair_block(const AttnArgs& a, int 
         const lds_u8* sq = smem + buf * STAGE_B;
         const lds_u8* sdo = sq + TILE_B;
         const lds_u8* x = xch + (h & 1) * kXchB + pr * 4096 + lane * 16;
-#ifdef PT_ABLATE
-        if (!(a.ablate & 1))
-#endif
         {
           // each k-step's LDS operands are read in one batch (the compiler otherwise re-uses one
           // register pair and waits out the LDS latency every two MFMAs): k-step 1's batch is
@@ -885,22 +823,12 @@ __device__ __forceinline__ void attn_bwd_dkdv_pair_block(const AttnArgs& a, int 
               tq[dt] = rd_tr<D>(sq, 2 * qh + st, dt, lane);
             }
             __builtin_amdgcn_sched_barrier(0);
-#ifdef PT_STAMP
-            if (st == 0) {
-              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-              stamp(j, 1);
-            }
-#endif
 #pragma unroll
             for (int dt = 0; dt < DT; ++dt) {
               dv[dt] = mfma(ta[dt], pb, dv[dt]);
               dk[dt] = mfma(tq[dt], db, dk[dt]);
             }
           }
-#ifdef PT_STAMP
-          asm volatile("" ::"v"(dv[DT - 1][15]), "v"(dk[DT - 1][15]));
-          stamp(j, 2);
-#endif
         }
       }
       if (j > 0 && qh) {
@@ -931,11 +859,6 @@ __device__ __forceinline__ void attn_bwd_dkdv_pair_block(const AttnArgs& a, int 
       }
     }
   }
-#ifdef PT_STAMP
-  if (a.stamps && wg_lin < 8)
-    for (int i = lane; i < 4 * kStampSteps; i += 64)
-      a.stamps[((int64_t)wg_lin * 8 + wave) * 4 * kStampSteps + i] = stl[i];
-#endif
 }
 
 template <int D>
@@ -1019,9 +942,6 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
   auto tile = [&](const lds_u8* sk, int kv0) {
     const lds_u8* sv = sk + TILE_B;
     if (a.causal && kv0 > q0 + 31) return;  // wave-uniform: every key of the tile is after my queries
-#ifdef PT_ABLATE
-    if (a.ablate & 32) return;  // diagnostic: the dQ kernel's DMA / barrier skeleton alone
-#endif
     // each 32-key half's dS feeds its two dQ k-steps right away: one dS tile live, not two
     // (16 VGPRs: d128's dQ kernel fits 2 waves per SIMD)
 #pragma unroll
@@ -1097,26 +1017,12 @@ void set_smem(K kern, int bytes) {
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
-// PICOTRON_ATTN_PAIR=0 turns the causal block pairing off (A/B measurement only)
-bool pair_enabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("PICOTRON_ATTN_PAIR");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
-}
+// causal block pairing (variant "attn_pair"; 0 = off, A/B measurement only)
+bool pair_enabled() { return pt_variant(PT_VAR_ATTN_PAIR) == 1; }
 
-// dK/dV kernel form per head dim: bit 0 = d64, bit 1 = d128 use the wave-pair split
-// (PICOTRON_ATTN_SPLIT, read per launch while it is being measured; default both)
-int split_mask() {
-  const char* e = getenv("PICOTRON_ATTN_SPLIT");
-  return e ? atoi(e) : 2;
-}
-int role_even() {
-  const char* e = getenv("PICOTRON_ATTN_ROLE_EVEN");
-  return e ? atoi(e) : 0;
-}
+// dK/dV kernel form per head dim (variant "attn_split"): bit 0 = d64, bit 1 = d128 use the wave-pair
+// split; default d128 only
+int split_mask() { return pt_variant(PT_VAR_ATTN_SPLIT); }
 
 int check_common(const AttnArgs& a, int D) {
   if (D != 64 && D != 128) return PT_EUNSUPPORTED;
@@ -1156,9 +1062,6 @@ int pt_attn_fwd(const void* q, const int64_t* q_str, const void* k, const int64_
   a.lse = lse;
   a.B = (int)B; a.H = (int)H; a.HKV = (int)HKV; a.Sq = (int)Sq; a.Sk = (int)Sk;
   a.scale = scale; a.causal = causal; a.merge = merge;
-#ifdef PT_ABLATE
-  a.ablate = getenv("PICOTRON_ATTN_ABLATE") ? atoi(getenv("PICOTRON_ATTN_ABLATE")) : 0;
-#endif
   int rc = check_common(a, (int)D);
   if (rc) return rc;
   const int nwk = (D == 128 && Sq % (8 * 32) == 0) ? 8 : NW;
@@ -1262,14 +1165,6 @@ int attn_bwd_impl(const void* q, const int64_t* q_str, const void* k, const int6
   const dim3 gk((unsigned)(a.pair ? nkb / 2 : nkb), (unsigned)HKV, (unsigned)B);
   const int smem_pair = 3 * (2 * KT * (int)D * 2 + 2 * KT * 4) + 2 * kXchB + kStampB;
   const bool split = (split_mask() >> (D == 64 ? 0 : 1)) & 1;
-  a.role_even = role_even();
-  a.prio = getenv("PICOTRON_ATTN_PRIO") ? atoi(getenv("PICOTRON_ATTN_PRIO")) : 1;
-#ifdef PT_STAMP
-  a.stamps = getenv("PICOTRON_ATTN_STAMPS") ? (unsigned long long*)strtoull(getenv("PICOTRON_ATTN_STAMPS"), nullptr, 10) : nullptr;
-#endif
-#ifdef PT_ABLATE
-  a.ablate = getenv("PICOTRON_ATTN_ABLATE") ? atoi(getenv("PICOTRON_ATTN_ABLATE")) : 0;
-#endif
   // dQ first: with delta_w set it produces the D the dK/dV kernel reads (same stream, in order)
   if (D == 64) {
     set_smem(attn_bwd_dq_kernel<64>, smem_kv);

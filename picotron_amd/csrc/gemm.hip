@@ -1206,12 +1206,8 @@ void set_smem_once(Kern k, int smem) {
 
 // per-problem tile grid + consecutive tile ids; returns the total tile count
 int group_m_for(int bm, int bn) {
-  static int env = -2;
-  if (env == -2) {  // PICOTRON_GEMM_GROUP_M overrides (A/B measurement)
-    const char* e = getenv("PICOTRON_GEMM_GROUP_M");
-    env = e ? atoi(e) : -1;
-  }
-  if (env > 0) return env;
+  const int g = pt_variant(PT_VAR_GEMM_GROUP_M);  // > 0: override (A/B measurement)
+  if (g > 0) return g;
   return bm == 2 * bn ? 4 : 8;
 }
 
@@ -1297,29 +1293,26 @@ int launch_4ph(GemmGroup g, hipStream_t stream) {
   return PT_OK;
 }
 
-// tile ids: 2 = simple 128x128, 3 = simple 64x64, 4 = simple 256x256, 5 = simple 256x128,
-//           8 / 9 = simple 256x256 / 128x128 with both k-substeps' fragments in flight,
+// tile ids: 2 = simple 128x128, 3 = simple 64x64 (the TP shards' few-tile problems),
 //           12 = 8-phase 256x256 (two half-image wave groups, one wait per K-tile)
 //           13 = 4-phase 256x128 (three K-tiles resident)
-//           (ids 0, 1, 6, 7, 10, 11 were pipelining experiments, measured slower and retired; so
+//           (ids 4, 5, 8, 9 -- the simple 256x256 / 256x128 kernels and their two-substep forms --
+//           were never picked once the phased kernels existed, and the 256x256 ones spilled: dropped
+//           from the library in round 4; ids 0, 1, 6, 7, 10, 11 were pipelining experiments, measured slower and retired; so
 //           was round 2's 14: the 8-phase tile with ONE barrier per K-tile and free-running
 //           phases, 3-13 % slower on every layer shape -- the per-phase ping-pong pays for its
 //           barriers)
 constexpr int kNumTiles = 14;
-const int kTileBM[kNumTiles] = {0, 0, 128, 64, 256, 256, 0, 0, 256, 128, 0, 0, 256, 256};
-const int kTileBN[kNumTiles] = {0, 0, 128, 64, 256, 128, 0, 0, 256, 128, 0, 0, 256, 128};
+const int kTileBM[kNumTiles] = {0, 0, 128, 64, 0, 0, 0, 0, 0, 0, 0, 0, 256, 256};
+const int kTileBN[kNumTiles] = {0, 0, 128, 64, 0, 0, 0, 0, 0, 0, 0, 0, 256, 128};
 
 template <bool AK, bool BKC, int EPI>
 int launch_layout(const GemmGroup& a, int tile, hipStream_t s) {
   switch (tile) {
-    case 8: return launch_t<256, 256, 2, 4, AK, BKC, EPI, 1>(a, s);
-    case 9: return launch_t<128, 128, 2, 2, AK, BKC, EPI, 1>(a, s);
     case 12: return launch_8ph<AK, BKC, EPI>(a, s);
     case 13: return launch_4ph<AK, BKC, EPI>(a, s);
     case 2: return launch_t<128, 128, 2, 2, AK, BKC, EPI>(a, s);
     case 3: return launch_t<64, 64, 2, 2, AK, BKC, EPI>(a, s);
-    case 4: return launch_t<256, 256, 2, 4, AK, BKC, EPI>(a, s);
-    case 5: return launch_t<256, 128, 4, 2, AK, BKC, EPI>(a, s);
     default: return PT_EUNSUPPORTED;
   }
 }
@@ -1476,15 +1469,8 @@ int pick_group_tile(const GemmGroup& g) {
 
 int launch_swiglu(GemmGroup& g, int a_kcontig, int b_kcontig, int epilogue, int tile, hipStream_t stream);
 
-// PICOTRON_GEMM_MIX=0 turns the mixed-tile q|k|v launch off (A/B measurement only)
-bool mix_enabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("PICOTRON_GEMM_MIX");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
-}
+// variant "gemm_mix" = 0 turns the mixed-tile q|k|v launch off (A/B measurement only)
+bool mix_enabled() { return pt_variant(PT_VAR_GEMM_MIX) == 1; }
 
 // q|k|v + RoPE as one mixed-tile launch: the rotated columns [0, rope_cols) in 256x256 tiles, the
 // rest (v) in 256x128 tiles.  PT_EUNSUPPORTED when the shape does not split that way (the caller

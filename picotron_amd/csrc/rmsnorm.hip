@@ -25,19 +25,14 @@ namespace {
 constexpr int kCUs = 256;
 
 // launch shape: waves per block and blocks per CU (grid cap) of the forward and backward kernels.
-// Measured at T 4096 (tools/norm_bench.py, profiles/r02_norm_bench.log, r02_notes.md): 4 x 4 /
-// 16 x 1 (backward + column sum 17.5-18.4 us vs 19.2 with 8 x 2: one 1024-thread block per CU
-// halves the partial rows); PT_NORM ("fwd_wpb,fwd_bpc,bwd_wpb,bwd_bpc", read once) overrides it.
-struct NormCfg { int fwd_wpb, fwd_bpc, bwd_wpb, bwd_bpc; };
-
-const NormCfg& norm_cfg() {
-  static const NormCfg cfg = [] {
-    NormCfg c{4, 4, 16, 1};
-    if (const char* e = getenv("PT_NORM")) sscanf(e, "%d,%d,%d,%d", &c.fwd_wpb, &c.fwd_bpc, &c.bwd_wpb, &c.bwd_bpc);
-    return c;
-  }();
-  return cfg;
-}
+// Measured at T 4096 (tools/norm_bench.py, profiles/r02_norm_bench.log, r02_notes.md): forward 4
+// waves x 4 blocks per CU; backward 16 waves x 1 block per CU (backward + column sum 17.5-18.4 us vs
+// 19.2 with 8 x 2: one 1024-thread block per CU halves the partial rows), 4 waves for the 8-chunk
+// rows (cols > 2048: 16 waves of those would not fit the LDS row buffers and spill).
+constexpr int kFwdWpb = 4, kFwdBpc = 4, kBwdBpc = 1;
+template <int NCH>
+constexpr int bwd_wpb_t() { return NCH == 8 ? 4 : 16; }
+constexpr int bwd_wpb(int nch) { return nch == 8 ? 4 : 16; }
 
 template <int NCH>
 __device__ __forceinline__ void load_row(const uint16_t* __restrict__ p, int lane, int nchunk, bf16x8 (&v)[NCH]) {
@@ -327,34 +322,26 @@ int grid_for(int64_t rows, int wpb, int bpc) {
   return (int)(g < cap ? g : cap);
 }
 
-// LDS: wpb * cols * 4 (<= 64 KiB at 8 waves, 128 KiB at 16)
-int bwd_wpb(int nch, const NormCfg& c) { return nch == 8 ? 4 : (nch > 4 && c.bwd_wpb == 16 ? 8 : c.bwd_wpb); }
-
 template <int NCH>
-void launch_fwd(int wpb, int grid, hipStream_t s, const uint16_t* X, const uint16_t* R, const uint16_t* W,
-                uint16_t* Y, uint16_t* Z, float* rstd, int64_t rows, int cols, float eps, int mode) {
-  if (wpb == 8) rmsnorm_fwd_kernel<NCH, 8><<<grid, 512, 0, s>>>(X, R, W, Y, Z, rstd, rows, cols, eps, mode);
-  else rmsnorm_fwd_kernel<NCH, 4><<<grid, 256, 0, s>>>(X, R, W, Y, Z, rstd, rows, cols, eps, mode);
+void launch_fwd(int grid, hipStream_t s, const uint16_t* X, const uint16_t* R, const uint16_t* W, uint16_t* Y,
+                uint16_t* Z, float* rstd, int64_t rows, int cols, float eps, int mode) {
+  rmsnorm_fwd_kernel<NCH, kFwdWpb><<<grid, kFwdWpb * 64, 0, s>>>(X, R, W, Y, Z, rstd, rows, cols, eps, mode);
 }
 
+// LDS: wpb * cols * 4 (128 KiB at 16 waves x 2048 columns)
 template <int NCH, bool SPLIT = false>
-void launch_bwd(int wpb, int grid, hipStream_t s, const uint16_t* DY, const uint16_t* Z, const uint16_t* W,
+void launch_bwd(int grid, hipStream_t s, const uint16_t* DY, const uint16_t* Z, const uint16_t* W,
                 const float* rstd, const uint16_t* DR, uint16_t* DX, float* part, int64_t rows, int cols, int mode,
                 const float* P1 = nullptr) {
-  const size_t lds = (size_t)wpb * cols * sizeof(float);
-  if (wpb == 16) {
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)rmsnorm_bwd_kernel<NCH, 16, SPLIT>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr = true;
-    }
-    rmsnorm_bwd_kernel<NCH, 16, SPLIT><<<grid, 1024, lds, s>>>(DY, Z, W, rstd, DR, DX, part, rows, cols, mode, P1);
-  } else if (wpb == 8) {
-    rmsnorm_bwd_kernel<NCH, 8, SPLIT><<<grid, 512, lds, s>>>(DY, Z, W, rstd, DR, DX, part, rows, cols, mode, P1);
-  } else {
-    rmsnorm_bwd_kernel<NCH, 4, SPLIT><<<grid, 256, lds, s>>>(DY, Z, W, rstd, DR, DX, part, rows, cols, mode, P1);
+  constexpr int WPB = bwd_wpb_t<NCH>();
+  const size_t lds = (size_t)WPB * cols * sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)rmsnorm_bwd_kernel<NCH, WPB, SPLIT>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
   }
+  rmsnorm_bwd_kernel<NCH, WPB, SPLIT><<<grid, WPB * 64, lds, s>>>(DY, Z, W, rstd, DR, DX, part, rows, cols, mode, P1);
 }
 
 }  // namespace
@@ -364,8 +351,7 @@ extern "C" {
 int pt_rmsnorm_bwd_partials(int64_t rows, int cols) {
   const int nch = nch_for(cols);
   if (nch < 0) return PT_EUNSUPPORTED;
-  const NormCfg& c = norm_cfg();
-  return grid_for(rows, bwd_wpb(nch, c), c.bwd_bpc);  // one partial row per bwd block
+  return grid_for(rows, bwd_wpb(nch), kBwdBpc);  // one partial row per bwd block
 }
 
 int pt_rmsnorm_fwd(const void* x, const void* residual, const void* weight, void* y, void* z_out,
@@ -374,19 +360,17 @@ int pt_rmsnorm_fwd(const void* x, const void* residual, const void* weight, void
   if (residual && !z_out) return PT_EINVAL;
   if (!pt_aligned16(x) || !pt_aligned16(weight) || !pt_aligned16(y)) return PT_EALIGN;
   if (residual && (!pt_aligned16(residual) || !pt_aligned16(z_out))) return PT_EALIGN;
-  const NormCfg& c = norm_cfg();
-  const int wpb = c.fwd_wpb == 8 ? 8 : 4;
-  const int grid = grid_for(rows, wpb, c.fwd_bpc);
+  const int grid = grid_for(rows, kFwdWpb, kFwdBpc);
   const auto* X = (const uint16_t*)x;
   const auto* R = (const uint16_t*)residual;
   const auto* W = (const uint16_t*)weight;
   auto* Y = (uint16_t*)y;
   auto* Z = (uint16_t*)z_out;
   switch (nch_for((int)cols)) {
-    case 1: launch_fwd<1>(wpb, grid, stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
-    case 2: launch_fwd<2>(wpb, grid, stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
-    case 4: launch_fwd<4>(wpb, grid, stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
-    case 8: launch_fwd<8>(wpb, grid, stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
+    case 1: launch_fwd<1>(grid, stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
+    case 2: launch_fwd<2>(grid, stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
+    case 4: launch_fwd<4>(grid, stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
+    case 8: launch_fwd<8>(grid, stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
     default: return PT_EUNSUPPORTED;
   }
   PT_CHECK_LAUNCH();
@@ -404,19 +388,17 @@ int pt_rmsnorm_bwd(const void* dy, const void* z, const void* weight, const floa
   if (nch < 0) return PT_EUNSUPPORTED;
   const int nmode = mode & 3;
   if (nmode > 1 || (mode & PT_DW_ACC_BF16 && mode & PT_DW_ACC_F32)) return PT_EINVAL;
-  const NormCfg& c = norm_cfg();
-  const int wpb = bwd_wpb(nch, c);
-  const int grid = grid_for(rows, wpb, c.bwd_bpc);
+  const int grid = grid_for(rows, bwd_wpb(nch), kBwdBpc);
   const auto* DY = (const uint16_t*)dy;
   const auto* Z = (const uint16_t*)z;
   const auto* W = (const uint16_t*)weight;
   const auto* DR = (const uint16_t*)dres;
   auto* DX = (uint16_t*)dx;
   switch (nch) {
-    case 1: launch_bwd<1>(wpb, grid, stream, DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
-    case 2: launch_bwd<2>(wpb, grid, stream, DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
-    case 4: launch_bwd<4>(wpb, grid, stream, DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
-    case 8: launch_bwd<8>(wpb, grid, stream, DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
+    case 1: launch_bwd<1>(grid, stream, DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
+    case 2: launch_bwd<2>(grid, stream, DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
+    case 4: launch_bwd<4>(grid, stream, DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
+    case 8: launch_bwd<8>(grid, stream, DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
     default: return PT_EUNSUPPORTED;
   }
   PT_CHECK_LAUNCH();
@@ -443,19 +425,17 @@ int pt_rmsnorm_bwd_splitk(const float* dy_p0, const float* dy_p1, const void* z,
   if (nch < 0) return PT_EUNSUPPORTED;
   const int nmode = mode & 3;
   if (nmode > 1 || (mode & PT_DW_ACC_BF16 && mode & PT_DW_ACC_F32)) return PT_EINVAL;
-  const NormCfg& c = norm_cfg();
-  const int wpb = bwd_wpb(nch, c);
-  const int grid = grid_for(rows, wpb, c.bwd_bpc);
+  const int grid = grid_for(rows, bwd_wpb(nch), kBwdBpc);
   const auto* P0 = (const uint16_t*)dy_p0;  // reinterpreted as float inside the SPLIT kernel
   const auto* Z = (const uint16_t*)z;
   const auto* W = (const uint16_t*)weight;
   const auto* DR = (const uint16_t*)dres;
   auto* DX = (uint16_t*)dx;
   switch (nch) {
-    case 1: launch_bwd<1, true>(wpb, grid, stream, P0, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode, dy_p1); break;
-    case 2: launch_bwd<2, true>(wpb, grid, stream, P0, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode, dy_p1); break;
-    case 4: launch_bwd<4, true>(wpb, grid, stream, P0, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode, dy_p1); break;
-    case 8: launch_bwd<8, true>(wpb, grid, stream, P0, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode, dy_p1); break;
+    case 1: launch_bwd<1, true>(grid, stream, P0, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode, dy_p1); break;
+    case 2: launch_bwd<2, true>(grid, stream, P0, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode, dy_p1); break;
+    case 4: launch_bwd<4, true>(grid, stream, P0, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode, dy_p1); break;
+    case 8: launch_bwd<8, true>(grid, stream, P0, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode, dy_p1); break;
     default: return PT_EUNSUPPORTED;
   }
   PT_CHECK_LAUNCH();

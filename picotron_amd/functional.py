@@ -30,6 +30,7 @@ import torch
 import torch.distributed as dist
 
 from . import kernels as K
+from .switches import S
 
 BF16 = torch.bfloat16
 
@@ -38,7 +39,7 @@ def _fuse():
     """PICOTRON_FUSE=0 turns the epilogue fusions (RoPE in the q|k|v GEMM and the attention
     backward, SwiGLU in the gate|up / down GEMMs) off -- for A/B measurement only; both paths are
     HIP kernels with identical results."""
-    return os.environ.get("PICOTRON_FUSE", "1") != "0"
+    return S.fuse != 0
 
 
 # ------------------------------------------------------------------------ gradient sinks
@@ -146,7 +147,7 @@ _PENDING_DW = {}   # autograd graph task id -> [(partial, weight, stream)]
 
 
 def _norm_defer_enabled():
-    return os.environ.get("PICOTRON_NORM_DEFER", "1") != "0"
+    return S.norm_defer != 0
 
 
 def _norm_dw_sink(weight):
@@ -330,7 +331,7 @@ def _take_ce_stats(lg):
 
 
 def ce_stats_enabled():
-    return os.getenv("PICOTRON_CE_STATS", "1") != "0"
+    return S.ce_stats != 0
 
 
 class LMHeadFunction(torch.autograd.Function):
@@ -433,7 +434,7 @@ def attn_block_fwd(h2, wq, wk, wv, wo, cos, sin, sh, tp):
 
 
 def _dual_qkv_enabled():
-    return os.environ.get("PICOTRON_DUAL_QKV", "1") != "0"
+    return S.dual_qkv != 0
 
 
 def attn_block_bwd(da, h2, saved, wq, wk, wv, wo, cos, sin, sh, tp, need_dx=True, keep_parts=False):
@@ -502,7 +503,7 @@ def mlp_block_fwd(h2, wg, wu, wd, tp, residual=None):
 
 
 def _dual_gu_enabled():
-    return os.environ.get("PICOTRON_DUAL_GU", "1") != "0"
+    return S.dual_gu != 0
 
 
 def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True, keep_parts=False):

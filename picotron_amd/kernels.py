@@ -7,12 +7,12 @@ validates with asserts (e.g. picotron/model.py:95-96, tensor_parallel.py:81,151,
 """
 import math
 
-import os
 import sys
 
 import torch
 
 from . import _C
+from .switches import S
 
 BF16 = torch.bfloat16
 
@@ -536,7 +536,7 @@ def _problem(A, lda, Bs, ldbs, b_bounds, b_seg_dim, Cs, ldcs, c_bounds, M, N, K)
 
 
 def _ksplit_enabled():
-    return os.environ.get("PICOTRON_KSPLIT", "1") != "0"
+    return S.ksplit != 0
 
 
 def wgrad_ksplit(mnks, extra_tiles=0):
@@ -668,7 +668,6 @@ def rope_fusable(T, head_dim, seq_len, widths=()):
 
 
 # fewer 256x256 tiles than this: q|k|v + RoPE as a plain GEMM + rope kernel (PICOTRON_ROPE_FUSE_MIN_TILES)
-_ROPE_FUSE_MIN_TILES = int(os.environ.get("PICOTRON_ROPE_FUSE_MIN_TILES", "96"))
 
 
 def linear_fwd_rope(x2d, weights, cos, sin, seq_len, rot_heads, head_dim):
@@ -683,7 +682,7 @@ def linear_fwd_rope(x2d, weights, cos, sin, seq_len, rot_heads, head_dim):
     _req(cos.shape[0] >= seq_len and rope_fusable(T, head_dim, seq_len), "linear_fwd_rope: shape")
     ns = [w.shape[0] for w in weights]
     N = sum(ns)
-    if (T // 256) * (N // 256) < _ROPE_FUSE_MIN_TILES:
+    if (T // 256) * (N // 256) < S.rope_fuse_min_tiles:
         # a TP shard's q|k|v (TP = 8: N 768, 48 tiles of 256x256 on 256 CUs): the phased kernels
         # the RoPE epilogue needs would leave most CUs idle; the plain GEMM picks a smaller tile and
         # csrc/rope.hip rotates q|k after it (bit-identical to the fused epilogue)
@@ -775,14 +774,12 @@ def swiglu_fusable(T, I, backward=False):
 # beside a plain GEMM (whose auto tile fills the CUs) -- a TP shard's I (TP = 8: 1024; 128 tiles
 # on 256 CUs); bit-identical either way.  The backward keeps its fused dual launch at every width
 # (TP = 8 proxy: 8.95 vs 9.08 ms per micro-batch split).  PICOTRON_SWIGLU_FUSE_MIN_TILES / _BWD_MIN_TILES.
-_SWIGLU_FUSE_MIN_TILES = int(os.environ.get("PICOTRON_SWIGLU_FUSE_MIN_TILES", "192"))
-_SWIGLU_BWD_MIN_TILES = int(os.environ.get("PICOTRON_SWIGLU_BWD_MIN_TILES", "0"))
 
 
 def swiglu_fuse_pays(T, I, backward=False):
     """swiglu_fusable and enough tiles that the fused (8-phase 256x256) launch fills the CUs."""
     tiles = (T // 256) * (I // (256 if backward else 128))
-    return swiglu_fusable(T, I, backward) and tiles >= (_SWIGLU_BWD_MIN_TILES if backward else _SWIGLU_FUSE_MIN_TILES)
+    return swiglu_fusable(T, I, backward) and tiles >= (S.swiglu_bwd_min_tiles if backward else S.swiglu_fuse_min_tiles)
 
 
 def linear_swiglu_fwd(x2d, wg, wu):
@@ -818,11 +815,11 @@ def linear_dgrad_swiglu(dy2d, wd, gu):
 
 
 def _splitk_enabled():
-    return os.environ.get("PICOTRON_SPLITK2", "1") != "0"
+    return S.splitk2 != 0
 
 
 def _splitk_min():
-    return int(os.environ.get("PICOTRON_SPLITK2_MIN", "8192"))
+    return S.splitk2_min
 
 
 def _splitk_halves(M, N, K, min_half=None):
@@ -914,14 +911,14 @@ def linear_dgrad(dy2d, weights, out=None, accumulate=False, tile=-1):
 
 def dual_enabled():
     """PICOTRON_DUAL=0 launches a layer's dX and dW GEMMs separately (A/B measurement only)."""
-    return os.environ.get("PICOTRON_DUAL", "1") != "0"
+    return S.dual != 0
 
 
 def _dual_order():
     """0: dX tiles first in every XCD, 1: dW first, 2 (default): staggered -- even XCDs dX first, odd XCDs
     dW first, so half the chip is in the dX tiles' HBM-bound SwiGLU-backward tail at a time (+0.8 %
     on the step, profiles/r03/dual_order_ab.txt)."""
-    return int(os.environ.get("PICOTRON_DUAL_ORDER", "2"))
+    return S.dual_order
 
 
 def dual_fits(dgrad_mn, wgrad_mns):
@@ -935,7 +932,7 @@ def dual_fits(dgrad_mn, wgrad_mns):
 def norm_splitk_enabled():
     """The post-attention norm backward takes the gate|up dX's split-K halves directly
     (PICOTRON_NORM_SPLITK=0: the sum pass + the plain norm backward, A/B only)."""
-    return os.environ.get("PICOTRON_NORM_SPLITK", "1") != "0"
+    return S.norm_splitk != 0
 
 
 def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None, keep_parts=False, split_min=None):
@@ -1120,7 +1117,7 @@ def attn_bwd(dout, q, k, v, out, lse, scale, causal, dq=None, dk=None, dv=None, 
     B, Sq, H, D = q.shape
     Sk, HKV = k.shape[1], k.shape[2]
     lib = _C.lib()
-    fuse_delta = delta is None and not grad_f32 and out.dtype == BF16 and os.environ.get("PICOTRON_FUSE_DELTA", "1") != "0"
+    fuse_delta = delta is None and not grad_f32 and out.dtype == BF16 and S.fuse_delta != 0
     if delta is None and not fuse_delta:
         ld0 = _lse_ld(lse, B, H, Sq)
         delta = attn_delta(dout, out, torch.empty(B, H, ld0, dtype=torch.float32, device=q.device)[:, :, :Sq]

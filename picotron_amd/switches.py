@@ -1,0 +1,79 @@
+"""Measurement switches of the HIP path, read ONCE from the environment when the package is imported.
+
+Every switch selects between HIP kernels with the same results (fused vs separate epilogues,
+split-K vs one pass, one launch vs two); the defaults are the production path, and nothing on the
+hot path reads the environment again.  `PICOTRON_<NAME>` (upper case) sets a switch for a whole
+process (an A/B run); tests and tools change one for a block with `override(name=value)`.
+
+The four native switches (attention causal pairing and dK/dV kernel form, GEMM tile-row grouping,
+the mixed-tile q|k|v launch) live in the library; `apply_native` pushes them through
+`pt_set_variant` when the library is loaded, and `override` pushes a changed one at once.
+"""
+import contextlib
+import os
+
+DEFAULTS = {
+    # functional.py: the fused epilogues (RoPE in the q|k|v GEMM and attention backward, SwiGLU in the
+    # gate|up / down GEMMs), deferred norm-weight column sums, lm_head CE statistics, the q|k|v and
+    # gate|up dX + dW dual launches
+    "fuse": 1, "norm_defer": 1, "ce_stats": 1, "dual_qkv": 1, "dual_gu": 1,
+    # kernels.py: weight-gradient K-slices, split-K dgrad halves (and their minimum K), dX + dW dual
+    # launches and their XCD order, the norm backward fed by split-K halves, the attention
+    # backward's fused delta, and the tile-count thresholds below which the RoPE / SwiGLU epilogues
+    # run as separate kernels (TP shard widths)
+    "ksplit": 1, "splitk2": 1, "splitk2_min": 8192, "dual": 1, "dual_order": 2, "norm_splitk": 1,
+    "fuse_delta": 1, "rope_fuse_min_tiles": 96, "swiglu_fuse_min_tiles": 192, "swiglu_bwd_min_tiles": 0,
+    # context_parallel.py: the zig-zag (load-balanced) ring where it tiles
+    "ring_zigzag": 1,
+    # native (libpicotron_hip.so, pt_set_variant)
+    "attn_pair": 1, "attn_split": 2, "gemm_group_m": -1, "gemm_mix": 1,
+}
+NATIVE = ("attn_pair", "attn_split", "gemm_group_m", "gemm_mix")
+
+
+class _Switches:
+    def __init__(self):
+        for k, d in DEFAULTS.items():
+            v = os.environ.get("PICOTRON_" + k.upper())
+            setattr(self, k, int(v) if v not in (None, "") else d)
+
+    def __repr__(self):
+        return "Switches(" + ", ".join(f"{k}={getattr(self, k)}" for k in DEFAULTS) + ")"
+
+
+S = _Switches()
+
+
+def apply_native(lib):
+    """Push the native switches into a freshly loaded library (called by _C.load_library)."""
+    for k in NATIVE:
+        rc = lib.pt_set_variant(k.encode(), int(getattr(S, k)))
+        if rc != 0:
+            raise RuntimeError(f"pt_set_variant({k!r}, {getattr(S, k)}) failed: {rc}")
+
+
+@contextlib.contextmanager
+def override(**kw):
+    """Set switches for the duration of a block (tests / A/B tools), native ones included."""
+    unknown = set(kw) - set(DEFAULTS)
+    if unknown:
+        raise KeyError(f"unknown switches {sorted(unknown)}")
+    old = {k: getattr(S, k) for k in kw}
+    try:
+        for k, v in kw.items():
+            setattr(S, k, int(v))
+        _push([k for k in kw if k in NATIVE])
+        yield S
+    finally:
+        for k, v in old.items():
+            setattr(S, k, v)
+        _push([k for k in kw if k in NATIVE])
+
+
+def _push(names):
+    if not names:
+        return
+    from . import _C
+    lib = _C.load_library()
+    for k in names:
+        lib.pt_set_variant(k.encode(), int(getattr(S, k)))

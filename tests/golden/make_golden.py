@@ -286,6 +286,113 @@ def g10m_pipeline(rank, world, engine):
     return res
 
 
+# ---------------------------------------------------------------- G12: BASELINE configs 1 / 4's grid
+# dp2 tp2 pp2 1F1B on 8 gloo processes -- the reference's README CPU command (README.md:43) at
+# config 1's shape: 5 layers, mbs 4, seq 128, grad_acc 2.  Two model sizes:
+#   "tiny":    G10m's dims (H 128), 6 AdamW steps at lr 1e-2 (a steep, sensitive curve);
+#   "smollm":  SmolLM-1.7B's own dims (H 2048, I 8192, 32 heads, V 49152), 4 steps at lr 1e-4.
+# The weights are not stored: every full parameter is drawn by `g12_full_param` from a generator
+# seeded by the parameter's name, so both sides materialise the same full model (then shard it as
+# apply_tensor_parallel shards and keep their pipeline stage's slice) without a 2 GB fixture.
+G12_CFGS = {
+    "tiny": dict(G10M_CFG, num_hidden_layers=5, max_position_embeddings=128),
+    "smollm": dict(hidden_size=2048, intermediate_size=8192, num_attention_heads=32, num_key_value_heads=32,
+                   rms_norm_eps=1e-5, max_position_embeddings=128, rope_theta=10000.0, vocab_size=49152,
+                   num_hidden_layers=5),
+}
+G12_RUN = {"tiny": dict(steps=6, lr=1e-2), "smollm": dict(steps=4, lr=1e-4)}
+G12_GA, G12_MBS = 2, 4
+
+
+def g12_full_param(name, shape):
+    """Deterministic full (unsharded) parameter `name` of G12's model: norms ones
+    (model.py:48-49,78-79), linears U(+-1/sqrt(fan_in)) (model.py:110-118,173-181), the embedding
+    N(0, 1) (model.py:221-222) -- the reference's init distributions, each from torch.Generator
+    seeded with crc32(name) instead of the global RNG order (which changes with TP / PP)."""
+    import zlib
+    g = torch.Generator().manual_seed(zlib.crc32(name.encode()))
+    if name.endswith("norm.weight"):
+        return torch.ones(shape)
+    if name.startswith("embedding"):
+        return torch.randn(shape, generator=g)
+    b = 1.0 / math.sqrt(shape[1])
+    return torch.rand(shape, generator=g) * (2 * b) - b
+
+
+def g12_tokens(V, S, dp=2):
+    """[dp, ga, mbs, S + 1] tokens (seed 1234), the same batch every step."""
+    g = torch.Generator().manual_seed(1234)
+    return torch.randint(0, V, (dp, G12_GA, G12_MBS, S + 1), generator=g)
+
+
+def g12_grid(rank, world, size):
+    """G12: the reference's own train.py composition for configs 1 / 4 (train.py:174-195: Llama ->
+    apply_tensor_parallel -> PipelineParallel -> weights -> DataParallelBucket) trained by its
+    train_step_pipeline_1f1b (pipeline_parallel.py:124-214) on 8 gloo CPU processes at
+    dp2 tp2 pp2, fp32, FLASH_ATTEN=0, AdamW (torch defaults); records the logged loss of every step
+    (train.py:228: average_loss_across_dp_cp_ranks of the last stage's loss) on every rank."""
+    import picotron.process_group_manager as pgm
+    torch.set_num_threads(1)
+    pgm.setup_process_group_manager(tp_size=2, cp_size=1, pp_size=2, dp_size=2)
+    m = pgm.process_group_manager
+    from picotron import model as M
+    from picotron.data_parallel.data_parallel import DataParallelBucket
+    from picotron.pipeline_parallel import pipeline_parallel as PP
+    from picotron.tensor_parallel.tensor_parallel import apply_tensor_parallel
+    from picotron.utils import average_loss_across_dp_cp_ranks
+    c = G12_CFGS[size]
+    cfg = types.SimpleNamespace(**c)
+    torch.manual_seed(7)
+    model = PP.PipelineParallel(apply_tensor_parallel(M.Llama(cfg)), cfg)
+    for layer in model.decoder_layers.values():
+        layer.cos, layer.sin = layer.cos.float(), layer.sin.float()
+    with torch.no_grad():
+        for n, p in model.named_parameters():
+            full = g12_full_param(n, _g12_full_shape(n, p, c))
+            p.copy_(_g10m_shard(full, p, m.tp_rank))
+    model = DataParallelBucket(model)
+    opt = torch.optim.AdamW(model.parameters(), lr=G12_RUN[size]["lr"])
+    S, V = c["max_position_embeddings"], c["vocab_size"]
+    ids = g12_tokens(V, S)
+
+    class Loader:
+        grad_acc_steps, micro_batch_size, seq_length_per_gpu = G12_GA, G12_MBS, S
+
+        def __init__(self):
+            self.i = 0
+
+        def __next__(self):
+            t = ids[m.dp_rank, self.i]
+            self.i += 1
+            return {"input_ids": t[:, :-1], "target_ids": t[:, 1:],
+                    "position_ids": torch.arange(S).expand(G12_MBS, S), "hidden_states": None}
+    losses = []
+    for _ in range(G12_RUN[size]["steps"]):
+        opt.zero_grad()
+        loss = PP.train_step_pipeline_1f1b(model, Loader(), (G12_MBS, S, c["hidden_size"]), "cpu", torch.float32)
+        losses.append(average_loss_across_dp_cp_ranks(loss, "cpu"))
+        opt.step()
+        model.reset()
+    return {"losses": torch.tensor(losses, dtype=torch.float64),
+            "grid": torch.tensor([m.dp_rank, m.pp_rank, m.cp_rank, m.tp_rank])}
+
+
+def _g12_full_shape(name, p, c):
+    """The unsharded shape of parameter `name` (TP shards dim 0 of column / vocab, dim 1 of row)."""
+    H, I, V = c["hidden_size"], c["intermediate_size"], c["vocab_size"]
+    d = H // c["num_attention_heads"]
+    kv = c["num_key_value_heads"] * d
+    tail = name.split(".")[-2]
+    return {"q_proj": (H, H), "k_proj": (kv, H), "v_proj": (kv, H), "out_proj": (H, H), "gate_proj": (I, H),
+            "up_proj": (I, H), "down_proj": (H, I), "embedding": (V, H), "final_proj": (V, H)}.get(tail, tuple(p.shape))
+
+
+def g12_all(ref):
+    import functools
+    for size in ("tiny", "smollm"):
+        _run_dist(functools.partial(g12_grid, size=size), 8, ref, f"G12_{size}")
+
+
 G11_STEPS, G11_GA, G11_MBS, G11_LR = 50, 2, 2, 1e-3
 
 
@@ -388,8 +495,12 @@ def g11_all(ref, dtypes=("bf16", "f32")):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
-    ap.add_argument("--only", choices=["G11", "G11bf16", "G10m_pp"], help="regenerate only these fixtures")
+    ap.add_argument("--only", choices=["G11", "G11bf16", "G10m_pp", "G12"], help="regenerate only these fixtures")
     args = ap.parse_args()
+    if args.only == "G12":
+        g12_all(args.ref)
+        print("wrote G12 fixtures")
+        return
     if args.only == "G10m_pp":
         g10m_pp_all(args.ref)
         print("wrote G10m_pp fixtures")
@@ -531,7 +642,9 @@ def main():
         _run_dist(functools.partial(g10m_multirank, tp=tp, cp=cp, dp=dp), 2, args.ref, name)
     g10m_pp_all(args.ref)
     g11_all(args.ref)
-    print("wrote", sorted(gold) + ["G7", "G8", "G10m_tp2", "G10m_cp2", "G10m_dp2", "G10m_pp2*", "G11_*", "G11f32_*"])
+    g12_all(args.ref)
+    print("wrote", sorted(gold) + ["G7", "G8", "G10m_tp2", "G10m_cp2", "G10m_dp2", "G10m_pp2*", "G11_*", "G11f32_*",
+                                   "G12_*"])
 
 
 if __name__ == "__main__":

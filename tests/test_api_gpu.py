@@ -19,6 +19,7 @@ import torch
 import torch.nn.functional as F
 
 from oracle import picotron_oracle as O
+from picotron_amd import switches
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -341,8 +342,7 @@ def test_cross_entropy_from_lm_head_statistics():
     ids = torch.randint(0, 512, (2, 129), generator=torch.Generator().manual_seed(8)).cuda()
     res = {}
     for flag in ("1", "0"):
-        os.environ["PICOTRON_CE_STATS"] = flag
-        try:
+        with switches.override(ce_stats=int(flag)):
             model, cfg = _tiny_llama()
             used = []
             orig = K.cross_entropy_loss_lse_stats
@@ -353,8 +353,6 @@ def test_cross_entropy_from_lm_head_statistics():
                 K.cross_entropy_loss_lse_stats = orig
             loss.backward()
             res[flag] = (loss.float().item(), {n: p.grad.float().clone() for n, p in model.named_parameters()}, used)
-        finally:
-            os.environ.pop("PICOTRON_CE_STATS", None)
     assert res["1"][2] == [1] and res["0"][2] == []
     assert abs(res["1"][0] - res["0"][0]) <= 1e-6 * abs(res["0"][0])
     for n, gr in res["0"][1].items():

@@ -7,6 +7,7 @@ import pytest
 import torch
 
 from oracle import picotron_oracle as O
+from picotron_amd import switches
 
 pytestmark = pytest.mark.gpu
 
@@ -142,7 +143,7 @@ def test_rmsnorm_deferred_dw_through_autograd(monkeypatch):
     dy = torch.randn(rows, cols).to(BF).to(DEV)
     grads = {}
     for defer in ("1", "0"):
-        monkeypatch.setenv("PICOTRON_NORM_DEFER", defer)
+        monkeypatch.setattr(switches.S, "norm_defer", int(defer))
         for w in ws:
             w.grad = None
         x = x0.clone().requires_grad_(True)
@@ -331,7 +332,7 @@ def test_wgrad_ksplit_tp8_shapes(epi, monkeypatch):
     outs, refs = [t.clone() for t in init], [t.clone() for t in init]
     K_.linear_wgrad_grouped([(dqkv, h, outs[:3]), (da, o, outs[3:4])], epilogue=epi)
     K_.linear_wgrad(dm, hh, outs[4:], epilogue=epi)
-    monkeypatch.setenv("PICOTRON_KSPLIT", "0")
+    monkeypatch.setattr(switches.S, "ksplit", 0)
     K_.linear_wgrad_grouped([(dqkv, h, refs[:3]), (da, o, refs[3:4])], epilogue=epi)
     K_.linear_wgrad(dm, hh, refs[4:], epilogue=epi)
     torch.cuda.synchronize()
@@ -358,7 +359,7 @@ def test_gemm_dual_with_ksplit_wgrad(epi, monkeypatch):
     init = torch.randn(H, I).to(dt).to(DEV)
     out_a, out_b = init.clone(), init.clone()
     dx_a = K_.linear_dgrad_dual(dm, [wd], [(dm, hh, [out_a])], epi, gu=gu)
-    monkeypatch.setenv("PICOTRON_KSPLIT", "0")
+    monkeypatch.setattr(switches.S, "ksplit", 0)
     dx_b = K_.linear_dgrad_dual(dm, [wd], [(dm, hh, [out_b])], epi, gu=gu)
     torch.cuda.synchronize()
     assert dx_a is not None and dx_b is not None and torch.equal(dx_a, dx_b)
@@ -436,8 +437,8 @@ def test_mlp_block_split_swiglu_equals_fused(monkeypatch):
     dm = torch.randn(T, H).to(BF).to(DEV)
     outs = []
     for thr in (0, 1 << 30):
-        monkeypatch.setattr(K_, "_SWIGLU_FUSE_MIN_TILES", thr)
-        monkeypatch.setattr(K_, "_SWIGLU_BWD_MIN_TILES", thr)
+        monkeypatch.setattr(switches.S, "swiglu_fuse_min_tiles", thr)
+        monkeypatch.setattr(switches.S, "swiglu_bwd_min_tiles", thr)
         wl = [w.clone().requires_grad_(True) for w in ws]
         tp = FN.TPContext()
         m, saved = FN.mlp_block_fwd(x, *wl, tp)
@@ -457,7 +458,7 @@ def test_gemm_dual_equals_separate(swiglu, epi, order, monkeypatch):
     beside its dW, and a K-segmented q|k|v dX beside the q|k|v + o_proj dWs (unsplit dW: the split-K
     dW beside a dX is test_gemm_dual_with_ksplit_wgrad)"""
     from picotron_amd import kernels as K_
-    monkeypatch.setenv("PICOTRON_KSPLIT", "0")
+    monkeypatch.setattr(switches.S, "ksplit", 0)
     T, H = 1024, 512
     dt = torch.float32 if epi == 3 else BF
     if swiglu:
@@ -510,12 +511,12 @@ def test_dgrad_splitk(T, Kin, ns, kmin, monkeypatch):
     halves cut through the middle weight, as q|k|v's) against the single pass (PICOTRON_SPLITK2=0)
     and an f32 reference: the same up to the f32 summation order (one bf16 rounding either way)"""
     from picotron_amd import kernels as K_
-    monkeypatch.setenv("PICOTRON_SPLITK2_MIN", str(kmin))
+    monkeypatch.setattr(switches.S, "splitk2_min", kmin)
     dy = torch.randn(T, sum(ns)).to(BF).to(DEV)
     ws = [(torch.randn(n, Kin) / math.sqrt(sum(ns))).to(BF).to(DEV) for n in ns]
     assert K_._splitk_halves(T, Kin, sum(ns)) is not None
     dx = K_.linear_dgrad(dy, ws)
-    monkeypatch.setenv("PICOTRON_SPLITK2", "0")
+    monkeypatch.setattr(switches.S, "splitk2", 0)
     ref1 = K_.linear_dgrad(dy, ws)
     ref = (dy.float() @ torch.cat(ws).float())
     torch.cuda.synchronize()
@@ -552,14 +553,14 @@ def test_fwd_splitk(residual, monkeypatch):
     """forward GEMM split in two K halves, the residual add (EPI_BF16_RES: bf16(R + bf16(acc))) in
     the sum pass, against the single pass and an f32 reference (down_proj's shape: K 8192)"""
     from picotron_amd import kernels as K_
-    monkeypatch.setenv("PICOTRON_SPLITK2_MIN", "4096")
+    monkeypatch.setattr(switches.S, "splitk2_min", 4096)
     T, K, N = 4096, 8192, 2048
     x = torch.randn(T, K).to(BF).to(DEV)
     w = (torch.randn(N, K) / math.sqrt(K)).to(BF).to(DEV)
     r = torch.randn(T, N).to(BF).to(DEV) if residual else None
     assert K_._splitk_halves(T, N, K) is not None
     y = K_.linear_fwd(x, [w], residual=r)
-    monkeypatch.setenv("PICOTRON_SPLITK2", "0")
+    monkeypatch.setattr(switches.S, "splitk2", 0)
     y1 = K_.linear_fwd(x, [w], residual=r)
     ref = x.float() @ w.float().t() + (r.float() if residual else 0)
     torch.cuda.synchronize()
@@ -575,7 +576,7 @@ def test_gemm_rope_fused(monkeypatch, nh, nkv, S, fuse):
     third and fourth shapes take the mixed 256x256 / 256x128 launch, the first two a single tile
     shape; fuse=False: a TP-shard width below the fusion threshold, plain GEMM + rope kernel)"""
     from picotron_amd import kernels as K_
-    monkeypatch.setattr(K_, "_ROPE_FUSE_MIN_TILES", 0 if fuse else 96)
+    monkeypatch.setattr(switches.S, "rope_fuse_min_tiles", 0 if fuse else 96)
     d, B = 64, 2
     T, H = B * S, 256
     x = torch.randn(T, H).to(BF).to(DEV)
@@ -722,14 +723,14 @@ def test_attention_dkdv_wave_pair_split_is_bit_identical(monkeypatch, B, S, H, H
     if rope:
         rp = tuple(t.to(DEV) for t in O.get_cos_sin(S, D, base=10000.0))
     outs = []
-    for mask in ("0", "3"):
-        monkeypatch.setenv("PICOTRON_ATTN_SPLIT", mask)
-        if f32:
-            g = [torch.full((B, S, n, D), 0.25, device=DEV) for n in (H, HKV, HKV)]
-            K_.attn_bwd(do, q, k, v, o, lse, scale, causal, dq=g[0], dk=g[1], dv=g[2], grad_f32=True)
-        else:
-            g = K_.attn_bwd(do, q, k, v, o, lse, scale, causal, rope=rp)[:3]
-        torch.cuda.synchronize()
+    for mask in (0, 3):
+        with switches.override(attn_split=mask):
+            if f32:
+                g = [torch.full((B, S, n, D), 0.25, device=DEV) for n in (H, HKV, HKV)]
+                K_.attn_bwd(do, q, k, v, o, lse, scale, causal, dq=g[0], dk=g[1], dv=g[2], grad_f32=True)
+            else:
+                g = K_.attn_bwd(do, q, k, v, o, lse, scale, causal, rope=rp)[:3]
+            torch.cuda.synchronize()
         outs.append([t.clone() for t in g])
     for a, b in zip(*outs):
         assert torch.equal(a, b)

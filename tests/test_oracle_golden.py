@@ -249,6 +249,54 @@ def test_oracle_reproduces_g11_first_steps():
         assert abs(acc - g["rank0.losses"][step].item()) < 1e-4 * abs(acc), (step, acc)
 
 
+@pytest.mark.parametrize("size", ["tiny", "smollm"])
+def test_g12_fixtures_are_reference_grid_curves(size):
+    """G12_*: the reference's dp2 tp2 pp2 1F1B run (8 gloo processes, make_golden.g12_grid): every
+    rank sits at its own (dp, pp, cp, tp) grid point (process_group_manager.py:13: view(dp, pp, cp,
+    tp), tp fastest), the last-stage ranks log the same falling curve, the first stage logs 0."""
+    g = load(f"G12_{size}")
+    seen = set()
+    for r in range(8):
+        d, p, c, t = g[f"rank{r}.grid"].tolist()
+        assert r == ((d * 2 + p) * 1 + c) * 2 + t
+        seen.add((d, p, t))
+        lo = g[f"rank{r}.losses"]
+        if p == 0:
+            assert not lo.any()
+        else:
+            assert torch.equal(lo, g["rank2.losses"]) and (lo[1:] < lo[:-1]).all()
+    assert len(seen) == 8
+
+
+def test_oracle_reproduces_g12_tiny_grid_curve():
+    """G12_tiny (the reference's dp2 tp2 pp2 1F1B, 5 layers, mbs 4 seq 128 ga 2, lr 1e-2): the oracle
+    restating what the grid computes -- each dp replica's gradient is the SUM over its micro-batches
+    of the mean CE (pipeline_parallel.py:103,153, not / grad_acc), DataParallelBucket averages the two
+    replicas (bucket.py all-reduce / cp_dp size), TP / PP change no arithmetic -- from the same
+    deterministic full weights reproduces all 6 logged losses (mean over dp of the stage's loss)."""
+    from tests import _g12
+    g = load("G12_tiny")
+    c = _g12.CFGS["tiny"]
+    params = {k: v.clone().requires_grad_(True) for k, v in _g12.full_params("tiny").items()}
+    opt = torch.optim.AdamW(list(params.values()), lr=_g12.RUN["tiny"]["lr"])
+    S, V = c["max_position_embeddings"], c["vocab_size"]
+    cos, sin = O.get_cos_sin(S, c["hidden_size"] // c["num_attention_heads"], base=c["rope_theta"])
+    ids = _g12.tokens(V, S)
+    for step in range(_g12.RUN["tiny"]["steps"]):
+        opt.zero_grad()
+        acc = 0.0
+        for d in range(2):
+            for i in range(_g12.GA):
+                t = ids[d, i]
+                lo = O.llama_forward(t[:, :-1], params, c, cos.float(), sin.float())
+                loss = torch.nn.functional.cross_entropy(lo.transpose(1, 2), t[:, 1:])
+                (loss / 2).backward()
+                acc += loss.item() / _g12.GA / 2
+        opt.step()
+        ref = g["rank2.losses"][step].item()
+        assert abs(acc - ref) < 1e-4 * abs(ref), (step, acc, ref)
+
+
 def test_oracle_reproduces_g10m_pp2_pipeline_curve():
     """G10m_pp2 / G10m_pp2afab: the reference's PipelineParallel at pp 2 (1F1B and AFAB: the same
     curve, 5.71 -> 3.04) from G10m's initial weights.  The oracle restating the engine's loss -- each

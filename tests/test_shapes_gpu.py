@@ -20,6 +20,7 @@ import pytest
 import torch
 
 from oracle import picotron_oracle as O
+from picotron_amd import switches
 
 pytestmark = pytest.mark.gpu
 TOL = 2e-2
@@ -73,10 +74,10 @@ def test_smollm_layer_norm_from_splitk_halves_is_bit_identical(monkeypatch):
     the post-attention norm backward (pt_rmsnorm_bwd_splitk) -- every output bit-identical to the
     sum pass + plain norm backward (PICOTRON_NORM_SPLITK=0).  The q|k|v dX stays one GEMM here
     (PICOTRON_DUAL_QKV=0; its split form is the next test)."""
-    monkeypatch.setenv("PICOTRON_DUAL_QKV", "0")
+    monkeypatch.setattr(switches.S, "dual_qkv", 0)
     outs = []
     for v in ("0", "1"):
-        monkeypatch.setenv("PICOTRON_NORM_SPLITK", v)
+        monkeypatch.setattr(switches.S, "norm_splitk", int(v))
         outs.append(_layer_grads(B=4, S=1024, H=2048, I=8192, nh=32, nkv=32, d=64, seed=11))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
@@ -90,7 +91,7 @@ def test_smollm_layer_qkv_dx_split_beside_dw(monkeypatch):
     (norm-relative 1e-3 here, far inside the 2e-2 tolerance)."""
     outs = []
     for v in ("0", "1"):
-        monkeypatch.setenv("PICOTRON_DUAL_QKV", v)
+        monkeypatch.setattr(switches.S, "dual_qkv", int(v))
         outs.append(_layer_grads(B=4, S=1024, H=2048, I=8192, nh=32, nkv=32, d=64, seed=11))
     (y0, dx0, *g0), (y1, dx1, *g1) = outs
     assert torch.equal(y0, y1)

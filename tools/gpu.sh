@@ -11,6 +11,7 @@
 #   configs      Llama-2-7B 1-GPU bench, TP=8 proxy, CP=8 proxy
 #   gloo2        bench.py --gpus 2 --backend gloo rehearsal (2 ranks on cuda:0)
 #   pp2          bench.py --gpus 2 --pp 2 --backend gloo rehearsal of the pipeline engine (config 4's 1F1B)
+#   grid8        bench.py --gpus 8 --backend gloo: DP=8, TP=8, config 4 (llama2-7b tp2 pp2), config 5 (cp8 32k)
 #   dp           bench.py --dp-bucket fp32 / bf16 vs plain (the per-GPU DP cost)
 #   attn         tools/attn_bench.py d64 and d128 (OLD=<lib> for an in-process A/B; ATTN64_ARGS for the d64 run)
 #   pmcattn      attention PMC passes (ATTN_ARGS="--B 1 --S 4096 --H 32 --D 128" for d128)
@@ -87,6 +88,20 @@ step_pp2() {
   timeout -k 10 400 python -u bench.py --gpus 2 --pp 2 --backend gloo --steps 1 --warmup 1 --grad-acc 4 --cpu-tokens 0 ${PP_ARGS} > $O.pp2.json 2> $O.pp2.err || { echo pp2 failed; tail -20 $O.pp2.err; return 1; }
   [ $(wc -l < $O.pp2.json) = 1 ] || { echo "pp2: stdout is not one line"; return 1; }
   python -c "import json; d=json.load(open('$O.pp2.json')); print('pp2', d['n_gpus'], d['ranks'], d['backend'], d['config']['parallelism'], round(d['value']), d['final_loss'])"
+}
+
+step_grid8() {   # every 8-rank grid the driver's 8-GPU run can launch, assembled once over gloo on cuda:0
+  local n=0
+  while IFS='|' read -r tag args; do
+    [ -n "$tag" ] || continue
+    n=$((n+1))
+    timeout -k 10 ${GRID8_TIMEOUT:-420} python -u bench.py --gpus 8 --backend gloo --steps 1 --warmup 1 --cpu-tokens 0 $args > $O.grid8_$tag.json 2> $O.grid8_$tag.err || { echo "grid8 $tag failed"; tail -20 $O.grid8_$tag.err; return 1; }
+    [ $(wc -l < $O.grid8_$tag.json) = 1 ] || { echo "grid8 $tag: stdout is not one line"; return 1; }
+    python -c "import json; d=json.load(open('$O.grid8_$tag.json')); print('grid8 $tag', d['n_gpus'], d['ranks'], d['backend'], d['config']['parallelism'], round(d['value']), d['final_loss'])"
+  done <<< "${GRID8:-dp8|--layers 2 --grad-acc 2
+tp8|--tp 8 --layers 2 --grad-acc 2
+cfg4|--model llama2-7b --tp 2 --pp 2 --layers 4 --grad-acc 4
+cfg5|--model llama2-7b --cp 8 --seq 32768 --mbs 1 --layers 2 --grad-acc 1}"
 }
 
 step_dp() {
