@@ -290,7 +290,10 @@ def g10m_pipeline(rank, world, engine):
 # dp2 tp2 pp2 1F1B on 8 gloo processes -- the reference's README CPU command (README.md:43) at
 # config 1's shape: 5 layers, mbs 4, seq 128, grad_acc 2.  Two model sizes:
 #   "tiny":    G10m's dims (H 128), 6 AdamW steps at lr 1e-2 (a steep, sensitive curve);
-#   "smollm":  SmolLM-1.7B's own dims (H 2048, I 8192, 32 heads, V 49152), 4 steps at lr 1e-4.
+#   "smollm":  SmolLM-1.7B's own dims (H 2048, I 8192, 32 heads, V 49152), 4 steps at lr 1e-4, in the
+#              reference's GPU training precision (bf16 model and AdamW states, train.py:76,190): at
+#              lr 1e-4 an update is about one bf16 ulp of these weights, so the precision, not the
+#              implementation, would set a bf16-vs-fp32 gap (G11's reason for its bf16 curves).
 # The weights are not stored: every full parameter is drawn by `g12_full_param` from a generator
 # seeded by the parameter's name, so both sides materialise the same full model (then shard it as
 # apply_tensor_parallel shards and keep their pipeline stage's slice) without a 2 GB fixture.
@@ -300,7 +303,7 @@ G12_CFGS = {
                    rms_norm_eps=1e-5, max_position_embeddings=128, rope_theta=10000.0, vocab_size=49152,
                    num_hidden_layers=5),
 }
-G12_RUN = {"tiny": dict(steps=6, lr=1e-2), "smollm": dict(steps=4, lr=1e-4)}
+G12_RUN = {"tiny": dict(steps=6, lr=1e-2, dtype="f32"), "smollm": dict(steps=4, lr=1e-4, dtype="bf16")}
 G12_GA, G12_MBS = 2, 4
 
 
@@ -329,7 +332,7 @@ def g12_grid(rank, world, size):
     """G12: the reference's own train.py composition for configs 1 / 4 (train.py:174-195: Llama ->
     apply_tensor_parallel -> PipelineParallel -> weights -> DataParallelBucket) trained by its
     train_step_pipeline_1f1b (pipeline_parallel.py:124-214) on 8 gloo CPU processes at
-    dp2 tp2 pp2, fp32, FLASH_ATTEN=0, AdamW (torch defaults); records the logged loss of every step
+    dp2 tp2 pp2, fp32 (tiny) or bf16 (smollm), FLASH_ATTEN=0, AdamW (torch defaults); records the logged loss of every step
     (train.py:228: average_loss_across_dp_cp_ranks of the last stage's loss) on every rank."""
     import picotron.process_group_manager as pgm
     torch.set_num_threads(1)
@@ -341,16 +344,17 @@ def g12_grid(rank, world, size):
     from picotron.tensor_parallel.tensor_parallel import apply_tensor_parallel
     from picotron.utils import average_loss_across_dp_cp_ranks
     c = G12_CFGS[size]
+    dtype = torch.bfloat16 if G12_RUN[size]["dtype"] == "bf16" else torch.float32
     cfg = types.SimpleNamespace(**c)
     torch.manual_seed(7)
     model = PP.PipelineParallel(apply_tensor_parallel(M.Llama(cfg)), cfg)
     for layer in model.decoder_layers.values():
-        layer.cos, layer.sin = layer.cos.float(), layer.sin.float()
+        layer.cos, layer.sin = layer.cos.to(dtype), layer.sin.to(dtype)
     with torch.no_grad():
         for n, p in model.named_parameters():
             full = g12_full_param(n, _g12_full_shape(n, p, c))
             p.copy_(_g10m_shard(full, p, m.tp_rank))
-    model = DataParallelBucket(model)
+    model = DataParallelBucket(model.to(dtype))   # train.py:190, 194-195
     opt = torch.optim.AdamW(model.parameters(), lr=G12_RUN[size]["lr"])
     S, V = c["max_position_embeddings"], c["vocab_size"]
     ids = g12_tokens(V, S)
@@ -369,7 +373,7 @@ def g12_grid(rank, world, size):
     losses = []
     for _ in range(G12_RUN[size]["steps"]):
         opt.zero_grad()
-        loss = PP.train_step_pipeline_1f1b(model, Loader(), (G12_MBS, S, c["hidden_size"]), "cpu", torch.float32)
+        loss = PP.train_step_pipeline_1f1b(model, Loader(), (G12_MBS, S, c["hidden_size"]), "cpu", dtype)
         losses.append(average_loss_across_dp_cp_ranks(loss, "cpu"))
         opt.step()
         model.reset()

@@ -374,9 +374,9 @@ def _grid_curve(rank, world, size, out_q):
 @pytest.mark.parametrize("size", ["tiny", "smollm"])
 def test_dp2_tp2_pp2_1f1b_loss_curve_matches_reference_g12(size):
     """BASELINE configs 1 and 4's dp2 tp2 pp2 1F1B grid against the reference's own run of it (G12:
-    its train.py composition on 8 gloo CPU processes, fp32; tiny = G10m dims, 5 layers, 6 steps at
-    lr 1e-2, 5.69 -> 2.24; smollm = SmolLM-1.7B dims, 5 layers -- config 1 itself -- 4 steps at lr
-    1e-4, 10.97 -> 7.96): the bf16 HIP path through picotron_amd's TP modules, pipeline engine and
+    its train.py composition on 8 gloo CPU processes; tiny = G10m dims, 5 layers, fp32, 6 steps at
+    lr 1e-2, 5.69 -> 2.24; smollm = SmolLM-1.7B dims, 5 layers -- config 1 itself -- in the
+    reference's bf16 training precision, 4 steps at lr 1e-4, 10.97 -> 7.67): the bf16 HIP path through picotron_amd's TP modules, pipeline engine and
     DataParallelBucket on 8 gloo ranks sharing cuda:0, within 1 % at every step."""
     import torch.multiprocessing as mp
     q = mp.get_context("spawn").SimpleQueue()
