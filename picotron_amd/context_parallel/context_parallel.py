@@ -24,23 +24,100 @@ What differs (MI355X-first):
     the visiting keys) when they come from a lower rank, (my second-half queries x all the visiting
     keys) otherwise -- and the outputs / gradients are re-laid back.  The external contract (rank r
     holds tokens [r S, (r + 1) S), data.py:105-109, update_rope_for_context_parallel) is unchanged.
-    PICOTRON_RING_ZIGZAG=0 runs the reference's schedule instead (A/B only).
+    PICOTRON_RING_ZIGZAG=0 runs the reference's schedule instead (A/B only);
+  * the residual stream stays in the zig-zag layout across the whole decoder stack: every op
+    outside attention is token-local, so apply_context_parallel re-lays the embedding's output once
+    on entry and the final norm's input once on exit (ZigzagRelayout, gradients the inverse way),
+    and the decoder layers run on zig-zag shards with zig-zag RoPE tables -- two exchanges of
+    [B, S, H] per forward instead of three (q, K|V, o) per layer (PICOTRON_ZIGZAG_RESIDUAL=0: the
+    per-layer re-lay, A/B only);
+  * with the zig-zag layout the K|V shards do not travel round a ring: MI355X's xGMI is a full mesh
+    (7 point-to-point links per GPU), so each rank fetches every other rank's K|V straight from its
+    owner in ONE batched p2p (C - 1 transfers on C - 1 distinct links at once, overlapped with the
+    causal diagonal block), and in the backward sends each visiting shard's fp32 dK|dV partial
+    straight back to its owner, which sums them -- one link-time of K|V per pass instead of C - 1
+    sequential ring hops (PICOTRON_RING_MESH=0: the ring, A/B only).
 """
 import math
 import os
-import weakref
 
 import torch
+import torch.distributed as dist
 
 from .. import kernels as K
 from .. import process_group_manager as pgm
-from ..switches import S
+from ..switches import S as SW
 from .cp_communications import ContextCommunicate, zigzag_exchange
 
 
 def apply_context_parallel(model):
-    os.environ["CONTEXT_PARALLEL"] = "1" if pgm.current().cp_world_size > 1 else "0"
+    """context_parallel.py:10-12 (sets CONTEXT_PARALLEL) plus, at cp > 1, the zig-zag residual
+    layout: the decoder layers of `model` (a Llama or a pipeline stage) are marked to run on zig-zag
+    shards, the embedding module's output is re-laid into that layout and the final norm's input
+    back out of it (forward hooks, so any container -- Llama.forward, either PipelineParallel --
+    keeps calling the modules unchanged; the returned logits are the rank's contiguous tokens).
+    Whether a given batch uses the layout is decided per call from its local sequence length
+    (zigzag_enabled), identically at the entry, in every layer and at the exit."""
+    cp = pgm.current().cp_world_size
+    os.environ["CONTEXT_PARALLEL"] = "1" if cp > 1 else "0"
+    if cp > 1 and SW.zigzag_residual != 0 and not getattr(model, "_pt_zigzag_residual", False):
+        from ..model import DecoderLayer
+        tables = {}
+        for name, mod in model.named_modules():
+            leaf = name.rsplit(".", 1)[-1]
+            if isinstance(mod, DecoderLayer):
+                key = mod._rope_args
+                if key not in tables:
+                    tables[key] = zigzag_rope_tables(*key)
+                mod.zz_cos, mod.zz_sin = tables[key]
+                mod.cp_zigzag_residual = True
+            elif leaf == "embedding" and not isinstance(mod, torch.nn.Identity):
+                mod.register_forward_hook(_zz_entry_hook)
+            elif leaf == "final_norm" and not isinstance(mod, torch.nn.Identity):
+                mod.register_forward_pre_hook(_zz_exit_hook)
+        model._pt_zigzag_residual = True
     return model
+
+
+class ZigzagRelayout(torch.autograd.Function):
+    """The residual stream between the reference's contiguous split and the zig-zag split, x
+    [B, S, ...] (sequence on dim 1); the gradient goes the inverse way."""
+
+    @staticmethod
+    def forward(ctx, x, to_zigzag):
+        ctx.to_zigzag = to_zigzag
+        (y,) = zigzag_exchange([x], [1], to_zigzag)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (dx,) = zigzag_exchange([g.contiguous()], [1], not ctx.to_zigzag)
+        return dx, None
+
+
+def _zz_entry_hook(module, inputs, output):
+    if output.dim() == 3 and zigzag_enabled(output.shape[1], True):
+        return ZigzagRelayout.apply(output, True)
+    return output
+
+
+def _zz_exit_hook(module, args):
+    x = args[0]
+    if x.dim() == 3 and zigzag_enabled(x.shape[1], True):
+        return (ZigzagRelayout.apply(x, False),) + tuple(args[1:])
+    return None
+
+
+def zigzag_rope_tables(seq_length, head_dim, base):
+    """get_cos_sin over the whole sequence, rows of this rank's zig-zag half-chunks r and 2C - 1 - r
+    (the positions of its zig-zag shard, row s of the local sequence = the token at local index s)."""
+    from ..model import get_cos_sin
+    m = pgm.current()
+    C, r = m.cp_world_size, m.cp_rank
+    cos, sin = get_cos_sin(seq_length, head_dim=head_dim, base=base)
+    h = seq_length // (2 * C)
+    rows = lambda t: torch.cat([t[r * h:(r + 1) * h], t[(2 * C - 1 - r) * h:(2 * C - r) * h]])  # noqa: E731
+    return rows(cos), rows(sin)
 
 
 def update_rope_for_context_parallel(cos, sin):
@@ -81,7 +158,7 @@ def zigzag_enabled(S, is_causal, blocks=HipBlocks):
     """The load-balanced layout applies to a causal ring of C > 1 whose half shards tile."""
     C = pgm.current().cp_world_size
     return (is_causal and C > 1 and S % (2 * getattr(blocks, "align", 1)) == 0
-            and S.ring_zigzag != 0)
+            and SW.ring_zigzag != 0)
 
 
 def _zz_kind(step, rank, world):
@@ -96,6 +173,8 @@ def ring_forward(q, kv, nkv, scale, is_causal, blocks=HipBlocks, comm=None, zigz
     q [B, S, nh, d] (any strides, d contiguous); kv [B*S, 2*nkv*d] contiguous (this rank's K|V).
     zigzag: q / kv are in the zig-zag layout (zigzag_exchange) and the balanced schedule runs.
     Returns (out_f32 [B, S, nh, d], lse f32 [B, nh, S])."""
+    if zigzag and comm is None and SW.ring_mesh != 0:
+        return mesh_forward(q, kv, nkv, scale, blocks)
     comm = comm or ContextCommunicate("comm")
     B, S, nh, d = q.shape
     acc = torch.zeros(B, S, nh, d, dtype=torch.float32, device=q.device)
@@ -125,6 +204,8 @@ def ring_backward(do, q, kv, o, lse, nkv, scale, is_causal, blocks=HipBlocks, kv
                   zigzag=False):
     """RingAttentionFunc.backward (context_parallel.py:53-110).  Returns (dq f32 [B,S,nh,d],
     dkv f32 [B*S, 2*nkv*d]) for this rank's own shards (zigzag: all in the zig-zag layout)."""
+    if zigzag and kv_comm is None and SW.ring_mesh != 0:
+        return mesh_backward(do, q, kv, o, lse, nkv, scale, blocks)
     kv_comm = kv_comm or ContextCommunicate("kv_comm")
     d_kv_comm = d_kv_comm or ContextCommunicate("d_kv_comm")
     B, S, nh, d = q.shape
@@ -163,53 +244,130 @@ def ring_backward(do, q, kv, o, lse, nkv, scale, is_causal, blocks=HipBlocks, kv
     return dq, next_dkv
 
 
+# ---- the full-mesh schedule (zig-zag layout) -------------------------------------------------
+def _p2p(ops, group):
+    """Post one batched isend/irecv (one RCCL group: the transfers to / from different peers run
+    concurrently on their own xGMI links).  gloo (the one-GPU tests) is not stream-ordered: the
+    host synchronises before the sends and after the receives, as ContextCommunicate does."""
+    sync = dist.get_backend(group) != "nccl" and torch.cuda.is_available()
+    if sync:
+        torch.cuda.synchronize()
+    return dist.batch_isend_irecv(ops), sync
+
+
+def _p2p_wait(pending):
+    reqs, sync = pending
+    for req in reqs:
+        req.wait()
+    if sync:
+        torch.cuda.synchronize()
+
+
+def mesh_gather_kv(kv):
+    """Post the fetch of every other cp rank's K|V shard straight from its owner: C - 1 sends of
+    this rank's kv and C - 1 receives, one batched p2p.  Returns ({rank: buffer}, pending)."""
+    m = pgm.current()
+    C, r, ids, group = m.cp_world_size, m.cp_rank, m.cp_group_ids, m.cp_group
+    bufs = {j: torch.empty_like(kv) for j in range(C) if j != r}
+    ops = [dist.P2POp(dist.isend, kv, ids[j], group=group) for j in bufs]
+    ops += [dist.P2POp(dist.irecv, bufs[j], ids[j], group=group) for j in bufs]
+    return bufs, _p2p(ops, group)
+
+
+def mesh_forward(q, kv, nkv, scale, blocks=HipBlocks):
+    """The zig-zag causal forward on the mesh: the diagonal block (local causal mask over this
+    rank's two half-chunks) runs while the K|V shards arrive; then each visiting shard j is half a
+    block -- j < r: all my queries x its first half ('kv0'), j > r: my second half x all of it
+    ('q1') -- merged into the running (out, LSE) by the kernel epilogue."""
+    m = pgm.current()
+    r = m.cp_rank
+    B, S, nh, d = q.shape
+    h = S // 2
+    acc = torch.zeros(B, S, nh, d, dtype=torch.float32, device=q.device)
+    lse = torch.full((B, nh, S), float("-inf"), dtype=torch.float32, device=q.device)
+    bufs, pending = mesh_gather_kv(kv)
+    k, v = _kv_views(kv, B, S, nkv, d)
+    blocks.fwd(q, k, v, scale, True, acc, lse)
+    _p2p_wait(pending)
+    for j, kvj in bufs.items():
+        k, v = _kv_views(kvj, B, S, nkv, d)
+        if j < r:
+            blocks.fwd(q, k[:, :h], v[:, :h], scale, False, acc, lse)
+        else:
+            blocks.fwd(q[:, h:], k, v, scale, False, acc[:, h:], lse[:, :, h:])
+    return acc, lse
+
+
+def mesh_backward(do, q, kv, o, lse, nkv, scale, blocks=HipBlocks):
+    """The zig-zag causal backward on the mesh: K|V gathered again under the diagonal block's
+    backward; each visiting shard's fp32 dK|dV partial (its first half for 'kv0', all of it for
+    'q1') is sent straight to its owner in one batched p2p, and the partials this rank receives
+    for its own K|V are summed into its dK|dV.  Returns (dq f32 [B,S,nh,d], dkv f32 [B*S, 2 w])."""
+    m = pgm.current()
+    r, ids, group = m.cp_rank, m.cp_group_ids, m.cp_group
+    B, S, nh, d = q.shape
+    h, w = S // 2, nkv * d
+    delta = blocks.delta(do, o)
+    dq = torch.zeros(B, S, nh, d, dtype=torch.float32, device=q.device)
+    dkv = torch.zeros(kv.shape, dtype=torch.float32, device=kv.device)
+    bufs, pending = mesh_gather_kv(kv)
+    k, v = _kv_views(kv, B, S, nkv, d)
+    dk, dv = _kv_views(dkv, B, S, nkv, d)
+    blocks.bwd(do, q, k, v, o, lse, delta, scale, True, dq, dk, dv)
+    _p2p_wait(pending)
+    parts = {}
+    for j, kvj in bufs.items():
+        k, v = _kv_views(kvj, B, S, nkv, d)
+        part = torch.zeros(B, h if j < r else S, 2 * w, dtype=torch.float32, device=kv.device)
+        pk = part[:, :, :w].view(B, part.shape[1], nkv, d)
+        pv = part[:, :, w:].view(B, part.shape[1], nkv, d)
+        if j < r:
+            blocks.bwd(do, q, k[:, :h], v[:, :h], o, lse, delta, scale, False, dq, pk, pv)
+        else:
+            blocks.bwd(do[:, h:], q[:, h:], k, v, o[:, h:], lse[:, :, h:], delta[:, :, h:], scale, False,
+                       dq[:, h:], pk, pv)
+        parts[j] = part
+    # from rank i's side this rank's shard was 'kv0' (r < i: first half) or 'q1' (r > i: all)
+    recv = {i: torch.empty(B, h if r < i else S, 2 * w, dtype=torch.float32, device=kv.device) for i in parts}
+    ops = [dist.P2POp(dist.isend, parts[j], ids[j], group=group) for j in parts]
+    ops += [dist.P2POp(dist.irecv, recv[i], ids[i], group=group) for i in recv]
+    _p2p_wait(_p2p(ops, group))
+    dkv3 = dkv.view(B, S, 2 * w)
+    for i, t in recv.items():
+        dkv3[:, :t.shape[1]] += t
+    return dq, dkv
+
+
 # ---- token-major entry points used by the fused decoder layer (functional.py) ----------------
-# The zig-zag forward keeps its re-laid q / K|V / o for the backward, keyed by the returned LSE
-# (which stays in the zig-zag layout: only the ring backward reads it), so the backward exchanges
-# only dO and the gradients.
-_ZZ_SAVED = {}
-
-
-def _zz_stash(lse, tensors):
-    for key in [k for k, e in _ZZ_SAVED.items() if e[0]() is None]:
-        del _ZZ_SAVED[key]
-    _ZZ_SAVED[lse.data_ptr()] = (weakref.ref(lse), lse._version, tensors)
-
-
-def _zz_take(lse):
-    e = _ZZ_SAVED.pop(lse.data_ptr(), None)
-    if e is None or e[0]() is not lse or lse._version != e[1]:
-        return None
-    return e[2]
-
-
-def ring_attention_tokens(qkv, sh, scale, is_causal):
-    """q|k|v from the fused projection [T, q|k|v] -> (o bf16 [B,S,nh,d], lse f32 [B,nh,S]; with the
-    zig-zag schedule the LSE is in the zig-zag layout)."""
+def ring_attention_tokens(qkv, sh, scale, is_causal, resident=False):
+    """q|k|v from the fused projection [T, q|k|v] -> (o bf16 [B,S,nh,d], lse f32 [B,nh,S]).
+    resident: qkv is already in the zig-zag layout (the decoder stack's residual stream is, see
+    apply_context_parallel) and so is o; otherwise, with the zig-zag schedule, q and K|V are re-laid
+    here and o re-laid back (the LSE stays in the zig-zag layout: only the ring backward reads it)."""
     B, S, T = sh.B, sh.S, sh.T
+    if resident:
+        acc, lse = ring_forward(sh.q(qkv), qkv[:, sh.wq:].contiguous(), sh.nkv, scale, is_causal, zigzag=True)
+        return acc.to(torch.bfloat16), lse
     if zigzag_enabled(S, is_causal):
         qz, kvz = zigzag_exchange([sh.q(qkv), qkv[:, sh.wq:].view(B, S, 2 * sh.wkv)], [1, 1], True)
-        kvz = kvz.view(T, 2 * sh.wkv)
-        acc, lse = ring_forward(qz, kvz, sh.nkv, scale, is_causal, zigzag=True)
-        oz = acc.to(torch.bfloat16)
-        (o,) = zigzag_exchange([oz], [1], False)
-        _zz_stash(lse, (qz, kvz, oz))
+        acc, lse = ring_forward(qz, kvz.view(T, 2 * sh.wkv), sh.nkv, scale, is_causal, zigzag=True)
+        (o,) = zigzag_exchange([acc.to(torch.bfloat16)], [1], False)
         return o, lse
     kv = qkv[:, sh.wq:].contiguous()
     acc, lse = ring_forward(sh.q(qkv), kv, sh.nkv, scale, is_causal)
     return acc.to(torch.bfloat16), lse
 
 
-def ring_attention_tokens_bwd(do, qkv, o, lse, sh, scale, is_causal, dqkv):
+def ring_attention_tokens_bwd(do, qkv, o, lse, sh, scale, is_causal, dqkv, resident=False):
     B, S, T = sh.B, sh.S, sh.T
-    if zigzag_enabled(S, is_causal):
-        saved = _zz_take(lse)
-        if saved is None:   # not the forward's LSE object: re-lay q / K|V / o again
-            saved = zigzag_exchange([sh.q(qkv), qkv[:, sh.wq:].view(B, S, 2 * sh.wkv), o], [1, 1, 1], True)
-            saved[1] = saved[1].view(T, 2 * sh.wkv)
-        qz, kvz, oz = saved
-        (doz,) = zigzag_exchange([do], [1], True)
-        dq, dkv = ring_backward(doz, qz, kvz, oz, lse, sh.nkv, scale, is_causal, zigzag=True)
+    if resident:
+        dq, dkv = ring_backward(do, sh.q(qkv), qkv[:, sh.wq:].contiguous(), o, lse, sh.nkv, scale, is_causal,
+                                zigzag=True)
+    elif zigzag_enabled(S, is_causal):
+        # the standalone layer (contiguous residual): q / K|V / o / dO re-laid in one exchange
+        qz, kvz, oz, doz = zigzag_exchange([sh.q(qkv), qkv[:, sh.wq:].view(B, S, 2 * sh.wkv), o, do],
+                                           [1, 1, 1, 1], True)
+        dq, dkv = ring_backward(doz, qz, kvz.view(T, 2 * sh.wkv), oz, lse, sh.nkv, scale, is_causal, zigzag=True)
         # rounded to bf16 before the way back (the same single rounding as the copy below)
         dq, dkv = zigzag_exchange([dq.to(torch.bfloat16), dkv.to(torch.bfloat16).view(B, S, 2 * sh.wkv)], [1, 1],
                                   False)

@@ -30,7 +30,7 @@ import torch
 import torch.distributed as dist
 
 from . import kernels as K
-from .switches import S
+from .switches import S as SW
 
 BF16 = torch.bfloat16
 
@@ -39,7 +39,7 @@ def _fuse():
     """PICOTRON_FUSE=0 turns the epilogue fusions (RoPE in the q|k|v GEMM and the attention
     backward, SwiGLU in the gate|up / down GEMMs) off -- for A/B measurement only; both paths are
     HIP kernels with identical results."""
-    return S.fuse != 0
+    return SW.fuse != 0
 
 
 # ------------------------------------------------------------------------ gradient sinks
@@ -147,7 +147,7 @@ _PENDING_DW = {}   # autograd graph task id -> [(partial, weight, stream)]
 
 
 def _norm_defer_enabled():
-    return S.norm_defer != 0
+    return SW.norm_defer != 0
 
 
 def _norm_dw_sink(weight):
@@ -331,7 +331,7 @@ def _take_ce_stats(lg):
 
 
 def ce_stats_enabled():
-    return S.ce_stats != 0
+    return SW.ce_stats != 0
 
 
 class LMHeadFunction(torch.autograd.Function):
@@ -375,10 +375,11 @@ def ring_enabled():
 class AttnShape:
     """Views of the fused [T, q | k | v] projection as token-major [B, S, heads, d] tensors."""
 
-    def __init__(self, B, S, nh, nkv, d):
+    def __init__(self, B, S, nh, nkv, d, zz=False):
         self.B, self.S, self.nh, self.nkv, self.d = B, S, nh, nkv, d
         self.T = B * S
         self.wq, self.wkv = nh * d, nkv * d
+        self.zz = zz    # the tokens are a zig-zag CP shard (context_parallel.apply_context_parallel)
 
     def q(self, t):
         return t[:, :self.wq].view(self.B, self.S, self.nh, self.d)
@@ -398,7 +399,7 @@ def attention_core_fwd(qkv, sh, cos, sin, scale, roped=False):
         K.rope_(qkv, sh.nh + sh.nkv, sh.d, cos, sin, sh.S)
     if ring_enabled():
         from .context_parallel.context_parallel import ring_attention_tokens
-        return ring_attention_tokens(qkv, sh, scale, True)
+        return ring_attention_tokens(qkv, sh, scale, True, resident=sh.zz)
     return K.attn_fwd(sh.q(qkv), sh.k(qkv), sh.v(qkv), scale, True)
 
 
@@ -407,7 +408,7 @@ def attention_core_bwd(do, qkv, o, lse, sh, cos, sin, scale):
     dqkv = torch.empty_like(qkv)
     if ring_enabled():
         from .context_parallel.context_parallel import ring_attention_tokens_bwd
-        ring_attention_tokens_bwd(do, qkv, o, lse, sh, scale, True, dqkv)
+        ring_attention_tokens_bwd(do, qkv, o, lse, sh, scale, True, dqkv, resident=sh.zz)
         K.rope_(dqkv, sh.nh + sh.nkv, sh.d, cos, sin, sh.S, inverse=True)
     elif _fuse():  # the RoPE backward is fused into the dq / dk stores
         K.attn_bwd(do, sh.q(qkv), sh.k(qkv), sh.v(qkv), o, lse, scale, True,
@@ -434,7 +435,7 @@ def attn_block_fwd(h2, wq, wk, wv, wo, cos, sin, sh, tp):
 
 
 def _dual_qkv_enabled():
-    return S.dual_qkv != 0
+    return SW.dual_qkv != 0
 
 
 def attn_block_bwd(da, h2, saved, wq, wk, wv, wo, cos, sin, sh, tp, need_dx=True, keep_parts=False):
@@ -503,7 +504,7 @@ def mlp_block_fwd(h2, wg, wu, wd, tp, residual=None):
 
 
 def _dual_gu_enabled():
-    return S.dual_gu != 0
+    return SW.dual_gu != 0
 
 
 def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True, keep_parts=False):
@@ -562,12 +563,13 @@ class DecoderLayerFunction(torch.autograd.Function):
         out = z + MLP(h2)                  (residual fused into the down_proj epilogue)
 
     Backward runs the same kernels in reverse; the residual gradients are fused into the norm
-    backward kernels (dres) and the TP dX all-reduces overlap the dW GEMMs."""
+    backward kernels (dres) and the TP dX all-reduces overlap the dW GEMMs.  zz: x is a zig-zag CP
+    shard (cos / sin its positions' tables): the ring runs on it with no re-lay."""
 
     @staticmethod
-    def forward(ctx, x, w1, w2, wq, wk, wv, wo, wg, wu, wd, cos, sin, eps, mode, nh, nkv, d):
+    def forward(ctx, x, w1, w2, wq, wk, wv, wo, wg, wu, wd, cos, sin, eps, mode, nh, nkv, d, zz=False):
         B, S, H = x.shape
-        sh = AttnShape(B, S, nh, nkv, d)
+        sh = AttnShape(B, S, nh, nkv, d, zz)
         tp = TPContext.current()
         x2 = _contig2d(x)
         h1, rstd1, _ = K.rmsnorm_fwd(x2, w1, eps, mode)
@@ -591,7 +593,7 @@ class DecoderLayerFunction(torch.autograd.Function):
         dz = norm_bwd(dh2, z, w2, rstd2, mode, dres=dout2)
         dh1 = attn_block_bwd(dz, h1, (qkv, o, lse), wq, wk, wv, wo, cos, sin, sh, tp, keep_parts=K.norm_splitk_enabled())
         dx = norm_bwd(dh1, x2, w1, rstd1, mode, dres=dz)   # (norm_bwd skips dW of frozen weights)
-        return (dx.view(sh.B, sh.S, -1),) + (None,) * 16
+        return (dx.view(sh.B, sh.S, -1),) + (None,) * 17
 
 
 # ------------------------------------------------------------------------ cross entropy

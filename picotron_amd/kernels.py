@@ -12,7 +12,7 @@ import sys
 import torch
 
 from . import _C
-from .switches import S
+from .switches import S as SW
 
 BF16 = torch.bfloat16
 
@@ -536,7 +536,7 @@ def _problem(A, lda, Bs, ldbs, b_bounds, b_seg_dim, Cs, ldcs, c_bounds, M, N, K)
 
 
 def _ksplit_enabled():
-    return S.ksplit != 0
+    return SW.ksplit != 0
 
 
 def wgrad_ksplit(mnks, extra_tiles=0):
@@ -682,7 +682,7 @@ def linear_fwd_rope(x2d, weights, cos, sin, seq_len, rot_heads, head_dim):
     _req(cos.shape[0] >= seq_len and rope_fusable(T, head_dim, seq_len), "linear_fwd_rope: shape")
     ns = [w.shape[0] for w in weights]
     N = sum(ns)
-    if (T // 256) * (N // 256) < S.rope_fuse_min_tiles:
+    if (T // 256) * (N // 256) < SW.rope_fuse_min_tiles:
         # a TP shard's q|k|v (TP = 8: N 768, 48 tiles of 256x256 on 256 CUs): the phased kernels
         # the RoPE epilogue needs would leave most CUs idle; the plain GEMM picks a smaller tile and
         # csrc/rope.hip rotates q|k after it (bit-identical to the fused epilogue)
@@ -779,7 +779,7 @@ def swiglu_fusable(T, I, backward=False):
 def swiglu_fuse_pays(T, I, backward=False):
     """swiglu_fusable and enough tiles that the fused (8-phase 256x256) launch fills the CUs."""
     tiles = (T // 256) * (I // (256 if backward else 128))
-    return swiglu_fusable(T, I, backward) and tiles >= (S.swiglu_bwd_min_tiles if backward else S.swiglu_fuse_min_tiles)
+    return swiglu_fusable(T, I, backward) and tiles >= (SW.swiglu_bwd_min_tiles if backward else SW.swiglu_fuse_min_tiles)
 
 
 def linear_swiglu_fwd(x2d, wg, wu):
@@ -815,11 +815,11 @@ def linear_dgrad_swiglu(dy2d, wd, gu):
 
 
 def _splitk_enabled():
-    return S.splitk2 != 0
+    return SW.splitk2 != 0
 
 
 def _splitk_min():
-    return S.splitk2_min
+    return SW.splitk2_min
 
 
 def _splitk_halves(M, N, K, min_half=None):
@@ -911,14 +911,14 @@ def linear_dgrad(dy2d, weights, out=None, accumulate=False, tile=-1):
 
 def dual_enabled():
     """PICOTRON_DUAL=0 launches a layer's dX and dW GEMMs separately (A/B measurement only)."""
-    return S.dual != 0
+    return SW.dual != 0
 
 
 def _dual_order():
     """0: dX tiles first in every XCD, 1: dW first, 2 (default): staggered -- even XCDs dX first, odd XCDs
     dW first, so half the chip is in the dX tiles' HBM-bound SwiGLU-backward tail at a time (+0.8 %
     on the step, profiles/r03/dual_order_ab.txt)."""
-    return S.dual_order
+    return SW.dual_order
 
 
 def dual_fits(dgrad_mn, wgrad_mns):
@@ -932,7 +932,7 @@ def dual_fits(dgrad_mn, wgrad_mns):
 def norm_splitk_enabled():
     """The post-attention norm backward takes the gate|up dX's split-K halves directly
     (PICOTRON_NORM_SPLITK=0: the sum pass + the plain norm backward, A/B only)."""
-    return S.norm_splitk != 0
+    return SW.norm_splitk != 0
 
 
 def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None, keep_parts=False, split_min=None):
@@ -1117,7 +1117,7 @@ def attn_bwd(dout, q, k, v, out, lse, scale, causal, dq=None, dk=None, dv=None, 
     B, Sq, H, D = q.shape
     Sk, HKV = k.shape[1], k.shape[2]
     lib = _C.lib()
-    fuse_delta = delta is None and not grad_f32 and out.dtype == BF16 and S.fuse_delta != 0
+    fuse_delta = delta is None and not grad_f32 and out.dtype == BF16 and SW.fuse_delta != 0
     if delta is None and not fuse_delta:
         ld0 = _lse_ld(lse, B, H, Sq)
         delta = attn_delta(dout, out, torch.empty(B, H, ld0, dtype=torch.float32, device=q.device)[:, :, :Sq]

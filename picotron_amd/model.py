@@ -256,24 +256,32 @@ class DecoderLayer(nn.Module):
         self.mlp = MLP(config)
         self.layer_idx = layer_idx
         head_dim = config.hidden_size // config.num_attention_heads
+        self._rope_args = (config.max_position_embeddings, head_dim, config.rope_theta)
         self.cos, self.sin = get_cos_sin(config.max_position_embeddings, head_dim=head_dim, base=config.rope_theta)
         self.cos, self.sin = context_parallel.update_rope_for_context_parallel(self.cos, self.sin)
+        # set by context_parallel.apply_context_parallel at cp > 1: the input is the zig-zag shard of
+        # the residual stream (zz_cos / zz_sin: that shard's positions) whenever its length tiles
+        self.cp_zigzag_residual = False
 
-    def _tables(self, device):
+    def _tables(self, device, zz=False):
         # tables follow the activations' device (the module may have been moved after init)
-        if self.cos.device != device or self.cos.dtype != torch.bfloat16:
-            self.cos = self.cos.to(device=device, dtype=torch.bfloat16)
-            self.sin = self.sin.to(device=device, dtype=torch.bfloat16)
-        return self.cos, self.sin
+        a, b = ("zz_cos", "zz_sin") if zz else ("cos", "sin")
+        cos, sin = getattr(self, a), getattr(self, b)
+        if cos.device != device or cos.dtype != torch.bfloat16:
+            cos, sin = cos.to(device=device, dtype=torch.bfloat16), sin.to(device=device, dtype=torch.bfloat16)
+            setattr(self, a, cos)
+            setattr(self, b, sin)
+        return cos, sin
 
     def forward(self, x, attention_mask=None, position_ids=None):
-        cos, sin = self._tables(x.device)
+        zz = self.cp_zigzag_residual and context_parallel.zigzag_enabled(x.shape[1], True)
+        cos, sin = self._tables(x.device, zz)
         n1, n2, at, mlp = self.input_layernorm, self.post_attention_layernorm, self.attention, self.mlp
         if _norm_mode(n1) != _norm_mode(n2) or _norm_eps(n1) != _norm_eps(n2):
             raise ValueError("DecoderLayer: both norms must be the same flavour")
         return FN.DecoderLayerFunction.apply(
             x, n1.weight, n2.weight, *at.weights(), mlp.gate_proj.weight, mlp.up_proj.weight, mlp.down_proj.weight,
-            cos, sin, _norm_eps(n1), _norm_mode(n1), at.num_local_heads, at.num_local_kv_heads, at.head_dim)
+            cos, sin, _norm_eps(n1), _norm_mode(n1), at.num_local_heads, at.num_local_kv_heads, at.head_dim, zz)
 
 
 class Embedding(nn.Module):

@@ -23,8 +23,9 @@ DEFAULTS = {
     # run as separate kernels (TP shard widths)
     "ksplit": 1, "splitk2": 1, "splitk2_min": 8192, "dual": 1, "dual_order": 2, "norm_splitk": 1,
     "fuse_delta": 1, "rope_fuse_min_tiles": 96, "swiglu_fuse_min_tiles": 192, "swiglu_bwd_min_tiles": 0,
-    # context_parallel.py: the zig-zag (load-balanced) ring where it tiles
-    "ring_zigzag": 1,
+    # context_parallel.py: the zig-zag (load-balanced) ring where it tiles, the residual stream kept
+    # in that layout across the decoder stack, the full-mesh K|V / dK|dV exchange instead of the ring
+    "ring_zigzag": 1, "zigzag_residual": 1, "ring_mesh": 1,
     # native (libpicotron_hip.so, pt_set_variant)
     "attn_pair": 1, "attn_split": 2, "gemm_group_m": -1, "gemm_mix": 1,
 }

@@ -242,11 +242,18 @@ class CountingBlocks(OracleBlocks):
         OracleBlocks.fwd(q, k, v, scale, causal, acc, lse)
 
 
-def _ring_zigzag(rank, world, nh, nkv):
-    """The load-balanced (zig-zag) ring: shards re-laid by zigzag_exchange, the balanced schedule,
-    outputs / gradients re-laid back -- equal to full causal attention over the whole sequence on
-    the reference's contiguous chunks, and every rank does the same causal work (the reference's
-    schedule: rank r does r + 1 blocks)."""
+def _ring_zigzag(rank, world, nh, nkv, mesh):
+    """The load-balanced (zig-zag) schedule: shards re-laid by zigzag_exchange, the balanced
+    schedule -- over the full mesh (mesh=1: every K|V shard fetched from its owner, dK|dV partials
+    sent back to it) or round the ring (mesh=0) -- outputs / gradients re-laid back: equal to full
+    causal attention over the whole sequence on the reference's contiguous chunks, and every rank
+    does the same causal work (the reference's schedule: rank r does r + 1 blocks)."""
+    from picotron_amd import switches
+    with switches.override(ring_mesh=mesh):
+        _ring_zigzag_body(rank, world, nh, nkv)
+
+
+def _ring_zigzag_body(rank, world, nh, nkv):
     from oracle import picotron_oracle as O
     from picotron_amd import process_group_manager as pgm
     from picotron_amd.context_parallel import context_parallel as CP
@@ -297,9 +304,42 @@ def _ring_zigzag(rank, world, nh, nkv):
     torch.testing.assert_close(dkv[:, :, w:].reshape(B, S, nkv, d), dv_ref, rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("mesh", [1, 0])
 @pytest.mark.parametrize("world,nh,nkv", [(2, 2, 2), (3, 2, 1), (4, 4, 2)])
-def test_zigzag_ring_is_balanced_and_exact(world, nh, nkv):
-    _dist.run(_ring_zigzag, world, nh, nkv)
+def test_zigzag_ring_is_balanced_and_exact(world, nh, nkv, mesh):
+    _dist.run(_ring_zigzag, world, nh, nkv, mesh)
+
+
+def _zz_residual(rank, world):
+    """The zig-zag residual stream's pieces (context_parallel.apply_context_parallel): the re-lay is
+    a permutation whose backward is the inverse permutation of the gradient, and the zig-zag RoPE
+    tables are get_cos_sin's rows at the positions of the rank's zig-zag shard."""
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.context_parallel import context_parallel as CP
+    from picotron_amd.model import get_cos_sin
+    pgm.setup_process_group_manager(tp_size=1, cp_size=world, pp_size=1, dp_size=1)
+    B, S, H = 2, 8, 3
+    full = torch.arange(B * world * S * H, dtype=torch.float32).view(B, world * S, H)
+    x = full[:, rank * S:(rank + 1) * S].clone().requires_grad_(True)
+    y = CP.ZigzagRelayout.apply(x, True)
+    h = S // 2
+    pos = list(range(rank * h, (rank + 1) * h)) + list(range((2 * world - 1 - rank) * h, (2 * world - rank) * h))
+    assert torch.equal(y.detach(), full[:, pos])
+    g = torch.randn(y.shape, generator=torch.Generator().manual_seed(rank))
+    y.backward(g)
+    # the gradient of sum(y * g) w.r.t. the contiguous shard: g laid back
+    (gb,) = CP.zigzag_exchange([g], [1], False)
+    assert torch.equal(x.grad, gb)
+    z = CP.ZigzagRelayout.apply(y.detach(), False)
+    assert torch.equal(z, x.detach())
+    cos, sin = CP.zigzag_rope_tables(world * S, 16, 10000.0)
+    cf, sf = get_cos_sin(world * S, 16, base=10000.0)
+    assert torch.equal(cos, cf[pos]) and torch.equal(sin, sf[pos])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_zigzag_residual_relayout_and_tables(world):
+    _dist.run(_zz_residual, world)
 
 
 # ----------------------------------------------------------------------------- PP p2p

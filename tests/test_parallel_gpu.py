@@ -74,19 +74,45 @@ def _setup(tp, cp, seq=256):
     return m, model, names, pf, ids, lo, loss_r
 
 
-def _llama(rank, world, tp, cp, seq=256, zigzag=False):
+def _llama(rank, world, tp, cp, seq=256, zigzag=False, residual=1, mesh=1):
+    from picotron_amd import switches
+    with switches.override(zigzag_residual=residual, ring_mesh=mesh):
+        _llama_body(rank, world, tp, cp, seq, zigzag, residual)
+
+
+def _llama_body(rank, world, tp, cp, seq, zigzag, residual):
     from picotron_amd import functional as FN
-    from picotron_amd.context_parallel.context_parallel import zigzag_enabled
+    from picotron_amd.context_parallel import context_parallel as CP
     m, model, names, pf, ids, lo, loss_r = _setup(tp, cp, seq)
     s = seq // cp
-    assert zigzag_enabled(s, True) == zigzag   # which ring schedule this case exercises
+    assert CP.zigzag_enabled(s, True) == zigzag   # which ring schedule this case exercises
     sl = slice(m.cp_rank * s, (m.cp_rank + 1) * s)                # data.py:105-109: contiguous chunks
     x, t = ids[:, :-1][:, sl].contiguous(), ids[:, 1:][:, sl].contiguous()
-    logits = model(x.cuda())
-    assert logits.shape == (2, s, CFG["vocab_size"])             # final_proj gathers its vocab shards
-    loss = FN.cross_entropy(logits.view(-1, CFG["vocab_size"]), t.reshape(-1).cuda())
-    loss.backward()
-    torch.cuda.synchronize()
+    calls = []
+    orig = CP.zigzag_exchange
+
+    def counted(*a, **k):
+        calls.append(a[2])
+        return orig(*a, **k)
+    CP.zigzag_exchange = counted
+    try:
+        logits = model(x.cuda())
+        n_fwd = len(calls)
+        assert logits.shape == (2, s, CFG["vocab_size"])             # final_proj gathers its vocab shards
+        loss = FN.cross_entropy(logits.view(-1, CFG["vocab_size"]), t.reshape(-1).cuda())
+        loss.backward()
+        torch.cuda.synchronize()
+    finally:
+        CP.zigzag_exchange = orig
+    if zigzag and residual:
+        # the residual stream is re-laid once on entry and once on exit (and its gradient twice),
+        # not per layer
+        assert n_fwd == 2 and len(calls) == 4, calls
+    elif zigzag:
+        # the standalone layers: q|K|V in and o out per layer, one combined exchange each way back
+        assert n_fwd == 2 * CFG["num_hidden_layers"] and len(calls) == 4 * CFG["num_hidden_layers"], calls
+    else:
+        assert not calls
     assert _rel(logits, lo[:, sl]) < TOL
     lsum = loss.detach().float().cpu().view(1)
     if cp > 1:
@@ -114,12 +140,15 @@ def test_tp2_cp2_llama():
     _dist.run(_llama, 4, 2, 2, device="cuda")
 
 
-@pytest.mark.parametrize("tp,cp,seq", [(1, 2, 512), (1, 4, 1024), (2, 2, 512)])
-def test_zigzag_ring_llama(tp, cp, seq):
-    """The load-balanced (zig-zag) causal ring (S_local = 256: its half shards tile the kernels):
+@pytest.mark.parametrize("tp,cp,seq,residual,mesh", [(1, 2, 512, 1, 1), (1, 4, 1024, 1, 1), (2, 2, 512, 1, 1),
+                                                    (1, 4, 1024, 0, 1), (1, 4, 1024, 1, 0)])
+def test_zigzag_ring_llama(tp, cp, seq, residual, mesh):
+    """The load-balanced (zig-zag) causal schedule (S_local = 256: its half shards tile the kernels):
     full Llama forward + backward at cp2 / cp4 / tp2.cp2 against the oracle on the whole sequence,
-    the reference's contiguous token chunks in and out."""
-    _dist.run(_llama, tp * cp, tp, cp, seq, True, device="cuda")
+    the reference's contiguous token chunks in and out -- with the residual stream kept in the
+    zig-zag layout (the default: two re-lays per pass) or re-laid per layer, and the K|V / dK|dV
+    exchanged over the full mesh (default) or round the ring."""
+    _dist.run(_llama, tp * cp, tp, cp, seq, True, residual, mesh, device="cuda")
 
 
 def _ring_api(rank, world):
