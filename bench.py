@@ -159,17 +159,29 @@ def tp_proxy(args, base, layers):
             "gemm_by_launch": {k: {"launches": v[0], "ms": v[1], "tflops": v[2]} for k, v in probe.by_label().items()}}
 
 
+XGMI_LINK_GBPS = 153.0   # one MI355X xGMI link, per direction (7 links per GPU, full mesh)
+
+
 def cp_proxy(args, base, layers):
     """The critical rank of a CP ring for one layer of Llama-2-7B at seq = C x S_local: the layer's
     GEMMs + its causal diagonal block (the fused layer at S_local) and the visiting blocks (forward
     with the LSE merge epilogue, backward from the global LSE, f32 dQ / dK / dV as the ring keeps
-    them), fwd + bwd.  No p2p.  Two schedules:
+    them), fwd + bwd, timed on one GPU.  Schedules:
       reference  (context_parallel.py:30-45): the last rank computes C - 1 full S_local^2 blocks;
       zig-zag    (the shipped one, context_parallel.zigzag_enabled): every rank computes C - 1 half
                  blocks -- rank r: r of [S_local x S_local/2] (its queries x the first half of the
                  keys) and C - 1 - r of [S_local/2 x S_local] -- the slowest rank sets the pace.
-    The zig-zag layout's shard exchange (q, K|V, o forward; dO, dq, dK|dV backward, over RCCL p2p)
-    is not in this 1-GPU proxy."""
+    Communication is not run (one GPU); it is costed per layer from its bytes at XGMI_LINK_GBPS per
+    link and direction, overlapped with the compute it can hide under:
+      ring (the reference's transport): step s sends the K|V shard to the next rank while the
+                 visiting block computes -- C - 1 sequential one-link hops forward; backward the K|V
+                 hops plus C hops of the fp32 dK|dV accumulator (context_parallel.py:72-106);
+      mesh (shipped with the zig-zag layout): all C - 1 K|V shards fetched at once from their owners
+                 on C - 1 distinct links under the diagonal block; backward the same gather under
+                 the diagonal block's backward, then each fp32 dK|dV partial sent straight to its
+                 owner (one transfer per link, the largest a full shard's 2 x bf16 bytes);
+      re-lay     the residual stream's zig-zag re-lay, twice per forward and twice per backward for
+                 the whole stack (apply_context_parallel), amortised per layer."""
     import math
     from picotron_amd import functional as FN
     from picotron_amd import kernels as K
@@ -207,45 +219,77 @@ def cp_proxy(args, base, layers):
 
     def layer():
         FN.DecoderLayerFunction.apply(x, *w, cos, sin, cfg.rms_norm_eps, 0, nh, nkv, d).backward(r(B, S, H))
-
-    def block_fwd():
-        K.attn_fwd(q, k, v, sc, False, out=acc, lse=lse, merge=True)
-
-    def block_bwd():
-        K.attn_bwd(do, q, k, v, o, lse, sc, False, dq=dq, dk=dk, dv=dv, grad_f32=True, delta=delta)
-
-    def kv0_fwd():    # all S_local queries x the first half of the visiting keys
-        K.attn_fwd(q, k[:, :h], v[:, :h], sc, False, out=acc, lse=lse, merge=True)
-
-    def kv0_bwd():
-        K.attn_bwd(do, q, k[:, :h], v[:, :h], o, lse, sc, False, dq=dq, dk=dk[:, :h], dv=dv[:, :h], grad_f32=True,
-                   delta=delta)
-
-    def q1_fwd():     # the second half of the queries x all the visiting keys
-        K.attn_fwd(q[:, h:], k, v, sc, False, out=acc[:, h:], lse=lse[:, :, h:], merge=True)
-
-    def q1_bwd():
-        K.attn_bwd(do[:, h:], q[:, h:], k, v, o[:, h:], lse[:, :, h:], sc, False, dq=dq[:, h:], dk=dk, dv=dv,
-                   grad_f32=True, delta=delta[:, :, h:])
+    fns = {
+        "diag_fwd": lambda: K.attn_fwd(q, k, v, sc, True, out=acc, lse=lse, merge=True),
+        "diag_bwd": lambda: K.attn_bwd(do, q, k, v, o, lse, sc, True, dq=dq, dk=dk, dv=dv, grad_f32=True, delta=delta),
+        "full_fwd": lambda: K.attn_fwd(q, k, v, sc, False, out=acc, lse=lse, merge=True),
+        "full_bwd": lambda: K.attn_bwd(do, q, k, v, o, lse, sc, False, dq=dq, dk=dk, dv=dv, grad_f32=True, delta=delta),
+        # all S_local queries x the first half of the visiting keys
+        "kv0_fwd": lambda: K.attn_fwd(q, k[:, :h], v[:, :h], sc, False, out=acc, lse=lse, merge=True),
+        "kv0_bwd": lambda: K.attn_bwd(do, q, k[:, :h], v[:, :h], o, lse, sc, False, dq=dq, dk=dk[:, :h], dv=dv[:, :h],
+                                      grad_f32=True, delta=delta),
+        # the second half of the queries x all the visiting keys
+        "q1_fwd": lambda: K.attn_fwd(q[:, h:], k, v, sc, False, out=acc[:, h:], lse=lse[:, :, h:], merge=True),
+        "q1_bwd": lambda: K.attn_bwd(do[:, h:], q[:, h:], k, v, o[:, h:], lse[:, :, h:], sc, False, dq=dq[:, h:], dk=dk,
+                                     dv=dv, grad_f32=True, delta=delta[:, :, h:]),
+    }
     t_layer = _events_time(layer, args.steps)
-    t_f = _events_time(block_fwd, args.steps * 4)
-    t_b = _events_time(block_bwd, args.steps * 4)
-    t_kv0 = _events_time(kv0_fwd, args.steps * 4) + _events_time(kv0_bwd, args.steps * 4)
-    t_q1 = _events_time(q1_fwd, args.steps * 4) + _events_time(q1_bwd, args.steps * 4)
+    t = {kname: _events_time(fn, args.steps * 4) for kname, fn in fns.items()}
     blk_flop = 4.0 * B * nh * S * S * d           # full block: QK^T + PV
+    t_f, t_b = t["full_fwd"], t["full_bwd"]
+    t_kv0, t_q1 = t["kv0_fwd"] + t["kv0_bwd"], t["q1_fwd"] + t["q1_bwd"]
     t_ref = t_layer + (C - 1) * (t_f + t_b)       # reference schedule: the last rank
-    t_zz = t_layer + max(rk * t_kv0 + (C - 1 - rk) * t_q1 for rk in range(C))
+    crit = max(range(C), key=lambda rk: rk * t_kv0 + (C - 1 - rk) * t_q1)
+    t_zz = t_layer + crit * t_kv0 + (C - 1 - crit) * t_q1
+
+    # ---- communication budget per layer (bytes per rank, link time, what stays exposed)
+    bw = XGMI_LINK_GBPS * 1e9
+    kv_b = B * S * 2 * nkv * d * 2               # one K|V shard, bf16
+    dkv_b = 2 * kv_b                             # its fp32 dK|dV accumulator
+    relay_b = 4 * B * S * H * 2                  # re-lay of [B, S, H] bf16: entry + exit, fwd + bwd, per pass
+    halves_f = [t["kv0_fwd"]] * crit + [t["q1_fwd"]] * (C - 1 - crit)
+    halves_b = [t["kv0_bwd"]] * crit + [t["q1_bwd"]] * (C - 1 - crit)
+    # ring: each step's transfer hides under that step's block
+    ring_f = sum(max(kv_b / bw, tf) - tf for tf in halves_f)
+    ring_b = sum(max((kv_b + dkv_b) / bw, tb) - tb for tb in halves_b) + dkv_b / bw   # + the last dK|dV hop
+    # mesh: the gather hides under the diagonal block; the partials' return is a tail
+    mesh_f = max(0.0, kv_b / bw - t["diag_fwd"])
+    mesh_b = max(0.0, kv_b / bw - t["diag_bwd"]) + dkv_b / bw
+    relay_t = relay_b / layers / (2 * bw)        # two peers, two links
+    comm = {"link_GBps_per_direction": XGMI_LINK_GBPS, "kv_shard_bytes": kv_b, "dkv_f32_bytes": dkv_b,
+            "ring": {"comm_bytes_per_layer": (C - 1) * kv_b + (C - 1) * kv_b + C * dkv_b,
+                     "link_time_ms": ((C - 1) * kv_b * 2 + C * dkv_b) / bw * 1e3,
+                     "exposed_ms": (ring_f + ring_b) * 1e3},
+            "mesh": {"comm_bytes_per_layer": (C - 1) * kv_b * 2 + crit * kv_b + (C - 1 - crit) * dkv_b,
+                     "link_time_ms": (2 * kv_b + dkv_b) / bw * 1e3, "links": C - 1,
+                     "exposed_ms": (mesh_f + mesh_b) * 1e3},
+            "relayout": {"comm_bytes_per_pass": relay_b, "per_layer_ms": relay_t * 1e3}}
+    t_mesh = t_zz + mesh_f + mesh_b + relay_t
+    t_ring_zz = t_zz + ring_f + ring_b + relay_t
+    attn_compute = t["diag_fwd"] + t["diag_bwd"] + sum(halves_f) + sum(halves_b)
     layer_flop_model = 6 * (2 * H * nh * d + 2 * H * nkv * d + 3 * H * I) + 12 * H * args.seq   # per token
     tok_gpu = B * S / (t_zz * layers)             # each rank holds S tokens; the ring's pace = its slowest rank
-    return {"metric": f"CP={C} critical-rank compute proxy (1 GPU, no p2p)", "value": tok_gpu,
-            "unit": "tokens/s/GPU (compute-only upper bound, lm_head/embedding excluded)",
+    tok_mesh = B * S / (t_mesh * layers)
+    return {"metric": f"CP={C} critical-rank proxy (1 GPU compute + costed xGMI communication)", "value": tok_mesh,
+            "unit": "tokens/s/GPU (zig-zag + mesh: compute measured, communication modelled)",
             "config": {"model": cfg_name(base), "layers": layers, "micro_batch": B, "seq_len": args.seq,
-                       "S_local": S, "head_dim": d, "schedule": "zig-zag (load-balanced)"},
+                       "S_local": S, "head_dim": d, "schedule": "zig-zag (load-balanced), full-mesh K|V exchange"},
+            "compute_only_tokens_per_s_per_gpu": tok_gpu,
+            "ring_transport_tokens_per_s_per_gpu": B * S / (t_ring_zz * layers),
             "layer_ms": t_layer * 1e3, "block_fwd_ms": t_f * 1e3, "block_bwd_ms": t_b * 1e3,
-            "half_block_kv0_ms": t_kv0 * 1e3, "half_block_q1_ms": t_q1 * 1e3,
-            "critical_rank_layer_ms": t_zz * 1e3, "reference_schedule_layer_ms": t_ref * 1e3,
+            "blocks_ms": {kname: v * 1e3 for kname, v in t.items()},
+            "half_block_kv0_ms": t_kv0 * 1e3, "half_block_q1_ms": t_q1 * 1e3, "critical_rank": crit,
+            "critical_rank_layer_ms": t_zz * 1e3, "critical_rank_layer_ms_with_comm": {"mesh": t_mesh * 1e3,
+                                                                                      "ring": t_ring_zz * 1e3},
+            "reference_schedule_layer_ms": t_ref * 1e3,
             "reference_schedule_tokens_per_s_per_gpu": B * S / (t_ref * layers),
+            "comm": comm,
+            "bound": {"mesh": "link" if mesh_f + mesh_b > 0.05 * attn_compute else "compute",
+                      "ring": "link" if ring_f + ring_b > 0.05 * attn_compute else "compute",
+                      "exposed_share_of_layer": {"mesh": (mesh_f + mesh_b + relay_t) / t_mesh,
+                                                 "ring": (ring_f + ring_b + relay_t) / t_ring_zz}},
             "mfu_upper_bound": tok_gpu * layer_flop_model * layers / MI355X_BF16_DENSE_PEAK,
+            "mfu_with_comm": tok_mesh * layer_flop_model * layers / MI355X_BF16_DENSE_PEAK,
             "roofline": {"bound": "mfma", "kernel": "attention block S_local x S_local d128 (fwd merge + bwd)",
                          "achieved": (blk_flop * 3.5) / (t_f + t_b) / 1e12, "peak": MI355X_BF16_DENSE_PEAK / 1e12,
                          "unit": "TFLOP/s", "frac": (blk_flop * 3.5) / (t_f + t_b) / MI355X_BF16_DENSE_PEAK,

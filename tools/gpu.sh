@@ -75,7 +75,7 @@ step_configs() {
   timeout -k 10 200 python -u bench.py --tp-proxy 8 --steps 3 > $O.tpproxy.json 2> $O.tpproxy.err || { echo tpproxy failed; tail $O.tpproxy.err; return 1; }
   jline $O.tpproxy.json tp8-proxy
   timeout -k 10 300 python -u bench.py --cp-proxy 8 --model llama2-7b --seq 32768 --mbs 1 --steps 3 $CP_ARGS > $O.cpproxy.json 2> $O.cpproxy.err || { echo cpproxy failed; tail $O.cpproxy.err; return 1; }
-  python -c "import json; d=json.load(open('$O.cpproxy.json')); print('cp8 proxy', round(d['value']), round(d['critical_rank_layer_ms'],2), round(d['roofline']['fwd_frac'],3), round(d['roofline']['bwd_frac'],3))"
+  python -c "import json; d=json.load(open('$O.cpproxy.json')); print('cp8 proxy', round(d['value']), round(d['compute_only_tokens_per_s_per_gpu']), {k: round(v,2) for k,v in d['critical_rank_layer_ms_with_comm'].items()}, d['bound'], round(d['roofline']['fwd_frac'],3), round(d['roofline']['bwd_frac'],3))"
 }
 
 step_gloo2() {
