@@ -450,7 +450,8 @@ def main():
                                    grad_type=torch.bfloat16 if args.grad_type == "bf16" else torch.float32)
         model._force_grad_sync = force_dp
     optimizer = AdamW(model.parameters(), lr=3e-4)
-    loader = SyntheticMicroBatchDataLoader(args.mbs, args.seq, args.grad_acc, cfg.vocab_size, device, seed=1234)
+    loader = SyntheticMicroBatchDataLoader(args.mbs, args.seq, args.grad_acc, cfg.vocab_size, device, seed=1234,
+                                           fresh=True)
     log(f"rank {rank}/{world}: model {num_params / 1e9:.3f} B params built in {time.time() - t0:.1f} s")
 
     probe = None
@@ -547,7 +548,7 @@ def main():
                "backend": dist.get_backend() if dist.is_initialized() else None,
                "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
                "scaling": "weak" if tp * cp * pp == 1 else "strong",
-               "vs_baseline": None, "dtype": "bf16", "data": "synthetic (seeded random tokens, random init)",
+               "vs_baseline": None, "dtype": "bf16", "data": "synthetic (seeded uniform random tokens, a fresh batch every step; random init)",
                "tokens_per_s_per_gpu": per_gpu, "mfu": mfu, "flops_per_token": fpt, "num_params": num_params,
                "final_loss": losses[-1] if losses else None,
                "config": {"workload": f"{model_name} dims, {layers} layers, train step (fwd+bwd+AdamW)",

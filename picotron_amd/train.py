@@ -38,9 +38,14 @@ def make_config(base, seq_length, **overrides):
 
 
 class SyntheticMicroBatchDataLoader:
-    """Seeded random tokens shaped like MicroBatchDataLoader's batches (data.py:102-136)."""
+    """Seeded random tokens shaped like MicroBatchDataLoader's batches (data.py:102-136).
+    fresh=False replays the same grad_acc micro-batches every step (a memorisation curve, what the
+    loss-curve tests want); fresh=True draws a new step's worth of tokens after each pass, on the
+    device (one launch per step), as the reference's loader streams new data (data.py:123-136) --
+    the first pass is the same either way.  Every rank of one dp replica (tp / cp / pp) draws the
+    same tokens: the generator is seeded by (seed, dp rank) only."""
 
-    def __init__(self, micro_batch_size, seq_length, grad_acc_steps, vocab_size, device, seed=1234):
+    def __init__(self, micro_batch_size, seq_length, grad_acc_steps, vocab_size, device, seed=1234, fresh=False):
         m = pgm.current()
         self.micro_batch_size = micro_batch_size
         self.seq_length = seq_length
@@ -58,12 +63,21 @@ class SyntheticMicroBatchDataLoader:
         self._targets = mine[:, :, 1:][:, :, lo:hi].contiguous().to(device)
         self._pos = torch.arange(lo, hi, device=device).unsqueeze(0).expand(micro_batch_size, -1)
         self._i = 0
+        self._fresh, self._vocab, self._span = fresh, vocab_size, (lo, hi)
+        if fresh:
+            self._gen = torch.Generator(device=device).manual_seed(seed * 1000003 + m.dp_rank)
 
     def __iter__(self):
         return self
 
     def __next__(self):
         i = self._i % self.grad_acc_steps
+        if self._fresh and i == 0 and self._i > 0:   # a new step: new tokens
+            lo, hi = self._span
+            t = torch.randint(0, self._vocab, (self.grad_acc_steps, self.micro_batch_size, self.seq_length + 1),
+                              generator=self._gen, device=self._inputs.device)
+            self._inputs = t[:, :, :-1][:, :, lo:hi].contiguous()
+            self._targets = t[:, :, 1:][:, :, lo:hi].contiguous()
         self._i += 1
         return {"input_ids": self._inputs[i], "target_ids": self._targets[i], "position_ids": self._pos,
                 "hidden_states": None}

@@ -72,3 +72,24 @@ def test_gloo_rehearsal_two_ranks_one_line():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["ranks"] == 2 and d["backend"] == "gloo"
     assert d["config"]["parallelism"] == "dp2"
+
+
+def test_synthetic_loader_fresh_batches():
+    """bench.py's loader draws a new step's tokens after each pass (fresh=True; the first pass is the
+    replaying loader's), so its final_loss is not a memorisation curve; fresh=False replays."""
+    import torch
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.train import SyntheticMicroBatchDataLoader
+    pgm.setup_process_group_manager(1, 1, 1, 1)
+    a = SyntheticMicroBatchDataLoader(2, 16, 3, 100, torch.device("cpu"), seed=5)
+    b = SyntheticMicroBatchDataLoader(2, 16, 3, 100, torch.device("cpu"), seed=5, fresh=True)
+    first_a = [next(a)["input_ids"].clone() for _ in range(3)]
+    first_b = [next(b) for _ in range(3)]
+    assert all(torch.equal(x, y["input_ids"]) for x, y in zip(first_a, first_b))
+    second_a = [next(a)["input_ids"] for _ in range(3)]
+    second_b = [next(b) for _ in range(3)]
+    assert all(torch.equal(x, y) for x, y in zip(first_a, second_a))
+    assert not any(torch.equal(x, y["input_ids"]) for x, y in zip(first_a, second_b))
+    for y in second_b:   # targets stay the inputs shifted by one
+        assert y["input_ids"].shape == (2, 16) and torch.equal(y["input_ids"][:, 1:], y["target_ids"][:, :-1])
+        assert int(y["input_ids"].max()) < 100
