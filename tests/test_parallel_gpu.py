@@ -295,3 +295,66 @@ def _pp_llama(rank, world, kind):
 @pytest.mark.parametrize("kind,world", [("1f1b", 2), ("afab", 2), ("1f1b", 3)])
 def test_pipeline_parallel_llama(kind, world):
     _dist.run(_pp_llama, world, kind, device="cuda")
+
+
+def _dp_overlap(rank, world):
+    """Row f3: the bucket all-reduces are issued DURING the last micro-batch's backward, not after
+    it (bucket.py:25-31: a bucket syncs once all its parameters reported ready; data_parallel.py:
+    122-165).  The fused kernels report a weight ready as soon as its wgrad GEMM is enqueued, so
+    with the backward running layers last-to-first, the buckets of layer L sync while layers
+    L - 1 .. 0 still compute.  Host-side order of decoder-layer backward calls ('L') and bucket
+    all-reduce issues ('B') over the last micro-batch: some 'B' precede the last 'L', every layer's
+    buckets sync right after that layer's backward, and only the embedding's comes last."""
+    import types
+    os.environ["FLASH_ATTEN"] = "1"
+    torch.cuda.set_device(0)
+    from picotron_amd import functional as FN
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.data_parallel import bucket as BK
+    from picotron_amd.data_parallel.data_parallel import DataParallelBucket
+    from picotron_amd.model import Llama
+    pgm.setup_process_group_manager(tp_size=1, cp_size=1, pp_size=1, dp_size=world)
+    cfg = types.SimpleNamespace(**dict(CFG, num_hidden_layers=4))
+    with torch.device("cuda"):
+        model = Llama(cfg)
+    model.to(torch.bfloat16)
+    # 0.25 MiB fp32 buckets: every layer's weights span several buckets
+    ddp = DataParallelBucket(model, bucket_cap_mb=0.25)
+    events = []
+    orig_bwd, orig_sync = FN.DecoderLayerFunction.backward, BK.Bucket.sync_gradient
+
+    def bwd(ctx, *g):
+        out = orig_bwd(ctx, *g)
+        events.append("L")
+        return out
+
+    def sync(self):
+        events.append(("B", self))
+        return orig_sync(self)
+    FN.DecoderLayerFunction.backward = staticmethod(bwd)
+    BK.Bucket.sync_gradient = sync
+    try:
+        g = torch.Generator().manual_seed(rank)
+        for i in range(2):
+            ddp.require_backward_grad_sync = i == 1
+            events.clear()
+            ids = torch.randint(0, CFG["vocab_size"], (2, CFG["max_position_embeddings"] + 1), generator=g).cuda()
+            lo = ddp(input_ids=ids[:, :-1])
+            loss = FN.cross_entropy(lo.reshape(-1, CFG["vocab_size"]), ids[:, 1:].reshape(-1)) / 2
+            loss.backward()
+    finally:
+        FN.DecoderLayerFunction.backward, BK.Bucket.sync_gradient = orig_bwd, orig_sync
+    torch.cuda.synchronize()
+    kinds = ["L" if e == "L" else "B" for e in events]
+    assert kinds.count("L") == 4 and kinds.count("B") == len(ddp.bucket_manager.buckets), kinds
+    last_l = max(i for i, k in enumerate(kinds) if k == "L")
+    assert kinds.index("B") < kinds.index("L"), kinds          # the lm_head's buckets before any layer
+    assert sum(k == "B" for k in kinds[:last_l]) >= len(kinds) // 2, kinds   # most overlap the backward
+    emb = ddp.bucket_manager.buckets[ddp.bucket_manager.params_to_bucket_location[model.embedding.weight][2]]
+    assert events[-1][1] is emb                               # only the embedding's bucket waits to the end
+    if rank == 0:
+        print("dp bucket issue order:", "".join(kinds))
+
+
+def test_dp_bucket_allreduce_overlaps_last_backward():
+    _dist.run(_dp_overlap, 2, device="cuda")
