@@ -559,6 +559,56 @@ def wgrad_ksplit(mnks, extra_tiles=0):
     return s
 
 
+def fewtile_ksplit(M, N, K):
+    """(ksplit, tile) for a forward / dX GEMM whose output tiles leave most of the 256 CUs idle -- the
+    TP-shard projections (TP = 8 at SmolLM-1.7B: the q|k|v forward 4096 x 768 is 48 tiles of
+    256x256, the o_proj dX 4096 x 256 only 16): K-slices of the phased 256x256 (256x128 when N only
+    tiles by 128) kernel, the largest power of two that keeps the launch within one round of the
+    256 CUs and every slice >= 256 deep, summed by pt_gemm_splitk_reduce through the GEMM's own
+    epilogue (bf16 store / residual add).  The small-tile kernels the unsplit launch would take
+    (128x128, 64x64) run at a third of the phased rate per CU.  (1, -1) = unsplit."""
+    if not _ksplit_enabled() or M % 256 or M < 2048 or K < 1024:
+        return 1, -1
+    if N % 256 == 0:
+        tile, tiles = 12, (M // 256) * (N // 256)
+    elif N % 128 == 0:
+        tile, tiles = 13, (M // 256) * (N // 128)
+    else:
+        return 1, -1
+    if tiles >= 96:
+        return 1, -1
+    s = 1
+    while s < 16 and tiles * s * 2 <= 256 and K % (s * 2 * 64) == 0 and K // (s * 2) >= 256:
+        s *= 2
+    return (s, tile) if s > 1 else (1, -1)
+
+
+def _gemm_ksplit(A, lda, a_kcontig, Bs, ldbs, b_bounds, b_kcontig, b_seg_dim, out, M, N, K, s, tile, epilogue,
+                 residual=None, ldr=0):
+    """C = A . B as s K-slices into f32 partials (one grouped launch of `tile`), then the reduce
+    pass through `epilogue` (EPI_BF16 / EPI_BF16_ACC / EPI_BF16_RES) into out [M, N]."""
+    dev = A.device
+    ws = torch.empty(s * M * N, dtype=torch.float32, device=dev)
+    probs = (_C.GemmProblem * 1)()
+    pr = _problem(A, lda, Bs, ldbs, b_bounds, b_seg_dim, [ws], [N], [0, M], M, N, K)
+    pr.ksplit, pr.kpart_stride = s, M * N
+    probs[0] = pr
+    probe = _PROBE
+    if probe is not None:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    stream = _C.stream_ptr(dev)
+    rc = _C.lib().pt_gemm_grouped(probs, 1, int(a_kcontig), int(b_kcontig), EPI_F32, int(tile), stream)
+    _C.check(rc, f"pt_gemm_grouped(M={M}, N={N}, K={K}, split-K {s}, tile {tile})")
+    rc = _C.lib().pt_gemm_splitk_reduce(_ptr(ws), s, M * N, M, N, _C.ptrarr([_ptr(out)]), _C.i64arr([out.stride(0)]),
+                                        _C.i64arr([0, M]), 1, int(epilogue), _ptr(residual), int(ldr), stream)
+    _C.check(rc, "pt_gemm_splitk_reduce")
+    if probe is not None:
+        ev1.record()
+        probe.records.append((ev0, ev1, 2.0 * M * N * K, _alg_bytes(M, N, K, epilogue), f"gemm {M}x{N}x{K} ks{s}"))
+    return out
+
+
 def _wgrad_ksplit_run(jobs, epilogue, s):
     """The wgrad jobs [(dy2d, x2d, outs)] as s-way split-K problems of ONE grouped launch (f32
     partials in one workspace), then one reduce pass per job into its outs through `epilogue`."""
@@ -652,6 +702,11 @@ def linear_fwd(x2d, weights, out=None, tile=-1, residual=None):
         h = _splitk_halves(T, N, K)
         if h is not None:
             return _linear_fwd_splitk(x2d, weights, h, y, residual)
+    if tile < 0 and y.stride(0) % 4 == 0:
+        s, t = fewtile_ksplit(T, N, K)
+        if s > 1 and all(n % (256 if t == 12 else 128) == 0 for n in ns):
+            return _gemm_ksplit(x2d, x2d.stride(0), 1, weights, [K] * len(weights), _bounds(ns), 1, 0, y, T, N, K, s, t,
+                                epi, residual=residual, ldr=ldr)
     _gemm(x2d, x2d.stride(0), 1, weights, [K] * len(weights), _bounds(ns), 1, 0, [y], [y.stride(0)], [0, T],
           T, N, K, epi, tile, residual=residual, ldr=ldr)
     return y
@@ -904,6 +959,11 @@ def linear_dgrad(dy2d, weights, out=None, accumulate=False, tile=-1):
                 all(n % 64 == 0 for n in ns):
             return _linear_dgrad_splitk(dy2d, weights, h, torch.empty(T, Kin, dtype=BF16, device=dy2d.device))
     dx = out if out is not None else torch.empty(T, Kin, dtype=BF16, device=dy2d.device)
+    if tile < 0 and dx.stride(1) == 1 and dx.stride(0) % 4 == 0:
+        s, t = fewtile_ksplit(T, Kin, N)
+        if s > 1 and all(n % 64 == 0 for n in ns):
+            return _gemm_ksplit(dy2d, dy2d.stride(0), 1, weights, [Kin] * len(weights), _bounds(ns), 0, 1, dx, T, Kin,
+                                N, s, t, EPI_BF16_ACC if accumulate else EPI_BF16)
     _gemm(dy2d, dy2d.stride(0), 1, weights, [Kin] * len(weights), _bounds(ns), 0, 1, [dx], [dx.stride(0)],
           [0, T], T, Kin, N, EPI_BF16_ACC if accumulate else EPI_BF16, tile)
     return dx

@@ -400,13 +400,13 @@ def g12_all(ref):
 G11_STEPS, G11_GA, G11_MBS, G11_LR = 50, 2, 2, 1e-3
 
 
-def _g11_data():
+def _g11_data(seq=None):
     """[steps, dp 2, ga, mbs, seq + 1] uint8 tokens (seed 2468): a FRESH batch every step, drawn from
     a fixed sparse bigram process (each token has 4 successors with probabilities .55 / .25 / .15 /
     .05, about 1.1 nats of entropy) -- learnable structure, so the 50-step loss falls from ln 256 =
     5.5 towards ~1.1 like a real run instead of memorising one batch."""
     g = torch.Generator().manual_seed(2468)
-    V, S = G10M_CFG["vocab_size"], G10M_CFG["max_position_embeddings"]
+    V, S = G10M_CFG["vocab_size"], seq or G10M_CFG["max_position_embeddings"]
     succ = torch.randint(0, V, (V, 4), generator=g)
     n = G11_STEPS * 2 * G11_GA * G11_MBS
     choice = torch.multinomial(torch.tensor([0.55, 0.25, 0.15, 0.05]).expand(n, 4), S, replacement=True,
@@ -418,7 +418,7 @@ def _g11_data():
     return seq.view(G11_STEPS, 2, G11_GA, G11_MBS, S + 1).to(torch.uint8)
 
 
-def g11_curve(rank, world, tp, cp, dp, dtype=torch.bfloat16):
+def g11_curve(rank, world, tp, cp, dp, dtype=torch.bfloat16, seq=None):
     """G11: north_star's "loss curve within 1 % over 50 steps", pinned by the reference itself:
     train.py's loop (train_step 29-55, the step loop 219-240) on gloo/CPU, FLASH_ATTEN=0, in the
     reference's GPU training precision (train.py:76,190: the model and so AdamW's states in bf16,
@@ -437,7 +437,7 @@ def g11_curve(rank, world, tp, cp, dp, dtype=torch.bfloat16):
     from picotron.data_parallel.data_parallel import DataParallelBucket
     from picotron.tensor_parallel.tensor_parallel import apply_tensor_parallel
     from picotron.utils import average_loss_across_dp_cp_ranks
-    cfg = types.SimpleNamespace(**G10M_CFG)
+    cfg = types.SimpleNamespace(**dict(G10M_CFG, max_position_embeddings=seq or G10M_CFG["max_position_embeddings"]))
     torch.set_num_threads(max(1, 8 // world))
     torch.manual_seed(7)
     model = M.Llama(cfg)
@@ -455,8 +455,8 @@ def g11_curve(rank, world, tp, cp, dp, dtype=torch.bfloat16):
     if dp > 1:
         model = DataParallelBucket(model)
     opt = torch.optim.AdamW(model.parameters(), lr=G11_LR)
-    ids = _g11_data()
-    S, V = G10M_CFG["max_position_embeddings"], G10M_CFG["vocab_size"]
+    ids = _g11_data(seq)
+    S, V = cfg.max_position_embeddings, G10M_CFG["vocab_size"]
     sl = slice(m.cp_rank * S // cp, (m.cp_rank + 1) * S // cp)
     losses = []
     for step in range(G11_STEPS):
@@ -489,6 +489,9 @@ def g10m_pp_all(ref):
 
 def g11_all(ref, dtypes=("bf16", "f32")):
     import functools
+    # cp2 at seq 512: 256 tokens per rank, the shard length from which the build runs its zig-zag
+    # (load-balanced) ring with the zig-zag residual layout -- that schedule against the reference
+    _run_dist(functools.partial(g11_curve, tp=1, cp=2, dp=1, dtype=torch.bfloat16, seq=512), 2, ref, "G11_cp2s512")
     for tag in dtypes:
         dt = torch.bfloat16 if tag == "bf16" else torch.float32
         for name, (tp, cp, dp) in (("1", (1, 1, 1)), ("tp2", (2, 1, 1)), ("cp2", (1, 2, 1)), ("dp2", (1, 1, 2))):
@@ -499,8 +502,15 @@ def g11_all(ref, dtypes=("bf16", "f32")):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
-    ap.add_argument("--only", choices=["G11", "G11bf16", "G10m_pp", "G12"], help="regenerate only these fixtures")
+    ap.add_argument("--only", choices=["G11", "G11bf16", "G11s512", "G10m_pp", "G12"],
+                    help="regenerate only these fixtures")
     args = ap.parse_args()
+    if args.only == "G11s512":
+        import functools
+        _run_dist(functools.partial(g11_curve, tp=1, cp=2, dp=1, dtype=torch.bfloat16, seq=512), 2, args.ref,
+                  "G11_cp2s512")
+        print("wrote G11_cp2s512")
+        return
     if args.only == "G12":
         g12_all(args.ref)
         print("wrote G12 fixtures")

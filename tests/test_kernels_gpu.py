@@ -910,3 +910,32 @@ def test_cross_entropy_mean_kernel():
         assert abs(loss.float().item() - ref) <= (1e-6 if dt == torch.float32 else 2 ** -8) * ref
     loss, _ = K._ce_mean(torch.zeros_like(rl), torch.full_like(tg, -100), -100, torch.float32)  # rows all 0
     assert math.isnan(loss.item())
+
+
+@pytest.mark.parametrize("M,N,K,kind,residual", [(4096, 768, 2048, "fwd", False), (4096, 256, 2048, "dgrad", False),
+                                                 (4096, 512, 2048, "fwd", True), (2048, 384, 1024, "fwd", False)])
+def test_fewtile_splitk_matches_single_pass(monkeypatch, M, N, K, kind, residual):
+    """The TP-shard forward / dX GEMMs whose tiles leave most CUs idle (SmolLM-1.7B at TP = 8: the
+    q|k|v forward 4096 x 768 x 2048, the o_proj dX 4096 x 256 x 2048) run as K-slices of the phased
+    kernel + the reduce pass (kernels.fewtile_ksplit): against an f32 reference and the unsplit
+    launch (PICOTRON_KSPLIT=0), equal up to the f32 summation order (<= 2 bf16 ulps)."""
+    from picotron_amd import kernels as K_
+    s, t = K_.fewtile_ksplit(M, N, K)
+    assert s > 1, (M, N, K)
+    if kind == "fwd":
+        x = torch.randn(M, K).to(BF).to(DEV)
+        ws = [(torch.randn(n, K) / math.sqrt(K)).to(BF).to(DEV) for n in (N // 2, N // 2)]
+        r = torch.randn(M, N).to(BF).to(DEV) if residual else None
+        run = lambda: K_.linear_fwd(x, ws, residual=r)  # noqa: E731
+        ref = x.float() @ torch.cat(ws).float().t() + (r.float() if residual else 0)
+    else:
+        dy = torch.randn(M, K).to(BF).to(DEV)
+        w = (torch.randn(K, N) / math.sqrt(K)).to(BF).to(DEV)
+        run = lambda: K_.linear_dgrad(dy, [w])  # noqa: E731
+        ref = dy.float() @ w.float()
+    y = run()
+    monkeypatch.setattr(switches.S, "ksplit", 0)
+    y1 = run()
+    torch.cuda.synchronize()
+    assert rel_err(y, ref) < 4e-3
+    assert maxabs(y, y1) <= 2 * y1.float().abs().max().item() * 2 ** -8

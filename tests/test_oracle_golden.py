@@ -224,6 +224,16 @@ def test_g11_fixtures_are_reference_50_step_curves(prec):
     assert (curves["tp2"] - curves["1"]).abs().max().item() < (1e-3 if prec == "G11f32" else 0.05)
 
 
+def test_g11_cp2_seq512_fixture_is_a_reference_curve():
+    """G11_cp2s512 (make_golden.g11_curve at seq 512, cp2, bf16): the reference's ring over 256-token
+    shards -- 50 finite losses, the logged value identical on both ranks, falling like G11_cp2."""
+    g = load("G11_cp2s512")
+    l0 = g["rank0.losses"]
+    assert l0.numel() == 50 and torch.isfinite(l0).all() and torch.equal(l0, g["rank1.losses"])
+    assert abs(l0[0].item() - math.log(256)) < 0.3 and l0[-1].item() < 0.45 * l0[0].item()
+    assert tuple(g["rank0.ids"].shape) == (50, 2, 2, 2, 513)
+
+
 def test_oracle_reproduces_g11_first_steps():
     """G11f32_1: the oracle's fp32 train step (llama_forward + CE / grad_acc + torch AdamW lr 1e-3) on G11_1's
     token stream from G10m's initial weights reproduces the reference's first 3 logged losses."""
