@@ -209,6 +209,25 @@ typedef struct {
 int pt_gemm_grouped(const pt_gemm_problem* probs, int nprob, int a_kcontig, int b_kcontig, int epilogue, int tile,
                     hipStream_t stream);
 
+/* pt_gemm_grouped's split-K problems (ksplit > 1; C = one f32 partials buffer [ksplit][M][N], ld N,
+ * kpart_stride apart) finished INSIDE the launch: the workgroup that completes a tile -- the last of
+ * its ksplit slices to arrive at the tile's counter -- sums the tile's partials in slice order and
+ * writes sinks[i] through `mode` (0 bf16 store, 1 bf16 accumulate, 3 f32 accumulate, 4 bf16
+ * residual add); no workgroup waits for another.  Replaces the grouped launch + pt_gemm_splitk_reduce
+ * pair (same results, bit for bit).  counters: int32, zero on entry, >= sum over problems of
+ * (M / 64) (N / 64) of them; the kernel leaves them zero.  N % 4 == 0. */
+typedef struct {
+  void* C[4];
+  int64_t ldc[4];
+  int64_t c_bounds[5];     /* nc + 1 row boundaries of the sink's segments */
+  int nc;
+  int mode;
+  const void* residual;    /* mode 4: [M, N] bf16, ld ldr */
+  int64_t ldr;
+} pt_splitk_sink;
+int pt_gemm_splitk_fused(const pt_gemm_problem* probs, int nprob, int a_kcontig, int b_kcontig, int tile,
+                         const pt_splitk_sink* sinks, int* counters, int64_t ncounters, hipStream_t stream);
+
 /* Two independent groups in ONE launch of 256x256 tiles, each with its own layouts and epilogue:
  * group 0 = dX (A = dY [M, K] K-contiguous, B = W [K, N] N-contiguous; epilogue 0 or 6 = the
  * SwiGLU backward, residual = g|u), group 1 = wgrad (dY^T X; both operands MN-contiguous;

@@ -5,6 +5,7 @@ Every function here runs the gfx950 kernels and nothing else; there is no CPU or
 fallback.  Shapes/dtypes/strides are validated in Python before the call, as the reference
 validates with asserts (e.g. picotron/model.py:95-96, tensor_parallel.py:81,151,226).
 """
+import ctypes
 import math
 
 import sys
@@ -597,16 +598,58 @@ def _gemm_ksplit(A, lda, a_kcontig, Bs, ldbs, b_bounds, b_kcontig, b_seg_dim, ou
     if probe is not None:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
-    stream = _C.stream_ptr(dev)
-    rc = _C.lib().pt_gemm_grouped(probs, 1, int(a_kcontig), int(b_kcontig), EPI_F32, int(tile), stream)
-    _C.check(rc, f"pt_gemm_grouped(M={M}, N={N}, K={K}, split-K {s}, tile {tile})")
-    rc = _C.lib().pt_gemm_splitk_reduce(_ptr(ws), s, M * N, M, N, _C.ptrarr([_ptr(out)]), _C.i64arr([out.stride(0)]),
-                                        _C.i64arr([0, M]), 1, int(epilogue), _ptr(residual), int(ldr), stream)
-    _C.check(rc, "pt_gemm_splitk_reduce")
+    _ksplit_launch(probs, 1, a_kcontig, b_kcontig, tile, [_sink([out], [0, M], epilogue, residual, ldr)], dev)
     if probe is not None:
         ev1.record()
         probe.records.append((ev0, ev1, 2.0 * M * N * K, _alg_bytes(M, N, K, epilogue), f"gemm {M}x{N}x{K} ks{s}"))
     return out
+
+
+_KCOUNT = {}
+_KCOUNT_N = 1 << 17
+
+
+def _kcounters(dev):
+    """The split-K arrival counters of pt_gemm_splitk_fused on `dev` (zero; every launch leaves them
+    zero): one int32 per potential 64x64 tile of a launch's problems."""
+    key = (dev.type, dev.index)
+    if key not in _KCOUNT:
+        _KCOUNT[key] = torch.zeros(_KCOUNT_N, dtype=torch.int32, device=dev)
+    return _KCOUNT[key]
+
+
+def _sink(outs, bounds, mode, residual=None, ldr=0):
+    sk = _C.SplitkSink()
+    for i, o in enumerate(outs):
+        sk.C[i], sk.ldc[i] = _ptr(o), int(o.stride(0))
+    for i, v in enumerate(bounds):
+        sk.c_bounds[i] = int(v)
+    sk.nc, sk.mode = len(outs), int(mode)
+    sk.residual, sk.ldr = _ptr(residual), int(ldr)
+    return sk
+
+
+def _ksplit_launch(probs, n, a_kcontig, b_kcontig, tile, sinks, dev):
+    """The split-K problems finished in-kernel (pt_gemm_splitk_fused) -- or, with ksplit_fused = 0,
+    the grouped launch + one reduce pass per problem (A/B)."""
+    stream = _C.stream_ptr(dev)
+    if SW.ksplit_fused:
+        cnt = _kcounters(dev)
+        arr = (_C.SplitkSink * n)(*sinks)
+        rc = _C.lib().pt_gemm_splitk_fused(probs, n, int(a_kcontig), int(b_kcontig), int(tile), arr, _ptr(cnt),
+                                           cnt.numel(), stream)
+        _C.check(rc, f"pt_gemm_splitk_fused({n} problems, split-K {probs[0].ksplit})")
+        return
+    rc = _C.lib().pt_gemm_grouped(probs, n, int(a_kcontig), int(b_kcontig), EPI_F32, int(tile), stream)
+    _C.check(rc, f"pt_gemm_grouped({n} problems, split-K {probs[0].ksplit})")
+    for j in range(n):
+        pr, sk = probs[j], sinks[j]
+        rc = _C.lib().pt_gemm_splitk_reduce(ctypes.c_void_p(pr.C[0]), pr.ksplit, pr.kpart_stride, pr.M, pr.N,
+                                            _C.ptrarr([sk.C[i] or 0 for i in range(sk.nc)]),
+                                            _C.i64arr([sk.ldc[i] for i in range(sk.nc)]),
+                                            _C.i64arr([sk.c_bounds[i] for i in range(sk.nc + 1)]), sk.nc, sk.mode,
+                                            ctypes.c_void_p(sk.residual), sk.ldr, stream)
+        _C.check(rc, "pt_gemm_splitk_reduce")
 
 
 def _wgrad_ksplit_run(jobs, epilogue, s):
@@ -634,16 +677,8 @@ def _wgrad_ksplit_run(jobs, epilogue, s):
     if probe is not None:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
-    stream = _C.stream_ptr(dev)
-    rc = _C.lib().pt_gemm_grouped(probs, len(jobs), 0, 0, EPI_F32, -1, stream)
-    _C.check(rc, f"pt_gemm_grouped({len(jobs)} problems, split-K {s})")
-    for (dy2d, x2d, outs), part in zip(jobs, views):
-        N, Kin = dy2d.shape[1], x2d.shape[1]
-        ns = [o.shape[0] for o in outs]
-        rc = _C.lib().pt_gemm_splitk_reduce(_ptr(part), s, N * Kin, N, Kin, _C.ptrarr([_ptr(o) for o in outs]),
-                                            _C.i64arr([o.stride(0) for o in outs]), _C.i64arr(_bounds(ns)), len(outs),
-                                            int(epilogue), None, 0, stream)
-        _C.check(rc, "pt_gemm_splitk_reduce")
+    sinks = [_sink(outs, _bounds([o.shape[0] for o in outs]), epilogue) for _, _, outs in jobs]
+    _ksplit_launch(probs, len(jobs), 0, 0, -1, sinks, dev)
     if probe is not None:
         ev1.record()
         probe.records.append((ev0, ev1, flops, nbytes, sys._getframe().f_code.co_name))
