@@ -445,13 +445,13 @@ def attn_block_bwd(da, h2, saved, wq, wk, wv, wo, cos, sin, sh, tp, need_dx=True
     scale = 1.0 / math.sqrt(sh.d)
     do2 = K.linear_dgrad(da, [wo])
     dqkv = attention_core_bwd(do2.view(sh.B, sh.S, sh.nh, sh.d), qkv, o, lse, sh, cos, sin, scale)
-    if need_dx and keep_parts and tp.world_size == 1 and _dual_qkv_enabled():
+    if need_dx and tp.world_size == 1 and _dual_qkv_enabled():
         # tp = 1 (no all-reduce to overlap): the q|k|v dX as two split-K halves (128 + 128 tiles of
-        # 256x256, summed by the input norm's backward) in ONE launch with the q|k|v and o_proj dW
-        # (192 + 64 tiles): 512 tiles = 2 whole rounds of the 256 CUs instead of a 128-tile dX launch
-        # and a 256-tile dW launch
+        # 256x256, summed by the input norm's backward -- or by the sum pass without keep_parts) in
+        # ONE launch with the q|k|v and o_proj dW (192 + 64 tiles): 512 tiles = 2 whole rounds of the
+        # 256 CUs instead of a 128-tile dX launch and a 256-tile dW launch
         return dgrad_with_wgrad(dqkv, [wq, wk, wv], [(dqkv, h2, [wq, wk, wv]), (da, o.view(sh.T, sh.wq), [wo])],
-                                keep_parts=True, split_min=1024)
+                                keep_parts=keep_parts, split_min=1024)
     dh = handle = None
     if need_dx:
         dh = K.linear_dgrad(dqkv, [wq, wk, wv])

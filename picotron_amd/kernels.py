@@ -1074,6 +1074,12 @@ def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None, keep
     dx_tiles = sum(p.M // 256 * (p.N // 256) for p in p0s)
     ws = wgrad_ksplit([(dy.shape[1], x.shape[1], dy.shape[0]) for dy, x, _ in wjobs], extra_tiles=dx_tiles) \
         if wepilogue in (EPI_BF16, EPI_BF16_ACC, EPI_F32_ACC) else 1
+    # the reduce pass writes 16-B (f32) / 8-B (bf16) row chunks: a sink it cannot address that way (a
+    # misaligned .grad / main_grad view) keeps the unsplit dW, decided before anything is launched
+    if ws > 1 and not all(o.stride(1) == 1 and o.stride(0) % 4 == 0 and
+                          o.data_ptr() % (16 if o.dtype == torch.float32 else 8) == 0
+                          for _, _, outs in wjobs for o in outs):
+        ws = 1
     wparts = []
     for j, (wdy, x2d, outs) in enumerate(wjobs):
         _bf16_rowmajor(wdy, "dy")

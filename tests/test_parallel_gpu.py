@@ -74,9 +74,14 @@ def _setup(tp, cp, seq=256):
     return m, model, names, pf, ids, lo, loss_r
 
 
-def _llama(rank, world, tp, cp, seq=256, zigzag=False, residual=1, mesh=1):
+def _llama(rank, world, tp, cp, seq=256, zigzag=False, residual=1, mesh=1, production_thresholds=False):
     from picotron_amd import switches
-    with switches.override(zigzag_residual=residual, ring_mesh=mesh):
+    # conftest.py zeroes the RoPE / SwiGLU fusion tile thresholds for the small test shapes;
+    # production_thresholds restores the shipped ones (96 / 192 / 0), under which these TP-shard
+    # widths take the split (GEMM + separate rope / swiglu kernel) paths
+    thr = dict(rope_fuse_min_tiles=96, swiglu_fuse_min_tiles=192, swiglu_bwd_min_tiles=0) \
+        if production_thresholds else {}
+    with switches.override(zigzag_residual=residual, ring_mesh=mesh, **thr):
         _llama_body(rank, world, tp, cp, seq, zigzag, residual)
 
 
@@ -130,6 +135,11 @@ def _llama_body(rank, world, tp, cp, seq, zigzag, residual):
 
 def test_tensor_parallel_llama_tp2():
     _dist.run(_llama, 2, 2, 1, device="cuda")
+
+
+def test_tensor_parallel_llama_tp2_production_thresholds():
+    """tp2 with the shipped fusion thresholds: the split RoPE / SwiGLU paths of narrow TP shards."""
+    _dist.run(_llama, 2, 2, 1, 256, False, 1, 1, True, device="cuda")
 
 
 def test_context_parallel_llama_cp2():
