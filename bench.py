@@ -187,7 +187,8 @@ def cp_proxy(args, base, layers):
                  the diagonal block's backward, then each fp32 dK|dV partial sent straight to its
                  owner (one transfer per link, the largest a full shard's 2 x bf16 bytes);
       re-lay     the residual stream's zig-zag re-lay, twice per forward and twice per backward for
-                 the whole stack (apply_context_parallel), amortised per layer."""
+                 the whole stack (context_parallel.enable_zigzag_residual: on with the cp gradient
+                 averaging of DataParallelBucket), amortised per layer."""
     import math
     from picotron_amd import functional as FN
     from picotron_amd import kernels as K

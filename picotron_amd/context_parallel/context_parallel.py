@@ -25,8 +25,9 @@ What differs (MI355X-first):
     keys) otherwise -- and the outputs / gradients are re-laid back.  The external contract (rank r
     holds tokens [r S, (r + 1) S), data.py:105-109, update_rope_for_context_parallel) is unchanged.
     PICOTRON_RING_ZIGZAG=0 runs the reference's schedule instead (A/B only);
-  * the residual stream stays in the zig-zag layout across the whole decoder stack: every op
-    outside attention is token-local, so apply_context_parallel re-lays the embedding's output once
+  * the residual stream stays in the zig-zag layout across the whole decoder stack wherever the
+    gradients are averaged over the cp group (enable_zigzag_residual, called by the data-parallel
+    wrappers): every op outside attention is token-local, so the embedding's output is re-laid once
     on entry and the final norm's input once on exit (ZigzagRelayout, gradients the inverse way),
     and the decoder layers run on zig-zag shards with zig-zag RoPE tables -- two exchanges of
     [B, S, H] per forward instead of three (q, K|V, o) per layer (PICOTRON_ZIGZAG_RESIDUAL=0: the
@@ -51,32 +52,44 @@ from .cp_communications import ContextCommunicate, zigzag_exchange
 
 
 def apply_context_parallel(model):
-    """context_parallel.py:10-12 (sets CONTEXT_PARALLEL) plus, at cp > 1, the zig-zag residual
-    layout: the decoder layers of `model` (a Llama or a pipeline stage) are marked to run on zig-zag
-    shards, the embedding module's output is re-laid into that layout and the final norm's input
-    back out of it (forward hooks, so any container -- Llama.forward, either PipelineParallel --
-    keeps calling the modules unchanged; the returned logits are the rank's contiguous tokens).
-    Whether a given batch uses the layout is decided per call from its local sequence length
-    (zigzag_enabled), identically at the entry, in every layer and at the exit."""
-    cp = pgm.current().cp_world_size
-    os.environ["CONTEXT_PARALLEL"] = "1" if cp > 1 else "0"
-    if cp > 1 and SW.zigzag_residual != 0 and not getattr(model, "_pt_zigzag_residual", False):
-        from ..model import DecoderLayer
-        tables = {}
-        for name, mod in model.named_modules():
-            leaf = name.rsplit(".", 1)[-1]
-            if isinstance(mod, DecoderLayer):
-                key = mod._rope_args
-                if key not in tables:
-                    tables[key] = zigzag_rope_tables(*key)
-                mod.zz_cos, mod.zz_sin = tables[key]
-                mod.cp_zigzag_residual = True
-            elif leaf == "embedding" and not isinstance(mod, torch.nn.Identity):
-                mod.register_forward_hook(_zz_entry_hook)
-            elif leaf == "final_norm" and not isinstance(mod, torch.nn.Identity):
-                mod.register_forward_pre_hook(_zz_exit_hook)
-        model._pt_zigzag_residual = True
+    """context_parallel.py:10-12: sets CONTEXT_PARALLEL (read by every attention call)."""
+    os.environ["CONTEXT_PARALLEL"] = "1" if pgm.current().cp_world_size > 1 else "0"
     return model
+
+
+def enable_zigzag_residual(model):
+    """Keep the residual stream of `model` (a Llama or a pipeline stage) in the zig-zag layout
+    across its decoder stack at cp > 1: the decoder layers run on zig-zag shards (with their
+    positions' RoPE tables), the embedding module's output is re-laid into the layout and the final
+    norm's input back out of it -- forward hooks, so any container (Llama.forward, either
+    PipelineParallel) calls the modules unchanged and the logits stay the rank's contiguous tokens.
+    Whether a batch uses the layout is decided per call from its local sequence length
+    (zigzag_enabled), identically at the entry, in every layer and at the exit.
+
+    The layout moves which tokens' weight-gradient contributions each cp rank holds (the sum over
+    the cp group is unchanged), so it is enabled by the gradient averaging over cp_dp_group --
+    DataParallelBucket / DataParallelNaive call this -- and not by apply_context_parallel: the
+    reference's train.py wraps a data-parallel module only for dp > 1 (train.py:194-195), and at
+    cp > 1 / dp = 1 each cp rank then steps on its own chunk's gradient, which the per-layer re-lay
+    inside the ring reproduces exactly.  Returns True when enabled."""
+    if pgm.current().cp_world_size == 1 or SW.zigzag_residual == 0 or getattr(model, "_pt_zigzag_residual", False):
+        return getattr(model, "_pt_zigzag_residual", False)
+    from ..model import DecoderLayer
+    tables = {}
+    for name, mod in model.named_modules():
+        leaf = name.rsplit(".", 1)[-1]
+        if isinstance(mod, DecoderLayer):
+            key = mod._rope_args
+            if key not in tables:
+                tables[key] = zigzag_rope_tables(*key)
+            mod.zz_cos, mod.zz_sin = tables[key]
+            mod.cp_zigzag_residual = True
+        elif leaf == "embedding" and not isinstance(mod, torch.nn.Identity):
+            mod.register_forward_hook(_zz_entry_hook)
+        elif leaf == "final_norm" and not isinstance(mod, torch.nn.Identity):
+            mod.register_forward_pre_hook(_zz_exit_hook)
+    model._pt_zigzag_residual = True
+    return True
 
 
 class ZigzagRelayout(torch.autograd.Function):

@@ -25,6 +25,14 @@ from .. import process_group_manager as pgm
 from .bucket import BucketManager
 
 
+def _cp_averaged(module):
+    """The wrapper averages gradients over cp_dp_group, cp ranks included: the residual stream of a
+    context-parallel model may then stay in the zig-zag layout (context_parallel.enable_zigzag_residual)."""
+    if pgm.current().cp_world_size > 1:
+        from ..context_parallel.context_parallel import enable_zigzag_residual
+        enable_zigzag_residual(module)
+
+
 class DataParallelNaive(nn.Module):
     """data_parallel.py:10-60: all-reduce (mean over cp_dp_group) every parameter's gradient once it
     is final for the backward.  Two triggers, as in DataParallelBucket: autograd's post-accumulate
@@ -37,6 +45,7 @@ class DataParallelNaive(nn.Module):
         super().__init__()
         self.module = module
         self.require_backward_grad_sync = True
+        _cp_averaged(module)
         for p in self.module.parameters():
             if p.requires_grad:
                 p.register_post_accumulate_grad_hook(self._allreduce_grads)
@@ -67,6 +76,7 @@ class DataParallelBucket(nn.Module):
         bucket_size = bucket_cap_mb * 1024 * 1024 // grad_size
         self.bucket_manager = BucketManager(module.parameters(), pgm.current().cp_dp_group, bucket_size, grad_type)
         self.register_backward_hook()
+        _cp_averaged(module)
         self._post_backward_callback_set = False
 
     def forward(self, *inputs, **kwargs):

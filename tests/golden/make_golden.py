@@ -418,7 +418,7 @@ def _g11_data(seq=None):
     return seq.view(G11_STEPS, 2, G11_GA, G11_MBS, S + 1).to(torch.uint8)
 
 
-def g11_curve(rank, world, tp, cp, dp, dtype=torch.bfloat16, seq=None):
+def g11_curve(rank, world, tp, cp, dp, dtype=torch.bfloat16, seq=None, avg=False):
     """G11: north_star's "loss curve within 1 % over 50 steps", pinned by the reference itself:
     train.py's loop (train_step 29-55, the step loop 219-240) on gloo/CPU, FLASH_ATTEN=0, in the
     reference's GPU training precision (train.py:76,190: the model and so AdamW's states in bf16,
@@ -452,7 +452,7 @@ def g11_curve(rank, world, tp, cp, dp, dtype=torch.bfloat16, seq=None):
         for n, p in model.named_parameters():
             p.copy_(_g10m_shard(full[n], p, m.tp_rank))
     model = model.to(dtype)            # train.py:190
-    if dp > 1:
+    if dp > 1 or avg:                  # avg: the reference's own DataParallelBucket over cp_dp at dp 1
         model = DataParallelBucket(model)
     opt = torch.optim.AdamW(model.parameters(), lr=G11_LR)
     ids = _g11_data(seq)
@@ -492,6 +492,10 @@ def g11_all(ref, dtypes=("bf16", "f32")):
     # cp2 at seq 512: 256 tokens per rank, the shard length from which the build runs its zig-zag
     # (load-balanced) ring with the zig-zag residual layout -- that schedule against the reference
     _run_dist(functools.partial(g11_curve, tp=1, cp=2, dp=1, dtype=torch.bfloat16, seq=512), 2, ref, "G11_cp2s512")
+    # ... and with the cp ranks' gradients averaged (the reference's DataParallelBucket over cp_dp_group,
+    # which its train.py applies only for dp > 1): the build then keeps its residual stream zig-zag
+    _run_dist(functools.partial(g11_curve, tp=1, cp=2, dp=1, dtype=torch.bfloat16, seq=512, avg=True), 2, ref,
+              "G11_cp2s512avg")
     for tag in dtypes:
         dt = torch.bfloat16 if tag == "bf16" else torch.float32
         for name, (tp, cp, dp) in (("1", (1, 1, 1)), ("tp2", (2, 1, 1)), ("cp2", (1, 2, 1)), ("dp2", (1, 1, 2))):
@@ -509,7 +513,9 @@ def main():
         import functools
         _run_dist(functools.partial(g11_curve, tp=1, cp=2, dp=1, dtype=torch.bfloat16, seq=512), 2, args.ref,
                   "G11_cp2s512")
-        print("wrote G11_cp2s512")
+        _run_dist(functools.partial(g11_curve, tp=1, cp=2, dp=1, dtype=torch.bfloat16, seq=512, avg=True), 2,
+                  args.ref, "G11_cp2s512avg")
+        print("wrote G11_cp2s512, G11_cp2s512avg")
         return
     if args.only == "G12":
         g12_all(args.ref)

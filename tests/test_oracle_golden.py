@@ -224,10 +224,12 @@ def test_g11_fixtures_are_reference_50_step_curves(prec):
     assert (curves["tp2"] - curves["1"]).abs().max().item() < (1e-3 if prec == "G11f32" else 0.05)
 
 
-def test_g11_cp2_seq512_fixture_is_a_reference_curve():
-    """G11_cp2s512 (make_golden.g11_curve at seq 512, cp2, bf16): the reference's ring over 256-token
-    shards -- 50 finite losses, the logged value identical on both ranks, falling like G11_cp2."""
-    g = load("G11_cp2s512")
+@pytest.mark.parametrize("name", ["G11_cp2s512", "G11_cp2s512avg"])
+def test_g11_cp2_seq512_fixture_is_a_reference_curve(name):
+    """G11_cp2s512(avg) (make_golden.g11_curve at seq 512, cp2, bf16; avg: the cp ranks' gradients
+    averaged by the reference's DataParallelBucket): the reference's ring over 256-token shards -- 50
+    finite losses, the logged value identical on both ranks, falling like G11_cp2."""
+    g = load(name)
     l0 = g["rank0.losses"]
     assert l0.numel() == 50 and torch.isfinite(l0).all() and torch.equal(l0, g["rank1.losses"])
     assert abs(l0[0].item() - math.log(256)) < 0.3 and l0[-1].item() < 0.45 * l0[0].item()

@@ -311,7 +311,7 @@ def test_zigzag_ring_is_balanced_and_exact(world, nh, nkv, mesh):
 
 
 def _zz_residual(rank, world):
-    """The zig-zag residual stream's pieces (context_parallel.apply_context_parallel): the re-lay is
+    """The zig-zag residual stream's pieces (context_parallel.enable_zigzag_residual): the re-lay is
     a permutation whose backward is the inverse permutation of the gradient, and the zig-zag RoPE
     tables are get_cos_sin's rows at the positions of the rank's zig-zag shard."""
     from picotron_amd import process_group_manager as pgm

@@ -89,6 +89,8 @@ def _llama_body(rank, world, tp, cp, seq, zigzag, residual):
     from picotron_amd import functional as FN
     from picotron_amd.context_parallel import context_parallel as CP
     m, model, names, pf, ids, lo, loss_r = _setup(tp, cp, seq)
+    if residual:   # what the data-parallel wrappers do at cp > 1 (the grads are checked summed over cp)
+        CP.enable_zigzag_residual(model)
     s = seq // cp
     assert CP.zigzag_enabled(s, True) == zigzag   # which ring schedule this case exercises
     sl = slice(m.cp_rank * s, (m.cp_rank + 1) * s)                # data.py:105-109: contiguous chunks
