@@ -349,6 +349,45 @@ def launch_ranks(argv, nproc):
     return rc
 
 
+def assemble_report(args, model, m, cfg, num_params, rank, world, result_out):
+    """--assemble-only: every rank reports its grid coordinates (process_group_manager.py:13: view(dp,
+    pp, cp, tp)), its shard (parameters held, pipeline layers, embedding / lm_head presence), the
+    zig-zag residual flag and the bucket count; rank 0 checks the grid covers every coordinate once
+    and that the ranks of one tp group hold equal shard sizes, then prints ONE JSON line."""
+    inner = model.module if hasattr(model, "bucket_manager") else model
+    names = [n for n, _ in inner.named_parameters()]
+    me = {"rank": rank, "grid": [m.dp_rank, m.pp_rank, m.cp_rank, m.tp_rank],
+          "params": sum(p.numel() for p in inner.parameters()),
+          "layers": sorted({int(n.split(".")[1]) for n in names if n.startswith("decoder_layers.")}),
+          "embedding": any(n.startswith("embedding.") for n in names),
+          "lm_head": any(n.startswith("final_proj.") for n in names),
+          "zigzag_residual": bool(getattr(inner, "_pt_zigzag_residual", False)),
+          "buckets": len(model.bucket_manager.buckets) if hasattr(model, "bucket_manager") else 0}
+    allr = [None] * world
+    if world > 1:
+        dist.all_gather_object(allr, me)
+    else:
+        allr = [me]
+    if rank == 0:
+        coords = {tuple(r["grid"]) for r in allr}
+        dims = (m.dp_world_size, m.pp_world_size, m.cp_world_size, m.tp_world_size)
+        assert len(coords) == world == dims[0] * dims[1] * dims[2] * dims[3], (coords, dims)
+        by_stage = {}
+        for r in allr:
+            by_stage.setdefault(r["grid"][1], set()).add(r["params"])
+        assert all(len(v) == 1 for v in by_stage.values()), by_stage   # same shard per stage, every dp/cp/tp
+        layers = sorted({i for r in allr for i in r["layers"]})
+        assert layers == list(range(cfg.num_hidden_layers)), layers
+        par = "-".join(f"{k}{v}" for k, v in zip(("dp", "pp", "cp", "tp"), dims) if v > 1 or k == "dp")
+        out = {"metric": "grid assembly (no step run)", "assembled": True, "ranks": world, "backend": "gloo",
+               "config": {"model": MODELS[args.model][0], "layers": cfg.num_hidden_layers, "seq_len": args.seq,
+                          "micro_batch": args.mbs, "parallelism": par},
+               "model_params": num_params, "per_rank": allr}
+        print(json.dumps(out), file=result_out, flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def build_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -372,6 +411,9 @@ def build_parser():
     ap.add_argument("--bucket-mb", type=float, default=25, help="DataParallelBucket bucket_cap_mb (reference: 25)")
     ap.add_argument("--grad-type", choices=["fp32", "bf16"], default="fp32",
                     help="DataParallelBucket grad_type: fp32 main_grad (reference default) or bf16")
+    ap.add_argument("--assemble-only", action="store_true",
+                    help="build the process grid, model shards and wrappers on the CPU (gloo), report them, "
+                         "run no step: rehearses an N-rank grid without a GPU")
     ap.add_argument("--dp-bucket", action="store_true",
                     help="N = 1 only: run the DP path anyway (DataParallelBucket, fp32 main_grad, bucket "
                          "all-reduce over a 1-rank RCCL group) -- the per-GPU cost of N > 1 minus the links")
@@ -398,12 +440,17 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     os.environ.setdefault("LOCAL_RANK", str(local_rank))
     os.environ.setdefault("FLASH_ATTEN", "1")
-    os.environ["DEVICE"] = "cuda"
+    os.environ["DEVICE"] = "cpu" if args.assemble_only else "cuda"
+    if args.assemble_only and args.backend != "gloo":
+        raise SystemExit("bench.py --assemble-only runs on the CPU: use --backend gloo")
     if args.backend == "gloo":
         local_rank = 0
         os.environ["LOCAL_RANK"] = "0"
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    if args.assemble_only:
+        device = torch.device("cpu")
+    else:
+        torch.cuda.set_device(local_rank)
+        device = torch.device("cuda", local_rank)
     force_dp = args.dp_bucket and world == 1
     if world > 1 or force_dp:
         if force_dp:
@@ -456,6 +503,8 @@ def main():
         model = DataParallelBucket(model, bucket_cap_mb=args.bucket_mb,
                                    grad_type=torch.bfloat16 if args.grad_type == "bf16" else torch.float32)
         model._force_grad_sync = force_dp
+    if args.assemble_only:
+        return assemble_report(args, model, m, cfg, num_params, rank, world, result_out)
     optimizer = AdamW(model.parameters(), lr=3e-4)
     loader = SyntheticMicroBatchDataLoader(args.mbs, args.seq, args.grad_acc, cfg.vocab_size, device, seed=1234,
                                            fresh=True)

@@ -93,3 +93,23 @@ def test_synthetic_loader_fresh_batches():
     for y in second_b:   # targets stay the inputs shifted by one
         assert y["input_ids"].shape == (2, 16) and torch.equal(y["input_ids"][:, 1:], y["target_ids"][:, :-1])
         assert int(y["input_ids"].max()) < 100
+
+
+def test_bench_assembles_the_8_rank_dp2_tp2_pp2_grid_on_cpu():
+    """`bench.py --gpus 8 --backend gloo --assemble-only`: the driver's 8-GPU grids are built before
+    any GPU run -- here config 4's dp2 tp2 pp2 (process_group_manager.py:13's view(dp, pp, cp, tp)):
+    every grid coordinate once, each pipeline stage's shard the same size on all of its ranks, the
+    stages' layers covering the model, the embedding on stage 0 and the lm_head on the last stage."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--backend", "gloo",
+                        "--assemble-only", "--tp", "2", "--pp", "2", "--layers", "2", "--seq", "256"],
+                       capture_output=True, text=True, timeout=600, env=_env(OMP_NUM_THREADS="1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["assembled"] and d["ranks"] == 8 and d["config"]["parallelism"] == "dp2-pp2-tp2"
+    for e in d["per_rank"]:
+        dp_, pp_, cp_, tp_ = e["grid"]
+        assert e["rank"] == ((dp_ * 2 + pp_) * 1 + cp_) * 2 + tp_
+        assert e["embedding"] == (pp_ == 0) and e["lm_head"] == (pp_ == 1)
+        assert e["layers"] == ([0] if pp_ == 0 else [1]) and e["buckets"] > 0
