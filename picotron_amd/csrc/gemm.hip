@@ -110,6 +110,7 @@ struct GemmArgs {
   // its ksplit workgroups to arrive at kcount[tile] -- sums the tile's partials in slice order and
   // writes the real sink F (fmode: EPI_BF16 / EPI_BF16_ACC / EPI_F32_ACC / EPI_BF16_RES with FR)
   int* kcount;
+  int slice_inner;  // split-K slice = the innermost tile index (all slices of a tile on one XCD)
   void* F[4];
   int64_t ldf[4];
   int64_t fseg[5];  // boundaries along M
@@ -219,8 +220,13 @@ __device__ __forceinline__ const GemmArgs& select_problem_pid(const GemmGroup& g
   const GemmArgs& a = g.p[pi];
   int pid = pid_all - g.start[pi];
   const int per_slice = a.tiles_m * a.tiles_n;
-  kslice = a.ksplit > 1 ? pid / per_slice : 0;
-  pid -= kslice * per_slice;
+  if (a.slice_inner) {  // pt_gemm_splitk_fused: a tile's ksplit slices are consecutive ids
+    kslice = pid % a.ksplit;
+    pid /= a.ksplit;
+  } else {
+    kslice = a.ksplit > 1 ? pid / per_slice : 0;
+    pid -= kslice * per_slice;
+  }
   const int GROUP = a.group_m;
   const int group_span = GROUP * a.tiles_n;
   const int gid = pid / group_span;
@@ -677,29 +683,29 @@ __device__ __forceinline__ const uint16_t* bimg_ptr(const BImg& b, bool bkc, int
 
 // ============================================================================ split-K fix-up
 // Called by every thread of a split-K (EPI_F32, ksplit > 1) workgroup after its partial is stored,
-// when the launch carries arrival counters (a.kcount): the workgroup releases its partial (device
-// scope) and counts itself in at the tile's counter; the one that arrives last -- no workgroup ever
-// waits for another -- acquires the others' partials, sums all ksplit of them in slice order
-// (deterministic: the same order whichever slice finishes last) and writes the sink through
-// a.fmode, then resets the counter for the next launch.  The sum starts while other tiles' slices
-// still compute, and reads partials that were just written (L2 / Infinity Cache), instead of a
-// separate reduce pass over all of them after the GEMM.
+// when the launch carries arrival counters (a.kcount): the workgroup counts itself in at the tile's
+// counter once its partial stores have completed; the one that arrives last -- no workgroup ever
+// waits for another -- sums all ksplit partials in slice order (deterministic: the same order
+// whichever slice finishes last), writes the sink through a.fmode and resets the counter.  A tile's
+// slices are consecutive workgroup ids (a.slice_inner), which the XCD-aware order keeps on ONE XCD
+// (the host guarantees whole tiles per XCD share): partials, counter and reads all meet in that
+// XCD's L2, so no device-scope cache write-back / invalidate is needed (vector L1 is write-through,
+// and this kernel reads no partial before the counter says it is complete).  The sum starts while
+// other tiles' slices still compute, instead of a separate reduce pass after the GEMM.
 template <int BM, int BN, int NT>
 __device__ __forceinline__ void ksplit_fixup(const GemmArgs& a, int tile_m, int tile_n) {
   __shared__ int s_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's partial stores have landed in L2
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's partial stores are in L2
   __syncthreads();
   int* cnt = a.kcount + tile_m * a.tiles_n + tile_n;
   if (threadIdx.x == 0) {
-    __threadfence();  // release: write the workgroup's partial back past this XCD's L2
-    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = old == a.ksplit - 1;
     if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = last;
   }
   __syncthreads();
   if (!s_last) return;
-  __threadfence();  // acquire: no stale L2 / L1 copy of the other slices' partials
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int64_t ldp = a.ldc[0];
   const float* P = (const float*)a.C[0] + (int64_t)m0 * ldp + n0;
@@ -1720,10 +1726,17 @@ int pt_gemm_splitk_fused(const pt_gemm_problem* probs, int nprob, int a_kcontig,
       a.ldfr = f.ldr;
     }
     a.kcount = counters + used;                          // this problem's tiles' arrival counters
+    a.slice_inner = 1;
     used += (q.M / 64) * (q.N / 64);                     // enough for any tile shape
   }
   if (used > ncounters) return PT_EINVAL;
-  return launch_group(g, a_kcontig, b_kcontig, EPI_F32, tile, stream);
+  // whole tiles per XCD: every problem's tile count a multiple of 8 keeps each tile's ksplit
+  // consecutive ids inside one XCD's contiguous share of the launch (xcd_remap)
+  const int t = tile < 0 ? pick_group_tile(g) : tile;
+  if (t < 0 || t >= kNumTiles || kTileBM[t] == 0) return PT_EUNSUPPORTED;
+  for (int i = 0; i < nprob; ++i)
+    if (((g.p[i].M / kTileBM[t]) * (g.p[i].N / kTileBN[t])) % 8) return PT_EUNSUPPORTED;
+  return launch_group(g, a_kcontig, b_kcontig, EPI_F32, t, stream);
 }
 
 int pt_gemm_grouped(const pt_gemm_problem* probs, int nprob, int a_kcontig, int b_kcontig, int epilogue, int tile,

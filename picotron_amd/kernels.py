@@ -568,7 +568,7 @@ def fewtile_ksplit(M, N, K):
     256 CUs and every slice >= 256 deep, summed by pt_gemm_splitk_reduce through the GEMM's own
     epilogue (bf16 store / residual add).  The small-tile kernels the unsplit launch would take
     (128x128, 64x64) run at a third of the phased rate per CU.  (1, -1) = unsplit."""
-    if not _ksplit_enabled() or M % 256 or M < 2048 or K < 1024:
+    if not _ksplit_enabled() or not SW.fewtile or M % 256 or M < 2048 or K < 1024:
         return 1, -1
     if N % 256 == 0:
         tile, tiles = 12, (M // 256) * (N // 256)
@@ -638,8 +638,9 @@ def _ksplit_launch(probs, n, a_kcontig, b_kcontig, tile, sinks, dev):
         arr = (_C.SplitkSink * n)(*sinks)
         rc = _C.lib().pt_gemm_splitk_fused(probs, n, int(a_kcontig), int(b_kcontig), int(tile), arr, _ptr(cnt),
                                            cnt.numel(), stream)
-        _C.check(rc, f"pt_gemm_splitk_fused({n} problems, split-K {probs[0].ksplit})")
-        return
+        if rc != -3:   # PT_EUNSUPPORTED: a tile count that does not split into whole tiles per XCD
+            _C.check(rc, f"pt_gemm_splitk_fused({n} problems, split-K {probs[0].ksplit})")
+            return
     rc = _C.lib().pt_gemm_grouped(probs, n, int(a_kcontig), int(b_kcontig), EPI_F32, int(tile), stream)
     _C.check(rc, f"pt_gemm_grouped({n} problems, split-K {probs[0].ksplit})")
     for j in range(n):
