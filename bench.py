@@ -183,9 +183,10 @@ def cp_proxy(args, base, layers):
                  visiting block computes -- C - 1 sequential one-link hops forward; backward the K|V
                  hops plus C hops of the fp32 dK|dV accumulator (context_parallel.py:72-106);
       mesh (shipped with the zig-zag layout): all C - 1 K|V shards fetched at once from their owners
-                 on C - 1 distinct links under the diagonal block; backward the same gather under
-                 the diagonal block's backward, then each fp32 dK|dV partial sent straight to its
-                 owner (one transfer per link, the largest a full shard's 2 x bf16 bytes);
+                 on C - 1 distinct links under the diagonal block; backward the K|V shards plus the
+                 visiting queries / dO (bf16) and LSE / D (f32) fetched the same way under the
+                 diagonal block's backward -- each rank computes its own keys' dK / dV, so no
+                 gradient partial travels;
       re-lay     the residual stream's zig-zag re-lay, twice per forward and twice per backward for
                  the whole stack (context_parallel.enable_zigzag_residual: on with the cp gradient
                  averaging of DataParallelBucket), amortised per layer."""
@@ -252,23 +253,24 @@ def cp_proxy(args, base, layers):
     # ---- communication budget per layer (bytes per rank, link time, what stays exposed)
     bw = XGMI_LINK_GBPS * 1e9
     kv_b = B * S * 2 * nkv * d * 2               # one K|V shard, bf16
-    dkv_b = 2 * kv_b                             # its fp32 dK|dV accumulator
+    dkv_b = 2 * kv_b                             # its fp32 dK|dV accumulator (the ring's)
+    qdo_b = B * S * 2 * nh * d * 2 + B * nh * S * 2 * 4   # a rank's queries + dO (bf16), LSE + D (f32)
     relay_b = 4 * B * S * H * 2                  # re-lay of [B, S, H] bf16: entry + exit, fwd + bwd, per pass
     halves_f = [t["kv0_fwd"]] * crit + [t["q1_fwd"]] * (C - 1 - crit)
     halves_b = [t["kv0_bwd"]] * crit + [t["q1_bwd"]] * (C - 1 - crit)
     # ring: each step's transfer hides under that step's block
     ring_f = sum(max(kv_b / bw, tf) - tf for tf in halves_f)
     ring_b = sum(max((kv_b + dkv_b) / bw, tb) - tb for tb in halves_b) + dkv_b / bw   # + the last dK|dV hop
-    # mesh: the gather hides under the diagonal block; the partials' return is a tail
+    # mesh: each gather hides under the diagonal block (the backward's carries K|V + Q|dO|LSE|D)
     mesh_f = max(0.0, kv_b / bw - t["diag_fwd"])
-    mesh_b = max(0.0, kv_b / bw - t["diag_bwd"]) + dkv_b / bw
+    mesh_b = max(0.0, (kv_b + qdo_b) / bw - t["diag_bwd"])
     relay_t = relay_b / layers / (2 * bw)        # two peers, two links
     comm = {"link_GBps_per_direction": XGMI_LINK_GBPS, "kv_shard_bytes": kv_b, "dkv_f32_bytes": dkv_b,
             "ring": {"comm_bytes_per_layer": (C - 1) * kv_b + (C - 1) * kv_b + C * dkv_b,
                      "link_time_ms": ((C - 1) * kv_b * 2 + C * dkv_b) / bw * 1e3,
                      "exposed_ms": (ring_f + ring_b) * 1e3},
-            "mesh": {"comm_bytes_per_layer": (C - 1) * kv_b * 2 + crit * kv_b + (C - 1 - crit) * dkv_b,
-                     "link_time_ms": (2 * kv_b + dkv_b) / bw * 1e3, "links": C - 1,
+            "mesh": {"comm_bytes_per_layer": (C - 1) * (2 * kv_b + qdo_b),
+                     "link_time_ms": (2 * kv_b + qdo_b) / bw * 1e3, "links": C - 1,
                      "exposed_ms": (mesh_f + mesh_b) * 1e3},
             "relayout": {"comm_bytes_per_pass": relay_b, "per_layer_ms": relay_t * 1e3}}
     t_mesh = t_zz + mesh_f + mesh_b + relay_t

@@ -209,25 +209,6 @@ typedef struct {
 int pt_gemm_grouped(const pt_gemm_problem* probs, int nprob, int a_kcontig, int b_kcontig, int epilogue, int tile,
                     hipStream_t stream);
 
-/* pt_gemm_grouped's split-K problems (ksplit > 1; C = one f32 partials buffer [ksplit][M][N], ld N,
- * kpart_stride apart) finished INSIDE the launch: the workgroup that completes a tile -- the last of
- * its ksplit slices to arrive at the tile's counter -- sums the tile's partials in slice order and
- * writes sinks[i] through `mode` (0 bf16 store, 1 bf16 accumulate, 3 f32 accumulate, 4 bf16
- * residual add); no workgroup waits for another.  Replaces the grouped launch + pt_gemm_splitk_reduce
- * pair (same results, bit for bit).  counters: int32, zero on entry, >= sum over problems of
- * (M / 64) (N / 64) of them; the kernel leaves them zero.  N % 4 == 0. */
-typedef struct {
-  void* C[4];
-  int64_t ldc[4];
-  int64_t c_bounds[5];     /* nc + 1 row boundaries of the sink's segments */
-  int nc;
-  int mode;
-  const void* residual;    /* mode 4: [M, N] bf16, ld ldr */
-  int64_t ldr;
-} pt_splitk_sink;
-int pt_gemm_splitk_fused(const pt_gemm_problem* probs, int nprob, int a_kcontig, int b_kcontig, int tile,
-                         const pt_splitk_sink* sinks, int* counters, int64_t ncounters, hipStream_t stream);
-
 /* Two independent groups in ONE launch of 256x256 tiles, each with its own layouts and epilogue:
  * group 0 = dX (A = dY [M, K] K-contiguous, B = W [K, N] N-contiguous; epilogue 0 or 6 = the
  * SwiGLU backward, residual = g|u), group 1 = wgrad (dY^T X; both operands MN-contiguous;
@@ -287,6 +268,16 @@ int pt_attn_bwd(const void* q, const int64_t* q_str, const void* k, const int64_
                 int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int64_t D, float scale, int causal,
                 int grad_f32, const void* rope_cos, const void* rope_sin, int64_t rope_stride, int64_t lse_ld,
                 hipStream_t stream);
+/* pt_attn_bwd computing only dQ (parts = 1) or only dK / dV (parts = 2), or both (3); the pointers
+ * of a gradient not computed may be NULL.  The context-parallel mesh backward
+ * (context_parallel.py:72-106's ring, restated for the xGMI full mesh) runs each rank's dQ against
+ * the visiting K / V and its own keys' dK / dV against the visiting queries, so no dK / dV partial
+ * travels. */
+int pt_attn_bwd_part(const void* q, const int64_t* q_str, const void* k, const int64_t* k_str, const void* v,
+                     const int64_t* v_str, const void* dout, const int64_t* do_str, const float* lse,
+                     const float* delta, void* dq, const int64_t* dq_str, void* dk, const int64_t* dk_str, void* dv,
+                     const int64_t* dv_str, int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int64_t D,
+                     float scale, int causal, int grad_f32, int64_t lse_ld, int parts, hipStream_t stream);
 /* pt_attn_bwd with the FA2 'D' = rowsum(dO * O) computed inside the dQ kernel (run first) from o
  * (bf16 [B, S, H, D] strides o_str) and written to delta_out [B, H, Sq] f32, which the dK/dV kernel
  * then reads: the separate pt_attn_bwd_delta pass disappears.  bf16 gradients only (no grad_f32). */

@@ -27,12 +27,6 @@ class GemmProblem(ctypes.Structure):
                 ("kpart_stride", _i64)]
 
 
-class SplitkSink(ctypes.Structure):
-    """pt_splitk_sink (include/picotron_hip.h)."""
-    _fields_ = [("C", _vp * 4), ("ldc", _i64 * 4), ("c_bounds", _i64 * 5), ("nc", _i32), ("mode", _i32),
-                ("residual", _vp), ("ldr", _i64)]
-
-
 # name -> (restype, argtypes); mirrors include/picotron_hip.h one to one
 SIGNATURES = {
     "pt_rmsnorm_fwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _f32, _i32, _vp]),
@@ -64,6 +58,8 @@ SIGNATURES = {
     "pt_attn_bwd": (_i32, [_vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _vp, _vp, _i64p, _vp, _i64p,
                            _vp, _i64p, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _i32, _i32, _vp, _vp, _i64, _i64,
                            _vp]),
+    "pt_attn_bwd_part": (_i32, [_vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _vp, _vp, _i64p, _vp, _i64p,
+                                _vp, _i64p, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _i32, _i32, _i64, _i32, _vp]),
     "pt_attn_bwd_fused_delta": (_i32, [_vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _vp, _vp,
                                        _i64p, _vp, _i64p, _vp, _i64p, _i64, _i64, _i64, _i64, _i64, _i64, _f32,
                                        _i32, _vp, _vp, _i64, _i64, _vp]),
@@ -72,8 +68,6 @@ SIGNATURES = {
     "pt_cross_entropy_fwd_stats": (_i32, [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i64, _i64, _vp, _vp]),
     "pt_cross_entropy_mean": (_i32, [_vp, _vp, _i64, _i64, _vp, _vp, _vp, _i32, _i32, _vp]),
     "pt_embedding_sort": (_i32, [_vp, _i64, _i64, _i64, _i32, _i64, _vp, _vp, _vp]),
-    "pt_gemm_splitk_fused": (_i32, [ctypes.POINTER(GemmProblem), _i32, _i32, _i32, _i32, ctypes.POINTER(SplitkSink),
-                                    _vp, _i64, _vp]),
     "pt_set_variant": (_i32, [ctypes.c_char_p, _i32]),
     "pt_get_variant": (_i32, [ctypes.c_char_p]),
     "pt_gemm_rope": (_i32, [_vp, _i64, _vpp, _i64p, _i64p, _i32, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _i64,

@@ -161,6 +161,14 @@ class HipBlocks:
     def bwd(do, q, k, v, o, lse, delta, scale, causal, dq, dk, dv):
         K.attn_bwd(do, q, k, v, o, lse, scale, causal, dq=dq, dk=dk, dv=dv, grad_f32=True, delta=delta)
 
+    @staticmethod
+    def bwd_dq(do, q, k, v, lse, delta, scale, causal, dq):
+        K.attn_bwd_part(do, q, k, v, lse, delta, scale, causal, dq=dq)
+
+    @staticmethod
+    def bwd_dkdv(do, q, k, v, lse, delta, scale, causal, dk, dv):
+        K.attn_bwd_part(do, q, k, v, lse, delta, scale, causal, dk=dk, dv=dv)
+
 
 def _kv_views(kv, B, S, nkv, d):
     w = nkv * d
@@ -312,42 +320,52 @@ def mesh_forward(q, kv, nkv, scale, blocks=HipBlocks):
 
 
 def mesh_backward(do, q, kv, o, lse, nkv, scale, blocks=HipBlocks):
-    """The zig-zag causal backward on the mesh: K|V gathered again under the diagonal block's
-    backward; each visiting shard's fp32 dK|dV partial (its first half for 'kv0', all of it for
-    'q1') is sent straight to its owner in one batched p2p, and the partials this rank receives
-    for its own K|V are summed into its dK|dV.  Returns (dq f32 [B,S,nh,d], dkv f32 [B*S, 2 w])."""
+    """The zig-zag causal backward on the mesh, with no gradient partial on the wire: every rank
+    fetches, besides the visiting K|V shards (for its own queries' dQ), the visiting ranks' queries,
+    dO, LSE and D = rowsum(dO * O) -- 64 MiB + 0.5 MiB per peer at Llama-2-7B CP8, half of an fp32
+    dK|dV partial -- in ONE batched p2p under its diagonal block's backward, and computes its own
+    keys' dK / dV against them (the FA2 split of the backward: dQ over the visiting keys, dK / dV
+    over the visiting queries).  Visiting block kinds as the forward's: for my queries, shard j < r
+    is 'kv0' (all my queries x its first half), j > r 'q1' (my second half x all of it); for my keys,
+    rank j > r sees them as 'kv0' (all its queries x my first half), j < r as 'q1' (its second-half
+    queries x all my keys).  Returns (dq f32 [B,S,nh,d], dkv f32 [B*S, 2 w]) for this rank's shards."""
     m = pgm.current()
-    r, ids, group = m.cp_rank, m.cp_group_ids, m.cp_group
+    C, r, ids, group = m.cp_world_size, m.cp_rank, m.cp_group_ids, m.cp_group
     B, S, nh, d = q.shape
     h, w = S // 2, nkv * d
     delta = blocks.delta(do, o)
     dq = torch.zeros(B, S, nh, d, dtype=torch.float32, device=q.device)
     dkv = torch.zeros(kv.shape, dtype=torch.float32, device=kv.device)
-    bufs, pending = mesh_gather_kv(kv)
+    # what the peers need from me: K|V (their dQ), my queries and dO (bf16) and LSE | D (f32) (their dK/dV)
+    qdo = torch.cat([q.reshape(B, S, nh * d), do.reshape(B, S, nh * d)], dim=2).contiguous()
+    ld = torch.stack([lse, delta], dim=2).contiguous()            # [B, nh, 2, S]
+    peers = [j for j in range(C) if j != r]
+    kvs = {j: torch.empty_like(kv) for j in peers}
+    qdos = {j: torch.empty_like(qdo) for j in peers}
+    lds = {j: torch.empty_like(ld) for j in peers}
+    ops = []
+    for j in peers:
+        ops += [dist.P2POp(dist.isend, t, ids[j], group=group) for t in (kv, qdo, ld)]
+    for j in peers:
+        ops += [dist.P2POp(dist.irecv, t[j], ids[j], group=group) for t in (kvs, qdos, lds)]
+    pending = _p2p(ops, group)
     k, v = _kv_views(kv, B, S, nkv, d)
     dk, dv = _kv_views(dkv, B, S, nkv, d)
     blocks.bwd(do, q, k, v, o, lse, delta, scale, True, dq, dk, dv)
     _p2p_wait(pending)
-    parts = {}
-    for j, kvj in bufs.items():
-        k, v = _kv_views(kvj, B, S, nkv, d)
-        part = torch.zeros(B, h if j < r else S, 2 * w, dtype=torch.float32, device=kv.device)
-        pk = part[:, :, :w].view(B, part.shape[1], nkv, d)
-        pv = part[:, :, w:].view(B, part.shape[1], nkv, d)
-        if j < r:
-            blocks.bwd(do, q, k[:, :h], v[:, :h], o, lse, delta, scale, False, dq, pk, pv)
-        else:
-            blocks.bwd(do[:, h:], q[:, h:], k, v, o[:, h:], lse[:, :, h:], delta[:, :, h:], scale, False,
-                       dq[:, h:], pk, pv)
-        parts[j] = part
-    # from rank i's side this rank's shard was 'kv0' (r < i: first half) or 'q1' (r > i: all)
-    recv = {i: torch.empty(B, h if r < i else S, 2 * w, dtype=torch.float32, device=kv.device) for i in parts}
-    ops = [dist.P2POp(dist.isend, parts[j], ids[j], group=group) for j in parts]
-    ops += [dist.P2POp(dist.irecv, recv[i], ids[i], group=group) for i in recv]
-    _p2p_wait(_p2p(ops, group))
-    dkv3 = dkv.view(B, S, 2 * w)
-    for i, t in recv.items():
-        dkv3[:, :t.shape[1]] += t
+    for j in peers:
+        kj, vj = _kv_views(kvs[j], B, S, nkv, d)
+        if j < r:    # my queries x its first half
+            blocks.bwd_dq(do, q, kj[:, :h], vj[:, :h], lse, delta, scale, False, dq)
+        else:        # my second half x all of it
+            blocks.bwd_dq(do[:, h:], q[:, h:], kj, vj, lse[:, :, h:], delta[:, :, h:], scale, False, dq[:, h:])
+        qj = qdos[j][:, :, :nh * d].view(B, S, nh, d)
+        doj = qdos[j][:, :, nh * d:].view(B, S, nh, d)
+        lsej, dj = lds[j][:, :, 0], lds[j][:, :, 1]
+        if j > r:    # all its queries x my first half
+            blocks.bwd_dkdv(doj, qj, k[:, :h], v[:, :h], lsej, dj, scale, False, dk[:, :h], dv[:, :h])
+        else:        # its second-half queries x all my keys
+            blocks.bwd_dkdv(doj[:, h:], qj[:, h:], k, v, lsej[:, :, h:], dj[:, :, h:], scale, False, dk, dv)
     return dq, dkv
 
 

@@ -1038,7 +1038,7 @@ int attn_bwd_impl(const void* q, const int64_t* q_str, const void* k, const int6
                   const int64_t* dv_str, int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int64_t D,
                   float scale, int causal, int grad_f32, const void* rope_cos, const void* rope_sin,
                   int64_t rope_stride, const void* o, const int64_t* o_str, float* delta_w, int64_t lse_ld,
-                  hipStream_t stream);
+                  hipStream_t stream, int parts = 3);
 
 }  // namespace
 
@@ -1131,8 +1131,10 @@ int attn_bwd_impl(const void* q, const int64_t* q_str, const void* k, const int6
                   const int64_t* dv_str, int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int64_t D,
                   float scale, int causal, int grad_f32, const void* rope_cos, const void* rope_sin,
                   int64_t rope_stride, const void* o, const int64_t* o_str, float* delta_w, int64_t lse_ld,
-                  hipStream_t stream) {
-  if (!q || !k || !v || !dout || !lse || !dq || !dk || !dv) return PT_EINVAL;
+                  hipStream_t stream, int parts) {
+  if (!q || !k || !v || !dout || !lse || parts < 1 || parts > 3) return PT_EINVAL;
+  if (((parts & 1) && (!dq || !dq_str)) || ((parts & 2) && (!dk || !dv || !dk_str || !dv_str))) return PT_EINVAL;
+  if (delta_w && parts != 3) return PT_EINVAL;   // the fused delta comes from the dQ kernel, for dK/dV
   if (lse_ld != 0 && lse_ld < Sq) return PT_EINVAL;
   if (rope_cos && (!rope_sin || grad_f32 || Sq != Sk || (rope_stride & 3) || !pt_aligned16(rope_cos) ||
                    !pt_aligned16(rope_sin)))
@@ -1144,9 +1146,11 @@ int attn_bwd_impl(const void* q, const int64_t* q_str, const void* k, const int6
   a.dout = (const uint16_t*)dout; a.do_sb = do_str[0]; a.do_ss = do_str[1]; a.do_sh = do_str[2];
   a.lse = (float*)lse; a.delta = delta;
   a.lse_ld = lse_ld ? lse_ld : Sq;
-  a.dq = dq; a.dq_sb = dq_str[0]; a.dq_ss = dq_str[1]; a.dq_sh = dq_str[2];
-  a.dk = dk; a.dk_sb = dk_str[0]; a.dk_ss = dk_str[1]; a.dk_sh = dk_str[2];
-  a.dv = dv; a.dv_sb = dv_str[0]; a.dv_ss = dv_str[1]; a.dv_sh = dv_str[2];
+  if (parts & 1) { a.dq = dq; a.dq_sb = dq_str[0]; a.dq_ss = dq_str[1]; a.dq_sh = dq_str[2]; }
+  if (parts & 2) {
+    a.dk = dk; a.dk_sb = dk_str[0]; a.dk_ss = dk_str[1]; a.dk_sh = dk_str[2];
+    a.dv = dv; a.dv_sb = dv_str[0]; a.dv_ss = dv_str[1]; a.dv_sh = dv_str[2];
+  }
   a.B = (int)B; a.H = (int)H; a.HKV = (int)HKV; a.Sq = (int)Sq; a.Sk = (int)Sk;
   a.scale = scale; a.causal = causal; a.grad_f32 = grad_f32;
   a.rope_cos = (const uint16_t*)rope_cos; a.rope_sin = (const uint16_t*)rope_sin; a.rope_ld = rope_stride;
@@ -1167,12 +1171,15 @@ int attn_bwd_impl(const void* q, const int64_t* q_str, const void* k, const int6
   const bool split = (split_mask() >> (D == 64 ? 0 : 1)) & 1;
   // dQ first: with delta_w set it produces the D the dK/dV kernel reads (same stream, in order)
   if (D == 64) {
-    set_smem(attn_bwd_dq_kernel<64>, smem_kv);
-    attn_bwd_dq_kernel<64><<<gq, NW * 64, smem_kv, stream>>>(a);
-    PT_CHECK_LAUNCH();
+    if (parts & 1) {
+      set_smem(attn_bwd_dq_kernel<64>, smem_kv);
+      attn_bwd_dq_kernel<64><<<gq, NW * 64, smem_kv, stream>>>(a);
+      PT_CHECK_LAUNCH();
+    }
     a.delta = a.delta_w ? a.delta_w : a.delta;
     a.delta_w = nullptr;
-    if (split) {
+    if (!(parts & 2)) {
+    } else if (split) {
       set_smem(attn_bwd_dkdv_pair_kernel<64>, smem_pair);
       attn_bwd_dkdv_pair_kernel<64><<<gk, 8 * 64, smem_pair, stream>>>(a);
     } else {
@@ -1180,12 +1187,15 @@ int attn_bwd_impl(const void* q, const int64_t* q_str, const void* k, const int6
       attn_bwd_dkdv_kernel<64><<<gk, NW * 64, smem_q, stream>>>(a);
     }
   } else {
-    set_smem(attn_bwd_dq_kernel<128>, smem_kv);
-    attn_bwd_dq_kernel<128><<<gq, NW * 64, smem_kv, stream>>>(a);
-    PT_CHECK_LAUNCH();
+    if (parts & 1) {
+      set_smem(attn_bwd_dq_kernel<128>, smem_kv);
+      attn_bwd_dq_kernel<128><<<gq, NW * 64, smem_kv, stream>>>(a);
+      PT_CHECK_LAUNCH();
+    }
     a.delta = a.delta_w ? a.delta_w : a.delta;
     a.delta_w = nullptr;
-    if (split) {
+    if (!(parts & 2)) {
+    } else if (split) {
       set_smem(attn_bwd_dkdv_pair_kernel<128>, smem_pair);
       attn_bwd_dkdv_pair_kernel<128><<<gk, 8 * 64, smem_pair, stream>>>(a);
     } else {
@@ -1200,6 +1210,20 @@ int attn_bwd_impl(const void* q, const int64_t* q_str, const void* k, const int6
 }  // namespace
 
 extern "C" {
+
+// pt_attn_bwd computing only dQ (parts 1) or only dK / dV (parts 2): the full-mesh context-parallel
+// backward runs each rank's dQ against the visiting K / V and its own keys' dK / dV against the
+// visiting queries (the other pointers may be NULL)
+int pt_attn_bwd_part(const void* q, const int64_t* q_str, const void* k, const int64_t* k_str, const void* v,
+                     const int64_t* v_str, const void* dout, const int64_t* do_str, const float* lse,
+                     const float* delta, void* dq, const int64_t* dq_str, void* dk, const int64_t* dk_str, void* dv,
+                     const int64_t* dv_str, int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int64_t D,
+                     float scale, int causal, int grad_f32, int64_t lse_ld, int parts, hipStream_t stream) {
+  if (!delta) return PT_EINVAL;
+  return attn_bwd_impl(q, q_str, k, k_str, v, v_str, dout, do_str, lse, delta, dq, dq_str, dk, dk_str, dv, dv_str,
+                       B, H, HKV, Sq, Sk, D, scale, causal, grad_f32, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
+                       lse_ld, stream, parts);
+}
 
 // pt_attn_bwd with D = rowsum(dO * O) computed inside the dQ kernel from o (bf16, strides o_str)
 // and written to delta_out [B, H, Sq] f32 (replaces the separate pt_attn_bwd_delta pass)

@@ -106,18 +106,6 @@ struct GemmArgs {
   // its f32 partial at C + s * kpart_stride (pt_gemm_splitk_reduce sums them into the real sink)
   int ksplit;
   int64_t kpart_stride;
-  // in-kernel split-K finish (pt_gemm_splitk_fused): the slice that completes a tile -- the last of
-  // its ksplit workgroups to arrive at kcount[tile] -- sums the tile's partials in slice order and
-  // writes the real sink F (fmode: EPI_BF16 / EPI_BF16_ACC / EPI_F32_ACC / EPI_BF16_RES with FR)
-  int* kcount;
-  int slice_inner;  // split-K slice = the innermost tile index (all slices of a tile on one XCD)
-  void* F[4];
-  int64_t ldf[4];
-  int64_t fseg[5];  // boundaries along M
-  int nfseg;
-  int fmode;
-  const uint16_t* FR;
-  int64_t ldfr;
 };
 
 // swizzles (chunk = 16 bytes); see tools/lds_swizzle_search.py
@@ -220,13 +208,8 @@ __device__ __forceinline__ const GemmArgs& select_problem_pid(const GemmGroup& g
   const GemmArgs& a = g.p[pi];
   int pid = pid_all - g.start[pi];
   const int per_slice = a.tiles_m * a.tiles_n;
-  if (a.slice_inner) {  // pt_gemm_splitk_fused: a tile's ksplit slices are consecutive ids
-    kslice = pid % a.ksplit;
-    pid /= a.ksplit;
-  } else {
-    kslice = a.ksplit > 1 ? pid / per_slice : 0;
-    pid -= kslice * per_slice;
-  }
+  kslice = a.ksplit > 1 ? pid / per_slice : 0;
+  pid -= kslice * per_slice;
   const int GROUP = a.group_m;
   const int group_span = GROUP * a.tiles_n;
   const int gid = pid / group_span;
@@ -681,64 +664,6 @@ __device__ __forceinline__ const uint16_t* bimg_ptr(const BImg& b, bool bkc, int
   return (const uint16_t*)((intptr_t)b.b0 + e1 + e2 + e3 + k_off * 2);
 }
 
-// ============================================================================ split-K fix-up
-// Called by every thread of a split-K (EPI_F32, ksplit > 1) workgroup after its partial is stored,
-// when the launch carries arrival counters (a.kcount): the workgroup counts itself in at the tile's
-// counter once its partial stores have completed; the one that arrives last -- no workgroup ever
-// waits for another -- sums all ksplit partials in slice order (deterministic: the same order
-// whichever slice finishes last), writes the sink through a.fmode and resets the counter.  A tile's
-// slices are consecutive workgroup ids (a.slice_inner), which the XCD-aware order keeps on ONE XCD
-// (the host guarantees whole tiles per XCD share): partials, counter and reads all meet in that
-// XCD's L2, so no device-scope cache write-back / invalidate is needed (vector L1 is write-through,
-// and this kernel reads no partial before the counter says it is complete).  The sum starts while
-// other tiles' slices still compute, instead of a separate reduce pass after the GEMM.
-template <int BM, int BN, int NT>
-__device__ __forceinline__ void ksplit_fixup(const GemmArgs& a, int tile_m, int tile_n) {
-  __shared__ int s_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's partial stores are in L2
-  __syncthreads();
-  int* cnt = a.kcount + tile_m * a.tiles_n + tile_n;
-  if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == a.ksplit - 1;
-    if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = last;
-  }
-  __syncthreads();
-  if (!s_last) return;
-  const int m0 = tile_m * BM, n0 = tile_n * BN;
-  const int64_t ldp = a.ldc[0];
-  const float* P = (const float*)a.C[0] + (int64_t)m0 * ldp + n0;
-  constexpr int C4 = BN / 4;
-  for (int i = threadIdx.x; i < BM * C4; i += NT) {
-    const int row = i / C4, c = (i % C4) * 4;
-    const float* p = P + (int64_t)row * ldp + c;
-    float4 v = *(const float4*)p;
-    for (int k = 1; k < a.ksplit; ++k) {
-      const float4 w = *(const float4*)(p + k * a.kpart_stride);
-      v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
-    }
-    const int64_t grow = m0 + row;
-    const int sg = find_seg(a.fseg, a.nfseg, grow);
-    const int64_t off = (grow - a.fseg[sg]) * a.ldf[sg] + n0 + c;
-    if (a.fmode == EPI_F32_ACC) {
-      float4* o = (float4*)((float*)a.F[sg] + off);
-      const float4 old = *o;
-      *o = make_float4(old.x + v.x, old.y + v.y, old.z + v.z, old.w + v.w);
-    } else {
-      uint2* o = (uint2*)((uint16_t*)a.F[sg] + off);
-      float f[4] = {v.x, v.y, v.z, v.w};
-      if (a.fmode == EPI_BF16_ACC || a.fmode == EPI_BF16_RES) {  // bf16(old + bf16(sum)), as the GEMM epilogue
-        const uint2 old = a.fmode == EPI_BF16_ACC ? *o : *(const uint2*)(a.FR + grow * a.ldfr + n0 + c);
-        const float of[4] = {lo_bf(old.x), hi_bf(old.x), lo_bf(old.y), hi_bf(old.y)};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) f[e] = of[e] + round_bf(f[e]);
-      }
-      *o = make_uint2(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]));
-    }
-  }
-}
-
 // ============================================================================ 8-phase 256x256
 // 256x256 tile, BK = 64, 8 waves as 2(M) x 4(N), each wave a 128 x 64 output (8 x 4 accumulators
 // of 16x16).  Each operand tile is held as two "half images" of 128 rows (A) / columns (B) x 64 k,
@@ -941,9 +866,6 @@ __device__ __forceinline__ void gemm_8ph_tile(const GemmArgs& a, const int tile_
       __syncthreads();
       if (wn == 0) ce_stats_merge<4, TM, TN>(a, xs, m0, n0, wm, lane);
     }
-    if constexpr (EPI == EPI_F32) {
-      if (a.kcount) ksplit_fixup<256, 256, 512>(a, tile_m, tile_n);
-    }
   }
 }
 
@@ -1141,9 +1063,6 @@ __device__ __forceinline__ void gemm_4ph_tile(const GemmArgs& a, const int tile_
     __syncthreads();
     if (wn == 0) ce_stats_merge<2, TM, TN>(a, xs, m0, n0, wm, lane);
   }
-  if constexpr (EPI == EPI_F32) {
-    if (a.kcount) ksplit_fixup<256, 128, 512>(a, tile_m, tile_n);
-  }
 }
 
 template <bool AK, bool BKC, int EPI>
@@ -1277,9 +1196,6 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const GemmGroup g) {
   }
   epilogue<TM, TN, EPI>(a, acc, smem + wave * (TM * (TN * 2 + 16)), m0, n0, wm, wn, lane, nullptr,
                         (int64_t)ks * a.kpart_stride);
-  if constexpr (EPI == EPI_F32) {
-    if (a.kcount) ksplit_fixup<BM, BN, WM * WN * 64>(a, tile_m, tile_n);
-  }
 }
 
 // ================================================================================== launch
@@ -1691,54 +1607,6 @@ int pt_gemm(const void* A, int64_t lda, int a_kcontig, const void* const* B, con
 }
 
 // Several independent problems in one launch (same layouts / epilogue; see include/picotron_hip.h).
-int pt_gemm_splitk_fused(const pt_gemm_problem* probs, int nprob, int a_kcontig, int b_kcontig, int tile,
-                         const pt_splitk_sink* sinks, int* counters, int64_t ncounters, hipStream_t stream) {
-  if (!probs || !sinks || !counters || nprob < 1 || nprob > kMaxProb) return PT_EINVAL;
-  GemmGroup g{};
-  g.nprob = nprob;
-  int64_t used = 0;
-  for (int i = 0; i < nprob; ++i) {
-    const pt_gemm_problem& q = probs[i];
-    const pt_splitk_sink& f = sinks[i];
-    if (q.nc != 1 || q.ksplit < 2) return PT_EINVAL;    // C = the f32 partials, one segment
-    int rc = fill_args(g.p[i], q.A, q.lda, q.B, q.ldb, q.b_bounds, q.nb, q.b_seg_dim, q.C, q.ldc, q.c_bounds,
-                       q.nc, q.M, q.N, q.K, EPI_F32, nullptr, 0);
-    if (!rc) rc = fill_split(g.p[i], q, EPI_F32);
-    if (rc) return rc;
-    GemmArgs& a = g.p[i];
-    if (a.ldc[0] != q.N || q.kpart_stride < q.M * q.N || !pt_aligned16(q.C[0])) return PT_EALIGN;
-    if (f.mode != EPI_BF16 && f.mode != EPI_BF16_ACC && f.mode != EPI_F32_ACC && f.mode != EPI_BF16_RES)
-      return PT_EINVAL;
-    if (f.nc < 1 || f.nc > 4 || (q.N & 3)) return PT_EINVAL;
-    const int esz = f.mode == EPI_F32_ACC ? 4 : 2;
-    a.nfseg = f.nc;
-    for (int j = 0; j <= f.nc; ++j) a.fseg[j] = f.c_bounds[j];
-    if (a.fseg[0] != 0 || a.fseg[f.nc] != q.M) return PT_EINVAL;
-    for (int j = 0; j < f.nc; ++j) {
-      if (!f.C[j] || ((uintptr_t)f.C[j] & (esz * 4 - 1)) || (f.ldc[j] & 3)) return PT_EALIGN;
-      a.F[j] = f.C[j];
-      a.ldf[j] = f.ldc[j];
-    }
-    a.fmode = f.mode;
-    if (f.mode == EPI_BF16_RES) {
-      if (!f.residual || ((uintptr_t)f.residual & 7) || (f.ldr & 3) || f.nc != 1) return PT_EINVAL;
-      a.FR = (const uint16_t*)f.residual;
-      a.ldfr = f.ldr;
-    }
-    a.kcount = counters + used;                          // this problem's tiles' arrival counters
-    a.slice_inner = 1;
-    used += (q.M / 64) * (q.N / 64);                     // enough for any tile shape
-  }
-  if (used > ncounters) return PT_EINVAL;
-  // whole tiles per XCD: every problem's tile count a multiple of 8 keeps each tile's ksplit
-  // consecutive ids inside one XCD's contiguous share of the launch (xcd_remap)
-  const int t = tile < 0 ? pick_group_tile(g) : tile;
-  if (t < 0 || t >= kNumTiles || kTileBM[t] == 0) return PT_EUNSUPPORTED;
-  for (int i = 0; i < nprob; ++i)
-    if (((g.p[i].M / kTileBM[t]) * (g.p[i].N / kTileBN[t])) % 8) return PT_EUNSUPPORTED;
-  return launch_group(g, a_kcontig, b_kcontig, EPI_F32, t, stream);
-}
-
 int pt_gemm_grouped(const pt_gemm_problem* probs, int nprob, int a_kcontig, int b_kcontig, int epilogue, int tile,
                     hipStream_t stream) {
   if (!probs || nprob < 1 || nprob > kMaxProb) return PT_EINVAL;

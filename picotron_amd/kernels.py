@@ -605,51 +605,26 @@ def _gemm_ksplit(A, lda, a_kcontig, Bs, ldbs, b_bounds, b_kcontig, b_seg_dim, ou
     return out
 
 
-_KCOUNT = {}
-_KCOUNT_N = 1 << 17
-
-
-def _kcounters(dev):
-    """The split-K arrival counters of pt_gemm_splitk_fused on `dev` (zero; every launch leaves them
-    zero): one int32 per potential 64x64 tile of a launch's problems."""
-    key = (dev.type, dev.index)
-    if key not in _KCOUNT:
-        _KCOUNT[key] = torch.zeros(_KCOUNT_N, dtype=torch.int32, device=dev)
-    return _KCOUNT[key]
-
-
 def _sink(outs, bounds, mode, residual=None, ldr=0):
-    sk = _C.SplitkSink()
-    for i, o in enumerate(outs):
-        sk.C[i], sk.ldc[i] = _ptr(o), int(o.stride(0))
-    for i, v in enumerate(bounds):
-        sk.c_bounds[i] = int(v)
-    sk.nc, sk.mode = len(outs), int(mode)
-    sk.residual, sk.ldr = _ptr(residual), int(ldr)
-    return sk
+    """(outs, row bounds, epilogue, residual, ldr) of a split-K problem's real sink."""
+    return outs, bounds, mode, residual, ldr
 
 
 def _ksplit_launch(probs, n, a_kcontig, b_kcontig, tile, sinks, dev):
-    """The split-K problems finished in-kernel (pt_gemm_splitk_fused) -- or, with ksplit_fused = 0,
-    the grouped launch + one reduce pass per problem (A/B)."""
+    """The split-K problems (f32 partials, one grouped launch), then one reduce pass per problem into
+    its sink through the GEMM's own epilogue (pt_gemm_splitk_reduce: the partials summed in slice
+    order over the whole chip).  (Finishing a tile inside the launch -- its last-arriving slice
+    summing the partials, tools/diag/ksplit_fused.patch -- measured 12-20 % slower at TP = 8: one
+    workgroup per tile then does the whole reduction after the other slices have left the CUs.)"""
     stream = _C.stream_ptr(dev)
-    if SW.ksplit_fused:
-        cnt = _kcounters(dev)
-        arr = (_C.SplitkSink * n)(*sinks)
-        rc = _C.lib().pt_gemm_splitk_fused(probs, n, int(a_kcontig), int(b_kcontig), int(tile), arr, _ptr(cnt),
-                                           cnt.numel(), stream)
-        if rc != -3:   # PT_EUNSUPPORTED: a tile count that does not split into whole tiles per XCD
-            _C.check(rc, f"pt_gemm_splitk_fused({n} problems, split-K {probs[0].ksplit})")
-            return
     rc = _C.lib().pt_gemm_grouped(probs, n, int(a_kcontig), int(b_kcontig), EPI_F32, int(tile), stream)
     _C.check(rc, f"pt_gemm_grouped({n} problems, split-K {probs[0].ksplit})")
     for j in range(n):
-        pr, sk = probs[j], sinks[j]
+        pr = probs[j]
+        outs, bounds, mode, residual, ldr = sinks[j]
         rc = _C.lib().pt_gemm_splitk_reduce(ctypes.c_void_p(pr.C[0]), pr.ksplit, pr.kpart_stride, pr.M, pr.N,
-                                            _C.ptrarr([sk.C[i] or 0 for i in range(sk.nc)]),
-                                            _C.i64arr([sk.ldc[i] for i in range(sk.nc)]),
-                                            _C.i64arr([sk.c_bounds[i] for i in range(sk.nc + 1)]), sk.nc, sk.mode,
-                                            ctypes.c_void_p(sk.residual), sk.ldr, stream)
+                                            _C.ptrarr([_ptr(o) for o in outs]), _C.i64arr([o.stride(0) for o in outs]),
+                                            _C.i64arr(bounds), len(outs), int(mode), _ptr(residual), int(ldr), stream)
         _C.check(rc, "pt_gemm_splitk_reduce")
 
 
@@ -1210,6 +1185,25 @@ def attn_delta(dout, out, delta=None):
                                     _C.stream_ptr(out.device))
     _C.check(rc, "pt_attn_bwd_delta")
     return delta
+
+
+def attn_bwd_part(dout, q, k, v, lse, delta, scale, causal, dq=None, dk=None, dv=None, grad_f32=True):
+    """Only dQ (dk = dv = None) or only dK / dV (dq = None) of one attention block, accumulated into the
+    given f32 (grad_f32) or stored into bf16 tensors (pt_attn_bwd_part); lse / delta: the queries'
+    rows (f32 [B, H, Sq], any row stride shared by both)."""
+    B, Sq, H, D = q.shape
+    Sk, HKV = k.shape[1], k.shape[2]
+    parts = (1 if dq is not None else 0) | (2 if dk is not None else 0)
+    _req(parts in (1, 2) and (dk is None) == (dv is None), "attn_bwd_part: dq alone, or dk and dv")
+    ld = _lse_ld(lse, B, H, Sq)
+    _req(_lse_ld(delta, B, H, Sq, "delta") == ld, "attn_bwd_part: delta and lse rows must share a stride")
+    z = _C.i64arr([0, 0, 0])
+    rc = _C.lib().pt_attn_bwd_part(_ptr(q), _str3(q), _ptr(k), _str3(k), _ptr(v), _str3(v), _ptr(dout), _str3(dout),
+                                   _ptr(lse), _ptr(delta), _ptr(dq), _str3(dq) if dq is not None else z, _ptr(dk),
+                                   _str3(dk) if dk is not None else z, _ptr(dv), _str3(dv) if dv is not None else z,
+                                   B, H, HKV, Sq, Sk, D, float(scale), int(bool(causal)), int(bool(grad_f32)), ld,
+                                   parts, _C.stream_ptr(q.device))
+    _C.check(rc, "pt_attn_bwd_part")
 
 
 def attn_bwd(dout, q, k, v, out, lse, scale, causal, dq=None, dk=None, dv=None, grad_f32=False, delta=None,

@@ -939,40 +939,3 @@ def test_fewtile_splitk_matches_single_pass(monkeypatch, M, N, K, kind, residual
     torch.cuda.synchronize()
     assert rel_err(y, ref) < 4e-3
     assert maxabs(y, y1) <= 2 * y1.float().abs().max().item() * 2 ** -8
-
-
-@pytest.mark.parametrize("kind", ["wgrad_bf16_acc", "wgrad_f32_acc", "fwd_res", "dgrad"])
-def test_ksplit_fused_finish_matches_reduce_pass(monkeypatch, kind):
-    """pt_gemm_splitk_fused (the tile's last-arriving K-slice sums the partials in slice order and
-    writes the sink) is bit-identical to the grouped launch + pt_gemm_splitk_reduce pair, for the
-    TP-shard wgrad sinks (bf16 .grad / f32 main_grad accumulate, q|k|v-style row segments) and the
-    few-tile forward (residual epilogue) / dX GEMMs; run twice, so the counters it leaves must be
-    zero again."""
-    from picotron_amd import kernels as K_
-    g = torch.Generator().manual_seed(3)
-    T = 4096
-    outs = []
-    for fused in (1, 0, 1):
-        monkeypatch.setattr(switches.S, "ksplit_fused", fused)
-        torch.manual_seed(0)
-        if kind.startswith("wgrad"):
-            dy = torch.randn(T, 768, generator=g).to(BF).to(DEV) if not outs else dy
-            x = torch.randn(T, 2048, generator=g).to(BF).to(DEV) if not outs else x
-            dt = torch.float32 if kind == "wgrad_f32_acc" else BF
-            base = [torch.full((256, 2048), 0.5, dtype=dt, device=DEV) for _ in range(3)]
-            epi = K_.EPI_F32_ACC if dt == torch.float32 else K_.EPI_BF16_ACC
-            assert K_.wgrad_ksplit([(768, 2048, T)]) > 1
-            K_.linear_wgrad_grouped([(dy, x, base)], epilogue=epi)
-            outs.append(torch.cat(base))
-        elif kind == "fwd_res":
-            x = torch.randn(T, 2048, generator=g).to(BF).to(DEV) if not outs else x
-            w = (torch.randn(512, 2048, generator=g) / 45).to(BF).to(DEV) if not outs else w
-            r = torch.randn(T, 512, generator=g).to(BF).to(DEV) if not outs else r
-            outs.append(K_.linear_fwd(x, [w], residual=r))
-        else:
-            dy = torch.randn(T, 2048, generator=g).to(BF).to(DEV) if not outs else dy
-            w = (torch.randn(2048, 256, generator=g) / 45).to(BF).to(DEV) if not outs else w
-            outs.append(K_.linear_dgrad(dy, [w]))
-    torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
-    assert int(K_._kcounters(torch.device(DEV)).abs().sum()) == 0

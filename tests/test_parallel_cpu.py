@@ -194,6 +194,41 @@ class OracleBlocks:
         dv += dv_.view(B, nkv, nh // nkv, Sk, d).sum(2).transpose(1, 2)
 
 
+def _oracle_bwd_dq(do, q, k, v, lse, delta, scale, causal, dq):
+    """dQ only: the oracle block backward with the given LSE (delta is implied by the oracle)."""
+    _oracle_part(do, q, k, v, lse, delta, scale, causal, dq, None, None)
+
+
+def _oracle_bwd_dkdv(do, q, k, v, lse, delta, scale, causal, dk, dv):
+    _oracle_part(do, q, k, v, lse, delta, scale, causal, None, dk, dv)
+
+
+def _oracle_part(do, q, k, v, lse, delta, scale, causal, dq, dk, dv):
+    """One block's gradients from the rows' LSE and D = rowsum(dO * O) (FA2: dS = P (dP - D)), the
+    contract of pt_attn_bwd_part: no O needed."""
+    nh, nkv = q.shape[2], k.shape[2]
+    qq = q.float().transpose(1, 2)
+    kk, vv = OracleBlocks._expand(k, nh), OracleBlocks._expand(v, nh)
+    dd = do.float().transpose(1, 2)
+    s_ = qq @ kk.transpose(-1, -2) * scale
+    if causal:
+        Sq, Sk = s_.shape[-2], s_.shape[-1]
+        s_ = s_.masked_fill(torch.ones(Sq, Sk, dtype=torch.bool).triu(1), float("-inf"))
+    p_ = torch.exp(s_ - lse.unsqueeze(-1))
+    dp = dd @ vv.transpose(-1, -2)
+    ds = p_ * (dp - delta.unsqueeze(-1))
+    B, Sk, _, d = k.shape
+    if dq is not None:
+        dq += (ds @ kk * scale).transpose(1, 2)
+    if dk is not None:
+        dk += (ds.transpose(-1, -2) @ qq * scale).view(B, nkv, nh // nkv, Sk, d).sum(2).transpose(1, 2)
+        dv += (p_.transpose(-1, -2) @ dd).view(B, nkv, nh // nkv, Sk, d).sum(2).transpose(1, 2)
+
+
+OracleBlocks.bwd_dq = staticmethod(_oracle_bwd_dq)
+OracleBlocks.bwd_dkdv = staticmethod(_oracle_bwd_dkdv)
+
+
 def _ring(rank, world, nh, nkv):
     from oracle import picotron_oracle as O
     from picotron_amd import process_group_manager as pgm
