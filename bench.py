@@ -46,7 +46,7 @@ if ROOT not in sys.path:
 
 # HBM bytes per GEMM launch from rocprofv3 PMC passes (tools/gpu.sh counters: bench.py --grad-acc 2, then
 # tools/traffic_summary.py); read for the roofline's `traffic`
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03", "gemm_traffic_r03f2.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r04", "gemm_traffic_r04f.json")
 
 
 def log(*a):
@@ -182,11 +182,12 @@ def cp_proxy(args, base, layers):
       ring (the reference's transport): step s sends the K|V shard to the next rank while the
                  visiting block computes -- C - 1 sequential one-link hops forward; backward the K|V
                  hops plus C hops of the fp32 dK|dV accumulator (context_parallel.py:72-106);
-      mesh (shipped with the zig-zag layout): all C - 1 K|V shards fetched at once from their owners
-                 on C - 1 distinct links under the diagonal block; backward the K|V shards plus the
-                 visiting queries / dO (bf16) and LSE / D (f32) fetched the same way under the
-                 diagonal block's backward -- each rank computes its own keys' dK / dV, so no
-                 gradient partial travels;
+      mesh (shipped with the zig-zag layout): the visiting K|V fetched from their owners on C - 1
+                 links at once, first half-chunks under the diagonal block, the second halves a
+                 'q1' block needs under the first blocks; backward the K|V shards (under the
+                 diagonal block's backward) then the visiting queries / dO (bf16) and LSE / D (f32)
+                 (under the dQ parts) -- each rank computes its own keys' dK / dV, so no gradient
+                 partial travels;
       re-lay     the residual stream's zig-zag re-lay, twice per forward and twice per backward for
                  the whole stack (context_parallel.enable_zigzag_residual: on with the cp gradient
                  averaging of DataParallelBucket), amortised per layer."""
@@ -240,6 +241,17 @@ def cp_proxy(args, base, layers):
         "q1_fwd": lambda: K.attn_fwd(q[:, h:], k, v, sc, False, out=acc[:, h:], lse=lse[:, :, h:], merge=True),
         "q1_bwd": lambda: K.attn_bwd(do[:, h:], q[:, h:], k, v, o[:, h:], lse[:, :, h:], sc, False, dq=dq[:, h:], dk=dk,
                                      dv=dv, grad_f32=True, delta=delta[:, :, h:]),
+        # the mesh schedule's launches: a 'q1' forward as two quarters (second-half queries x one
+        # half-chunk of keys), the backward halves as dQ-only / dK|dV-only parts
+        "q1q_fwd": lambda: K.attn_fwd(q[:, h:], k[:, :h], v[:, :h], sc, False, out=acc[:, h:], lse=lse[:, :, h:],
+                                      merge=True),
+        "kv0_dq": lambda: K.attn_bwd_part(do, q, k[:, :h], v[:, :h], lse, delta, sc, False, dq=dq),
+        "q1_dq": lambda: K.attn_bwd_part(do[:, h:], q[:, h:], k, v, lse[:, :, h:], delta[:, :, h:], sc, False,
+                                         dq=dq[:, h:]),
+        "kv0_dkdv": lambda: K.attn_bwd_part(do, q, k[:, :h], v[:, :h], lse, delta, sc, False, dk=dk[:, :h],
+                                            dv=dv[:, :h]),
+        "q1_dkdv": lambda: K.attn_bwd_part(do[:, h:], q[:, h:], k, v, lse[:, :, h:], delta[:, :, h:], sc, False,
+                                           dk=dk, dv=dv),
     }
     t_layer = _events_time(layer, args.steps)
     t = {kname: _events_time(fn, args.steps * 4) for kname, fn in fns.items()}
@@ -261,19 +273,37 @@ def cp_proxy(args, base, layers):
     # ring: each step's transfer hides under that step's block
     ring_f = sum(max(kv_b / bw, tf) - tf for tf in halves_f)
     ring_b = sum(max((kv_b + dkv_b) / bw, tb) - tb for tb in halves_b) + dkv_b / bw   # + the last dK|dV hop
-    # mesh: each gather hides under the diagonal block (the backward's carries K|V + Q|dO|LSE|D)
-    mesh_f = max(0.0, kv_b / bw - t["diag_fwd"])
-    mesh_b = max(0.0, (kv_b + qdo_b) / bw - t["diag_bwd"])
+    # mesh (context_parallel.mesh_forward / mesh_backward), rank rk's own schedule: forward, batch A =
+    # every peer's first half-chunk (hidden under the diagonal block), batch B = the second halves
+    # of the peers j > rk, waited for after the 'kv0' blocks and the first 'q1' quarters; backward,
+    # batch A = the K|V shards (under the diagonal block's backward), batch B = Q|dO|LSE|D (under the
+    # dQ parts).  Per link the batches run back to back.
+    def mesh_rank(rk):
+        lo, hi = rk, C - 1 - rk                  # peers below / above
+        c_f = lo * t["kv0_fwd"] + hi * 2 * t["q1q_fwd"]
+        dq_parts = lo * t["kv0_dq"] + hi * t["q1_dq"]
+        c_b = dq_parts + hi * t["kv0_dkdv"] + lo * t["q1_dkdv"]
+        a_f = max(t["diag_fwd"], kv_b / 2 / bw)
+        x_f = a_f - t["diag_fwd"]
+        if hi:
+            x_f += max(0.0, kv_b / bw - (a_f + lo * t["kv0_fwd"] + hi * t["q1q_fwd"]))
+        a_b = max(t["diag_bwd"], kv_b / bw)
+        x_b = a_b - t["diag_bwd"] + max(0.0, (kv_b + qdo_b) / bw - (a_b + dq_parts))
+        return c_f + c_b, x_f, x_b
+    crit_m = max(range(C), key=lambda rk: sum(mesh_rank(rk)))
+    mesh_c, mesh_f, mesh_b = mesh_rank(crit_m)
     relay_t = relay_b / layers / (2 * bw)        # two peers, two links
     comm = {"link_GBps_per_direction": XGMI_LINK_GBPS, "kv_shard_bytes": kv_b, "dkv_f32_bytes": dkv_b,
             "ring": {"comm_bytes_per_layer": (C - 1) * kv_b + (C - 1) * kv_b + C * dkv_b,
                      "link_time_ms": ((C - 1) * kv_b * 2 + C * dkv_b) / bw * 1e3,
                      "exposed_ms": (ring_f + ring_b) * 1e3},
-            "mesh": {"comm_bytes_per_layer": (C - 1) * (2 * kv_b + qdo_b),
-                     "link_time_ms": (2 * kv_b + qdo_b) / bw * 1e3, "links": C - 1,
+            # received by the critical rank; its busiest link
+            "mesh": {"comm_bytes_per_layer": (C - 1) * (kv_b / 2 + kv_b + qdo_b) + (C - 1 - crit_m) * kv_b / 2,
+                     "link_time_ms": ((kv_b if crit_m < C - 1 else kv_b / 2) + kv_b + qdo_b) / bw * 1e3,
+                     "links": C - 1,
                      "exposed_ms": (mesh_f + mesh_b) * 1e3},
             "relayout": {"comm_bytes_per_pass": relay_b, "per_layer_ms": relay_t * 1e3}}
-    t_mesh = t_zz + mesh_f + mesh_b + relay_t
+    t_mesh = t_layer + mesh_c + mesh_f + mesh_b + relay_t
     t_ring_zz = t_zz + ring_f + ring_b + relay_t
     attn_compute = t["diag_fwd"] + t["diag_bwd"] + sum(halves_f) + sum(halves_b)
     layer_flop_model = 6 * (2 * H * nh * d + 2 * H * nkv * d + 3 * H * I) + 12 * H * args.seq   # per token
@@ -288,13 +318,15 @@ def cp_proxy(args, base, layers):
             "layer_ms": t_layer * 1e3, "block_fwd_ms": t_f * 1e3, "block_bwd_ms": t_b * 1e3,
             "blocks_ms": {kname: v * 1e3 for kname, v in t.items()},
             "half_block_kv0_ms": t_kv0 * 1e3, "half_block_q1_ms": t_q1 * 1e3, "critical_rank": crit,
+            "critical_rank_mesh": crit_m, "critical_rank_mesh_compute_ms": (t_layer + mesh_c) * 1e3,
             "critical_rank_layer_ms": t_zz * 1e3, "critical_rank_layer_ms_with_comm": {"mesh": t_mesh * 1e3,
                                                                                       "ring": t_ring_zz * 1e3},
             "reference_schedule_layer_ms": t_ref * 1e3,
             "reference_schedule_tokens_per_s_per_gpu": B * S / (t_ref * layers),
             "comm": comm,
-            "bound": {"mesh": "link" if mesh_f + mesh_b > 0.05 * attn_compute else "compute",
-                      "ring": "link" if ring_f + ring_b > 0.05 * attn_compute else "compute",
+            # link-bound: the layer's link time exceeds the attention compute it could hide under
+            "bound": {"mesh": "link" if comm["mesh"]["link_time_ms"] * 1e-3 > attn_compute else "compute",
+                      "ring": "link" if comm["ring"]["link_time_ms"] * 1e-3 > attn_compute else "compute",
                       "exposed_share_of_layer": {"mesh": (mesh_f + mesh_b + relay_t) / t_mesh,
                                                  "ring": (ring_f + ring_b + relay_t) / t_ring_zz}},
             "mfu_upper_bound": tok_gpu * layer_flop_model * layers / MI355X_BF16_DENSE_PEAK,

@@ -284,38 +284,54 @@ def _p2p_wait(pending):
         torch.cuda.synchronize()
 
 
-def mesh_gather_kv(kv):
-    """Post the fetch of every other cp rank's K|V shard straight from its owner: C - 1 sends of
-    this rank's kv and C - 1 receives, one batched p2p.  Returns ({rank: buffer}, pending)."""
-    m = pgm.current()
-    C, r, ids, group = m.cp_world_size, m.cp_rank, m.cp_group_ids, m.cp_group
-    bufs = {j: torch.empty_like(kv) for j in range(C) if j != r}
-    ops = [dist.P2POp(dist.isend, kv, ids[j], group=group) for j in bufs]
-    ops += [dist.P2POp(dist.irecv, bufs[j], ids[j], group=group) for j in bufs]
-    return bufs, _p2p(ops, group)
+def _mesh_ops(sends, recvs, group, ids):
+    """P2P ops of one batch: sends = [(tensor, rank)], recvs = [(tensor, rank)]."""
+    return ([dist.P2POp(dist.isend, t, ids[j], group=group) for t, j in sends]
+            + [dist.P2POp(dist.irecv, t, ids[j], group=group) for t, j in recvs])
+
+
+def _halves(kv, B, S):
+    """kv [B*S, 2w] -> its first / second half-chunk token rows, each [B*h, 2w] contiguous."""
+    h, w2 = S // 2, kv.shape[1]
+    kv3 = kv.view(B, S, w2)
+    return kv3[:, :h].contiguous().view(B * h, w2), kv3[:, h:].contiguous().view(B * h, w2)
 
 
 def mesh_forward(q, kv, nkv, scale, blocks=HipBlocks):
     """The zig-zag causal forward on the mesh: the diagonal block (local causal mask over this
-    rank's two half-chunks) runs while the K|V shards arrive; then each visiting shard j is half a
+    rank's two half-chunks) runs while the visiting K|V arrive; then each visiting shard j is half a
     block -- j < r: all my queries x its first half ('kv0'), j > r: my second half x all of it
-    ('q1') -- merged into the running (out, LSE) by the kernel epilogue."""
+    ('q1') -- merged into the running (out, LSE) by the kernel epilogue.  The fetch is two batched
+    p2ps, every peer's first half-chunk (all C - 1 links, half a shard each: hidden under the
+    diagonal block), then the second halves of the peers j > r only (the 'q1' peers), which arrive
+    while my second half x their first halves computes -- a 'q1' block runs as those two quarters."""
     m = pgm.current()
-    r = m.cp_rank
+    C, r, ids, group = m.cp_world_size, m.cp_rank, m.cp_group_ids, m.cp_group
     B, S, nh, d = q.shape
     h = S // 2
     acc = torch.zeros(B, S, nh, d, dtype=torch.float32, device=q.device)
     lse = torch.full((B, nh, S), float("-inf"), dtype=torch.float32, device=q.device)
-    bufs, pending = mesh_gather_kv(kv)
+    first, second = _halves(kv, B, S)
+    peers = [j for j in range(C) if j != r]
+    f = {j: torch.empty_like(first) for j in peers}
+    s = {j: torch.empty_like(second) for j in peers if j > r}
+    pend_a = _p2p(_mesh_ops([(first, j) for j in peers], [(f[j], j) for j in peers], group, ids), group)
+    ops_b = _mesh_ops([(second, j) for j in peers if j < r], [(s[j], j) for j in s], group, ids)
+    pend_b = _p2p(ops_b, group) if ops_b else None
     k, v = _kv_views(kv, B, S, nkv, d)
     blocks.fwd(q, k, v, scale, True, acc, lse)
-    _p2p_wait(pending)
-    for j, kvj in bufs.items():
-        k, v = _kv_views(kvj, B, S, nkv, d)
+    _p2p_wait(pend_a)
+    for j in peers:
+        k, v = _kv_views(f[j], B, h, nkv, d)
         if j < r:
-            blocks.fwd(q, k[:, :h], v[:, :h], scale, False, acc, lse)
+            blocks.fwd(q, k, v, scale, False, acc, lse)
         else:
             blocks.fwd(q[:, h:], k, v, scale, False, acc[:, h:], lse[:, :, h:])
+    if pend_b is not None:
+        _p2p_wait(pend_b)
+    for j in s:
+        k, v = _kv_views(s[j], B, h, nkv, d)
+        blocks.fwd(q[:, h:], k, v, scale, False, acc[:, h:], lse[:, :, h:])
     return acc, lse
 
 
@@ -323,16 +339,17 @@ def mesh_backward(do, q, kv, o, lse, nkv, scale, blocks=HipBlocks):
     """The zig-zag causal backward on the mesh, with no gradient partial on the wire: every rank
     fetches, besides the visiting K|V shards (for its own queries' dQ), the visiting ranks' queries,
     dO, LSE and D = rowsum(dO * O) -- 64 MiB + 0.5 MiB per peer at Llama-2-7B CP8, half of an fp32
-    dK|dV partial -- in ONE batched p2p under its diagonal block's backward, and computes its own
-    keys' dK / dV against them (the FA2 split of the backward: dQ over the visiting keys, dK / dV
-    over the visiting queries).  Visiting block kinds as the forward's: for my queries, shard j < r
-    is 'kv0' (all my queries x its first half), j > r 'q1' (my second half x all of it); for my keys,
-    rank j > r sees them as 'kv0' (all its queries x my first half), j < r as 'q1' (its second-half
-    queries x all my keys).  Returns (dq f32 [B,S,nh,d], dkv f32 [B*S, 2 w]) for this rank's shards."""
+    dK|dV partial -- and computes its own keys' dK / dV against them (the FA2 split of the backward:
+    dQ over the visiting keys, dK / dV over the visiting queries).  Two batched p2ps on all C - 1
+    links: the K|V shards (under the diagonal block's backward), then Q|dO|LSE|D (under the dQ
+    blocks).  Visiting block kinds as the forward's: for my queries, shard j < r is 'kv0' (all my
+    queries x its first half), j > r 'q1' (my second half x all of it); for my keys, rank j > r sees
+    them as 'kv0' (all its queries x my first half), j < r as 'q1' (its second-half queries x all my
+    keys).  Returns (dq f32 [B,S,nh,d], dkv f32 [B*S, 2 w]) for this rank's shards."""
     m = pgm.current()
     C, r, ids, group = m.cp_world_size, m.cp_rank, m.cp_group_ids, m.cp_group
     B, S, nh, d = q.shape
-    h, w = S // 2, nkv * d
+    h = S // 2
     delta = blocks.delta(do, o)
     dq = torch.zeros(B, S, nh, d, dtype=torch.float32, device=q.device)
     dkv = torch.zeros(kv.shape, dtype=torch.float32, device=kv.device)
@@ -343,22 +360,21 @@ def mesh_backward(do, q, kv, o, lse, nkv, scale, blocks=HipBlocks):
     kvs = {j: torch.empty_like(kv) for j in peers}
     qdos = {j: torch.empty_like(qdo) for j in peers}
     lds = {j: torch.empty_like(ld) for j in peers}
-    ops = []
-    for j in peers:
-        ops += [dist.P2POp(dist.isend, t, ids[j], group=group) for t in (kv, qdo, ld)]
-    for j in peers:
-        ops += [dist.P2POp(dist.irecv, t[j], ids[j], group=group) for t in (kvs, qdos, lds)]
-    pending = _p2p(ops, group)
+    pend_kv = _p2p(_mesh_ops([(kv, j) for j in peers], [(kvs[j], j) for j in peers], group, ids), group)
+    pend_q = _p2p(_mesh_ops([(t, j) for j in peers for t in (qdo, ld)],
+                            [(t[j], j) for j in peers for t in (qdos, lds)], group, ids), group)
     k, v = _kv_views(kv, B, S, nkv, d)
     dk, dv = _kv_views(dkv, B, S, nkv, d)
     blocks.bwd(do, q, k, v, o, lse, delta, scale, True, dq, dk, dv)
-    _p2p_wait(pending)
+    _p2p_wait(pend_kv)
     for j in peers:
         kj, vj = _kv_views(kvs[j], B, S, nkv, d)
         if j < r:    # my queries x its first half
             blocks.bwd_dq(do, q, kj[:, :h], vj[:, :h], lse, delta, scale, False, dq)
         else:        # my second half x all of it
             blocks.bwd_dq(do[:, h:], q[:, h:], kj, vj, lse[:, :, h:], delta[:, :, h:], scale, False, dq[:, h:])
+    _p2p_wait(pend_q)
+    for j in peers:
         qj = qdos[j][:, :, :nh * d].view(B, S, nh, d)
         doj = qdos[j][:, :, nh * d:].view(B, S, nh, d)
         lsej, dj = lds[j][:, :, 0], lds[j][:, :, 1]

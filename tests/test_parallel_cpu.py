@@ -279,8 +279,9 @@ class CountingBlocks(OracleBlocks):
 
 def _ring_zigzag(rank, world, nh, nkv, mesh):
     """The load-balanced (zig-zag) schedule: shards re-laid by zigzag_exchange, the balanced
-    schedule -- over the full mesh (mesh=1: every K|V shard fetched from its owner, dK|dV partials
-    sent back to it) or round the ring (mesh=0) -- outputs / gradients re-laid back: equal to full
+    schedule -- over the full mesh (mesh=1: K|V half-chunks and, in the backward, the peers'
+    Q|dO|LSE|D fetched from their owners; no gradient travels) or round the ring (mesh=0) --
+    outputs / gradients re-laid back: equal to full
     causal attention over the whole sequence on the reference's contiguous chunks, and every rank
     does the same causal work (the reference's schedule: rank r does r + 1 blocks)."""
     from picotron_amd import switches

@@ -8,11 +8,12 @@
 #   prof         rocprofv3 --kernel-trace --stats of bench.py --steps 2 (kernel table -> profiles via tools/prof_summary.py)
 #   pmc          GEMM/all-kernel HBM traffic: separate FETCH_SIZE and WRITE_SIZE passes over bench.py --grad-acc 2
 #   pmcx         extra counter sets over bench.py --grad-acc 1 (SQ busy/VALU/MFMA, TCC hit/miss/EA reads)
-#   configs      Llama-2-7B 1-GPU bench, TP=8 proxy, CP=8 proxy
+#   configs      llama + tp + cp: Llama-2-7B 1-GPU bench, TP=8 proxy, CP=8 proxy (each also a step)
 #   gloo2        bench.py --gpus 2 --backend gloo rehearsal (2 ranks on cuda:0)
 #   pp2          bench.py --gpus 2 --pp 2 --backend gloo rehearsal of the pipeline engine (config 4's 1F1B)
 #   grid8        bench.py --gpus 8 --backend gloo: DP=8, TP=8, config 4 (llama2-7b tp2 pp2), config 5 (cp8 32k)
 #   dp           bench.py --dp-bucket fp32 / bf16 vs plain (the per-GPU DP cost)
+#   dpprof       rocprofv3 kernel table of bench.py --dp-bucket (GT=fp32|bf16)
 #   attn         tools/attn_bench.py d64 and d128 (OLD=<lib> for an in-process A/B; ATTN64_ARGS for the d64 run)
 #   pmcattn      attention PMC passes (ATTN_ARGS="--B 1 --S 4096 --H 32 --D 128" for d128)
 #   norm         tools/norm_bench.py (OLD=<lib> for an A/B)
@@ -69,14 +70,22 @@ step_pmcx() {
   done
 }
 
-step_configs() {
+step_llama() {
   timeout -k 10 400 python -u bench.py --model llama2-7b --grad-acc 8 --steps 2 --warmup 1 --cpu-tokens 0 > $O.llama.json 2> $O.llama.err || { echo llama failed; tail $O.llama.err; return 1; }
   jline $O.llama.json llama2-7b
+}
+
+step_tp() {
   timeout -k 10 200 python -u bench.py --tp-proxy 8 --steps 3 > $O.tpproxy.json 2> $O.tpproxy.err || { echo tpproxy failed; tail $O.tpproxy.err; return 1; }
   jline $O.tpproxy.json tp8-proxy
-  timeout -k 10 300 python -u bench.py --cp-proxy 8 --model llama2-7b --seq 32768 --mbs 1 --steps 3 $CP_ARGS > $O.cpproxy.json 2> $O.cpproxy.err || { echo cpproxy failed; tail $O.cpproxy.err; return 1; }
-  python -c "import json; d=json.load(open('$O.cpproxy.json')); print('cp8 proxy', round(d['value']), round(d['compute_only_tokens_per_s_per_gpu']), {k: round(v,2) for k,v in d['critical_rank_layer_ms_with_comm'].items()}, d['bound'], round(d['roofline']['fwd_frac'],3), round(d['roofline']['bwd_frac'],3))"
 }
+
+step_cp() {
+  timeout -k 10 300 python -u bench.py --cp-proxy 8 --model llama2-7b --seq 32768 --mbs 1 --steps 3 $CP_ARGS > $O.cpproxy.json 2> $O.cpproxy.err || { echo cpproxy failed; tail $O.cpproxy.err; return 1; }
+  python -c "import json; d=json.load(open('$O.cpproxy.json')); print('cp8 proxy', round(d['value']), round(d['compute_only_tokens_per_s_per_gpu']), {k: round(v,2) for k,v in d['critical_rank_layer_ms_with_comm'].items()}, d['bound'], d['comm']['mesh']['exposed_ms'], round(d['roofline']['fwd_frac'],3), round(d['roofline']['bwd_frac'],3))"
+}
+
+step_configs() { step_llama && step_tp && step_cp; }
 
 step_gloo2() {
   timeout -k 10 400 python -u bench.py --gpus 2 --backend gloo --steps 1 --warmup 1 --grad-acc 4 > $O.gloo2.json 2> $O.gloo2.err || { echo gloo2 failed; tail -20 $O.gloo2.err; return 1; }
@@ -111,6 +120,12 @@ step_dp() {
   done
   timeout -k 10 300 python -u bench.py --steps 3 --cpu-tokens 0 > $O.plain.json 2>/dev/null || { echo plain failed; return 1; }
   jline $O.plain.json plain
+}
+
+step_dpprof() {   # kernel table of the DP path on a 1-rank RCCL group (fp32 main_grad sinks), beside prof's plain table
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O.dpprof -o k -- python -u bench.py --dp-bucket --grad-type ${GT:-fp32} --steps 2 --warmup 1 --cpu-tokens 0 > $O.dpprof.log 2>&1 || { echo dpprof failed; tail $O.dpprof.log; return 1; }
+  gzip -f $O.dpprof/k_kernel_trace.csv
+  python tools/prof_summary.py --trace $O.dpprof/k_kernel_trace.csv.gz --steps 3 > $O.dpkernels.md || true
 }
 
 step_attn() {
