@@ -1072,6 +1072,175 @@ __global__ __launch_bounds__(512) void gemm_4ph_kernel(const GemmGroup g) {
   gemm_4ph_tile<AK, BKC, EPI>(a, tile_m, tile_n, ks);
 }
 
+// ================================================================ 256x128, K-halves (tile 14)
+// The 4-phase kernel's tile and images with the 8-phase kernel's wave tile: the two wave groups
+// (waves 0-3, 4-7) take the two k-substeps of every K-tile (k 0-31 / 32-63), and inside a group
+// 2(M) x 2(N) waves each own a 128 x 64 output (8 x 4 accumulators) -- 12 LDS fragment reads per
+// 32 MFMAs instead of the 4-phase kernel's 16 (64 x 64 wave tiles), the LDS read rate the 8-phase
+// kernel runs at.  Images per K-tile: At / Ab = the 8-phase kernel's A half images (rows 0-63 /
+// 64-127 of each M-wave's 128), B = all 128 columns; the 4-phase kernel's three-K-tile ring, phase
+// anatomy, single counted wait per K-tile and wave-group stagger, unchanged.  After the K loop the
+// groups swap halves through LDS: group 0 finishes rows 0-63 of each wave tile, group 1 rows
+// 64-127 (each adds the other group's partial: g0 + g1 for every element), and each wave writes
+// its 64 x 64 through the common epilogue.
+template <bool AK, bool BKC, int EPI>
+__device__ __forceinline__ void gemm_kh_tile(const GemmArgs& a, const int tile_m, const int tile_n, const int ks = 0) {
+  constexpr int IMG = 128 * BK * 2;           // 16 KiB
+  constexpr int BUF = 3 * IMG;                // At, B, Ab
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+  lds_u8* smem = (lds_u8*)smem_raw;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = wave >> 2, wm = (wave >> 1) & 1, wn = wave & 1;
+  const int m0 = tile_m * 256, n0 = tile_n * 128;
+
+  const BImg bi = bimg_make(a, BKC, n0);
+  const int64_t ldb = bi.ld;
+  const int64_t lda = a.lda;
+  uint32_t vA[2][2], vB[2];
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int i = it * 8 + wave;
+    vA[0][it] = himg_voff<AK, 64>(i, lane, lda, 0);
+    vA[1][it] = himg_voff<AK, 64>(i, lane, lda, 64);
+    vB[it] = himg_voff<BKC, 128>(i, lane, ldb, 0);
+  }
+  const int kb = kslice_begin(a, ks);
+  const uint16_t* Ab0 = AK ? a.A + (int64_t)m0 * lda + kb : a.A + m0 + (int64_t)kb * lda;
+  auto a_ptr = [&](int t) { return AK ? Ab0 + t * BK : Ab0 + (int64_t)t * BK * lda; };
+  auto b_ptr = [&](int t) { return bimg_ptr(bi, BKC, kb + t * BK); };
+  // image h (0 At, 1 B, 2 Ab) of K-tile t into buffer buf: 2 DMA instructions per wave
+  auto stage = [&](int t, int buf, int h) {
+    lds_u8* dst = smem + buf * BUF + h * IMG;
+    const uint16_t* base = h == 1 ? b_ptr(t) : a_ptr(t);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const uint32_t vo = h == 1 ? vB[it] : vA[h == 2 ? 1 : 0][it];
+      glds16_asm(base, vo, dst + (it * 8 + wave) * 1024);
+    }
+  };
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = kslice_tiles(a);
+  stage(0, 0, 0); stage(0, 0, 1); stage(0, 0, 2);
+  if (nk > 1) {
+    stage(1, 1, 0); stage(1, 1, 1); stage(1, 1, 2);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+
+  auto bar = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  const int s = __builtin_amdgcn_readfirstlane(grp);  // this group's k-substep
+  bf16x8_t af[4], bf[4];
+  auto mma = [&](int i0) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i0 + i][j] = mfma16(af[i], bf[j], acc[i0 + i][j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  const bool late = s == 1;
+  if (late) bar();
+
+  auto ktile = [&](int t, auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
+    constexpr int nbuf = (buf + 2) % 3;  // K-tile t+2's buffer (freed by K-tile t-1)
+    const lds_u8* sAt = smem + buf * BUF;
+    const lds_u8* sB = sAt + IMG;
+    const lds_u8* sAb = sAt + 2 * IMG;
+    const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
+    // phase 1: At rows + B cols of substep s; stage At(t+2); rows 0-63 of the wave tile
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = read_frag<128, AK>(sAt, wm * 64 + i * 16, s, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[j] = read_frag<128, BKC>(sB, wn * 64 + j * 16, s, lane);
+    if (n2) stage(t + 2, nbuf, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    mma(0);
+    bar();
+    // phase 2: Ab rows; stage B, Ab of t+2; retire K-tile t+1; rows 64-127
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = read_frag<128, AK>(sAb, wm * 64 + i * 16, s, lane);
+    if (n2) {
+      stage(t + 2, nbuf, 1);
+      stage(t + 2, nbuf, 2);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else if (n1) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    mma(4);
+    bar();
+  };
+
+  int t = 0;
+  for (; t + 2 < nk; t += 3) {
+    ktile(t, std::integral_constant<int, 0>{});
+    ktile(t + 1, std::integral_constant<int, 1>{});
+    ktile(t + 2, std::integral_constant<int, 2>{});
+  }
+  if (t < nk) ktile(t, std::integral_constant<int, 0>{});
+  if (t + 1 < nk) ktile(t + 1, std::integral_constant<int, 1>{});
+  if (!late) bar();
+  __syncthreads();
+  // swap halves: wave w hands the 4 x 4 fragments the partner wave (w ^ 4) finishes -- group 0 its
+  // rows 64-127, group 1 its rows 0-63 -- through slot w (16 B per lane, lane-contiguous)
+  typedef __attribute__((address_space(3))) f32x4_t lds_f4;
+  lds_f4* slot = (lds_f4*)smem + wave * 16 * 64 + lane;
+  // (constant accumulator indices in each branch: an index that depends on the group would put
+  // the accumulators in scratch)
+  if (s == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) slot[(i * 4 + j) * 64] = acc[4 + i][j];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) slot[(i * 4 + j) * 64] = acc[i][j];
+  }
+  __syncthreads();
+  const lds_f4* peer = (const lds_f4*)smem + (wave ^ 4) * 16 * 64 + lane;
+  f32x4_t out[4][4];
+  if (s == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) out[i][j] = acc[i][j] + peer[(i * 4 + j) * 64];       // g0 + g1
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) out[i][j] = peer[(i * 4 + j) * 64] + acc[4 + i][j];   // g0 + g1
+  }
+  __syncthreads();
+  // the wave's 64 x 64 output: tile rows wm * 128 + s * 64 .., columns wn * 64 ..
+  epilogue<64, 64, EPI>(a, out, smem + wave * (64 * (64 * 2 + 16)), m0, n0, wm * 2 + s, wn, lane, nullptr,
+                        (int64_t)ks * a.kpart_stride);
+}
+
+template <bool AK, bool BKC, int EPI>
+__global__ __launch_bounds__(512) void gemm_kh_kernel(const GemmGroup g) {
+  int tile_m, tile_n, ks;
+  const GemmArgs& a = select_problem(g, tile_m, tile_n, ks);
+  gemm_kh_tile<AK, BKC, EPI>(a, tile_m, tile_n, ks);
+}
+
 // ------------------------------------------------------------------- mixed-tile launch (q|k|v)
 // One problem whose output columns [0, n_split) are covered by 256x256 8-phase tiles and
 // [n_split, N) by 256x128 4-phase tiles, in ONE launch.  For the q|k|v projection with RoPE
@@ -1293,24 +1462,42 @@ int launch_4ph(GemmGroup g, hipStream_t stream) {
   return PT_OK;
 }
 
+template <bool AK, bool BKC, int EPI>
+int launch_kh(GemmGroup g, hipStream_t stream) {
+  static_assert(EPI != EPI_CE_STATS && EPI != EPI_SWIGLU_FWD && EPI != EPI_SWIGLU_BWD, "tile 14 epilogues");
+  const int tiles = group_tiles(g, 256, 128);
+  constexpr int smem = 9 * 128 * BK * 2;  // 144 KiB: the ring; the half swap (128 KiB) and staging fit
+  static_assert(8 * 16 * 64 * 16 <= smem && 8 * 64 * (64 * 2 + 16) <= smem && smem <= 160 * 1024, "LDS budget");
+  static bool attr_set = false;
+  if (!attr_set) {
+    set_smem_once(gemm_kh_kernel<AK, BKC, EPI>, smem);
+    attr_set = true;
+  }
+  gemm_kh_kernel<AK, BKC, EPI><<<tiles, 512, smem, stream>>>(g);
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
+
 // tile ids: 2 = simple 128x128, 3 = simple 64x64 (the TP shards' few-tile problems),
 //           12 = 8-phase 256x256 (two half-image wave groups, one wait per K-tile)
 //           13 = 4-phase 256x128 (three K-tiles resident)
+//           14 = 256x128 with the K-tile's two k-substeps over two wave groups (128 x 64 wave tiles)
 //           (ids 4, 5, 8, 9 -- the simple 256x256 / 256x128 kernels and their two-substep forms --
 //           were never picked once the phased kernels existed, and the 256x256 ones spilled: dropped
 //           from the library in round 4; ids 0, 1, 6, 7, 10, 11 were pipelining experiments, measured slower and retired; so
 //           was round 2's 14: the 8-phase tile with ONE barrier per K-tile and free-running
 //           phases, 3-13 % slower on every layer shape -- the per-phase ping-pong pays for its
 //           barriers)
-constexpr int kNumTiles = 14;
-const int kTileBM[kNumTiles] = {0, 0, 128, 64, 0, 0, 0, 0, 0, 0, 0, 0, 256, 256};
-const int kTileBN[kNumTiles] = {0, 0, 128, 64, 0, 0, 0, 0, 0, 0, 0, 0, 256, 128};
+constexpr int kNumTiles = 15;
+const int kTileBM[kNumTiles] = {0, 0, 128, 64, 0, 0, 0, 0, 0, 0, 0, 0, 256, 256, 256};
+const int kTileBN[kNumTiles] = {0, 0, 128, 64, 0, 0, 0, 0, 0, 0, 0, 0, 256, 128, 128};
 
 template <bool AK, bool BKC, int EPI>
 int launch_layout(const GemmGroup& a, int tile, hipStream_t s) {
   switch (tile) {
     case 12: return launch_8ph<AK, BKC, EPI>(a, s);
     case 13: return launch_4ph<AK, BKC, EPI>(a, s);
+    case 14: return launch_kh<AK, BKC, EPI>(a, s);
     case 2: return launch_t<128, 128, 2, 2, AK, BKC, EPI>(a, s);
     case 3: return launch_t<64, 64, 2, 2, AK, BKC, EPI>(a, s);
     default: return PT_EUNSUPPORTED;
@@ -1423,7 +1610,7 @@ bool args_fit(const GemmArgs& a, int tile) {
   if (a.bdim == 0)
     for (int i = 0; i <= a.nbseg; ++i)
       if (a.bseg[i] % bn) return false;
-  if ((tile == 12 || tile == 13) && a.bdim == 1)  // the phased kernels keep one B ld per tile
+  if (tile >= 12 && a.bdim == 1)  // the phased kernels keep one B ld per tile
     for (int i = 1; i < a.nbseg; ++i)
       if (a.ldb[i] != a.ldb[0]) return false;
   return true;
@@ -1471,6 +1658,18 @@ int launch_swiglu(GemmGroup& g, int a_kcontig, int b_kcontig, int epilogue, int 
 
 // variant "gemm_mix" = 0 turns the mixed-tile q|k|v launch off (A/B measurement only)
 bool mix_enabled() { return pt_variant(PT_VAR_GEMM_MIX) == 1; }
+// variant "gemm_kh": where the auto pick chose 256x128 tiles, tile 14 (K-halves) instead of 13 --
+// 2 (default): when every problem's K (per split slice) is >= 4096, 1: always, 0: never.  Measured
+// (tools/gemm_bench.py, profiles/r04/notes_r04.md): +2-11 % at K 4096-49152 (down_proj forward
+// 1309 vs 1253 TF/s), equal or -4.5 % at K 2048 (o_proj forward / dX), where the half swap
+// through LDS is a larger share of a short K loop.
+bool kh_enabled(const GemmGroup& g) {
+  const int v = pt_variant(PT_VAR_GEMM_KH);
+  if (v != 2) return v == 1;
+  for (int i = 0; i < g.nprob; ++i)
+    if (g.p[i].K / (g.p[i].ksplit > 1 ? g.p[i].ksplit : 1) < 4096) return false;
+  return true;
+}
 
 // q|k|v + RoPE as one mixed-tile launch: the rotated columns [0, rope_cols) in 256x256 tiles, the
 // rest (v) in 256x128 tiles.  PT_EUNSUPPORTED when the shape does not split that way (the caller
@@ -1512,14 +1711,17 @@ int launch_group(GemmGroup& g, int a_kcontig, int b_kcontig, int epilogue, int t
     const int rc = launch_mix_rope(g.p[0], stream);
     if (rc != PT_EUNSUPPORTED) return rc;
   }
+  const bool auto_tile = tile < 0;
   if (epilogue == EPI_ROPE && tile < 0) tile = args_fit(g.p[0], 13) ? 13 : 12;
   if (tile < 0) tile = pick_group_tile(g);
+  if (auto_tile && tile == 13 && kh_enabled(g) && epilogue != EPI_CE_STATS) tile = 14;
   if (epilogue == EPI_ROPE) {
     if (!a_kcontig || !b_kcontig) return PT_EUNSUPPORTED;
     for (int i = 0; i < g.nprob; ++i)
       if (!args_fit(g.p[i], tile)) return PT_EUNSUPPORTED;
     if (tile == 12) return launch_8ph<true, true, EPI_ROPE>(g, stream);
     if (tile == 13) return launch_4ph<true, true, EPI_ROPE>(g, stream);
+    if (tile == 14) return launch_kh<true, true, EPI_ROPE>(g, stream);
     return PT_EUNSUPPORTED;
   }
   for (int i = 0; i < g.nprob; ++i)

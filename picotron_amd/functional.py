@@ -522,11 +522,15 @@ def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True, keep_parts=False)
         K.swiglu_bwd(dhh, gu[:, :I], gu[:, I:], dg=dgu[:, :I], du=dgu[:, I:])
         wgrad(dm, hh, [wd])
     dh = handle = None
+    split = SW.gu_splitk != 0
     if need_dx and tp.world_size == 1 and _dual_gu_enabled() and \
-            K._splitk_halves(dgu.shape[0], h2.shape[1], dgu.shape[1]) is not None:
-        # the split-K gate|up dX (two f32 K halves, 256 tiles) and the gate|up dW (512 tiles) in one
-        # dual launch: 3 whole rounds of the 256 CUs (no TP all-reduce to overlap at tp = 1)
-        return dgrad_with_wgrad(dgu, [wg, wu], [(dgu, h2, [wg, wu])], keep_parts=keep_parts)
+            (not split or K._splitk_halves(dgu.shape[0], h2.shape[1], dgu.shape[1]) is not None):
+        # the gate|up dX and dW (512 tiles) in one dual launch (no TP all-reduce to overlap at
+        # tp = 1): the dX as two split-K f32 halves (256 tiles: 3 whole rounds of the 256 CUs), or
+        # (gu_splitk = 0) unsplit -- 128 tiles twice as long as a dW tile, beside which the other
+        # CUs run four dW tiles each, and a bf16 dX for the norm backward to read
+        return dgrad_with_wgrad(dgu, [wg, wu], [(dgu, h2, [wg, wu])], keep_parts=keep_parts,
+                                split_min=None if split else 1 << 30)
     if need_dx:
         dh = K.linear_dgrad(dgu, [wg, wu])
         handle = tp.all_reduce(dh, async_op=True)

@@ -1079,8 +1079,14 @@ def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None, keep
     if probe is not None:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
+    if order is None:
+        order = _dual_order()
+        # unsplit dX tiles longer (in K) than the dW tiles: dX first on every XCD, the dW tiles
+        # chaining on the other CUs around them (a dW-first XCD would start its dX tiles last)
+        if e0 == EPI_BF16 and wjobs and N > max(dy.shape[0] for dy, _, _ in wjobs):
+            order = 0
     rc = _C.lib().pt_gemm_dual(p0s, len(p0s), 1, 0, e0, p1s, len(wjobs), 0, 0, EPI_F32 if ws > 1 else int(wepilogue),
-                               _dual_order() if order is None else int(order), _C.stream_ptr(dy2d.device))
+                               int(order), _C.stream_ptr(dy2d.device))
     if rc == -3:   # PT_EUNSUPPORTED: outside the dual tiling (e.g. C segments not on 256 rows)
         return None
     _C.check(rc, f"pt_gemm_dual(dX epi {e0}, {len(wjobs)} wgrads epi {wepilogue}, split {ws})")

@@ -15,8 +15,8 @@ import os
 DEFAULTS = {
     # functional.py: the fused epilogues (RoPE in the q|k|v GEMM and attention backward, SwiGLU in the
     # gate|up / down GEMMs), deferred norm-weight column sums, lm_head CE statistics, the q|k|v and
-    # gate|up dX + dW dual launches
-    "fuse": 1, "norm_defer": 1, "ce_stats": 1, "dual_qkv": 1, "dual_gu": 1,
+    # gate|up dX + dW dual launches (the latter's dX as split-K halves or unsplit)
+    "fuse": 1, "norm_defer": 1, "ce_stats": 1, "dual_qkv": 1, "dual_gu": 1, "gu_splitk": 1,
     # kernels.py: weight-gradient / few-tile forward and dX K-slices, split-K dgrad halves (and their minimum K), dX + dW dual
     # launches and their XCD order, the norm backward fed by split-K halves, the attention
     # backward's fused delta, and the tile-count thresholds below which the RoPE / SwiGLU epilogues
@@ -27,9 +27,9 @@ DEFAULTS = {
     # in that layout across the decoder stack, the full-mesh K|V / dK|dV exchange instead of the ring
     "ring_zigzag": 1, "zigzag_residual": 1, "ring_mesh": 1,
     # native (libpicotron_hip.so, pt_set_variant)
-    "attn_pair": 1, "attn_split": 2, "gemm_group_m": -1, "gemm_mix": 1,
+    "attn_pair": 1, "attn_split": 2, "gemm_group_m": -1, "gemm_mix": 1, "gemm_kh": 2,
 }
-NATIVE = ("attn_pair", "attn_split", "gemm_group_m", "gemm_mix")
+NATIVE = ("attn_pair", "attn_split", "gemm_group_m", "gemm_mix", "gemm_kh")
 
 
 class _Switches:

@@ -245,7 +245,7 @@ def test_gemm_fwd_nt(M, N, K):
     assert rel_err(y, _ref_mm(x, w.t())) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [2, 3, 12, 13])
+@pytest.mark.parametrize("tile", [2, 3, 12, 13, 14])
 def test_gemm_every_tile_every_layout(tile):
     from picotron_amd import kernels as K_
     M, N, K = 512, 512, 256
@@ -276,12 +276,12 @@ def test_gemm_retired_tiles_are_refused():
             K_.linear_fwd(a, [b], tile=t)
 
 
-@pytest.mark.parametrize("tile", [12, 13])
+@pytest.mark.parametrize("tile", [12, 13, 14])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 192), (768, 512, 512), (256, 512, 2048),
                                    (512, 256, 320), (256, 256, 128)])
 def test_gemm_8phase_shapes(M, N, K, tile):
-    """the phased kernels (tile 12: 256x256, 13: 256x128): 1-5 K-tiles (every remainder of the
-    2- and 3-buffer loops), every layout"""
+    """the phased kernels (tile 12: 256x256, 13: 256x128, 14: 256x128 K-halves): 1-5 K-tiles (every
+    remainder of the 2- and 3-buffer loops), every layout"""
     from picotron_amd import kernels as K_
     a = torch.randn(M, K).to(BF)
     b = (torch.randn(N, K) / 16).to(BF)
@@ -302,6 +302,35 @@ def test_gemm_8phase_shapes(M, N, K, tile):
     y = K_.linear_fwd(eye.to(DEV), [b.to(DEV)], tile=tile)
     torch.cuda.synchronize()
     assert torch.equal(y.cpu()[:min(M, K)], b.t()[:min(M, K)])
+
+
+@pytest.mark.parametrize("T,N,K", [(4096, 2048, 2048), (4096, 2048, 8192), (1024, 384, 1024)])
+def test_gemm_khalves_tile_at_layer_shapes(T, N, K):
+    """Tile 14 (256x128, the K-tile's two k-substeps over two wave groups, partials summed through
+    LDS) on the layer's 256x128 launches -- o_proj forward / dX (K 2048), down_proj forward with the
+    residual (K 8192) -- against the fp32 reference and the 4-phase tile 13 (a different f32
+    summation order: within bf16 rounding of it), and the auto pick under switch gemm_kh."""
+    from picotron_amd import kernels as K_
+    from picotron_amd import switches
+    g = torch.Generator().manual_seed(T + N + K)
+    x = torch.randn(T, K, generator=g).to(BF)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(BF)
+    res = torch.randn(T, N, generator=g).to(BF)
+    xd, wd, rd = x.to(DEV), w.to(DEV), res.to(DEV)
+    ref = _ref_mm(x, w.t())
+    y14 = K_.linear_fwd(xd, [wd], tile=14)
+    y13 = K_.linear_fwd(xd, [wd], tile=13)
+    assert rel_err(y14, ref) < 1e-2 and rel_err(y14, y13.float().cpu()) < 1e-2
+    yr = K_.linear_fwd(xd, [wd], tile=14, residual=rd)
+    assert rel_err(yr, (res.float() + y14.float().cpu()).to(BF).float()) < 1e-2
+    dy = torch.randn(T, N, generator=g).to(BF)
+    w2 = (torch.randn(N, K, generator=g) / N ** 0.5).to(BF)
+    dx = K_.linear_dgrad(dy.to(DEV), [w2.to(DEV)], tile=14)
+    assert rel_err(dx, _ref_mm(dy, w2)) < 1e-2
+    with switches.override(gemm_kh=1):
+        ya = K_.linear_fwd(xd, [wd])
+    torch.cuda.synchronize()
+    assert rel_err(ya, ref) < 1e-2
 
 
 @pytest.mark.parametrize("epi", [0, 1, 3])

@@ -103,6 +103,25 @@ def test_smollm_layer_qkv_dx_split_beside_dw(monkeypatch):
     assert rel(dx1, dx0) < 1e-3
 
 
+def test_smollm_layer_gate_up_dx_unsplit_beside_dw(monkeypatch):
+    """gu_splitk = 0: the gate|up dX runs unsplit (bf16, 128 tiles) beside the gate|up dW in the
+    dual launch (dX tiles first on every XCD) and the post-attention norm reads it directly.  The dW
+    tiles and the forward are bit-identical to the split form; dX, the norm's weight gradient and
+    everything below them differ only by the f32 split-K order."""
+    outs = []
+    for v in (1, 0):
+        monkeypatch.setattr(switches.S, "gu_splitk", v)
+        outs.append(_layer_grads(B=4, S=1024, H=2048, I=8192, nh=32, nkv=32, d=64, seed=13))
+    (y0, dx0, *g0), (y1, dx1, *g1) = outs
+    assert torch.equal(y0, y1)
+    for n, a, b in zip(NAMES, g0, g1):
+        if n in ("mlp.gate_proj.weight", "mlp.up_proj.weight", "mlp.down_proj.weight"):
+            assert torch.equal(a, b), n
+        else:
+            assert rel(b, a) < 5e-3, n
+    assert rel(dx1, dx0) < 5e-3
+
+
 def _layer_parity(B, S, H, I, nh, nkv, d, seed=0, main_grad=False):
     """One decoder layer (model.py:204-209) fwd + bwd through functional.DecoderLayerFunction (the
     node model.DecoderLayer runs) at these dims vs the oracle.  main_grad: every weight carries an

@@ -14,6 +14,7 @@
 #   grid8        bench.py --gpus 8 --backend gloo: DP=8, TP=8, config 4 (llama2-7b tp2 pp2), config 5 (cp8 32k)
 #   dp           bench.py --dp-bucket fp32 / bf16 vs plain (the per-GPU DP cost)
 #   dpprof       rocprofv3 kernel table of bench.py --dp-bucket (GT=fp32|bf16)
+#   gemm         tools/gemm_bench.py --brief (GTILES=12,13,14, GEMM_ARGS)
 #   attn         tools/attn_bench.py d64 and d128 (OLD=<lib> for an in-process A/B; ATTN64_ARGS for the d64 run)
 #   pmcattn      attention PMC passes (ATTN_ARGS="--B 1 --S 4096 --H 32 --D 128" for d128)
 #   norm         tools/norm_bench.py (OLD=<lib> for an A/B)
@@ -126,6 +127,11 @@ step_dpprof() {   # kernel table of the DP path on a 1-rank RCCL group (fp32 mai
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O.dpprof -o k -- python -u bench.py --dp-bucket --grad-type ${GT:-fp32} --steps 2 --warmup 1 --cpu-tokens 0 > $O.dpprof.log 2>&1 || { echo dpprof failed; tail $O.dpprof.log; return 1; }
   gzip -f $O.dpprof/k_kernel_trace.csv
   python tools/prof_summary.py --trace $O.dpprof/k_kernel_trace.csv.gz --steps 3 > $O.dpkernels.md || true
+}
+
+step_gemm() {    # tools/gemm_bench.py over the layer's shapes (GTILES, GEMM_ARGS e.g. "--tp 8")
+  timeout -k 10 300 python -u tools/gemm_bench.py --tiles ${GTILES:-12,13,14} --brief $GEMM_ARGS > $O.gemm.log 2>&1 || { echo gemm failed; tail $O.gemm.log; return 1; }
+  cat $O.gemm.log
 }
 
 step_attn() {
