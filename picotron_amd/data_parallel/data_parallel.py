@@ -12,7 +12,9 @@ Two gradient paths feed the buckets:
   * parameters consumed by the fused kernels (every projection and norm weight) have their
     gradient written into main_grad by the kernel epilogue itself; the kernels then call
     `param._pt_grad_ready`, which does the reference hook's remaining work (queue the
-    post-backward callback, mark the parameter ready).
+    post-backward callback, mark the parameter ready); `param._pt_grad_sync()` tells them whether
+    this backward all-reduces at all (outside `no_sync`), so the norm weights' column sums can be
+    batched at the end of the micro-batches that do not.
 """
 import contextlib
 
@@ -50,9 +52,14 @@ class DataParallelNaive(nn.Module):
             if p.requires_grad:
                 p.register_post_accumulate_grad_hook(self._allreduce_grads)
                 p._pt_grad_ready = self._allreduce_grads
+                p._pt_grad_sync = self._sync_wanted
 
     def forward(self, *inputs, **kwargs):
         return self.module(*inputs, **kwargs)
+
+    def _sync_wanted(self):
+        """Whether this backward all-reduces (the fused kernels then report each gradient at once)."""
+        return self.require_backward_grad_sync
 
     def _allreduce_grads(self, param):
         if self.require_backward_grad_sync and param.grad is not None:
@@ -94,6 +101,7 @@ class DataParallelBucket(nn.Module):
                 grad_acc_fn.register_hook(self._make_param_hook(param))
                 self.grad_accs.append(grad_acc_fn)
                 param._pt_grad_ready = self._fused_grad_ready
+                param._pt_grad_sync = self._sync_wanted
 
     def _ready(self, param):
         if self.require_backward_grad_sync:
@@ -114,6 +122,9 @@ class DataParallelBucket(nn.Module):
 
     def _fused_grad_ready(self, param):
         self._ready(param)
+
+    def _sync_wanted(self):
+        return self.require_backward_grad_sync
 
     @contextlib.contextmanager
     def no_sync(self):

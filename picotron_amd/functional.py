@@ -141,8 +141,9 @@ def dgrad_with_wgrad(dy2d, weights, wjobs, gu=None, keep_parts=False, split_min=
 # no DataParallelBucket owner waiting on it leaves its per-block partial rows here, and one
 # pt_rmsnorm_colsum_batch launch at the end of the backward (an engine final callback) sums them
 # all into their sinks -- 2 L + 1 column-sum launches per micro-batch become one.  Norms whose
-# weights carry a _pt_grad_ready hook keep the immediate sum (their bucket's all-reduce overlaps the
-# rest of the backward).  PICOTRON_NORM_DEFER=0 turns this off (A/B only).
+# weights' owner all-reduces during this backward (a _pt_grad_ready hook, and _pt_grad_sync() true:
+# the last micro-batch of a step) keep the immediate sum, so their bucket's all-reduce overlaps the
+# rest of the backward; under no_sync (the other grad_acc - 1 micro-batches) they defer too.  PICOTRON_NORM_DEFER=0 turns this off (A/B only).
 _PENDING_DW = {}   # autograd graph task id -> [(partial, weight, stream)]
 
 
@@ -186,7 +187,10 @@ def norm_bwd(dy2, z, weight, rstd, mode, dres=None, need_dw=True):
         dx, _ = K.rmsnorm_bwd(dy2, z, weight, rstd, mode, dres=dres)
         return dx
     task = torch._C._current_graph_task_id()   # -1 outside an autograd backward
-    if getattr(weight, "_pt_grad_ready", None) is None and z.is_cuda and task != -1 and _norm_defer_enabled():
+    # an owner that all-reduces this backward (a data-parallel wrapper outside no_sync) is told at once
+    sync = getattr(weight, "_pt_grad_sync", None)
+    waiting = getattr(weight, "_pt_grad_ready", None) is not None and (sync is None or sync())
+    if not waiting and z.is_cuda and task != -1 and _norm_defer_enabled():
         dx, partial = K.rmsnorm_bwd(dy2, z, weight, rstd, mode, dres=dres, defer_dw=True)
         if task not in _PENDING_DW:
             _PENDING_DW[task] = []
