@@ -56,7 +56,9 @@ def main():
     ap.add_argument("--old", default="")
     ap.add_argument("--model-path", action="store_true",
                     help="causal: time the backward as the layer calls it (delta inside, no precomputed delta)")
-    ap.add_argument("--env-ab", default="", help="VAR: time the new library with VAR=1 and with VAR=0 (an env A/B)")
+    ap.add_argument("--variant", default="",
+                    help="NAME=V1,V2,...: time the new library once per value of this native variant "
+                         "(pt_set_variant; e.g. attn_fwd64=0,1,2), compared like --old builds")
     ap.add_argument("--full", action="store_true",
                     help="the CP ring's visiting block: no causal mask, f32 dq/dk/dv accumulators (grad_f32)")
     ap.add_argument("--rounds", type=int, default=2, help="interleaved rounds; medians are printed at the end")
@@ -74,11 +76,15 @@ def main():
     libs = {"new": _C.load_library()}
     for i, path in enumerate(x for x in a.old.split(",") if x):   # comma-separated: old, old1, old2 ...
         libs["old" if i == 0 else f"old{i}"] = _C.load_library(os.path.abspath(path), strict=False)
-    envs = {name: {} for name in libs}
-    if a.env_ab:   # the new library with VAR=1 ("new") and once more with VAR=0 ("old" in the comparison)
-        envs["new"] = {a.env_ab: "1"}
-        libs["old" if "old" not in libs else "new_" + a.env_ab + "0"] = libs["new"]
-        envs[list(libs)[-1]] = {a.env_ab: "0"}
+    variants = {name: {} for name in libs}
+    if a.variant:   # the new library once per value: arm "new" = the first value, "<var>=<v>" the others
+        var, vals = a.variant.split("=")
+        vals = [int(x) for x in vals.split(",")]
+        variants["new"] = {var: vals[0]}
+        for v in vals[1:]:
+            libs[f"{var}={v}"] = libs["new"]
+            variants[f"{var}={v}"] = {var: v}
+    defaults = {}
     outs = {}
     med = {name: {"fwd": [], "bwd": []} for name in libs}
     for rnd in range(a.rounds):
@@ -86,9 +92,10 @@ def main():
         order = order[rnd % len(order):] + order[:rnd % len(order)]   # rotate who goes first
         for name, lib in order:
             _C._lib = lib
-            for var in {v for e in envs.values() for v in e}:
-                os.environ.pop(var, None)
-            os.environ.update(envs[name])
+            for var, val in variants[name].items():
+                if var not in defaults:
+                    defaults[var] = lib.pt_get_variant(var.encode())
+                lib.pt_set_variant(var.encode(), int(val))
             o, lse = K.attn_fwd(q, k, v, scale, causal)
             delta = K.attn_delta(do, o)
             if a.full:
@@ -110,6 +117,8 @@ def main():
             outs[name] = [t.clone() for t in (o, lse, dq, dk, dv)]
             t_fwd = graph_us(lambda: K.attn_fwd(q, k, v, scale, causal, out=o, lse=lse), a.reps)
             t_bwd = graph_us(bwd, a.reps)
+            for var, val in defaults.items():
+                lib.pt_set_variant(var.encode(), int(val))
             med[name]["fwd"].append(t_fwd)
             med[name]["bwd"].append(t_bwd)
             print(json.dumps({"lib": f"{name}:r{rnd}", "B": B, "S": S, "H": H, "D": D, "causal": causal,
