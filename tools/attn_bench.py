@@ -81,9 +81,9 @@ def main():
         var, vals = a.variant.split("=")
         vals = [int(x) for x in vals.split(",")]
         variants["new"] = {var: vals[0]}
-        for v in vals[1:]:
-            libs[f"{var}={v}"] = libs["new"]
-            variants[f"{var}={v}"] = {var: v}
+        for val in vals[1:]:
+            libs[f"{var}={val}"] = libs["new"]
+            variants[f"{var}={val}"] = {var: val}
     defaults = {}
     outs = {}
     med = {name: {"fwd": [], "bwd": []} for name in libs}
