@@ -292,7 +292,7 @@ constexpr int dq_stages() { return D == 64 ? 4 : 2; }
 // ============================================================================ forward
 // NWK waves per workgroup (32 query rows each): 4, or 8 at d 128 (the K/V tiles staged once for
 // twice the queries; measured 7-8 % faster at S_local 4096, equal at d 64)
-template <int D, int NWK, int NS_ = fwd_stages<D, NWK>()>
+template <int D, int NWK>
 __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_or_hk, int b) {
   constexpr int DT = D / 32, KS = D / 16;
   constexpr int TILE_B = KT * D * 2;
@@ -322,7 +322,7 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
   for (int i = 0; i < DT; ++i) o[i] = zero16();
   float m = -INFINITY, l = 0.f;
 
-  constexpr int NS = NS_, OPS = 2 * (KT * D * 2 / 1024) / NWK;
+  constexpr int NS = fwd_stages<D, NWK>(), OPS = 2 * (KT * D * 2 / 1024) / NWK;
   auto stage = [&](int kt, int buf) {
     lds_u8* sk = smem + buf * 2 * TILE_B;
     stage_rows<D, NWK>(kbase + (int64_t)kt * KT * a.k_ss, a.k_ss, sk, wave, lane);
@@ -453,13 +453,13 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
   }
 }
 
-template <int D, int NWK, int NS = fwd_stages<D, NWK>(), int WPE = 1>
-__global__ __launch_bounds__(NWK * 64) __attribute__((amdgpu_waves_per_eu(WPE))) void attn_fwd_kernel(AttnArgs a) {
+template <int D, int NWK>
+__global__ __launch_bounds__(NWK * 64) void attn_fwd_kernel(AttnArgs a) {
   int bx, hh, b;
   attn_coords(a, bx, hh, b);
   for (int pass = 0; pass <= a.pair; ++pass) {  // one inlined body: no register growth
     if (pass) __syncthreads();
-    attn_fwd_block<D, NWK, NS>(a, pass ? a.Sq / (NWK * 32) - 1 - bx : bx, hh, b);
+    attn_fwd_block<D, NWK>(a, pass ? a.Sq / (NWK * 32) - 1 - bx : bx, hh, b);
   }
 }
 
@@ -872,7 +872,7 @@ __global__ __launch_bounds__(8 * 64) void attn_bwd_dkdv_pair_kernel(AttnArgs a) 
 }
 
 // ============================================================================ dQ
-template <int D, int NS_ = dq_stages<D>()>
+template <int D>
 __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int h_or_hk, int b) {
   constexpr int DT = D / 32, KS = D / 16;
   constexpr int TILE_B = KT * D * 2;
@@ -918,7 +918,7 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
 #pragma unroll
   for (int i = 0; i < DT; ++i) dq[i] = zero16();
 
-  constexpr int NS = NS_, OPS = 2 * (KT * D * 2 / 1024) / NW;
+  constexpr int NS = dq_stages<D>(), OPS = 2 * (KT * D * 2 / 1024) / NW;
   auto stage = [&](int kt, int buf) {
     lds_u8* sk = smem + buf * 2 * TILE_B;
     stage_rows<D>(kbase + (int64_t)kt * KT * a.k_ss, a.k_ss, sk, wave, lane);
@@ -1001,14 +1001,14 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
   }
 }
 
-template <int D, int NS = dq_stages<D>(), int WPE = (D == 128 ? 2 : 1)>
-__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
+template <int D>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(D == 128 ? 2 : 1)))
 void attn_bwd_dq_kernel(AttnArgs a) {
   int bx, hh, b;
   attn_coords(a, bx, hh, b);
   for (int pass = 0; pass <= a.pair; ++pass) {  // one inlined body: no register growth
     if (pass) __syncthreads();
-    attn_bwd_dq_block<D, NS>(a, pass ? nqb_of(a) - 1 - bx : bx, hh, b);
+    attn_bwd_dq_block<D>(a, pass ? nqb_of(a) - 1 - bx : bx, hh, b);
   }
 }
 
@@ -1019,15 +1019,6 @@ void set_smem(K kern, int bytes) {
 
 // causal block pairing (variant "attn_pair"; 0 = off, A/B measurement only)
 bool pair_enabled() { return pt_variant(PT_VAR_ATTN_PAIR) == 1; }
-
-// d64 forward occupancy form (variant "attn_fwd64"): 0 = 4-stage K/V ring (64 KiB LDS), causal
-// pairs, two workgroups per CU; 1 / 2 = 2-stage ring (32 KiB), one block per workgroup (heavy
-// blocks first), registers capped for 3 / 4 workgroups per CU -- more waves per SIMD to hide the
-// per-tile dependency chain instead of a deeper DMA ring
-int fwd64_form() { return pt_variant(PT_VAR_ATTN_FWD64); }
-// d64 dQ kernel form (variant "attn_dq64"): 0 = 4-stage ring, causal pairs; 1 = 2-stage ring, one
-// block per workgroup, registers capped for 3 workgroups per CU (as attn_fwd64 = 1)
-int dq64_form() { return pt_variant(PT_VAR_ATTN_DQ64); }
 
 // dK/dV kernel form per head dim (variant "attn_split"): bit 0 = d64, bit 1 = d128 use the wave-pair
 // split; default d128 only
@@ -1075,17 +1066,10 @@ int pt_attn_fwd(const void* q, const int64_t* q_str, const void* k, const int64_
   if (rc) return rc;
   const int nwk = (D == 128 && Sq % (8 * 32) == 0) ? 8 : NW;
   const int nqb = (int)(Sq / (nwk * 32));
-  const int form = D == 64 ? fwd64_form() : 0;
-  a.pair = causal && nqb % 2 == 0 && pair_enabled() && form == 0;
+  a.pair = causal && nqb % 2 == 0 && pair_enabled();
   const dim3 grid((unsigned)(a.pair ? nqb / 2 : nqb), (unsigned)H, (unsigned)B);
   const int stage_b = 2 * KT * (int)D * 2;
-  if (D == 64 && form == 1) {
-    set_smem(attn_fwd_kernel<64, NW, 2, 3>, 2 * stage_b);
-    attn_fwd_kernel<64, NW, 2, 3><<<grid, NW * 64, 2 * stage_b, stream>>>(a);
-  } else if (D == 64 && form == 2) {
-    set_smem(attn_fwd_kernel<64, NW, 2, 4>, 2 * stage_b);
-    attn_fwd_kernel<64, NW, 2, 4><<<grid, NW * 64, 2 * stage_b, stream>>>(a);
-  } else if (D == 64) {
+  if (D == 64) {
     const int smem = fwd_stages<64, NW>() * stage_b;
     set_smem(attn_fwd_kernel<64, NW>, smem);
     attn_fwd_kernel<64, NW><<<grid, NW * 64, smem, stream>>>(a);
@@ -1187,14 +1171,7 @@ int attn_bwd_impl(const void* q, const int64_t* q_str, const void* k, const int6
   const bool split = (split_mask() >> (D == 64 ? 0 : 1)) & 1;
   // dQ first: with delta_w set it produces the D the dK/dV kernel reads (same stream, in order)
   if (D == 64) {
-    if ((parts & 1) && dq64_form() == 1) {
-      AttnArgs aq = a;
-      aq.pair = 0;
-      const int smem2 = 2 * 2 * KT * 64 * 2;
-      set_smem(attn_bwd_dq_kernel<64, 2, 3>, smem2);
-      attn_bwd_dq_kernel<64, 2, 3><<<dim3((unsigned)nqb, (unsigned)H, (unsigned)B), NW * 64, smem2, stream>>>(aq);
-      PT_CHECK_LAUNCH();
-    } else if (parts & 1) {
+    if (parts & 1) {
       set_smem(attn_bwd_dq_kernel<64>, smem_kv);
       attn_bwd_dq_kernel<64><<<gq, NW * 64, smem_kv, stream>>>(a);
       PT_CHECK_LAUNCH();

@@ -777,50 +777,6 @@ def test_attention_dkdv_wave_pair_split_is_bit_identical(monkeypatch, B, S, H, H
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("B,S,H,HKV,causal,merge", [(4, 1024, 8, 8, True, False), (1, 512, 4, 2, True, False),
-                                                     (2, 256, 2, 2, False, False), (1, 512, 4, 4, False, True)])
-def test_attention_fwd64_occupancy_forms_are_bit_identical(B, S, H, HKV, causal, merge):
-    """The d64 forward's occupancy forms (variant attn_fwd64: 2-stage K/V ring, unpaired blocks, 3 or
-    4 workgroups per CU) run every block's tiles in the same order as the 4-stage paired form: o and
-    lse bit-identical, the ring-merge epilogue included."""
-    from picotron_amd import kernels as K_
-    q, k, v = _qkv(B, S, H, HKV, 64)
-    outs = []
-    for form in (0, 1, 2):
-        with switches.override(attn_fwd64=form):
-            if merge:
-                o = torch.full((B, S, H, 64), 0.5, device=DEV)
-                lse = torch.full((B, H, S), 0.25, device=DEV)
-                K_.attn_fwd(q, k, v, 0.125, causal, out=o, lse=lse, merge=True)
-            else:
-                o, lse = K_.attn_fwd(q, k, v, 0.125, causal)
-            torch.cuda.synchronize()
-        outs.append((o.clone(), lse.clone()))
-    for o, lse in outs[1:]:
-        assert torch.equal(o, outs[0][0]) and torch.equal(lse, outs[0][1])
-
-
-@pytest.mark.parametrize("B,S,H,HKV,causal,rope", [(4, 1024, 8, 8, True, True), (1, 512, 4, 2, True, False),
-                                                    (2, 256, 2, 2, False, False)])
-def test_attention_dq64_forms_are_bit_identical(B, S, H, HKV, causal, rope):
-    """The d64 dQ kernel's occupancy form (variant attn_dq64 = 1: 2-stage ring, unpaired blocks, 3
-    workgroups per CU) runs each block's tiles in the same order: dq (and the dK/dV it feeds through
-    the fused delta) bit-identical to the paired 4-stage form."""
-    from picotron_amd import kernels as K_
-    q, k, v = _qkv(B, S, H, HKV, 64)
-    o, lse = K_.attn_fwd(q, k, v, 0.125, causal)
-    do = torch.randn(o.shape).to(BF).to(DEV)
-    rp = tuple(t.to(DEV) for t in O.get_cos_sin(S, 64, base=10000.0)) if rope else None
-    outs = []
-    for form in (0, 1):
-        with switches.override(attn_dq64=form):
-            g = K_.attn_bwd(do, q, k, v, o, lse, 0.125, causal, rope=rp)[:3]
-            torch.cuda.synchronize()
-        outs.append([t.clone() for t in g])
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
-
-
 def test_attention_ring_merge_matches_full():
     """Two key blocks merged by the fused update_out_and_lse epilogue == attention over both
     (context_parallel.py:157-187), and the backward with the global LSE sums to the full grads."""
