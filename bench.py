@@ -46,7 +46,7 @@ if ROOT not in sys.path:
 
 # HBM bytes per GEMM launch from rocprofv3 PMC passes (tools/gpu.sh counters: bench.py --grad-acc 2, then
 # tools/traffic_summary.py); read for the roofline's `traffic`
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r04", "gemm_traffic_r04f.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r04", "gemm_traffic_r04m.json")
 
 
 def log(*a):
@@ -107,8 +107,9 @@ def _events_time(fn, reps):
 def tp_proxy(args, base, layers):
     """One TP rank's compute for a micro-batch (no collectives): `layers` decoder layers with the
     shard widths (heads / tp, I / tp; the layer kernels read shards exactly like this inside the
-    TP model), the embedding lookup and the lm_head's vocab shard (ColumnParallel, V / tp) plus the
-    cross-entropy over the gathered vocabulary, fwd + bwd.  Returns the JSON line."""
+    TP model) and the launch forms of a tp > 1 group (its all-reduces no-ops), the embedding lookup
+    and the lm_head's vocab shard (ColumnParallel, V / tp) plus the cross-entropy over the gathered
+    vocabulary, fwd + bwd.  Returns the JSON line."""
     import math
     from picotron_amd import functional as FN
     from picotron_amd import kernels as K
@@ -141,14 +142,24 @@ def tp_proxy(args, base, layers):
         lg = FN.linear(x.view(T, H), head)                         # this rank's vocab shard
         full = torch.cat([lg] * tp, dim=1) if tp > 1 else lg         # stands in for the all-gather
         FN.cross_entropy(full, tgt).backward()
-    probe = K.GemmProbe()
-    for _ in range(args.warmup + 1):
-        micro_batch()
-    torch.cuda.synchronize()
-    t = _events_time(micro_batch, args.steps)
-    with probe:
-        micro_batch()
-    s = probe.summary()
+    # the layers see a tp group of `tp` ranks whose all-reduces are no-ops, so they take the TP
+    # launch forms (dX and dW as separate launches around the dX all-reduce), not tp = 1's duals
+    class _TPNoComm(FN.TPContext):
+        def all_reduce(self, t, async_op=False):
+            return None
+    current = FN.TPContext.current
+    FN.TPContext.current = staticmethod(lambda: _TPNoComm(None, tp, 0))
+    try:
+        probe = K.GemmProbe()
+        for _ in range(args.warmup + 1):
+            micro_batch()
+        torch.cuda.synchronize()
+        t = _events_time(micro_batch, args.steps)
+        with probe:
+            micro_batch()
+        s = probe.summary()
+    finally:
+        FN.TPContext.current = current
     fpt_rank = 6 * sum(p.numel() for w in stack for p in w) + 6 * head.numel() + 12 * layers * nh * d * args.seq
     ach = s["avg_flop"] / (s["avg_ms"] * 1e-3) / 1e12
     tok_gpu = T / t / tp          # tp ranks share these tokens

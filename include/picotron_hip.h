@@ -230,8 +230,10 @@ int pt_gemm_splitk_sum(const float* p0, const float* p1, const void* residual, v
                        hipStream_t stream);
 /* Split-K finish for nparts f32 partials [nparts][M][N] (ld N, part_stride >= M N elements apart):
  * the sum in part order through `mode` = the GEMM epilogue it completes -- 0 bf16 store, 1 bf16
- * accumulate, 2 f32 store, 3 f32 accumulate (main_grad), 4 bf16 residual (residual [M, N], ld ldr)
- * -- into nc (<= 4) row segments of C (c_bounds, NULL = one), each with its own ld.  N % 4 == 0. */
+ * accumulate, 2 f32 store, 3 f32 accumulate (main_grad), 4 bf16 residual (residual [M, N], ld ldr),
+ * 6 SwiGLU backward (the sum is dh of a split-K down_proj dX, model.py:186; residual = g|u [M, 2N]
+ * ld ldr; C[0] = dg|du [M, 2N], nc = 1) -- into nc (<= 4) row segments of C (c_bounds, NULL = one),
+ * each with its own ld.  N % 4 == 0. */
 int pt_gemm_splitk_reduce(const float* parts, int nparts, int64_t part_stride, int64_t M, int64_t N, void* const* C,
                           const int64_t* ldc, const int64_t* c_bounds, int nc, int mode, const void* residual,
                           int64_t ldr, hipStream_t stream);

@@ -1831,8 +1831,10 @@ namespace {
 // Split-K finish for nparts f32 partials [nparts][M][N] (ld N, part stride M N): out = the sum in
 // part order (deterministic), through the sink's epilogue -- 0 bf16 store, 1 bf16 accumulate
 // (bf16(C + bf16(sum)), the wgrad's .grad accumulation), 2 f32 store, 3 f32 accumulate (main_grad),
-// 4 bf16 residual (bf16(R + bf16(sum))) -- into up to 4 row segments of C (c_bounds), each with its
-// own pointer and leading dimension.  4 columns per thread-iteration (16-B partial loads).
+// 4 bf16 residual (bf16(R + bf16(sum))), 6 the SwiGLU backward of a split-K down_proj dX (sum = dh,
+// R = g|u [M, 2N], C = dg|du [M, 2N]: the fused epilogue's math) -- into up to 4 row segments of C
+// (c_bounds), each with its own pointer and leading dimension.  4 columns per thread-iteration
+// (16-B partial loads).
 struct ReduceArgs {
   const float* parts;
   int nparts;
@@ -1862,7 +1864,23 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const ReduceArgs r) 
       if (j < r.nc && row >= r.cseg[j]) seg = j;
     const int64_t off = (row - r.cseg[seg]) * r.ldc[seg] + c4 * 4;
     const float v[4] = {acc.x, acc.y, acc.z, acc.w};
-    if (MODE == EPI_F32 || MODE == EPI_F32_ACC) {
+    if (MODE == EPI_SWIGLU_BWD) {
+      // the sum is dh (rounded to bf16 as the fused epilogue stages it); R = g|u, C = dg|du [M, 2N]
+      const uint16_t* gr = r.R + row * r.ldr + c4 * 4;
+      const uint2 gw = *(const uint2*)gr, uw = *(const uint2*)(gr + r.N);
+      const float g[4] = {lo_bf(gw.x), hi_bf(gw.x), lo_bf(gw.y), hi_bf(gw.y)};
+      const float u[4] = {lo_bf(uw.x), hi_bf(uw.x), lo_bf(uw.y), hi_bf(uw.y)};
+      float og[4], ou[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = round_bf(v[e]), sg = silu_sig(g[e]);
+        ou[e] = d * round_bf(g[e] * sg);
+        og[e] = round_bf(d * u[e]) * (sg * (1.0f + g[e] * (1.0f - sg)));
+      }
+      uint16_t* o = (uint16_t*)r.C[0] + off;
+      *(uint2*)o = make_uint2(pack_bf2(og[0], og[1]), pack_bf2(og[2], og[3]));
+      *(uint2*)(o + r.N) = make_uint2(pack_bf2(ou[0], ou[1]), pack_bf2(ou[2], ou[3]));
+    } else if (MODE == EPI_F32 || MODE == EPI_F32_ACC) {
       float4* o = (float4*)((float*)r.C[seg] + off);
       float4 w = make_float4(v[0], v[1], v[2], v[3]);
       if (MODE == EPI_F32_ACC) {
@@ -1896,7 +1914,9 @@ int pt_gemm_splitk_reduce(const float* parts, int nparts, int64_t part_stride, i
                           int64_t ldr, hipStream_t stream) {
   if (!parts || nparts < 1 || M <= 0 || N <= 0 || (N & 3) || !C || nc < 1 || nc > 4) return PT_EINVAL;
   if (part_stride < M * N || !pt_aligned16(parts) || (part_stride & 3)) return PT_EALIGN;
-  if (mode == EPI_BF16_RES && (!residual || ((uintptr_t)residual & 7) || (ldr & 3))) return PT_EINVAL;
+  if ((mode == EPI_BF16_RES || mode == EPI_SWIGLU_BWD) && (!residual || ((uintptr_t)residual & 7) || (ldr & 3)))
+    return PT_EINVAL;
+  if (mode == EPI_SWIGLU_BWD && nc != 1) return PT_EINVAL;   // one dg|du [M, 2N] output
   ReduceArgs r{};
   r.parts = parts; r.nparts = nparts; r.M = M; r.N = N; r.part_stride = part_stride;
   r.nc = nc;
@@ -1919,6 +1939,7 @@ int pt_gemm_splitk_reduce(const float* parts, int nparts, int64_t part_stride, i
     case EPI_F32: splitk_reduce_kernel<EPI_F32><<<(int)grid, 256, 0, stream>>>(r); break;
     case EPI_F32_ACC: splitk_reduce_kernel<EPI_F32_ACC><<<(int)grid, 256, 0, stream>>>(r); break;
     case EPI_BF16_RES: splitk_reduce_kernel<EPI_BF16_RES><<<(int)grid, 256, 0, stream>>>(r); break;
+    case EPI_SWIGLU_BWD: splitk_reduce_kernel<EPI_SWIGLU_BWD><<<(int)grid, 256, 0, stream>>>(r); break;
     default: return PT_EINVAL;
   }
   PT_CHECK_LAUNCH();

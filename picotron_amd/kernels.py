@@ -560,6 +560,21 @@ def wgrad_ksplit(mnks, extra_tiles=0):
     return s
 
 
+def swiglu_dx_ksplit(T, I, H):
+    """K-slices for the down_proj dX with the SwiGLU backward (dual launch beside the down_proj dW)
+    when its 256x256 tiles fill under half the CUs -- the TP shards (TP = 8 at SmolLM-1.7B: 64
+    tiles with K 2048, the launch's critical path beside 128 dW slices of K 1024): the largest power
+    of two keeping the dX slices within half a round and >= 512 deep, the SwiGLU backward then in
+    the reduce pass (pt_gemm_splitk_reduce mode 6).  1 = unsplit (the fused epilogue)."""
+    if not _ksplit_enabled() or not SW.swiglu_splitk or T % 256 or I % 256:
+        return 1
+    tiles = (T // 256) * (I // 256)
+    s = 1
+    while s < 8 and tiles * s * 2 <= 128 and H % (s * 2 * 64) == 0 and H // (s * 2) >= 512:
+        s *= 2
+    return s
+
+
 def fewtile_ksplit(M, N, K):
     """(ksplit, tile) for a forward / dX GEMM whose output tiles leave most of the 256 CUs idle -- the
     TP-shard projections (TP = 8 at SmolLM-1.7B: the q|k|v forward 4096 x 768 is 48 tiles of
@@ -1013,6 +1028,7 @@ def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None, keep
     the problems do not tile for it -- the caller then launches them separately."""
     _bf16_rowmajor(dy2d, "dy")
     T, N = dy2d.shape
+    dxs = 1   # K-slices of a few-tile SwiGLU dX (finished by the reduce pass's SwiGLU backward)
     if gu is not None:
         wd = weights[0]
         I = wd.shape[1]
@@ -1020,9 +1036,17 @@ def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None, keep
         _req(len(weights) == 1 and wd.is_contiguous() and wd.shape[0] == N and tuple(gu.shape) == (T, 2 * I),
              "dual: down weight [H, I], gu [T, 2I]")
         dx = torch.empty(T, 2 * I, dtype=BF16, device=dy2d.device)
-        p0 = _problem(dy2d, dy2d.stride(0), [wd], [I], [0, I], 0, [dx], [dx.stride(0)], [0, T], T, I, N)
-        p0.residual, p0.ldr = _ptr(gu), gu.stride(0)
-        e0, flops, nbytes = EPI_SWIGLU_BWD, 2.0 * T * I * N, _alg_bytes(T, I, N, EPI_SWIGLU_BWD)
+        dxs = swiglu_dx_ksplit(T, I, N)
+        if dxs > 1:   # TP shard widths: dh as K-slices into f32 partials beside the dW slices
+            dxpart = torch.empty(dxs * T * I, dtype=torch.float32, device=dy2d.device)
+            p0 = _problem(dy2d, dy2d.stride(0), [wd], [I], [0, I], 0, [dxpart], [I], [0, T], T, I, N)
+            p0.ksplit, p0.kpart_stride = dxs, T * I
+            e0 = EPI_F32
+        else:
+            p0 = _problem(dy2d, dy2d.stride(0), [wd], [I], [0, I], 0, [dx], [dx.stride(0)], [0, T], T, I, N)
+            p0.residual, p0.ldr = _ptr(gu), gu.stride(0)
+            e0 = EPI_SWIGLU_BWD
+        flops, nbytes = 2.0 * T * I * N, _alg_bytes(T, I, N, EPI_SWIGLU_BWD)
     else:
         Kin = weights[0].shape[1]
         ns = [w.shape[0] for w in weights]
@@ -1043,11 +1067,11 @@ def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None, keep
                 p0s[i] = _problem(dy2d[:, lo:], dy2d.stride(0), bs, [Kin] * len(bs), _bounds([n for _, _, n in segs]),
                                   1, [parts[i]], [Kin], [0, T], T, Kin, hi - lo)
             e0 = EPI_F32
-    if e0 != EPI_F32:
+    if e0 != EPI_F32 or dxs > 1:
         p0s = (_C.GemmProblem * 1)(p0)
     p1s = (_C.GemmProblem * len(wjobs))()
     # the TP shards' few-tile dW as split-K slices beside the dX tiles (f32 partials, reduced below)
-    dx_tiles = sum(p.M // 256 * (p.N // 256) for p in p0s)
+    dx_tiles = sum(p.M // 256 * (p.N // 256) * max(1, p.ksplit) for p in p0s)
     ws = wgrad_ksplit([(dy.shape[1], x.shape[1], dy.shape[0]) for dy, x, _ in wjobs], extra_tiles=dx_tiles) \
         if wepilogue in (EPI_BF16, EPI_BF16_ACC, EPI_F32_ACC) else 1
     # the reduce pass writes 16-B (f32) / 8-B (bf16) row chunks: a sink it cannot address that way (a
@@ -1097,7 +1121,12 @@ def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None, keep
                                             _C.i64arr([o.stride(0) for o in outs]), _C.i64arr(_bounds(ns)), len(outs),
                                             int(wepilogue), None, 0, _C.stream_ptr(dy2d.device))
         _C.check(rc, "pt_gemm_splitk_reduce")
-    if e0 == EPI_F32:
+    if dxs > 1:   # dg|du = the SwiGLU backward of the summed dh slices
+        rc = _C.lib().pt_gemm_splitk_reduce(_ptr(dxpart), dxs, T * I, T, I, _C.ptrarr([_ptr(dx)]),
+                                            _C.i64arr([dx.stride(0)]), _C.i64arr([0, T]), 1, EPI_SWIGLU_BWD,
+                                            _ptr(gu), gu.stride(0), _C.stream_ptr(dy2d.device))
+        _C.check(rc, "pt_gemm_splitk_reduce(SwiGLU backward)")
+    elif e0 == EPI_F32:
         if keep_parts:   # the consumer (rmsnorm_bwd) sums the halves
             dx = SplitKParts(parts[0], parts[1])
         else:

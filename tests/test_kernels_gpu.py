@@ -333,6 +333,36 @@ def test_gemm_khalves_tile_at_layer_shapes(T, N, K):
     assert rel_err(ya, ref) < 1e-2
 
 
+def test_swiglu_dx_ksplit_beside_dw_slices():
+    """TP = 8 shard widths (I 1024): the down_proj dX with the SwiGLU backward runs as two K-slices
+    beside the dW slices in the dual launch and the reduce pass applies the SwiGLU backward (mode 6).
+    dg|du within bf16 rounding of the fused single-pass form and of the fp32 reference; the dW slices
+    are the same launch either way (bit-identical)."""
+    from picotron_amd import kernels as K_
+    T, H, I = 4096, 2048, 1024
+    assert K_.swiglu_dx_ksplit(T, I, H) == 2
+    g = torch.Generator().manual_seed(5)
+    dm = torch.randn(T, H, generator=g).to(BF).to(DEV)
+    hh = torch.randn(T, I, generator=g).to(BF).to(DEV)
+    wd = (torch.randn(H, I, generator=g) / I ** 0.5).to(BF).to(DEV)
+    gu = torch.randn(T, 2 * I, generator=g).to(BF).to(DEV)
+    outs = []
+    for v in (0, 1):
+        gw = torch.zeros(H, I, dtype=BF, device=DEV)
+        with switches.override(swiglu_splitk=v):
+            dgu = K_.linear_dgrad_dual(dm, [wd], [(dm, hh, [gw])], K_.EPI_BF16_ACC, gu=gu)
+        torch.cuda.synchronize()
+        outs.append((dgu.clone(), gw.clone()))
+    assert rel_err(outs[1][0], outs[0][0]) < 1e-2
+    assert torch.equal(outs[1][1], outs[0][1])
+    dh = (dm.float() @ wd.float()).to(BF).float()
+    gg, uu = gu[:, :I].float(), gu[:, I:].float()
+    sg = torch.sigmoid(gg)
+    du = dh * (gg * sg).to(BF).float()
+    dg = (dh * uu).to(BF).float() * (sg * (1 + gg * (1 - sg)))
+    assert rel_err(outs[1][0], torch.cat([dg, du], dim=1)) < 2e-2
+
+
 @pytest.mark.parametrize("epi", [0, 1, 3])
 def test_gemm_grouped_wgrad(epi):
     """dW of q|k|v (3 outputs) and dW of o_proj in one pt_gemm_grouped launch == separate GEMMs"""
