@@ -464,8 +464,10 @@ def test_wgrad_ksplit_tp8_shapes(epi, monkeypatch):
 def test_gemm_dual_with_ksplit_wgrad(epi, monkeypatch):
     """TP = 8 down_proj backward: the SwiGLU-backward dX (64 tiles) beside the split-K down_proj dW
     (32 tiles x 4 slices: one round with the dX tiles; f32 partials + reduce) in one dual launch == the unsplit dual launch up to
-    the dW's f32 summation order; the dX bit for bit."""
+    the dW's f32 summation order; the dX bit for bit (its own K-slicing, swiglu_splitk, is off here:
+    test_swiglu_dx_ksplit_beside_dw_slices covers it)."""
     from picotron_amd import kernels as K_
+    monkeypatch.setattr(switches.S, "swiglu_splitk", 0)
     T, H, I = 4096, 2048, 1024
     dm = torch.randn(T, H).to(BF).to(DEV)
     wd = (torch.randn(H, I) / math.sqrt(I)).to(BF).to(DEV)
