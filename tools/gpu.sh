@@ -3,7 +3,7 @@
 # Run from the repo root ON THE BOX (through gpurun):   bash tools/gpu.sh <tag> <step>[,<step>...] [k=v ...]
 #
 # steps (run in the order given; the first failure ends the call -- no retries on the GPU):
-#   suite        pytest -m gpu (whole suite; TESTS=... to narrow), then smoke()
+#   suite        pytest -m gpu (whole suite; TESTS=... files / node ids, TESTK=... a -k expression), then smoke()
 #   bench        bench.py N=1 (BENCH_RUNS=2 lines), default arguments
 #   prof         rocprofv3 --kernel-trace --stats of bench.py --steps 2 (kernel table -> profiles via tools/prof_summary.py)
 #   pmc          GEMM/all-kernel HBM traffic: separate FETCH_SIZE and WRITE_SIZE passes over bench.py --grad-acc 2
@@ -36,7 +36,7 @@ jline() {  # print a bench JSON line's headline fields
 }
 
 step_suite() {
-  timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 300 --timeout-method thread > $O.pytest.log 2>&1 || { echo pytest failed; grep -E "Error|FAILED|assert" $O.pytest.log | head -30; return 1; }
+  timeout -k 10 900 python -u -m pytest ${TESTS:-tests} ${TESTK:+-k "$TESTK"} -m gpu -x -q --timeout 300 --timeout-method thread > $O.pytest.log 2>&1 || { echo pytest failed; grep -E "Error|FAILED|assert" $O.pytest.log | head -30; return 1; }
   tail -1 $O.pytest.log
   timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O.smoke.log 2>&1 || { echo smoke failed; tail $O.smoke.log; return 1; }
   tail -1 $O.smoke.log
