@@ -596,8 +596,6 @@ def fewtile_ksplit(M, N, K):
     s = 1
     while s < 16 and tiles * s * 2 <= 256 and K % (s * 2 * 64) == 0 and K // (s * 2) >= 256:
         s *= 2
-    if s >= 4 and tile == 12 and N % 128 == 0 and SW.ksplit_kh:
-        return s // 2, 14   # half the slices on 256x128 K-halves tiles (as _wgrad_ksplit_form)
     return (s, tile) if s > 1 else (1, -1)
 
 

@@ -357,27 +357,6 @@ def test_tp_wgrad_ksplit_on_khalves_tiles(epi):
     assert rel_err(res[1][1].float() - base, _ref_mm(da.t(), xo)) < 2e-2
 
 
-@pytest.mark.parametrize("M,N,K,dgrad", [(4096, 768, 2048, False), (4096, 256, 2048, True)])
-def test_fewtile_ksplit_on_khalves_tiles(M, N, K, dgrad):
-    """TP = 8 q|k|v forward (48 tiles) and o_proj dX (16 tiles): half the K-slices on tile 14 --
-    within f32 rounding of the 256x256 slices and of the fp32 reference."""
-    from picotron_amd import kernels as K_
-    with switches.override(ksplit_kh=1):
-        s, t = K_.fewtile_ksplit(M, N, K)
-    assert t == 14 and s >= 2
-    g = torch.Generator().manual_seed(M + N)
-    a = torch.randn(M, K, generator=g).to(BF)
-    w = (torch.randn(K, N, generator=g) / K ** 0.5).to(BF) if dgrad else (torch.randn(N, K, generator=g) / K ** 0.5).to(BF)
-    res = []
-    for kh in (0, 1):
-        with switches.override(ksplit_kh=kh):
-            y = K_.linear_dgrad(a.to(DEV), [w.to(DEV)]) if dgrad else K_.linear_fwd(a.to(DEV), [w.to(DEV)])
-        torch.cuda.synchronize()
-        res.append(y.clone())
-    ref = _ref_mm(a, w) if dgrad else _ref_mm(a, w.t())
-    assert rel_err(res[1], res[0]) < 1e-2 and rel_err(res[1], ref) < 1e-2
-
-
 def test_swiglu_dx_ksplit_beside_dw_slices():
     """TP = 8 shard widths (I 1024): the down_proj dX with the SwiGLU backward runs as two K-slices
     beside the dW slices in the dual launch and the reduce pass applies the SwiGLU backward (mode 6).
