@@ -643,19 +643,7 @@ def _ksplit_launch(probs, n, a_kcontig, b_kcontig, tile, sinks, dev):
         _C.check(rc, "pt_gemm_splitk_reduce")
 
 
-def _wgrad_ksplit_form(mnks):
-    """(ksplit, tile) of a stand-alone split-K wgrad group: wgrad_ksplit's slices of 256x256 tiles,
-    or -- where those would be 8+ slices of K <= 512 (TP = 8: the q|k|v + o_proj dW, 32 tiles) --
-    half as many slices of 256x128 K-halves tiles (tile 14): the same workgroup count, twice the K
-    per slice and half the f32 partial bytes through the reduce pass."""
-    s = wgrad_ksplit(mnks)
-    if s >= 8 and SW.ksplit_kh and all(n % 128 == 0 for _, n, _ in mnks) and \
-            all(k % (s // 2 * 64) == 0 for _, _, k in mnks):
-        return s // 2, 14
-    return s, -1
-
-
-def _wgrad_ksplit_run(jobs, epilogue, s, tile=-1):
+def _wgrad_ksplit_run(jobs, epilogue, s):
     """The wgrad jobs [(dy2d, x2d, outs)] as s-way split-K problems of ONE grouped launch (f32
     partials in one workspace), then one reduce pass per job into its outs through `epilogue`."""
     dev = jobs[0][0].device
@@ -681,7 +669,7 @@ def _wgrad_ksplit_run(jobs, epilogue, s, tile=-1):
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
     sinks = [_sink(outs, _bounds([o.shape[0] for o in outs]), epilogue) for _, _, outs in jobs]
-    _ksplit_launch(probs, len(jobs), 0, 0, tile, sinks, dev)
+    _ksplit_launch(probs, len(jobs), 0, 0, -1, sinks, dev)
     if probe is not None:
         ev1.record()
         probe.records.append((ev0, ev1, flops, nbytes, sys._getframe().f_code.co_name))
@@ -692,9 +680,9 @@ def linear_wgrad_grouped(jobs, epilogue=EPI_BF16, tile=-1):
     (pt_gemm_grouped): e.g. dW of q|k|v (192 tiles) + dW of o_proj (64 tiles) fill 256 CUs.  A group
     that would leave most CUs idle (TP shards) runs split-K (wgrad_ksplit)."""
     if tile < 0 and epilogue in (EPI_BF16, EPI_BF16_ACC, EPI_F32_ACC):
-        s, t = _wgrad_ksplit_form([(dy.shape[1], x.shape[1], dy.shape[0]) for dy, x, _ in jobs])
+        s = wgrad_ksplit([(dy.shape[1], x.shape[1], dy.shape[0]) for dy, x, _ in jobs])
         if s > 1 and all(o.stride(1) == 1 and o.stride(0) % 4 == 0 for _, _, outs in jobs for o in outs):
-            return _wgrad_ksplit_run(jobs, epilogue, s, t)
+            return _wgrad_ksplit_run(jobs, epilogue, s)
     probs = (_C.GemmProblem * len(jobs))()
     flops = nbytes = 0.0
     for j, (dy2d, x2d, outs) in enumerate(jobs):
@@ -1161,7 +1149,7 @@ def linear_wgrad(dy2d, x2d, outs, epilogue=EPI_BF16, tile=-1):
     _req(sum(ns) == N, "wgrad: output rows must cover dY's width")
     if tile < 0 and epilogue in (EPI_BF16, EPI_BF16_ACC, EPI_F32_ACC) and wgrad_ksplit([(N, Kin, T)]) > 1 and \
             all(o.stride(1) == 1 and o.stride(0) % 4 == 0 for o in outs):
-        _wgrad_ksplit_run([(dy2d, x2d, outs)], epilogue, *_wgrad_ksplit_form([(N, Kin, T)]))
+        _wgrad_ksplit_run([(dy2d, x2d, outs)], epilogue, wgrad_ksplit([(N, Kin, T)]))
         return outs
     _gemm(dy2d, dy2d.stride(0), 0, [x2d], [x2d.stride(0)], [0, Kin], 0, 0, outs, [o.stride(0) for o in outs],
           _bounds(ns), N, Kin, T, epilogue, tile)

@@ -21,7 +21,7 @@ DEFAULTS = {
     # launches and their XCD order, the norm backward fed by split-K halves, the attention
     # backward's fused delta, and the tile-count thresholds below which the RoPE / SwiGLU epilogues
     # run as separate kernels (TP shard widths)
-    "ksplit": 1, "ksplit_kh": 1, "fewtile": 1, "swiglu_splitk": 1, "splitk2": 1, "splitk2_min": 8192, "dual": 1, "dual_order": 2, "norm_splitk": 1,
+    "ksplit": 1, "fewtile": 1, "swiglu_splitk": 1, "splitk2": 1, "splitk2_min": 8192, "dual": 1, "dual_order": 2, "norm_splitk": 1,
     "fuse_delta": 1, "rope_fuse_min_tiles": 96, "swiglu_fuse_min_tiles": 192, "swiglu_bwd_min_tiles": 0,
     # context_parallel.py: the zig-zag (load-balanced) ring where it tiles, the residual stream kept
     # in that layout across the decoder stack, the full-mesh K|V / dK|dV exchange instead of the ring

@@ -333,30 +333,6 @@ def test_gemm_khalves_tile_at_layer_shapes(T, N, K):
     assert rel_err(ya, ref) < 1e-2
 
 
-@pytest.mark.parametrize("epi", [0, 1, 3])
-def test_tp_wgrad_ksplit_on_khalves_tiles(epi):
-    """TP = 8 q|k|v + o_proj dW (32 tiles of 256x256: 8 slices of K 512) run as 4 slices of tile 14
-    (256x128 K-halves) -- the same sums to f32 rounding, through every sink epilogue."""
-    from picotron_amd import kernels as K_
-    T, H = 4096, 2048
-    assert K_._wgrad_ksplit_form([(768, H, T), (H, 256, T)]) == (4, 14)
-    g = torch.Generator().manual_seed(epi)
-    dq, xa = torch.randn(T, 768, generator=g).to(BF), torch.randn(T, H, generator=g).to(BF)
-    da, xo = torch.randn(T, H, generator=g).to(BF), torch.randn(T, 256, generator=g).to(BF)
-    dt = torch.float32 if epi == 3 else BF
-    res = []
-    for kh in (0, 1):
-        w1, w2 = torch.full((768, H), 0.5, dtype=dt, device=DEV), torch.full((H, 256), 0.5, dtype=dt, device=DEV)
-        with switches.override(ksplit_kh=kh):
-            K_.linear_wgrad_grouped([(dq.to(DEV), xa.to(DEV), [w1]), (da.to(DEV), xo.to(DEV), [w2])], epilogue=epi)
-        torch.cuda.synchronize()
-        res.append((w1.clone(), w2.clone()))
-    base = 0.5 if epi in (1, 3) else 0.0
-    assert rel_err(res[1][0], res[0][0]) < 1e-2 and rel_err(res[1][1], res[0][1]) < 1e-2
-    assert rel_err(res[1][0].float() - base, _ref_mm(dq.t(), xa)) < 2e-2
-    assert rel_err(res[1][1].float() - base, _ref_mm(da.t(), xo)) < 2e-2
-
-
 def test_swiglu_dx_ksplit_beside_dw_slices():
     """TP = 8 shard widths (I 1024): the down_proj dX with the SwiGLU backward runs as two K-slices
     beside the dW slices in the dual launch and the reduce pass applies the SwiGLU backward (mode 6).
