@@ -1019,8 +1019,6 @@ void set_smem(K kern, int bytes) {
 
 // causal block pairing (variant "attn_pair"; 0 = off, A/B measurement only)
 bool pair_enabled() { return pt_variant(PT_VAR_ATTN_PAIR) == 1; }
-// d64 forward with 8-wave workgroups (256 query rows per staged K/V tile; variant "attn_fwd64_w8")
-bool fwd64_w8() { return pt_variant(PT_VAR_ATTN_FWD64_W8) == 1; }
 
 // dK/dV kernel form per head dim (variant "attn_split"): bit 0 = d64, bit 1 = d128 use the wave-pair
 // split; default d128 only
@@ -1066,16 +1064,12 @@ int pt_attn_fwd(const void* q, const int64_t* q_str, const void* k, const int64_
   a.scale = scale; a.causal = causal; a.merge = merge;
   int rc = check_common(a, (int)D);
   if (rc) return rc;
-  const int nwk = ((D == 128 || fwd64_w8()) && Sq % (8 * 32) == 0) ? 8 : NW;
+  const int nwk = (D == 128 && Sq % (8 * 32) == 0) ? 8 : NW;
   const int nqb = (int)(Sq / (nwk * 32));
   a.pair = causal && nqb % 2 == 0 && pair_enabled();
   const dim3 grid((unsigned)(a.pair ? nqb / 2 : nqb), (unsigned)H, (unsigned)B);
   const int stage_b = 2 * KT * (int)D * 2;
-  if (D == 64 && nwk == 8) {
-    const int smem = fwd_stages<64, 8>() * stage_b;
-    set_smem(attn_fwd_kernel<64, 8>, smem);
-    attn_fwd_kernel<64, 8><<<grid, 8 * 64, smem, stream>>>(a);
-  } else if (D == 64) {
+  if (D == 64) {
     const int smem = fwd_stages<64, NW>() * stage_b;
     set_smem(attn_fwd_kernel<64, NW>, smem);
     attn_fwd_kernel<64, NW><<<grid, NW * 64, smem, stream>>>(a);

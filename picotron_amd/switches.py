@@ -27,9 +27,9 @@ DEFAULTS = {
     # in that layout across the decoder stack, the full-mesh K|V / dK|dV exchange instead of the ring
     "ring_zigzag": 1, "zigzag_residual": 1, "ring_mesh": 1,
     # native (libpicotron_hip.so, pt_set_variant)
-    "attn_pair": 1, "attn_split": 2, "gemm_group_m": -1, "gemm_mix": 1, "gemm_kh": 2, "attn_fwd64_w8": 0,
+    "attn_pair": 1, "attn_split": 2, "gemm_group_m": -1, "gemm_mix": 1, "gemm_kh": 2,
 }
-NATIVE = ("attn_pair", "attn_split", "gemm_group_m", "gemm_mix", "gemm_kh", "attn_fwd64_w8")
+NATIVE = ("attn_pair", "attn_split", "gemm_group_m", "gemm_mix", "gemm_kh")
 
 
 class _Switches:

@@ -809,21 +809,6 @@ def test_attention_dkdv_wave_pair_split_is_bit_identical(monkeypatch, B, S, H, H
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("B,S,H,HKV,causal", [(4, 1024, 8, 8, True), (1, 512, 4, 2, True), (2, 256, 2, 2, False)])
-def test_attention_fwd64_w8_is_bit_identical(B, S, H, HKV, causal):
-    """The d64 forward with 8-wave workgroups (variant attn_fwd64_w8: 256 query rows per staged K/V
-    tile) runs every query row's tiles in the same order: o and lse bit-identical to 4 waves."""
-    from picotron_amd import kernels as K_
-    q, k, v = _qkv(B, S, H, HKV, 64)
-    outs = []
-    for w8 in (0, 1):
-        with switches.override(attn_fwd64_w8=w8):
-            o, lse = K_.attn_fwd(q, k, v, 0.125, causal)
-            torch.cuda.synchronize()
-        outs.append((o.clone(), lse.clone()))
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
-
-
 def test_attention_ring_merge_matches_full():
     """Two key blocks merged by the fused update_out_and_lse epilogue == attention over both
     (context_parallel.py:157-187), and the backward with the global LSE sums to the full grads."""
