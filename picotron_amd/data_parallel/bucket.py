@@ -40,13 +40,21 @@ class Bucket:
         self.grad_data = grad_data
         self.process_group = process_group
         self.process_group_size = dist.get_world_size(group=process_group)
+        self.avg_op = dist.get_backend(process_group) == "nccl"
         self.handle = None
         self.reset()
 
     def sync_gradient(self) -> None:
-        """Mean over the group: pre-divide, then one async all-reduce (SUM) of the whole buffer."""
+        """Mean over the group, one async all-reduce of the whole buffer: RCCL's AVG (the 1 / N
+        scaling inside the collective -- no separate pass over the buffer on the compute stream,
+        where the reference pre-divides; the same values for the power-of-two group sizes of one
+        node), or on gloo the reference's pre-divide + SUM."""
         if self.handle is not None:
             raise RuntimeError("bucket all-reduce launched twice in one backward")
+        if self.avg_op:
+            self.handle = dist.all_reduce(self.grad_data, op=dist.ReduceOp.AVG, group=self.process_group,
+                                          async_op=True)
+            return
         self.grad_data.div_(self.process_group_size)
         self.handle = dist.all_reduce(self.grad_data, group=self.process_group, async_op=True)
 
