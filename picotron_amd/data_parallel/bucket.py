@@ -31,6 +31,13 @@ def plan_buckets(sizes: List[int], cap: int) -> Tuple[List[Tuple[int, int, int]]
     return places, totals
 
 
+def _backend(group):
+    try:
+        return dist.get_backend(group)
+    except (ValueError, RuntimeError):   # not a registered group (tests' stand-ins)
+        return None
+
+
 class Bucket:
     """One flat gradient buffer and the parameters whose main_grad lives in it."""
 
@@ -40,7 +47,7 @@ class Bucket:
         self.grad_data = grad_data
         self.process_group = process_group
         self.process_group_size = dist.get_world_size(group=process_group)
-        self.avg_op = dist.get_backend(process_group) == "nccl"
+        self.avg_op = _backend(process_group) == "nccl"
         self.handle = None
         self.reset()
 
