@@ -193,9 +193,9 @@ struct GemmGroup {
 };
 
 // tile order: XCD remap over the whole grid (consecutive ids share an XCD), then the problem,
-// then group `group_m` tile-rows so an XCD's 32 consecutive tiles form a compact block of the
-// output (A and B panels shared through that XCD's L2): 8 for 256x256 tiles, 4 for 256x128
-// (32 tiles = 1024 x 1024 elements either way)
+// then group `group_m` tile-rows so an XCD's consecutive tiles form a compact block of the
+// output (A and B panels shared through that XCD's L2): 6 rows (group_m_for: measured faster
+// than the 8 / 4 rows that made 32 tiles one 2048 x 1024 / 1024 x 1024 block)
 // tile id pid_all (already in XCD order) of group g -> its problem and (tile_m, tile_n)
 // (split-K: the K-slice is the outermost index of a problem's tiles, so an XCD's consecutive tiles
 // share one slice's A / B panels)
@@ -1374,10 +1374,13 @@ void set_smem_once(Kern k, int smem) {
 }
 
 // per-problem tile grid + consecutive tile ids; returns the total tile count
+// tile-rows per group of the tile order: 6 for both phased tiles.  Whole-step A/B (round 4,
+// profiles/r04/group_m/, two boxes, interleaved): 6 -> 156.6-157.5 k, 5 / 7 -> 156.2-157.8 k,
+// 4 -> 155.4-155.9 k, the previous 8 (256x256) / 4 (256x128) -> 154.9-155.0 k tokens/s
 int group_m_for(int bm, int bn) {
+  (void)bm; (void)bn;
   const int g = pt_variant(PT_VAR_GEMM_GROUP_M);  // > 0: override (A/B measurement)
-  if (g > 0) return g;
-  return bm == 2 * bn ? 4 : 8;
+  return g > 0 ? g : 6;
 }
 
 inline int group_tiles(GemmGroup& g, int bm, int bn) {
