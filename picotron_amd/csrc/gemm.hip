@@ -275,13 +275,11 @@ __device__ __forceinline__ void ce_stats_merge(const GemmArgs& a, const float2* 
 // move 134 MB at ~4.5 TB/s -- and a stream that alternates loads and stores runs it fastest:
 // issuing all 2 x NIT loads before any math measured 3 % slower than 2 chunks per group
 // (profiles/r02_notes.md).
-#ifndef PT_SWIGLU_GRP
-#define PT_SWIGLU_GRP 2
-#endif
+constexpr int kSwigluGroup = 2;   // chunks per load group (4: equal, 16: -0.4 %; profiles/r04/notes_r04.md)
 template <int TM, int TN>
 __device__ __forceinline__ void swiglu_bwd_tail(const GemmArgs& a, const lds_u8* st, int64_t mrow0, int ncol0,
                                                 int64_t ldc, uint16_t* C, int lane) {
-  constexpr int ROWB = TN * 2 + 16, CPR = TN / 8, RPI = 64 / CPR, NIT = TM / RPI, SG = PT_SWIGLU_GRP;
+  constexpr int ROWB = TN * 2 + 16, CPR = TN / 8, RPI = 64 / CPR, NIT = TM / RPI, SG = kSwigluGroup;
   static_assert(NIT % SG == 0, "chunk groups");
   typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
   const int lrow = lane / CPR, ch = lane % CPR;

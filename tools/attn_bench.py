@@ -58,7 +58,7 @@ def main():
                     help="causal: time the backward as the layer calls it (delta inside, no precomputed delta)")
     ap.add_argument("--variant", default="",
                     help="NAME=V1,V2,...: time the new library once per value of this native variant "
-                         "(pt_set_variant; e.g. attn_fwd64=0,1,2), compared like --old builds")
+                         "(pt_set_variant; e.g. attn_pair=1,0), compared like --old builds")
     ap.add_argument("--full", action="store_true",
                     help="the CP ring's visiting block: no causal mask, f32 dq/dk/dv accumulators (grad_f32)")
     ap.add_argument("--rounds", type=int, default=2, help="interleaved rounds; medians are printed at the end")
