@@ -151,11 +151,14 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(min_wa
   bf16x8 wv[NCH];
   load_row<NCH>(w, lane, nchunk, wv);
   // the wave's dw accumulator is its own LDS row (not 8*NCH registers): read-modify-written once
-  // per chunk per row, no barrier needed until the cross-wave combine
+  // per chunk per row, no barrier needed until the cross-wave combine.  Planar: columns 0-3 of
+  // chunk c at [4c], columns 4-7 at [cols / 2 + 4c], so a wave's 16-byte accesses are lane-
+  // contiguous (chunk-interleaved 32-byte lanes were 2-way bank conflicts)
   float* dwrow = red + wid * cols;
+  const int half = cols >> 1;
   for (int c = lane; c < nchunk; c += PT_WAVE) {
-    *(float4*)(dwrow + c * 8) = make_float4(0.f, 0.f, 0.f, 0.f);
-    *(float4*)(dwrow + c * 8 + 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+    *(float4*)(dwrow + c * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+    *(float4*)(dwrow + half + c * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 
   for (; row < rows; row += stride) {
@@ -182,11 +185,12 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(min_wa
           dot += d[j] * wf[j] * xh;
           g[j] = d[j] * (mode == 0 ? xh : round_bf(xh));
         }
-        float4* acc = (float4*)(dwrow + c * 8);
-        float4 a0 = acc[0], a1 = acc[1];
+        float4* acc0 = (float4*)(dwrow + c * 4);
+        float4* acc1 = (float4*)(dwrow + half + c * 4);
+        float4 a0 = *acc0, a1 = *acc1;
         a0.x += g[0]; a0.y += g[1]; a0.z += g[2]; a0.w += g[3];
         a1.x += g[4]; a1.y += g[5]; a1.z += g[6]; a1.w += g[7];
-        acc[0] = a0; acc[1] = a1;
+        *acc0 = a0; *acc1 = a1;
       }
     }
     // the f32 unpacked row is not kept live across the reduction (it would double the VGPRs
@@ -223,9 +227,10 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(min_wa
   // combine the block's waves (fixed order), one partial row per block
   __syncthreads();
   for (int col = threadIdx.x; col < cols; col += WPB * 64) {
+    const int at = ((col & 7) >> 2) * half + (col >> 3) * 4 + (col & 3);   // the planar slot
     float s = 0.f;
 #pragma unroll
-    for (int k = 0; k < WPB; ++k) s += red[k * cols + col];
+    for (int k = 0; k < WPB; ++k) s += red[k * cols + at];
     dw_partial[(int64_t)blockIdx.x * cols + col] = s;
   }
 }

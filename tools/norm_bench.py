@@ -2,11 +2,10 @@
 shape (T 4096, H 2048): us per call from a HIP graph of `reps` back-to-back calls (no host gaps) and
 the achieved HBM rate on algorithmic bytes (fwd 4 B/elem, fwd+res 8, bwd+dres 8).
 
-    [PT_NORM=fwd_wpb,fwd_bpc,bwd_wpb,bwd_bpc] python tools/norm_bench.py [--rows 4096 --cols 2048] [--old lib.so]
+    python tools/norm_bench.py [--rows 4096 --cols 2048] [--old lib.so]
 
-PT_NORM (read once per process by the library) selects the launch shape; sweep it with one process
-per value.  --old: a library holding another build of the pt_rmsnorm_* entry points, timed in the
-same process.
+--old: a library holding another build of the pt_rmsnorm_* entry points, timed in the same process.
+bwd_split: the backward fed by a split-K dX's two f32 halves (pt_rmsnorm_bwd_splitk, 16 B/elem).
 """
 import argparse
 import json
@@ -57,6 +56,7 @@ def main():
     x, r, dy, dres = (torch.randn(R, C, device="cuda", generator=g).to(bf) for _ in range(4))
     w = (1 + 0.1 * torch.randn(C, device="cuda", generator=g)).to(bf)
     mg = torch.zeros(C, device="cuda", dtype=torch.float32)
+    p0, p1 = (torch.randn(R, C, device="cuda", generator=g) for _ in range(2))
     n = R * C
 
     def measure(tag):
@@ -67,9 +67,12 @@ def main():
         t_f = graph_us(lambda: K.rmsnorm_fwd(x, w, 1e-5, 0))
         t_r = graph_us(lambda: K.rmsnorm_fwd(x, w, 1e-5, 0, residual=r))
         t_b = graph_us(lambda: K.rmsnorm_bwd(dy, z, w, rstd, 0, dres=dres, dw_out=mg, dw_sink=K.DW_ACC_F32))
+        sp = K.SplitKParts(p0, p1)
+        t_s = graph_us(lambda: K.rmsnorm_bwd(sp, z, w, rstd, 0, dres=dres, dw_out=mg, dw_sink=K.DW_ACC_F32))
         row = {"cfg": tag, "fwd_us": round(t_f, 2), "fwd_TBps": round(4 * n / t_f / 1e6, 2),
                "fwdres_us": round(t_r, 2), "fwdres_TBps": round(8 * n / t_r / 1e6, 2),
-               "bwd_us": round(t_b, 2), "bwd_TBps": round(8 * n / t_b / 1e6, 2)}
+               "bwd_us": round(t_b, 2), "bwd_TBps": round(8 * n / t_b / 1e6, 2),
+               "bwd_split_us": round(t_s, 2), "bwd_split_TBps": round(14 * n / t_s / 1e6, 2)}
         print(json.dumps(row), flush=True)
         return ref
 
@@ -77,11 +80,10 @@ def main():
     libs = {"new": _C.load_library()}
     if a.old:
         libs["old"] = _C.load_library(os.path.abspath(a.old), strict=False)
-    cfg = os.environ.get("PT_NORM", "default")
-    for rnd in range(2):
-        for name, lib in libs.items():
+    for rnd in range(3):
+        for name, lib in (list(libs.items())[::-1] if rnd % 2 else libs.items()):
             _C._lib = lib
-            refs[name] = measure(f"{name}:{cfg if name == 'new' else 'default'}:r{rnd}")
+            refs[name] = measure(f"{name}:r{rnd}")
     _C._lib = libs["new"]
     if "old" in libs:
         o = refs["old"]
