@@ -1376,8 +1376,9 @@ void set_smem_once(Kern k, int smem) {
 // profiles/r04/group_m/, two boxes, interleaved): 6 -> 156.6-157.5 k, 5 / 7 -> 156.2-157.8 k,
 // 4 -> 155.4-155.9 k, the previous 8 (256x256) / 4 (256x128) -> 154.9-155.0 k tokens/s
 int group_m_for(int bm, int bn) {
-  (void)bm; (void)bn;
-  const int g = pt_variant(PT_VAR_GEMM_GROUP_M);  // > 0: override (A/B measurement)
+  // variant > 0: override (A/B measurement); >= 100: 256x256 tiles take g / 100, 256x128 g % 100
+  const int g = pt_variant(PT_VAR_GEMM_GROUP_M);
+  if (g >= 100) return bm == 2 * bn ? g % 100 : g / 100;
   return g > 0 ? g : 6;
 }
 
