@@ -1,0 +1,41 @@
+"""Host-side launch-shape choices of picotron_amd.kernels (pure functions, no GPU): the K-slice
+counts of the TP-shard GEMMs and of the SwiGLU-backward dX, and the split-K halves of the long-K
+dX projections -- at the shapes the layer and the TP = 8 proxy launch."""
+from picotron_amd import kernels as K
+from picotron_amd import switches
+
+T, H, I, V = 4096, 2048, 8192, 49152
+
+
+def test_swiglu_dx_ksplit_only_at_tp_shard_widths():
+    assert K.swiglu_dx_ksplit(T, I // 8, H) == 2          # TP = 8: 64 tiles -> 2 slices (128)
+    assert K.swiglu_dx_ksplit(T, I, H) == 1               # TP = 1: 512 tiles, fused epilogue
+    assert K.swiglu_dx_ksplit(T, I // 2, H) == 1          # TP = 2: 256 tiles
+    assert K.swiglu_dx_ksplit(T, I // 4, H) == 1          # TP = 4: 128 tiles (already half a round)
+    assert K.swiglu_dx_ksplit(T, 5504 // 8, 4096) == 1    # not on 256-column tiles
+    with switches.override(swiglu_splitk=0):
+        assert K.swiglu_dx_ksplit(T, I // 8, H) == 1
+
+
+def test_wgrad_ksplit_fills_one_round():
+    q, o = 3 * H // 8, H // 8
+    assert K.wgrad_ksplit([(q, H, T), (H, o, T)]) == 8    # 24 + 8 tiles x 8 = 256
+    assert K.wgrad_ksplit([(2 * I // 8, H, T)]) == 4      # gate|up dW: 64 tiles x 4
+    assert K.wgrad_ksplit([(H, I // 8, T)], extra_tiles=128) == 4   # down dW: 32 tiles x 4 beside 128 dX slices
+    assert K.wgrad_ksplit([(2 * I, H, T)]) == 1           # TP = 1: 512 tiles
+    with switches.override(ksplit=0):
+        assert K.wgrad_ksplit([(q, H, T), (H, o, T)]) == 1
+
+
+def test_fewtile_ksplit_for_tp_projections():
+    assert K.fewtile_ksplit(T, 3 * H // 8, H) == (4, 12)   # q|k|v forward: 48 tiles x 4
+    assert K.fewtile_ksplit(T, H // 8, H) == (8, 12)       # o_proj dX: 16 tiles x 8
+    assert K.fewtile_ksplit(T, H, H) == (1, -1)            # 128 tiles: unsplit
+    assert K.fewtile_ksplit(1024, 256, 2048) == (1, -1)    # short M: unsplit
+
+
+def test_splitk_halves_for_long_k_dx():
+    assert K._splitk_halves(T, H, 2 * I) == I              # gate|up dX: two K-8192 halves
+    assert K._splitk_halves(T, H, V) == V // 2             # lm_head dX
+    assert K._splitk_halves(T, H, H) is None               # o_proj dX: K 2048
+    assert K._splitk_halves(T, H, 3 * H, min_half=1024) == 3 * H // 2   # q|k|v dX beside its dW
