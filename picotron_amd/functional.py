@@ -103,7 +103,7 @@ def wgrad_group(jobs):
             _grad_ready(p)
 
 
-def dgrad_with_wgrad(dy2d, weights, wjobs, gu=None, keep_parts=False, split_min=None):
+def dgrad_with_wgrad(dy2d, weights, wjobs, gu=None, keep_parts=False, split_min=None, order=None):
     """dX = dY . [W_0; ...] (with gu: the down_proj dX's SwiGLU backward, dg|du) AND the wgrads
     wjobs [(dy2d, x2d, params)] of the same layer in ONE launch (K.linear_dgrad_dual) when the
     shapes tile for it and every sink takes one epilogue; otherwise the separate launches.
@@ -117,7 +117,8 @@ def dgrad_with_wgrad(dy2d, weights, wjobs, gu=None, keep_parts=False, split_min=
         if len(epis) == 1:
             epi = epis.pop()
             wk = [(dy, x, [t for t, _ in tg]) for (dy, x, _), tg in zip(wjobs, targets)]
-            dx = K.linear_dgrad_dual(dy2d, weights, wk, epi, gu=gu, keep_parts=keep_parts, split_min=split_min)
+            dx = K.linear_dgrad_dual(dy2d, weights, wk, epi, gu=gu, keep_parts=keep_parts, split_min=split_min,
+                                     order=order)
             if dx is None:   # not tileable after all: the same sinks, separate launches
                 dx = K.linear_dgrad_swiglu(dy2d, weights[0], gu) if gu is not None else K.linear_dgrad(dy2d, weights)
                 K.linear_wgrad_grouped(wk, epilogue=epi)
@@ -534,7 +535,8 @@ def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True, keep_parts=False)
         # (gu_splitk = 0) unsplit -- 128 tiles twice as long as a dW tile, beside which the other
         # CUs run four dW tiles each, and a bf16 dX for the norm backward to read
         return dgrad_with_wgrad(dgu, [wg, wu], [(dgu, h2, [wg, wu])], keep_parts=keep_parts,
-                                split_min=None if split else 1 << 30)
+                                split_min=None if split else 1 << 30,
+                                order=SW.gu_dual_order if SW.gu_dual_order >= 0 else None)
     if need_dx:
         dh = K.linear_dgrad(dgu, [wg, wu])
         handle = tp.all_reduce(dh, async_op=True)
