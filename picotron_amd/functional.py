@@ -456,7 +456,8 @@ def attn_block_bwd(da, h2, saved, wq, wk, wv, wo, cos, sin, sh, tp, need_dx=True
         # ONE launch with the q|k|v and o_proj dW (192 + 64 tiles): 512 tiles = 2 whole rounds of the
         # 256 CUs instead of a 128-tile dX launch and a 256-tile dW launch
         return dgrad_with_wgrad(dqkv, [wq, wk, wv], [(dqkv, h2, [wq, wk, wv]), (da, o.view(sh.T, sh.wq), [wo])],
-                                keep_parts=keep_parts, split_min=1024)
+                                keep_parts=keep_parts, split_min=1024,
+                                order=SW.qkv_dual_order if SW.qkv_dual_order >= 0 else None)
     dh = handle = None
     if need_dx:
         dh = K.linear_dgrad(dqkv, [wq, wk, wv])

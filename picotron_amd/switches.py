@@ -16,7 +16,7 @@ DEFAULTS = {
     # functional.py: the fused epilogues (RoPE in the q|k|v GEMM and attention backward, SwiGLU in the
     # gate|up / down GEMMs), deferred norm-weight column sums, lm_head CE statistics, the q|k|v and
     # gate|up dX + dW dual launches (the latter's dX as split-K halves or unsplit)
-    "fuse": 1, "norm_defer": 1, "ce_stats": 1, "dual_qkv": 1, "dual_gu": 1, "gu_splitk": 1, "gu_dual_order": 1,
+    "fuse": 1, "norm_defer": 1, "ce_stats": 1, "dual_qkv": 1, "dual_gu": 1, "gu_splitk": 1, "gu_dual_order": 1, "qkv_dual_order": -1,
     # kernels.py: weight-gradient / few-tile forward and dX K-slices (the SwiGLU-backward dX's too), split-K dgrad halves (and their minimum K), dX + dW dual
     # launches and their XCD order, the norm backward fed by split-K halves, the attention
     # backward's fused delta, and the tile-count thresholds below which the RoPE / SwiGLU epilogues
