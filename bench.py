@@ -135,18 +135,49 @@ def tp_proxy(args, base, layers):
     ids = torch.randint(0, V // tp, (args.mbs, args.seq), device=dev, generator=g)
     tgt = torch.randint(0, V, (T,), device=dev, generator=g)
 
+    class _GatherStandIn(torch.autograd.Function):
+        """ColumnParallelLinear(gather_output=True)'s all-gather of the vocab shards (tp_communications.py:51-72)
+        as one rank sees it: forward writes the [T, V] gathered logits (here tp copies of the shard),
+        backward hands this rank its own column slice (no sum: the reference's backward is a split)."""
+
+        @staticmethod
+        def forward(ctx, shard):
+            return torch.cat([shard] * tp, dim=1)
+
+        @staticmethod
+        def backward(ctx, g):
+            return g[:, :g.shape[1] // tp]
+
+    from picotron_amd.switches import S as SW
+    sp = tp > 1 and SW.tp_sp != 0 and args.seq % tp == 0   # sequence parallelism (sequence_parallel.py)
+
     def micro_batch():
         x = FN.embedding(ids, emb)
+        if sp:   # this rank's token rows of the residual stream (the entry hook's slice)
+            x = x.view(T, H)[:T // tp].view(args.mbs, args.seq // tp, H)
         for w in stack:
-            x = FN.DecoderLayerFunction.apply(x, *w, cos, sin, cfg.rms_norm_eps, 0, nh, nkv, d)
+            x = FN.DecoderLayerFunction.apply(x, *w, cos, sin, cfg.rms_norm_eps, 0, nh, nkv, d, False, sp)
+        if sp:   # the exit hook's all-gather before the final norm
+            x = _TPNoComm(None, tp, 0).all_gather_rows(x.reshape(T // tp, H))
         lg = FN.linear(x.view(T, H), head)                         # this rank's vocab shard
-        full = torch.cat([lg] * tp, dim=1) if tp > 1 else lg         # stands in for the all-gather
+        full = _GatherStandIn.apply(lg) if tp > 1 else lg           # stands in for the all-gather
         FN.cross_entropy(full, tgt).backward()
     # the layers see a tp group of `tp` ranks whose all-reduces are no-ops, so they take the TP
     # launch forms (dX and dW as separate launches around the dX all-reduce), not tp = 1's duals
     class _TPNoComm(FN.TPContext):
+        """The tp group's collectives as one rank's memory traffic, without the links: the
+        all-gather writes its [T, H] output (tp copies of the shard), the reduce-scatter its shard."""
+
         def all_reduce(self, t, async_op=False):
             return None
+
+        def all_gather_rows(self, t):
+            out = torch.empty((self.world_size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+            out.view(self.world_size, *t.shape).copy_(t.unsqueeze(0).expand(self.world_size, *t.shape))
+            return out
+
+        def reduce_scatter_rows(self, t, async_op=False):
+            return t[:t.shape[0] // self.world_size].contiguous(), None
     current = FN.TPContext.current
     FN.TPContext.current = staticmethod(lambda: _TPNoComm(None, tp, 0))
     try:
@@ -168,7 +199,8 @@ def tp_proxy(args, base, layers):
             "unit": "tokens/s/GPU (compute-only upper bound)", "ms_per_microbatch": t * 1e3,
             "mfu_upper_bound": tok_gpu * (fpt_rank * tp) / MI355X_BF16_DENSE_PEAK,
             "config": {"model": cfg_name(base), "layers": layers, "micro_batch": args.mbs, "seq_len": args.seq,
-                       "shard": {"q|k|v": 3 * nh * d, "I": I, "heads": nh, "vocab": V // tp}},
+                       "shard": {"q|k|v": 3 * nh * d, "I": I, "heads": nh, "vocab": V // tp},
+                       "sequence_parallel": sp},
             "roofline": {"bound": "mfma", "kernel": "gemm (every GEMM launch of one micro-batch)", "achieved": ach,
                          "peak": MI355X_BF16_DENSE_PEAK / 1e12, "unit": "TFLOP/s",
                          "frac": ach / (MI355X_BF16_DENSE_PEAK / 1e12), "launches": s["launches"],
@@ -320,8 +352,12 @@ def cp_proxy(args, base, layers):
     layer_flop_model = 6 * (2 * H * nh * d + 2 * H * nkv * d + 3 * H * I) + 12 * H * args.seq   # per token
     tok_gpu = B * S / (t_zz * layers)             # each rank holds S tokens; the ring's pace = its slowest rank
     tok_mesh = B * S / (t_mesh * layers)
-    return {"metric": f"CP={C} critical-rank proxy (1 GPU compute + costed xGMI communication)", "value": tok_mesh,
-            "unit": "tokens/s/GPU (zig-zag + mesh: compute measured, communication modelled)",
+    return {"metric": f"CP={C} critical-rank proxy (1 GPU, compute measured; xGMI communication costed separately)",
+            "value": tok_gpu, "unit": "tokens/s/GPU (compute-only, measured: zig-zag schedule's critical rank)",
+            # modelled, not measured: the mesh transfers costed at XGMI_LINK_GBPS (an assumed per-link
+            # rate) and overlapped as the schedule overlaps them
+            "modelled_with_mesh_comm_tokens_per_s_per_gpu": tok_mesh,
+            "comm_model": f"{XGMI_LINK_GBPS} GB/s per xGMI link and direction (assumed, not measured on this box)",
             "config": {"model": cfg_name(base), "layers": layers, "micro_batch": B, "seq_len": args.seq,
                        "S_local": S, "head_dim": d, "schedule": "zig-zag (load-balanced), full-mesh K|V exchange"},
             "compute_only_tokens_per_s_per_gpu": tok_gpu,

@@ -78,6 +78,11 @@ int pt_swiglu_bwd(const void* dh, int64_t dh_stride, const void* g, int64_t g_st
                   int64_t u_stride, void* dg, int64_t dg_stride, void* du, int64_t du_stride, int64_t rows,
                   int64_t cols, hipStream_t stream);
 
+/* ---- residual add: out = bf16(x + r), n contiguous bf16 (n % 8 == 0, 16-B aligned) ------------
+ * replaces picotron/model.py:208 `x + self.mlp(...)` where the sequence-parallel TP layer adds the
+ * residual to its reduce-scattered MLP output (no GEMM epilogue can carry it there). */
+int pt_residual_add(const void* x, const void* r, void* out, int64_t n, hipStream_t stream);
+
 /* ---- fused cross-entropy forward + backward -----------------------------------------------
  * replaces train.py:49 F.cross_entropy(logits, targets, 'mean') / grad_acc (+ autograd bwd) and
  * pipeline_parallel.py:103,153.  row_loss[r] = lse - logit[target]; dlogits (may alias logits) =

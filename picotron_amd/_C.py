@@ -46,6 +46,7 @@ SIGNATURES = {
     "pt_rope": (_i32, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _i32, _vp]),
     "pt_swiglu_fwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp]),
     "pt_swiglu_bwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp]),
+    "pt_residual_add": (_i32, [_vp, _vp, _vp, _i64, _vp]),
     "pt_cross_entropy_fwd_bwd": (_i32, [_vp, _i64, _vp, _vp, _i64, _vp, _i64, _i64, _f32, _vp, _i64, _vp, _vp]),
     "pt_cross_entropy_fwd_lse": (_i32, [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp]),
     "pt_cross_entropy_bwd_lse": (_i32, [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _i64, _i64, _vp]),

@@ -75,15 +75,10 @@ def enable_zigzag_residual(model):
     if pgm.current().cp_world_size == 1 or SW.zigzag_residual == 0 or getattr(model, "_pt_zigzag_residual", False):
         return getattr(model, "_pt_zigzag_residual", False)
     from ..model import DecoderLayer
-    tables = {}
     for name, mod in model.named_modules():
         leaf = name.rsplit(".", 1)[-1]
         if isinstance(mod, DecoderLayer):
-            key = mod._rope_args
-            if key not in tables:
-                tables[key] = zigzag_rope_tables(*key)
-            mod.zz_cos, mod.zz_sin = tables[key]
-            mod.cp_zigzag_residual = True
+            mod.cp_zigzag_residual = True   # its tables are built per local length (DecoderLayer._tables)
         elif leaf == "embedding" and not isinstance(mod, torch.nn.Identity):
             mod.register_forward_hook(_zz_entry_hook)
         elif leaf == "final_norm" and not isinstance(mod, torch.nn.Identity):
@@ -121,16 +116,26 @@ def _zz_exit_hook(module, args):
     return None
 
 
-def zigzag_rope_tables(seq_length, head_dim, base):
-    """get_cos_sin over the whole sequence, rows of this rank's zig-zag half-chunks r and 2C - 1 - r
-    (the positions of its zig-zag shard, row s of the local sequence = the token at local index s)."""
+def zigzag_rope_tables(max_positions, head_dim, base, S=None):
+    """The RoPE rows of this rank's zig-zag shard of local length S (default max_positions / C).
+
+    The reference rotates rank c's contiguous chunk with rows [c P, c P + S) of get_cos_sin(max_positions),
+    P = max_positions / C (update_rope_for_context_parallel's slice, of which Attention.forward uses
+    the first S rows: model.py:134-135, context_parallel.py:189-195).  Zig-zag half-chunk c (S / 2
+    tokens) is rank c // 2's half c % 2, so its rows are (c // 2) P + (c % 2) S / 2 + i; the shard
+    holds half-chunks r and 2C - 1 - r.  With max_positions == C S that is just c S / 2 + i; for
+    max_positions > C S the rows follow the reference's (non-contiguous) positions exactly."""
     from ..model import get_cos_sin
     m = pgm.current()
     C, r = m.cp_world_size, m.cp_rank
-    cos, sin = get_cos_sin(seq_length, head_dim=head_dim, base=base)
-    h = seq_length // (2 * C)
-    rows = lambda t: torch.cat([t[r * h:(r + 1) * h], t[(2 * C - 1 - r) * h:(2 * C - r) * h]])  # noqa: E731
-    return rows(cos), rows(sin)
+    P = max_positions // C
+    S = P if S is None else S
+    if S % 2 or S > P:
+        raise ValueError(f"zigzag_rope_tables: local sequence {S} must be even and <= max_positions / cp = {P}")
+    cos, sin = get_cos_sin(max_positions, head_dim=head_dim, base=base)
+    h = S // 2
+    idx = torch.cat([torch.arange(h) + (c // 2) * P + (c % 2) * h for c in (r, 2 * C - 1 - r)])
+    return cos[idx], sin[idx]
 
 
 def update_rope_for_context_parallel(cos, sin):
@@ -353,15 +358,18 @@ def mesh_backward(do, q, kv, o, lse, nkv, scale, blocks=HipBlocks):
     delta = blocks.delta(do, o)
     dq = torch.zeros(B, S, nh, d, dtype=torch.float32, device=q.device)
     dkv = torch.zeros(kv.shape, dtype=torch.float32, device=kv.device)
-    # what the peers need from me: K|V (their dQ), my queries and dO (bf16) and LSE | D (f32) (their dK/dV)
+    # what the peers need from me: K|V (their dQ), my queries and dO (bf16) and LSE | D (f32) (their
+    # dK/dV) -- all of them for a lower rank (it sees my keys as 'kv0': all my queries), only my
+    # second half-chunk's for a higher one (it sees them as 'q1')
     qdo = torch.cat([q.reshape(B, S, nh * d), do.reshape(B, S, nh * d)], dim=2).contiguous()
     ld = torch.stack([lse, delta], dim=2).contiguous()            # [B, nh, 2, S]
+    qdo_hi, ld_hi = qdo[:, h:].contiguous(), ld[..., h:].contiguous()
     peers = [j for j in range(C) if j != r]
     kvs = {j: torch.empty_like(kv) for j in peers}
-    qdos = {j: torch.empty_like(qdo) for j in peers}
-    lds = {j: torch.empty_like(ld) for j in peers}
+    qdos = {j: torch.empty_like(qdo if j > r else qdo_hi) for j in peers}
+    lds = {j: torch.empty_like(ld if j > r else ld_hi) for j in peers}
     pend_kv = _p2p(_mesh_ops([(kv, j) for j in peers], [(kvs[j], j) for j in peers], group, ids), group)
-    pend_q = _p2p(_mesh_ops([(t, j) for j in peers for t in (qdo, ld)],
+    pend_q = _p2p(_mesh_ops([(t, j) for j in peers for t in ((qdo, ld) if j < r else (qdo_hi, ld_hi))],
                             [(t[j], j) for j in peers for t in (qdos, lds)], group, ids), group)
     k, v = _kv_views(kv, B, S, nkv, d)
     dk, dv = _kv_views(dkv, B, S, nkv, d)
@@ -373,15 +381,17 @@ def mesh_backward(do, q, kv, o, lse, nkv, scale, blocks=HipBlocks):
             blocks.bwd_dq(do, q, kj[:, :h], vj[:, :h], lse, delta, scale, False, dq)
         else:        # my second half x all of it
             blocks.bwd_dq(do[:, h:], q[:, h:], kj, vj, lse[:, :, h:], delta[:, :, h:], scale, False, dq[:, h:])
+    kvs = kj = vj = None   # the visiting K|V shards are done with: release them before the dK|dV parts
     _p2p_wait(pend_q)
     for j in peers:
-        qj = qdos[j][:, :, :nh * d].view(B, S, nh, d)
-        doj = qdos[j][:, :, nh * d:].view(B, S, nh, d)
+        n = qdos[j].shape[1]   # S (j > r: all its queries) or h (j < r: its second half only)
+        qj = qdos[j][:, :, :nh * d].view(B, n, nh, d)
+        doj = qdos[j][:, :, nh * d:].view(B, n, nh, d)
         lsej, dj = lds[j][:, :, 0], lds[j][:, :, 1]
         if j > r:    # all its queries x my first half
             blocks.bwd_dkdv(doj, qj, k[:, :h], v[:, :h], lsej, dj, scale, False, dk[:, :h], dv[:, :h])
         else:        # its second-half queries x all my keys
-            blocks.bwd_dkdv(doj[:, h:], qj[:, h:], k, v, lsej[:, :, h:], dj[:, :, h:], scale, False, dk, dv)
+            blocks.bwd_dkdv(doj, qj, k, v, lsej, dj, scale, False, dk, dv)
     return dq, dkv
 
 

@@ -298,7 +298,7 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
   constexpr int TILE_B = KT * D * 2;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
   lds_u8* smem = (lds_u8*)smem_raw;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: an SGPR
   const int nqb = a.Sq / (NWK * 32);
   const int h = h_or_hk;
   const int qb = a.causal ? nqb - 1 - bx : bx;  // heavy blocks first
@@ -499,7 +499,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, i
   constexpr int TILE_B = KT * D * 2;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
   lds_u8* smem = (lds_u8*)smem_raw;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: an SGPR
   const int kb = bx, hk = h_or_hk;
   const int k0 = kb * NW * 32 + wave * 32;
   const int mykey = k0 + (lane & 31);
@@ -667,7 +667,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_pair_block(const AttnArgs& a, int 
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
   lds_u8* smem = (lds_u8*)smem_raw;
   lds_u8* xch = smem + NSTG * STAGE_B;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: an SGPR
   const bool score = wave < 4;
   const int pr = wave & 3;
   const int k0 = bx * 128 + pr * 32;
@@ -878,7 +878,7 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
   constexpr int TILE_B = KT * D * 2;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
   lds_u8* smem = (lds_u8*)smem_raw;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: an SGPR
   const int nqb = a.Sq / (NW * 32);
   const int h = h_or_hk;
   const int qb = a.causal ? nqb - 1 - bx : bx;
@@ -986,10 +986,15 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
   }
 
   if (!a.grad_f32) {
-    uint16_t* dqr = (uint16_t*)a.dq + b * a.dq_sb + (int64_t)myq * a.dq_ss + h * a.dq_sh;
+    // the row index re-derived behind an opaque copy: the epilogue's row pointers (and the RoPE
+    // tables') are then formed here, not hoisted into the prologue and held across the loop (at d128
+    // that spilled them to scratch)
+    int myq_e = myq, lane_e = lane;
+    asm volatile("" : "+v"(myq_e), "+v"(lane_e));
+    uint16_t* dqr = (uint16_t*)a.dq + b * a.dq_sb + (int64_t)myq_e * a.dq_ss + h * a.dq_sh;
     if (a.rope_cos) {
-      store_T_bf16_unrope<DT>(dqr, dq, a.scale, a.rope_cos + (int64_t)myq * a.rope_ld,
-                              a.rope_sin + (int64_t)myq * a.rope_ld, lane);
+      store_T_bf16_unrope<DT>(dqr, dq, a.scale, a.rope_cos + (int64_t)myq_e * a.rope_ld,
+                              a.rope_sin + (int64_t)myq_e * a.rope_ld, lane_e);
     } else {
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) store_T_bf16(dqr, dt, dq[dt], a.scale, lane);

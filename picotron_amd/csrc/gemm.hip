@@ -709,7 +709,7 @@ __device__ __forceinline__ void gemm_8ph_tile(const GemmArgs& a, const int tile_
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
   lds_u8* smem = (lds_u8*)smem_raw;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: an SGPR
   const int wm = wave >> 2, wn = wave & 3;
   const int m0 = tile_m * 256, n0 = tile_n * 256;
 
@@ -937,7 +937,7 @@ __device__ __forceinline__ void gemm_4ph_tile(const GemmArgs& a, const int tile_
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
   lds_u8* smem = (lds_u8*)smem_raw;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: an SGPR
   const int wm = wave >> 1, wn = wave & 1;
   const int m0 = tile_m * 256, n0 = tile_n * 128;
 
@@ -1088,7 +1088,7 @@ __device__ __forceinline__ void gemm_kh_tile(const GemmArgs& a, const int tile_m
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
   lds_u8* smem = (lds_u8*)smem_raw;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: an SGPR
   const int grp = wave >> 2, wm = (wave >> 1) & 1, wn = wave & 1;
   const int m0 = tile_m * 256, n0 = tile_n * 128;
 
@@ -1282,7 +1282,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const GemmGroup g) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
   lds_u8* smem = (lds_u8*)smem_raw;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: an SGPR
   const int wm = wave / WN, wn = wave % WN;
   int tile_m, tile_n, ks;
   const GemmArgs& a = select_problem(g, tile_m, tile_n, ks);
@@ -1496,13 +1496,21 @@ const int kTileBN[kNumTiles] = {0, 0, 128, 64, 0, 0, 0, 0, 0, 0, 0, 0, 256, 128,
 
 template <bool AK, bool BKC, int EPI>
 int launch_layout(const GemmGroup& a, int tile, hipStream_t s) {
-  switch (tile) {
-    case 12: return launch_8ph<AK, BKC, EPI>(a, s);
-    case 13: return launch_4ph<AK, BKC, EPI>(a, s);
-    case 14: return launch_kh<AK, BKC, EPI>(a, s);
-    case 2: return launch_t<128, 128, 2, 2, AK, BKC, EPI>(a, s);
-    case 3: return launch_t<64, 64, 2, 2, AK, BKC, EPI>(a, s);
-    default: return PT_EUNSUPPORTED;
+  if constexpr (!AK && BKC) {  // A M-contiguous with B K-contiguous: no layer GEMM takes this layout,
+    switch (tile) {            // so only the simple tiles are built for it (pick_group_tile knows)
+      case 2: return launch_t<128, 128, 2, 2, AK, BKC, EPI>(a, s);
+      case 3: return launch_t<64, 64, 2, 2, AK, BKC, EPI>(a, s);
+      default: return PT_EUNSUPPORTED;
+    }
+  } else {
+    switch (tile) {
+      case 12: return launch_8ph<AK, BKC, EPI>(a, s);
+      case 13: return launch_4ph<AK, BKC, EPI>(a, s);
+      case 14: return launch_kh<AK, BKC, EPI>(a, s);
+      case 2: return launch_t<128, 128, 2, 2, AK, BKC, EPI>(a, s);
+      case 3: return launch_t<64, 64, 2, 2, AK, BKC, EPI>(a, s);
+      default: return PT_EUNSUPPORTED;
+    }
   }
 }
 
@@ -1625,7 +1633,7 @@ bool args_fit(const GemmArgs& a, int tile) {
 // smallest modelled time, rounds x tile work / the kernel's sustained rate (one CU per workgroup:
 // ceil(tiles / 256) rounds; in-situ TF/s 1.30 / 1.20 / 0.85 / 0.45 for 256x256 / 256x128 / 128x128
 // / 64x64), which trades the phased kernels' rate for the smaller tiles' parallelism.
-int pick_group_tile(const GemmGroup& g) {
+int pick_group_tile(const GemmGroup& g, bool simple_only = false) {
   auto fits = [&](int t) {
     for (int i = 0; i < g.nprob; ++i)
       if (!args_fit(g.p[i], t)) return false;
@@ -1641,14 +1649,14 @@ int pick_group_tile(const GemmGroup& g) {
     const int64_t tiles = ntiles(t);
     return (double)tiles / (double)(((tiles + 255) / 256) * 256);
   };
-  const bool f12 = fits(12), f13 = fits(13);
+  const bool f12 = !simple_only && fits(12), f13 = !simple_only && fits(13);
   const int phased = f12 && (!f13 || fill(12) >= fill(13)) ? 12 : (f13 ? 13 : -1);
   if (phased >= 0 && ntiles(phased) >= 128) return phased;
   const int cand[4] = {12, 13, 2, 3};
   const double rate[4] = {1.30, 1.20, 0.85, 0.45};
   int best = -1;
   double best_cost = 0.0;
-  for (int i = 0; i < 4; ++i) {
+  for (int i = simple_only ? 2 : 0; i < 4; ++i) {
     if (!fits(cand[i])) continue;
     const double c = (double)((ntiles(cand[i]) + 255) / 256) * kTileBM[cand[i]] * kTileBN[cand[i]] / rate[i];
     if (best < 0 || c < best_cost) best = cand[i], best_cost = c;
@@ -1715,7 +1723,7 @@ int launch_group(GemmGroup& g, int a_kcontig, int b_kcontig, int epilogue, int t
   }
   const bool auto_tile = tile < 0;
   if (epilogue == EPI_ROPE && tile < 0) tile = args_fit(g.p[0], 13) ? 13 : 12;
-  if (tile < 0) tile = pick_group_tile(g);
+  if (tile < 0) tile = pick_group_tile(g, !a_kcontig && b_kcontig);
   if (auto_tile && tile == 13 && kh_enabled(g) && epilogue != EPI_CE_STATS) tile = 14;
   if (epilogue == EPI_ROPE) {
     if (!a_kcontig || !b_kcontig) return PT_EUNSUPPORTED;

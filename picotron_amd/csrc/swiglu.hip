@@ -59,6 +59,22 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const uint16_t* __restr
   }
 }
 
+// out = bf16(x + r) over n contiguous elements (n % 8 == 0): the residual add of model.py:208
+// (`x = x + self.mlp(...)`, torch's bf16 add: the fp32 sum rounded once) where it cannot ride in a
+// GEMM epilogue -- the sequence-parallel TP layer adds the residual to the reduce-scattered MLP
+// output.  HBM-bound, 6 bytes per element.
+__global__ __launch_bounds__(256) void residual_add_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ r,
+                                                           uint16_t* __restrict__ out, int64_t n8) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    float a[8], b[8], o[8];
+    unpack8(ld8(x + i * 8), a);
+    unpack8(ld8(r + i * 8), b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = a[j] + b[j];
+    st8(out + i * 8, pack8(o));
+  }
+}
+
 int grid_for(int64_t total) {
   int64_t g = (total + 255) / 256;
   return (int)(g < PT_STREAM_GRID_CAP * 2 ? g : PT_STREAM_GRID_CAP * 2);
@@ -90,6 +106,15 @@ int pt_swiglu_bwd(const void* dh, int64_t dh_stride, const void* g, int64_t g_st
   swiglu_bwd_kernel<<<grid_for(rows * (cols / 8)), 256, 0, stream>>>(
       (const uint16_t*)dh, dh_stride, (const uint16_t*)g, g_stride, (const uint16_t*)u, u_stride, (uint16_t*)dg,
       dg_stride, (uint16_t*)du, du_stride, rows, (int)cols);
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
+
+int pt_residual_add(const void* x, const void* r, void* out, int64_t n, hipStream_t stream) {
+  if (!x || !r || !out || n <= 0) return PT_EINVAL;
+  if ((n & 7) || !pt_aligned16(x) || !pt_aligned16(r) || !pt_aligned16(out)) return PT_EALIGN;
+  residual_add_kernel<<<grid_for(n / 8), 256, 0, stream>>>((const uint16_t*)x, (const uint16_t*)r, (uint16_t*)out,
+                                                           n / 8);
   PT_CHECK_LAUNCH();
   return PT_OK;
 }

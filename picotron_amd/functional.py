@@ -163,13 +163,39 @@ def _norm_dw_sink(weight):
     return weight.grad, K.DW_ACC_BF16
 
 
+def _sp_sum_partials(pending):
+    """Sequence-parallel norms (entries with a tp group): each rank's column sums cover only its
+    token rows, so their sum over the tp group is the weight gradient the reference computes on every
+    rank.  Their partials are summed into one f32 [n, H] block per (width, stream, group), ONE
+    all-reduce of it runs over the tp group, and each row re-enters the queue as a one-row partial
+    (the sinks then see exactly the non-SP path's colsum).  Returns the rewritten entry list."""
+    out, sp = [], {}
+    for e in pending:
+        if e[3] is None:
+            out.append(e)
+        else:
+            part, weight, stream, tp = e
+            sp.setdefault((part.shape[1], part.device, stream, id(tp.group)), []).append(e)
+    for (cols, dev, stream, _), es in sp.items():
+        with torch.cuda.stream(stream):
+            tot = torch.zeros(len(es), cols, dtype=torch.float32, device=dev)
+            for i in range(0, len(es), 32):
+                K.rmsnorm_colsum_batch([(p, tot[j], K.DW_ACC_F32) for j, (p, _, _, _) in enumerate(es[i:i + 32], i)])
+            es[0][3].all_reduce(tot)
+            out += [(tot[j:j + 1], w, st, None, True) for j, (_, w, st, _) in enumerate(es)]
+    return out
+
+
 def _flush_norm_dw(task):
     """Sum every pending partial into its sink.  Sinks are resolved here, in backward order, so a
     .grad is only created (and stored into) once its sum is launched; a weight used by several
     norms of one backward gets a store and then accumulates, and jobs that share a sink go into
     separate, stream-ordered launches (generation g = the g-th job on that sink)."""
     groups, seen = {}, {}
-    for part, weight, stream in _PENDING_DW.pop(task, []):
+    notify = []
+    for part, weight, stream, *rest in _sp_sum_partials(_PENDING_DW.pop(task, [])):
+        if rest and rest[-1] is True:   # a sequence-parallel norm's summed gradient: tell its owner
+            notify.append(weight)
         buf, sink = _norm_dw_sink(weight)
         gen = seen.get(buf.data_ptr(), 0)
         seen[buf.data_ptr()] = gen + 1
@@ -178,16 +204,34 @@ def _flush_norm_dw(task):
         with torch.cuda.stream(stream):   # the stream the partials were produced on
             for i in range(0, len(js), 32):
                 K.rmsnorm_colsum_batch(js[i:i + 32])
+    for w in notify:
+        _grad_ready(w)
 
 
-def norm_bwd(dy2, z, weight, rstd, mode, dres=None, need_dw=True):
+def norm_bwd(dy2, z, weight, rstd, mode, dres=None, need_dw=True, sp=None):
     """RMSNorm backward with the weight gradient summed straight into p's sink (bf16 .grad store or
     accumulate -- autograd's AccumulateGrad -- or the f32 main_grad of DataParallelBucket).  A frozen
-    weight (requires_grad=False) gets no gradient, as under autograd."""
+    weight (requires_grad=False) gets no gradient, as under autograd.  sp: the TPContext whose ranks
+    hold the other token rows (sequence parallelism): the weight gradient is the sum over that group
+    of this rank's column sums (_sp_sum_partials, at the end of the backward)."""
     if not (need_dw and weight.requires_grad):
         dx, _ = K.rmsnorm_bwd(dy2, z, weight, rstd, mode, dres=dres)
         return dx
     task = torch._C._current_graph_task_id()   # -1 outside an autograd backward
+    if sp is not None and sp.world_size > 1:
+        dx, partial = K.rmsnorm_bwd(dy2, z, weight, rstd, mode, dres=dres, defer_dw=True)
+        entry = (partial, weight, torch.cuda.current_stream(z.device), sp)
+        if task == -1:   # not inside an autograd backward: sum and store now
+            for part, w, st, *_ in _sp_sum_partials([entry]):
+                buf, sink = _norm_dw_sink(w)
+                K.rmsnorm_colsum_batch([(part, buf, sink)])
+                _grad_ready(w)
+            return dx
+        if task not in _PENDING_DW:
+            _PENDING_DW[task] = []
+            torch.autograd.Variable._execution_engine.queue_callback(lambda: _flush_norm_dw(task))
+        _PENDING_DW[task].append(entry)
+        return dx
     # an owner that all-reduces this backward (a data-parallel wrapper outside no_sync) is told at once
     sync = getattr(weight, "_pt_grad_sync", None)
     waiting = getattr(weight, "_pt_grad_ready", None) is not None and (sync is None or sync())
@@ -196,7 +240,7 @@ def norm_bwd(dy2, z, weight, rstd, mode, dres=None, need_dw=True):
         if task not in _PENDING_DW:
             _PENDING_DW[task] = []
             torch.autograd.Variable._execution_engine.queue_callback(lambda: _flush_norm_dw(task))
-        _PENDING_DW[task].append((partial, weight, torch.cuda.current_stream(z.device)))
+        _PENDING_DW[task].append((partial, weight, torch.cuda.current_stream(z.device), None))
         return dx
     buf, sink = _norm_dw_sink(weight)
     dx, _ = K.rmsnorm_bwd(dy2, z, weight, rstd, mode, dres=dres, dw_out=buf, dw_sink=sink)
@@ -224,6 +268,37 @@ class TPContext:
         if self.world_size == 1:
             return None
         return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+
+    # ---- sequence parallelism (tensor_parallel/sequence_parallel.py): the residual stream between
+    # the TP blocks is sharded by token rows over the tp group; the all-reduce of a row-parallel
+    # output becomes a reduce-scatter onto the shards, a column-parallel input an all-gather of them
+    def _nccl(self):
+        return dist.get_backend(self.group) == "nccl"
+
+    def all_gather_rows(self, t):
+        """This rank's [n, ...] rows -> [world * n, ...] (rank i's rows at i * n)."""
+        if self.world_size == 1:
+            return t
+        t = t.contiguous()
+        out = torch.empty((self.world_size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        if self._nccl():
+            dist.all_gather_into_tensor(out, t, group=self.group)
+        else:   # gloo (CPU tests, one-GPU rehearsals): the list form
+            dist.all_gather(list(out.chunk(self.world_size)), t, group=self.group)
+        return out
+
+    def reduce_scatter_rows(self, t, async_op=False):
+        """[world * n, ...] partial sums -> (this rank's [n, ...] rows of their sum, handle or None)."""
+        if self.world_size == 1:
+            return t, None
+        n = t.shape[0] // self.world_size
+        if self._nccl():
+            out = torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+            h = dist.reduce_scatter_tensor(out, t.contiguous(), op=dist.ReduceOp.SUM, group=self.group,
+                                           async_op=async_op)
+            return out, h
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)   # gloo: the sum, then my rows
+        return t[self.rank * n:(self.rank + 1) * n], None
 
 
 def _contig2d(x):
@@ -425,8 +500,9 @@ def attention_core_bwd(do, qkv, o, lse, sh, cos, sin, scale):
     return dqkv
 
 
-def attn_block_fwd(h2, wq, wk, wv, wo, cos, sin, sh, tp):
-    """h2 [T,H] -> (a [T,H], saved).  Row-parallel out_proj: a = sum over tp of o W_o^T."""
+def attn_block_fwd(h2, wq, wk, wv, wo, cos, sin, sh, tp, reduce=True):
+    """h2 [T,H] -> (a [T,H], saved).  Row-parallel out_proj: a = sum over tp of o W_o^T (reduce=False:
+    this rank's partial, for the sequence-parallel reduce-scatter)."""
     scale = 1.0 / math.sqrt(sh.d)
     if _fuse() and K.rope_fusable(h2.shape[0], sh.d, sh.S, (wq.shape[0], wk.shape[0], wv.shape[0])):   # RoPE of q|k in the projection's epilogue
         qkv = K.linear_fwd_rope(h2, [wq, wk, wv], cos, sin, sh.S, sh.nh + sh.nkv, sh.d)
@@ -435,7 +511,8 @@ def attn_block_fwd(h2, wq, wk, wv, wo, cos, sin, sh, tp):
         qkv = K.linear_fwd(h2, [wq, wk, wv])
         o, lse = attention_core_fwd(qkv, sh, cos, sin, scale)
     a = K.linear_fwd(o.view(sh.T, sh.wq), [wo])
-    tp.all_reduce(a)
+    if reduce:
+        tp.all_reduce(a)
     return a, (qkv, o, lse)
 
 
@@ -443,9 +520,10 @@ def _dual_qkv_enabled():
     return SW.dual_qkv != 0
 
 
-def attn_block_bwd(da, h2, saved, wq, wk, wv, wo, cos, sin, sh, tp, need_dx=True, keep_parts=False):
+def attn_block_bwd(da, h2, saved, wq, wk, wv, wo, cos, sin, sh, tp, need_dx=True, keep_parts=False, sp=False):
     """keep_parts: the q|k|v dX may come back as K.SplitKParts (two f32 K halves) for a following
-    rmsnorm backward to sum."""
+    rmsnorm backward to sum.  sp: the column-parallel dX is reduce-scattered onto this rank's token
+    rows (sequence parallelism) instead of all-reduced."""
     qkv, o, lse = saved
     scale = 1.0 / math.sqrt(sh.d)
     do2 = K.linear_dgrad(da, [wo])
@@ -461,7 +539,10 @@ def attn_block_bwd(da, h2, saved, wq, wk, wv, wo, cos, sin, sh, tp, need_dx=True
     dh = handle = None
     if need_dx:
         dh = K.linear_dgrad(dqkv, [wq, wk, wv])
-        handle = tp.all_reduce(dh, async_op=True)
+        if sp:
+            dh, handle = tp.reduce_scatter_rows(dh, async_op=True)
+        else:
+            handle = tp.all_reduce(dh, async_op=True)
     # dW of q|k|v and of o_proj in one launch: 192 + 64 tiles of 256x256 at SmolLM-1.7B dims,
     # where either alone leaves CUs idle (o_proj's wgrad was deferred from above; its inputs
     # da and o stay alive until here anyway)
@@ -495,8 +576,9 @@ class AttentionFunction(torch.autograd.Function):
 
 
 # ------------------------------------------------------------------------ MLP block
-def mlp_block_fwd(h2, wg, wu, wd, tp, residual=None):
-    """h2 [T,H] -> down(silu(gate) * up) (+ residual, entering the tp sum once, from tp rank 0)."""
+def mlp_block_fwd(h2, wg, wu, wd, tp, residual=None, reduce=True):
+    """h2 [T,H] -> down(silu(gate) * up) (+ residual, entering the tp sum once, from tp rank 0;
+    reduce=False: this rank's partial, no residual, for the sequence-parallel reduce-scatter)."""
     I = wg.shape[0]
     if _fuse() and K.swiglu_fuse_pays(h2.shape[0], I):   # SwiGLU in the gate|up GEMM's epilogue
         gu, hh = K.linear_swiglu_fwd(h2, wg, wu)
@@ -505,7 +587,8 @@ def mlp_block_fwd(h2, wg, wu, wd, tp, residual=None):
         hh = K.swiglu_fwd(gu[:, :I], gu[:, I:])
     res = residual if (residual is not None and tp.rank == 0) else None
     m = K.linear_fwd(hh, [wd], residual=res)
-    tp.all_reduce(m)
+    if reduce:
+        tp.all_reduce(m)
     return m, (gu, hh)
 
 
@@ -513,9 +596,10 @@ def _dual_gu_enabled():
     return SW.dual_gu != 0
 
 
-def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True, keep_parts=False):
+def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True, keep_parts=False, sp=False):
     """keep_parts: the gate|up dX may come back as K.SplitKParts (its split-K halves unsummed) for a
-    following rmsnorm backward to sum."""
+    following rmsnorm backward to sum.  sp: the column-parallel dX is reduce-scattered onto this
+    rank's token rows instead of all-reduced."""
     gu, hh = saved
     I = wg.shape[0]
     if _fuse() and K.swiglu_fuse_pays(dm.shape[0], I, backward=True):   # SwiGLU bwd in the down dX epilogue
@@ -542,7 +626,10 @@ def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True, keep_parts=False)
                                 order=SW.gu_dual_order if SW.gu_dual_order >= 0 else None)
     if need_dx:
         dh = K.linear_dgrad(dgu, [wg, wu])
-        handle = tp.all_reduce(dh, async_op=True)
+        if sp:
+            dh, handle = tp.reduce_scatter_rows(dh, async_op=True)
+        else:
+            handle = tp.all_reduce(dh, async_op=True)
     wgrad(dgu, h2, [wg, wu])
     if handle is not None:
         handle.wait()
@@ -580,7 +667,11 @@ class DecoderLayerFunction(torch.autograd.Function):
     shard (cos / sin its positions' tables): the ring runs on it with no re-lay."""
 
     @staticmethod
-    def forward(ctx, x, w1, w2, wq, wk, wv, wo, wg, wu, wd, cos, sin, eps, mode, nh, nkv, d, zz=False):
+    def forward(ctx, x, w1, w2, wq, wk, wv, wo, wg, wu, wd, cos, sin, eps, mode, nh, nkv, d, zz=False, sp=False):
+        if sp:
+            return DecoderLayerFunction._forward_sp(ctx, x, w1, w2, wq, wk, wv, wo, wg, wu, wd, cos, sin, eps, mode,
+                                                    nh, nkv, d)
+        ctx.sp = False
         B, S, H = x.shape
         sh = AttnShape(B, S, nh, nkv, d, zz)
         tp = TPContext.current()
@@ -595,7 +686,56 @@ class DecoderLayerFunction(torch.autograd.Function):
         return out.view(B, S, H)
 
     @staticmethod
+    def _forward_sp(ctx, x, w1, w2, wq, wk, wv, wo, wg, wu, wd, cos, sin, eps, mode, nh, nkv, d):
+        """Sequence-parallel TP layer (tensor_parallel/sequence_parallel.py): x is this rank's shard
+        of the residual stream, token rows [r T/tp, (r+1) T/tp) of the flattened [B*S, H] batch, viewed
+        as [B, S/tp, H].  The norms and residual adds run on the shard; the column-parallel inputs
+        are all-gathered ([T, H], as the reference's replicated norm output), the row-parallel outputs
+        reduce-scattered onto the shards (the reference's all-reduce, keeping only this rank's rows):
+
+            h1 = AG(norm1(x));  a = RS(attn(h1));  z = x + a (fused into norm2);  h2 = AG(norm2(z))
+            out = z + RS(mlp(h2))
+
+        The same values as the reference's layer (model.py:204-209 with tp_communications.py:35-49),
+        row by row; per rank the norms / adds touch T/tp rows instead of T."""
+        tp = TPContext.current()
+        B, Sl, H = x.shape
+        S = Sl * tp.world_size
+        sh = AttnShape(B, S, nh, nkv, d)
+        x2 = _contig2d(x)
+        h1r, rstd1, _ = K.rmsnorm_fwd(x2, w1, eps, mode)
+        h1 = tp.all_gather_rows(h1r)
+        a, asaved = attn_block_fwd(h1, wq, wk, wv, wo, cos, sin, sh, tp, reduce=False)
+        ar, _ = tp.reduce_scatter_rows(a)
+        h2r, rstd2, z = K.rmsnorm_fwd(ar, w2, eps, mode, residual=x2)
+        h2 = tp.all_gather_rows(h2r)
+        m, msaved = mlp_block_fwd(h2, wg, wu, wd, tp, reduce=False)
+        mr, _ = tp.reduce_scatter_rows(m)
+        out = K.residual_add(z, mr.contiguous())
+        ctx.save_for_backward(x2, h1, rstd1, *asaved, z, h2, rstd2, *msaved,
+                              w1, w2, wq, wk, wv, wo, wg, wu, wd, cos, sin)
+        ctx.sh, ctx.mode, ctx.sp = sh, mode, True
+        return out.view(B, Sl, H)
+
+    @staticmethod
+    def _backward_sp(ctx, dout):
+        (x2, h1, rstd1, qkv, o, lse, z, h2, rstd2, gu, hh,
+         w1, w2, wq, wk, wv, wo, wg, wu, wd, cos, sin) = ctx.saved_tensors
+        sh, mode = ctx.sh, ctx.mode
+        tp = TPContext.current()
+        dout2 = _contig2d(dout)                       # [T/tp, H]: the residual's gradient rows
+        dm = tp.all_gather_rows(dout2)                # the row-parallel down_proj sees every row
+        dh2 = mlp_block_bwd(dm, h2, (gu, hh), wg, wu, wd, tp, sp=True)
+        dz = norm_bwd(dh2, z, w2, rstd2, mode, dres=dout2, sp=tp)
+        da = tp.all_gather_rows(dz)
+        dh1 = attn_block_bwd(da, h1, (qkv, o, lse), wq, wk, wv, wo, cos, sin, sh, tp, sp=True)
+        dx = norm_bwd(dh1, x2, w1, rstd1, mode, dres=dz, sp=tp)
+        return (dx.view(dout.shape),) + (None,) * 18
+
+    @staticmethod
     def backward(ctx, dout):
+        if ctx.sp:
+            return DecoderLayerFunction._backward_sp(ctx, dout)
         (x2, h1, rstd1, qkv, o, lse, z, h2, rstd2, gu, hh,
          w1, w2, wq, wk, wv, wo, wg, wu, wd, cos, sin) = ctx.saved_tensors
         sh, mode = ctx.sh, ctx.mode
@@ -606,7 +746,7 @@ class DecoderLayerFunction(torch.autograd.Function):
         dz = norm_bwd(dh2, z, w2, rstd2, mode, dres=dout2)
         dh1 = attn_block_bwd(dz, h1, (qkv, o, lse), wq, wk, wv, wo, cos, sin, sh, tp, keep_parts=K.norm_splitk_enabled())
         dx = norm_bwd(dh1, x2, w1, rstd1, mode, dres=dz)   # (norm_bwd skips dW of frozen weights)
-        return (dx.view(sh.B, sh.S, -1),) + (None,) * 17
+        return (dx.view(sh.B, sh.S, -1),) + (None,) * 18
 
 
 # ------------------------------------------------------------------------ cross entropy

@@ -257,6 +257,16 @@ def swiglu_bwd(dh, g, u, dg=None, du=None):
     return dg, du
 
 
+def residual_add(x, r):
+    """bf16(x + r) of two contiguous bf16 tensors of one shape (model.py:208's residual add)."""
+    _req(x.dtype == BF16 and r.dtype == BF16 and x.shape == r.shape and x.is_contiguous() and r.is_contiguous(),
+         "residual_add: contiguous bf16 tensors of one shape")
+    out = torch.empty_like(x)
+    rc = _C.lib().pt_residual_add(_ptr(x), _ptr(r), _ptr(out), x.numel(), _C.stream_ptr(x.device))
+    _C.check(rc, "pt_residual_add")
+    return out
+
+
 # ---------------------------------------------------------------------------- device status
 STATUS_BAD_TARGET = 1   # PT_STATUS_BAD_TARGET (include/picotron_hip.h)
 _STATUS = {}
@@ -620,6 +630,16 @@ def _gemm_ksplit(A, lda, a_kcontig, Bs, ldbs, b_bounds, b_kcontig, b_seg_dim, ou
     return out
 
 
+def _reduce_sink_ok(out, residual=None):
+    """pt_gemm_splitk_reduce writes 16-B (f32) / 8-B (bf16) row chunks and reads the residual the same
+    way: a sink (or residual) it cannot address so -- a misaligned view -- keeps the unsplit GEMM,
+    decided before anything is launched (the reduce pass would refuse it after the partial GEMM)."""
+    for t in (out,) if residual is None else (out, residual):
+        if t.stride(1) != 1 or t.stride(0) % 4 or t.data_ptr() % (16 if t.dtype == torch.float32 else 8):
+            return False
+    return True
+
+
 def _sink(outs, bounds, mode, residual=None, ldr=0):
     """(outs, row bounds, epilogue, residual, ldr) of a split-K problem's real sink."""
     return outs, bounds, mode, residual, ldr
@@ -681,7 +701,7 @@ def linear_wgrad_grouped(jobs, epilogue=EPI_BF16, tile=-1):
     that would leave most CUs idle (TP shards) runs split-K (wgrad_ksplit)."""
     if tile < 0 and epilogue in (EPI_BF16, EPI_BF16_ACC, EPI_F32_ACC):
         s = wgrad_ksplit([(dy.shape[1], x.shape[1], dy.shape[0]) for dy, x, _ in jobs])
-        if s > 1 and all(o.stride(1) == 1 and o.stride(0) % 4 == 0 for _, _, outs in jobs for o in outs):
+        if s > 1 and all(_reduce_sink_ok(o) for _, _, outs in jobs for o in outs):
             return _wgrad_ksplit_run(jobs, epilogue, s)
     probs = (_C.GemmProblem * len(jobs))()
     flops = nbytes = 0.0
@@ -728,7 +748,7 @@ def linear_fwd(x2d, weights, out=None, tile=-1, residual=None):
         h = _splitk_halves(T, N, K)
         if h is not None:
             return _linear_fwd_splitk(x2d, weights, h, y, residual)
-    if tile < 0 and y.stride(0) % 4 == 0:
+    if tile < 0 and _reduce_sink_ok(y, residual):
         s, t = fewtile_ksplit(T, N, K)
         if s > 1 and all(n % (256 if t == 12 else 128) == 0 for n in ns):
             return _gemm_ksplit(x2d, x2d.stride(0), 1, weights, [K] * len(weights), _bounds(ns), 1, 0, y, T, N, K, s, t,
@@ -985,7 +1005,7 @@ def linear_dgrad(dy2d, weights, out=None, accumulate=False, tile=-1):
                 all(n % 64 == 0 for n in ns):
             return _linear_dgrad_splitk(dy2d, weights, h, torch.empty(T, Kin, dtype=BF16, device=dy2d.device))
     dx = out if out is not None else torch.empty(T, Kin, dtype=BF16, device=dy2d.device)
-    if tile < 0 and dx.stride(1) == 1 and dx.stride(0) % 4 == 0:
+    if tile < 0 and _reduce_sink_ok(dx):
         s, t = fewtile_ksplit(T, Kin, N)
         if s > 1 and all(n % 64 == 0 for n in ns):
             return _gemm_ksplit(dy2d, dy2d.stride(0), 1, weights, [Kin] * len(weights), _bounds(ns), 0, 1, dx, T, Kin,
@@ -1076,9 +1096,7 @@ def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None, keep
         if wepilogue in (EPI_BF16, EPI_BF16_ACC, EPI_F32_ACC) else 1
     # the reduce pass writes 16-B (f32) / 8-B (bf16) row chunks: a sink it cannot address that way (a
     # misaligned .grad / main_grad view) keeps the unsplit dW, decided before anything is launched
-    if ws > 1 and not all(o.stride(1) == 1 and o.stride(0) % 4 == 0 and
-                          o.data_ptr() % (16 if o.dtype == torch.float32 else 8) == 0
-                          for _, _, outs in wjobs for o in outs):
+    if ws > 1 and not all(_reduce_sink_ok(o) for _, _, outs in wjobs for o in outs):
         ws = 1
     wparts = []
     for j, (wdy, x2d, outs) in enumerate(wjobs):
@@ -1148,7 +1166,7 @@ def linear_wgrad(dy2d, x2d, outs, epilogue=EPI_BF16, tile=-1):
     ns = [o.shape[0] for o in outs]
     _req(sum(ns) == N, "wgrad: output rows must cover dY's width")
     if tile < 0 and epilogue in (EPI_BF16, EPI_BF16_ACC, EPI_F32_ACC) and wgrad_ksplit([(N, Kin, T)]) > 1 and \
-            all(o.stride(1) == 1 and o.stride(0) % 4 == 0 for o in outs):
+            all(_reduce_sink_ok(o) for o in outs):
         _wgrad_ksplit_run([(dy2d, x2d, outs)], epilogue, wgrad_ksplit([(N, Kin, T)]))
         return outs
     _gemm(dy2d, dy2d.stride(0), 0, [x2d], [x2d.stride(0)], [0, Kin], 0, 0, outs, [o.stride(0) for o in outs],

@@ -26,6 +26,7 @@ from . import functional as FN
 from . import kernels as K
 from . import process_group_manager as pgm
 from .context_parallel import context_parallel
+from .tensor_parallel import sequence_parallel
 
 
 def _flash():
@@ -260,28 +261,39 @@ class DecoderLayer(nn.Module):
         self.cos, self.sin = get_cos_sin(config.max_position_embeddings, head_dim=head_dim, base=config.rope_theta)
         self.cos, self.sin = context_parallel.update_rope_for_context_parallel(self.cos, self.sin)
         # set by context_parallel.apply_context_parallel at cp > 1: the input is the zig-zag shard of
-        # the residual stream (zz_cos / zz_sin: that shard's positions) whenever its length tiles
+        # the residual stream (RoPE rows: that shard's positions, _tables) whenever its length tiles
         self.cp_zigzag_residual = False
+        # set by tensor_parallel.apply_tensor_parallel at tp > 1: the input is this rank's token-row
+        # shard of the residual stream whenever the batch was sharded (sequence_parallel.local_len)
+        self.tp_sequence_parallel = False
 
-    def _tables(self, device, zz=False):
-        # tables follow the activations' device (the module may have been moved after init)
-        a, b = ("zz_cos", "zz_sin") if zz else ("cos", "sin")
-        cos, sin = getattr(self, a), getattr(self, b)
+    def _tables(self, device, zz_len=0):
+        # tables follow the activations' device (the module may have been moved after init); the
+        # zig-zag shard's rows depend on its local length zz_len (context_parallel.zigzag_rope_tables)
+        if zz_len:
+            cache = self.__dict__.setdefault("_zz_tables", {})
+            key = (zz_len, device)
+            if key not in cache:
+                cos, sin = context_parallel.zigzag_rope_tables(*self._rope_args, S=zz_len)
+                cache[key] = (cos.to(device=device, dtype=torch.bfloat16), sin.to(device=device, dtype=torch.bfloat16))
+            return cache[key]
+        cos, sin = self.cos, self.sin
         if cos.device != device or cos.dtype != torch.bfloat16:
             cos, sin = cos.to(device=device, dtype=torch.bfloat16), sin.to(device=device, dtype=torch.bfloat16)
-            setattr(self, a, cos)
-            setattr(self, b, sin)
+            self.cos, self.sin = cos, sin
         return cos, sin
 
     def forward(self, x, attention_mask=None, position_ids=None):
         zz = self.cp_zigzag_residual and context_parallel.zigzag_enabled(x.shape[1], True)
-        cos, sin = self._tables(x.device, zz)
+        cos, sin = self._tables(x.device, x.shape[1] if zz else 0)
         n1, n2, at, mlp = self.input_layernorm, self.post_attention_layernorm, self.attention, self.mlp
         if _norm_mode(n1) != _norm_mode(n2) or _norm_eps(n1) != _norm_eps(n2):
             raise ValueError("DecoderLayer: both norms must be the same flavour")
+        # a token-row shard of the residual stream (tensor_parallel/sequence_parallel.py)?
+        sp = self.tp_sequence_parallel and sequence_parallel.local_len() == x.shape[1]
         return FN.DecoderLayerFunction.apply(
             x, n1.weight, n2.weight, *at.weights(), mlp.gate_proj.weight, mlp.up_proj.weight, mlp.down_proj.weight,
-            cos, sin, _norm_eps(n1), _norm_mode(n1), at.num_local_heads, at.num_local_kv_heads, at.head_dim, zz)
+            cos, sin, _norm_eps(n1), _norm_mode(n1), at.num_local_heads, at.num_local_kv_heads, at.head_dim, zz, sp)
 
 
 class Embedding(nn.Module):

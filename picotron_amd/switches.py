@@ -26,6 +26,8 @@ DEFAULTS = {
     # context_parallel.py: the zig-zag (load-balanced) ring where it tiles, the residual stream kept
     # in that layout across the decoder stack, the full-mesh K|V / dK|dV exchange instead of the ring
     "ring_zigzag": 1, "zigzag_residual": 1, "ring_mesh": 1,
+    # tensor_parallel/sequence_parallel.py: the residual stream sharded by token rows over the tp group
+    "tp_sp": 1,
     # native (libpicotron_hip.so, pt_set_variant)
     "attn_pair": 1, "attn_split": 2, "gemm_group_m": -1, "gemm_mix": 1, "gemm_kh": 2,
 }

@@ -17,6 +17,7 @@ import torch.nn.functional as F
 
 from .. import functional as FN
 from .. import process_group_manager as pgm
+from .sequence_parallel import enable_sequence_parallel
 from .tp_communications import (GatherFromModelParallelRegion, ReduceFromModelParallelRegion,
                                 linear_with_all_reduce, linear_with_async_all_reduce)
 
@@ -52,6 +53,9 @@ def apply_tensor_parallel(model):
             _replace_module(getattr(layer, module_name), linear_proj_name, style)
     _replace_module(model, "embedding", "vocab")
     _replace_module(model, "final_proj", "column", args={"gather_output": True})
+    # MI355X-first addition: the residual stream sharded by token rows between the TP blocks
+    # (sequence_parallel.py: same values, the norms / adds on T / tp rows per rank)
+    enable_sequence_parallel(model)
     return model
 
 

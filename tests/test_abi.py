@@ -47,3 +47,19 @@ def test_argument_errors_map_to_codes():
     assert lib.pt_rmsnorm_fwd(None, None, None, None, None, None, 0, 0, 1e-5, 0, None) == -1
     assert lib.pt_gemm_pick_tile(4096, 2048, None, 0, None, 0) >= 0
     assert lib.pt_gemm_pick_tile(100, 100, None, 0, None, 0) == -1
+
+
+def test_no_kernel_spills_to_scratch():
+    """Every kernel of the library keeps its registers: no VGPR spill and no scratch (private
+    segment) memory in any gfx950 code object (tools/spills.py reads the AMDGPU metadata notes)."""
+    import glob
+    import subprocess
+    import sys
+    objs = glob.glob(os.path.join(ROOT, "picotron_amd", "lib", "obj", "*.o"))
+    if not objs or not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-readelf"):
+        pytest.skip("no built objects / ROCm LLVM tools")
+    from picotron_amd import build
+    build.build(verbose=False)   # the objects match the sources
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "spills.py")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 kernel(s) with VGPR spills or scratch memory" in r.stdout

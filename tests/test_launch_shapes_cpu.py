@@ -39,3 +39,18 @@ def test_splitk_halves_for_long_k_dx():
     assert K._splitk_halves(T, H, V) == V // 2             # lm_head dX
     assert K._splitk_halves(T, H, H) is None               # o_proj dX: K 2048
     assert K._splitk_halves(T, H, 3 * H, min_half=1024) == 3 * H // 2   # q|k|v dX beside its dW
+
+
+def test_reduce_sink_alignment_decided_before_launch():
+    """A split-K sink the reduce pass cannot address in 8-B (bf16) / 16-B (f32) row chunks -- or a
+    misaligned residual -- keeps the unsplit GEMM (decided before the partial GEMM)."""
+    import torch
+    buf = torch.empty(64 * 64 + 8, dtype=torch.bfloat16)
+    ok = buf[:64 * 64].view(64, 64)
+    assert K._reduce_sink_ok(ok)
+    assert not K._reduce_sink_ok(buf[1:1 + 64 * 64].view(64, 64))            # 2-B offset
+    assert K._reduce_sink_ok(ok, residual=ok)
+    assert not K._reduce_sink_ok(ok, residual=buf[2:2 + 64 * 64].view(64, 64))   # 4-B offset residual
+    f = torch.empty(64 * 64 + 4, dtype=torch.float32)
+    assert not K._reduce_sink_ok(f[2:2 + 64 * 64].view(64, 64))              # 8-B offset f32
+    assert not K._reduce_sink_ok(ok.t())                                     # column-major

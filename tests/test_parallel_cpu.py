@@ -371,6 +371,26 @@ def _zz_residual(rank, world):
     cos, sin = CP.zigzag_rope_tables(world * S, 16, 10000.0)
     cf, sf = get_cos_sin(world * S, 16, base=10000.0)
     assert torch.equal(cos, cf[pos]) and torch.equal(sin, sf[pos])
+    # max_position_embeddings > C * S: the reference rotates rank c's chunk with rows [c P, c P + S)
+    # of the max_pos table (P = max_pos / C; update_rope_for_context_parallel, then the first S rows)
+    maxp = 3 * world * S
+    P = maxp // world
+    cos, sin = CP.zigzag_rope_tables(maxp, 16, 10000.0, S=S)
+    cf, sf = get_cos_sin(maxp, 16, base=10000.0)
+    rows = [(g // S) * P + g % S for g in pos]
+    assert torch.equal(cos, cf[rows]) and torch.equal(sin, sf[rows])
+    # and a DecoderLayer on the zig-zag shard takes exactly those rows (keyed by its local length)
+    from picotron_amd.model import DecoderLayer
+    from picotron_amd.train import make_config
+    cfg = make_config(dict(hidden_size=32, intermediate_size=64, num_attention_heads=2, num_key_value_heads=2,
+                           vocab_size=64, rms_norm_eps=1e-5, rope_theta=10000.0), S, num_hidden_layers=1)
+    cfg.max_position_embeddings = maxp
+    layer = DecoderLayer(cfg, 0)
+    layer.cp_zigzag_residual = True
+    zc, zs = layer._tables(torch.device("cpu"), S)
+    assert torch.equal(zc, cf[rows].to(torch.bfloat16)) and torch.equal(zs, sf[rows].to(torch.bfloat16))
+    with pytest.raises(ValueError):
+        CP.zigzag_rope_tables(world * S, 16, 10000.0, S=2 * S)   # longer than the rank's reference slice
 
 
 @pytest.mark.parametrize("world", [2, 4])
@@ -593,3 +613,65 @@ def test_pipeline_engine_matches_unsplit_model(kind, world, dp):
     DataParallelBucket, whose all-reduce only the stage's last backward triggers): the last stage's logging loss is the mean micro-batch loss and every
     stage's gradients equal the unsplit model's on the same micro-batches."""
     _dist.run(_pp_engine, world, kind, dp)
+
+
+# ----------------------------------------------------------------------------- TP sequence parallel
+def _sp_host(rank, world):
+    """tensor_parallel/sequence_parallel.py's host pieces over gloo: the row all-gather /
+    reduce-scatter of TPContext, the entry / exit regions (values and gradients) and the hooks,
+    against the unsharded computation."""
+    from picotron_amd import functional as FN
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.tensor_parallel import sequence_parallel as SPM
+    m = pgm.setup_process_group_manager(tp_size=world, cp_size=1, pp_size=1, dp_size=1)
+    tp = FN.TPContext.current()
+    assert tp.world_size == world and tp.rank == m.tp_rank
+    B, S, H = 2, 4 * world, 3
+    n = B * S // world
+    full = torch.arange(B * S * H, dtype=torch.float32).view(B * S, H)
+    # all-gather of token rows / reduce-scatter of partial sums
+    mine = full[rank * n:(rank + 1) * n]
+    assert torch.equal(tp.all_gather_rows(mine), full)
+    part = full * (rank + 1)
+    red, h = tp.reduce_scatter_rows(part.clone())
+    assert h is None and torch.equal(red, (full * sum(range(1, world + 1)))[rank * n:(rank + 1) * n])
+    # entry / exit regions: values and gradients
+    x = full.view(B, S, H).clone().requires_grad_(True)
+    shard = SPM.ScatterToSequenceRegion.apply(x)
+    assert shard.shape == (B, S // world, H) and torch.equal(shard.reshape(n, H), mine)
+    y = SPM.GatherFromSequenceRegion.apply(shard * 2)
+    assert torch.equal(y, 2 * full.view(B, S, H))
+    g = torch.randn(B, S, H, generator=torch.Generator().manual_seed(3))   # replicated upstream gradient
+    y.backward(g)
+    assert torch.equal(x.grad, 2 * g)   # each rank's rows came back, all-gathered
+    # the hooks: an embedding / final_norm pair around a token-local body; a length that does not
+    # divide by tp stays unsharded
+
+    class Toy(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            torch.manual_seed(0)   # the same (replicated) weights on every rank
+            self.embedding = torch.nn.Linear(H, H)
+            self.final_norm = torch.nn.Linear(H, H)
+
+        def forward(self, t):
+            z = self.embedding(t)
+            self.seen = z.shape
+            return self.final_norm(z * 3)
+    toy = Toy()
+    ref = toy(full.view(B, S, H))
+    assert SPM.sp_supported() and SPM.enable_sequence_parallel(toy)
+    out = toy(full.view(B, S, H))
+    assert toy.seen == (B, S // world, H) and torch.allclose(out, ref)
+    out.sum().backward()
+    ref_toy = Toy()
+    ref_toy(full.view(B, S, H)).sum().backward()
+    for (n, p), q in zip(toy.named_parameters(), ref_toy.parameters()):
+        assert torch.allclose(p.grad, q.grad), n
+    toy(torch.randn(B, S + 1, H))
+    assert toy.seen == (B, S + 1, H) and SPM.local_len() == 0
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sequence_parallel_host_logic(world):
+    _dist.run(_sp_host, world)

@@ -38,7 +38,7 @@ def _shard(full, local, rank):
     return full.narrow(d, rank * n, n)
 
 
-def _setup(tp, cp, seq=256):
+def _setup(tp, cp, seq=256, cfg_over=None):
     import types
     os.environ["FLASH_ATTEN"] = "1"
     torch.cuda.set_device(0)
@@ -48,9 +48,10 @@ def _setup(tp, cp, seq=256):
     from picotron_amd.model import Llama
     from picotron_amd.tensor_parallel.tensor_parallel import apply_tensor_parallel
     m = pgm.setup_process_group_manager(tp_size=tp, cp_size=cp, pp_size=1, dp_size=1)
-    c = dict(CFG, max_position_embeddings=seq)
+    base = dict(CFG, **(cfg_over or {}))
+    c = dict(base, max_position_embeddings=seq)
     cfg = types.SimpleNamespace(**c)
-    full = {k: v.to(torch.bfloat16) for k, v in O.init_params(dict(CFG), seed=7).items()}
+    full = {k: v.to(torch.bfloat16) for k, v in O.init_params(dict(base), seed=7).items()}
     with torch.device("cuda"):
         model = Llama(cfg)
         if tp > 1:
@@ -68,27 +69,39 @@ def _setup(tp, cp, seq=256):
     # the oracle on the full model, fp32 from the same bf16 weights
     pf = {k: v.float().requires_grad_(True) for k, v in full.items()}
     cos, sin = O.get_cos_sin(seq, 64, base=CFG["rope_theta"])
-    lo = O.llama_forward(ids[:, :-1], pf, dict(CFG), cos.float(), sin.float(), norm=O.rmsnorm_flash_semantics)
+    lo = O.llama_forward(ids[:, :-1], pf, dict(base), cos.float(), sin.float(), norm=O.rmsnorm_flash_semantics)
     loss_r = F.cross_entropy(lo.reshape(-1, CFG["vocab_size"]), ids[:, 1:].reshape(-1))
     loss_r.backward()
     return m, model, names, pf, ids, lo, loss_r
 
 
-def _llama(rank, world, tp, cp, seq=256, zigzag=False, residual=1, mesh=1, production_thresholds=False):
+def _llama(rank, world, tp, cp, seq=256, zigzag=False, residual=1, mesh=1, production_thresholds=False, sp=1,
+           cfg_over=None):
     from picotron_amd import switches
     # conftest.py zeroes the RoPE / SwiGLU fusion tile thresholds for the small test shapes;
     # production_thresholds restores the shipped ones (96 / 192 / 0), under which these TP-shard
     # widths take the split (GEMM + separate rope / swiglu kernel) paths
     thr = dict(rope_fuse_min_tiles=96, swiglu_fuse_min_tiles=192, swiglu_bwd_min_tiles=0) \
         if production_thresholds else {}
-    with switches.override(zigzag_residual=residual, ring_mesh=mesh, **thr):
-        _llama_body(rank, world, tp, cp, seq, zigzag, residual)
+    with switches.override(zigzag_residual=residual, ring_mesh=mesh, tp_sp=sp, **thr):
+        _llama_body(rank, world, tp, cp, seq, zigzag, residual, cfg_over)
 
 
-def _llama_body(rank, world, tp, cp, seq, zigzag, residual):
+def _llama_body(rank, world, tp, cp, seq, zigzag, residual, cfg_over=None):
     from picotron_amd import functional as FN
+    from picotron_amd import switches
     from picotron_amd.context_parallel import context_parallel as CP
-    m, model, names, pf, ids, lo, loss_r = _setup(tp, cp, seq)
+    m, model, names, pf, ids, lo, loss_r = _setup(tp, cp, seq, cfg_over)
+    # sequence parallelism (tensor_parallel/sequence_parallel.py): on at tp > 1 without cp, by default
+    sp_on = tp > 1 and cp == 1 and switches.S.tp_sp != 0
+    assert all(layer.tp_sequence_parallel == sp_on for layer in model.decoder_layers)
+    gathers = []
+    orig_ag = FN.TPContext.all_gather_rows
+
+    def counted_ag(self, t):
+        gathers.append(tuple(t.shape))
+        return orig_ag(self, t)
+    FN.TPContext.all_gather_rows = counted_ag
     if residual:   # what the data-parallel wrappers do at cp > 1 (the grads are checked summed over cp)
         CP.enable_zigzag_residual(model)
     s = seq // cp
@@ -105,12 +118,20 @@ def _llama_body(rank, world, tp, cp, seq, zigzag, residual):
     try:
         logits = model(x.cuda())
         n_fwd = len(calls)
+        n_ag_fwd = len(gathers)
         assert logits.shape == (2, s, CFG["vocab_size"])             # final_proj gathers its vocab shards
         loss = FN.cross_entropy(logits.view(-1, CFG["vocab_size"]), t.reshape(-1).cuda())
         loss.backward()
         torch.cuda.synchronize()
     finally:
         CP.zigzag_exchange = orig
+        FN.TPContext.all_gather_rows = orig_ag
+    L, H = CFG["num_hidden_layers"], CFG["hidden_size"]
+    if sp_on:   # per layer 2 gathers each way, plus the exit (forward) / the entry (backward)
+        assert n_ag_fwd == 2 * L + 1 and len(gathers) == 4 * L + 2, gathers
+        assert all(g == (2 * s // tp, H) for g in gathers), gathers   # every gather is of T / tp rows
+    else:
+        assert not gathers
     if zigzag and residual:
         # the residual stream is re-laid once on entry and once on exit (and its gradient twice),
         # not per layer
@@ -142,6 +163,19 @@ def test_tensor_parallel_llama_tp2():
 def test_tensor_parallel_llama_tp2_production_thresholds():
     """tp2 with the shipped fusion thresholds: the split RoPE / SwiGLU paths of narrow TP shards."""
     _dist.run(_llama, 2, 2, 1, 256, False, 1, 1, True, device="cuda")
+
+
+def test_tensor_parallel_llama_tp2_replicated_stream():
+    """tp2 without sequence parallelism (PICOTRON_TP_SP=0): the reference's replicated residual
+    stream and row-parallel all-reduces."""
+    _dist.run(_llama, 2, 2, 1, 256, False, 1, 1, False, 0, device="cuda")
+
+
+@pytest.mark.parametrize("sp", [1, 0])
+def test_tensor_parallel_llama_tp4(sp):
+    """tp4 (4 q / 4 kv heads: one head of each per rank) against the oracle on the full model, with
+    the residual stream sharded by token rows (128 of the 512 per rank) and without."""
+    _dist.run(_llama, 4, 4, 1, 256, False, 1, 1, False, sp, dict(num_key_value_heads=4), device="cuda")
 
 
 def test_context_parallel_llama_cp2():

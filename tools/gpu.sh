@@ -83,7 +83,7 @@ step_tp() {
 
 step_cp() {
   timeout -k 10 300 python -u bench.py --cp-proxy 8 --model llama2-7b --seq 32768 --mbs 1 --steps 3 $CP_ARGS > $O.cpproxy.json 2> $O.cpproxy.err || { echo cpproxy failed; tail $O.cpproxy.err; return 1; }
-  python -c "import json; d=json.load(open('$O.cpproxy.json')); print('cp8 proxy', round(d['value']), round(d['compute_only_tokens_per_s_per_gpu']), {k: round(v,2) for k,v in d['critical_rank_layer_ms_with_comm'].items()}, d['bound'], d['comm']['mesh']['exposed_ms'], round(d['roofline']['fwd_frac'],3), round(d['roofline']['bwd_frac'],3))"
+  python -c "import json; d=json.load(open('$O.cpproxy.json')); print('cp8 proxy', round(d['value']), round(d['modelled_with_mesh_comm_tokens_per_s_per_gpu']), {k: round(v,2) for k,v in d['critical_rank_layer_ms_with_comm'].items()}, d['bound'], d['comm']['mesh']['exposed_ms'], round(d['roofline']['fwd_frac'],3), round(d['roofline']['bwd_frac'],3))"
 }
 
 step_configs() { step_llama && step_tp && step_cp; }
