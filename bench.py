@@ -53,6 +53,12 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+def _md5(path):
+    import hashlib
+    with open(path, "rb") as f:
+        return hashlib.md5(f.read()).hexdigest()
+
+
 def cpu_baseline(cfg, tokens):
     """The oracle's training step -- fwd + bwd of the full model and torch's AdamW over every
     parameter -- on one [1, tokens] micro-batch, on this host's cores (the reference's own path cannot
@@ -164,20 +170,24 @@ def tp_proxy(args, base, layers):
         FN.cross_entropy(full, tgt).backward()
     # the layers see a tp group of `tp` ranks whose all-reduces are no-ops, so they take the TP
     # launch forms (dX and dW as separate launches around the dX all-reduce), not tp = 1's duals
+    gathered = {}
+
     class _TPNoComm(FN.TPContext):
-        """The tp group's collectives as one rank's memory traffic, without the links: the
-        all-gather writes its [T, H] output (tp copies of the shard), the reduce-scatter its shard."""
+        """The tp group's collectives as no-ops, as the compute-only proxy treats the all-reduces:
+        the all-gather hands back a [T, H] buffer of this shape (filled once, then reused -- the
+        values do not matter to the timing), the reduce-scatter this rank's rows of its input."""
 
         def all_reduce(self, t, async_op=False):
             return None
 
         def all_gather_rows(self, t):
-            out = torch.empty((self.world_size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-            out.view(self.world_size, *t.shape).copy_(t.unsqueeze(0).expand(self.world_size, *t.shape))
-            return out
+            key = (tuple(t.shape), t.dtype)
+            if key not in gathered:
+                gathered[key] = torch.cat([t] * self.world_size)
+            return gathered[key]
 
         def reduce_scatter_rows(self, t, async_op=False):
-            return t[:t.shape[0] // self.world_size].contiguous(), None
+            return t[:t.shape[0] // self.world_size], None
     current = FN.TPContext.current
     FN.TPContext.current = staticmethod(lambda: _TPNoComm(None, tp, 0))
     try:
@@ -656,16 +666,25 @@ def main():
     if probe:
         s = probe.summary()
         achieved = s["avg_flop"] / (s["avg_ms"] * 1e-3) / 1e12
-        traffic, tsrc = None, None
+        traffic, tsrc, tnote = None, None, "no PMC traffic file"
         if os.path.exists(TRAFFIC_FILE):   # PMC-measured HBM bytes per GEMM launch (offline passes)
             with open(TRAFFIC_FILE) as f:
                 tj = json.load(f)
-            traffic, tsrc = tj["gemm_avg_bytes_per_launch"], os.path.relpath(TRAFFIC_FILE, ROOT)
+            # only a measurement of THIS line's workload with THIS library build counts
+            wl = {"model": model_name, "layers": layers, "micro_batch": args.mbs, "seq_len": args.seq,
+                  "parallelism": f"dp{dp}" if tp * cp * pp == 1 and not force_dp else None}
+            mine = _md5(K._C.LIB_PATH)
+            if tj.get("workload") != wl:
+                tnote = f"{os.path.relpath(TRAFFIC_FILE, ROOT)} measured another workload ({tj.get('workload')})"
+            elif tj.get("library_md5") != mine:
+                tnote = f"{os.path.relpath(TRAFFIC_FILE, ROOT)} measured another library build"
+            else:
+                traffic, tsrc, tnote = tj["gemm_avg_bytes_per_launch"], os.path.relpath(TRAFFIC_FILE, ROOT), None
         roofline = {"bound": "mfma", "kernel": "gemm (all bf16 MFMA GEMM launches of micro-batch "
                     f"{probe_mb} of every timed step)", "achieved": achieved,
                     "peak": MI355X_BF16_DENSE_PEAK / 1e12, "unit": "TFLOP/s",
                     "frac": achieved / (MI355X_BF16_DENSE_PEAK / 1e12), "traffic": traffic,
-                    "traffic_unit": "bytes per launch", "traffic_source": tsrc,
+                    "traffic_unit": "bytes per launch", "traffic_source": tsrc, "traffic_note": tnote,
                     "algorithmic_bytes_per_launch": s["avg_alg_bytes"],
                     "launches": s["launches"], "avg_launch_ms": s["avg_ms"], "avg_launch_gflop": s["avg_flop"] / 1e9,
                     "gemm_share_of_step": s["total_ms"] * 1e-3 * args.grad_acc / elapsed}

@@ -1239,6 +1239,170 @@ __global__ __launch_bounds__(512) void gemm_kh_kernel(const GemmGroup g) {
   gemm_kh_tile<AK, BKC, EPI>(a, tile_m, tile_n, ks);
 }
 
+// ================================================================ 128x128, k-substep groups (tile 15)
+// For the few-tile problems of the TP shards (TP = 8 at SmolLM-1.7B: q|k|v 4096 x 768, o_proj
+// 4096 x 256, the weight gradients 768 x 2048 / 2048 x 2048 at K 4096): a 128x128 tile puts four
+// times the 256x256 kernel's workgroups on the 256 CUs at the same K, so the launch fills the chip
+// without K-slices and their f32 partial round trip.  8 waves: the two wave groups (waves 0-3, 4-7)
+// take the two k-substeps of every K-tile (k 0-31 / 32-63), and inside a group 2(M) x 2(N) waves own
+// a 64 x 64 output (4 x 4 accumulators): 8 LDS fragment reads per 16 MFMAs, the 4-phase kernel's
+// ratio.  Per K-tile the images A (128 rows x 64 k) and B (128 columns x 64 k), 32 KiB, in a 4-deep
+// ring (128 KiB: one workgroup per CU): K-tile t + 3 is staged during K-tile t into the buffer
+// K-tile t - 1 freed, and the one counted wait per K-tile retires t + 1 with t + 2 and t + 3 in
+// flight.  One phase per K-tile { reads; DMA; waits; barrier; 16 MFMAs; barrier } with group 1 one
+// barrier behind (its reads beside group 0's MFMAs on every SIMD, and vice versa).  After the loop
+// the groups swap halves through LDS as tile 14 does: group 0 finishes rows 0-31 of each wave tile,
+// group 1 rows 32-63 (g0 + g1 for every element), through the common epilogue.
+template <bool AK, bool BKC, int EPI>
+__device__ __forceinline__ void gemm_hq_tile(const GemmArgs& a, const int tile_m, const int tile_n, const int ks = 0) {
+  constexpr int IMG = 128 * BK * 2;           // 16 KiB
+  constexpr int BUF = 2 * IMG;                // A, B
+  constexpr int NS = 4;                       // ring depth (K-tiles resident)
+  constexpr int OPS = 4;                      // DMA instructions per wave and K-tile
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+  lds_u8* smem = (lds_u8*)smem_raw;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: an SGPR
+  const int grp = wave >> 2, wm = (wave >> 1) & 1, wn = wave & 1;
+  const int m0 = tile_m * 128, n0 = tile_n * 128;
+
+  const BImg bi = bimg_make(a, BKC, n0);
+  const int64_t ldb = bi.ld;
+  const int64_t lda = a.lda;
+  uint32_t vA[2], vB[2];
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int i = it * 8 + wave;
+    vA[it] = himg_voff<AK, 128>(i, lane, lda, 0);
+    vB[it] = himg_voff<BKC, 128>(i, lane, ldb, 0);
+  }
+  const int kb = kslice_begin(a, ks);
+  const uint16_t* Ab0 = AK ? a.A + (int64_t)m0 * lda + kb : a.A + m0 + (int64_t)kb * lda;
+  auto a_ptr = [&](int t) { return AK ? Ab0 + t * BK : Ab0 + (int64_t)t * BK * lda; };
+  auto b_ptr = [&](int t) { return bimg_ptr(bi, BKC, kb + t * BK); };
+  // K-tile t's two images into buffer buf: OPS = 4 DMA instructions per wave
+  auto stage = [&](int t, int buf) {
+    lds_u8* dst = smem + buf * BUF;
+    const uint16_t* ap = a_ptr(t);
+    const uint16_t* bp = b_ptr(t);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      glds16_asm(ap, vA[it], dst + (it * 8 + wave) * 1024);
+      glds16_asm(bp, vB[it], dst + IMG + (it * 8 + wave) * 1024);
+    }
+  };
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = kslice_tiles(a);
+  const int pre = nk < NS - 1 ? nk : NS - 1;
+  for (int t = 0; t < pre; ++t) stage(t, t);
+  // K-tile 0 landed; the ones after it stay in flight
+  if (pre >= 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (pre == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  auto bar = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  const int s = __builtin_amdgcn_readfirstlane(grp);  // this group's k-substep
+  const bool late = s == 1;
+  if (late) bar();
+  bf16x8_t af[4], bf[4];
+
+  auto ktile = [&](int t, auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
+    const lds_u8* sA = smem + buf * BUF;
+    const lds_u8* sB = sA + IMG;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = read_frag<128, AK>(sA, wm * 64 + i * 16, s, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[j] = read_frag<128, BKC>(sB, wn * 64 + j * 16, s, lane);
+    // K-tile t + 3 into the buffer K-tile t - 1 used (every wave's reads of it retired before the
+    // barrier that ended its phase)
+    const int tn = t + NS - 1;
+    if (tn < nk) stage(tn, (buf + NS - 1) % NS);
+    // K-tile t + 1 must have landed before the next phase's reads: the younger K-tiles in flight
+    // (issued so far, after t + 1) may stay
+    const int issued = tn < nk ? tn : nk - 1;
+    const int younger = issued - (t + 1);
+    if (t + 1 < nk) {
+      if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+  };
+
+  int t = 0;
+  for (; t + 3 < nk; t += 4) {
+    ktile(t, std::integral_constant<int, 0>{});
+    ktile(t + 1, std::integral_constant<int, 1>{});
+    ktile(t + 2, std::integral_constant<int, 2>{});
+    ktile(t + 3, std::integral_constant<int, 3>{});
+  }
+  if (t < nk) ktile(t, std::integral_constant<int, 0>{});
+  if (t + 1 < nk) ktile(t + 1, std::integral_constant<int, 1>{});
+  if (t + 2 < nk) ktile(t + 2, std::integral_constant<int, 2>{});
+  if (!late) bar();
+  __syncthreads();
+  // swap halves: wave w hands the 2 x 4 fragments its partner (w ^ 4) finishes -- group 0 its rows
+  // 32-63, group 1 its rows 0-31 -- through slot w (16 B per lane, lane-contiguous)
+  typedef __attribute__((address_space(3))) f32x4_t lds_f4;
+  lds_f4* slot = (lds_f4*)smem + wave * 8 * 64 + lane;
+  if (s == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) slot[(i * 4 + j) * 64] = acc[2 + i][j];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) slot[(i * 4 + j) * 64] = acc[i][j];
+  }
+  __syncthreads();
+  const lds_f4* peer = (const lds_f4*)smem + (wave ^ 4) * 8 * 64 + lane;
+  f32x4_t out[2][4];
+  if (s == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) out[i][j] = acc[i][j] + peer[(i * 4 + j) * 64];       // g0 + g1
+  } else {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) out[i][j] = peer[(i * 4 + j) * 64] + acc[2 + i][j];   // g0 + g1
+  }
+  __syncthreads();
+  // the wave's 32 x 64 output: tile rows wm * 64 + s * 32 .., columns wn * 64 ..
+  epilogue<32, 64, EPI>(a, out, smem + wave * (32 * (64 * 2 + 16)), m0, n0, wm * 2 + s, wn, lane, nullptr,
+                        (int64_t)ks * a.kpart_stride);
+}
+
+template <bool AK, bool BKC, int EPI>
+__global__ __launch_bounds__(512) void gemm_hq_kernel(const GemmGroup g) {
+  int tile_m, tile_n, ks;
+  const GemmArgs& a = select_problem(g, tile_m, tile_n, ks);
+  gemm_hq_tile<AK, BKC, EPI>(a, tile_m, tile_n, ks);
+}
+
 // ------------------------------------------------------------------- mixed-tile launch (q|k|v)
 // One problem whose output columns [0, n_split) are covered by 256x256 8-phase tiles and
 // [n_split, N) by 256x128 4-phase tiles, in ONE launch.  For the q|k|v projection with RoPE
@@ -1376,9 +1540,9 @@ void set_smem_once(Kern k, int smem) {
 // profiles/r04/group_m/, two boxes, interleaved): 6 -> 156.6-157.5 k, 5 / 7 -> 156.2-157.8 k,
 // 4 -> 155.4-155.9 k, the previous 8 (256x256) / 4 (256x128) -> 154.9-155.0 k tokens/s
 int group_m_for(int bm, int bn) {
-  // variant > 0: override (A/B measurement); >= 100: 256x256 tiles take g / 100, 256x128 g % 100
+  // variant > 0: override (A/B measurement; the per-tile-shape form measured within noise: retired)
+  (void)bm; (void)bn;
   const int g = pt_variant(PT_VAR_GEMM_GROUP_M);
-  if (g >= 100) return bm == 2 * bn ? g % 100 : g / 100;
   return g > 0 ? g : 6;
 }
 
@@ -1480,19 +1644,38 @@ int launch_kh(GemmGroup g, hipStream_t stream) {
   return PT_OK;
 }
 
+template <bool AK, bool BKC, int EPI>
+int launch_hq(GemmGroup g, hipStream_t stream) {
+  static_assert(EPI != EPI_CE_STATS && EPI != EPI_SWIGLU_FWD && EPI != EPI_SWIGLU_BWD && EPI != EPI_ROPE,
+                "tile 15 epilogues");
+  const int tiles = group_tiles(g, 128, 128);
+  constexpr int smem = 4 * 2 * 128 * BK * 2;  // 128 KiB: the ring; the half swap (64 KiB) and staging fit
+  static_assert(8 * 8 * 64 * 16 <= smem && 8 * 32 * (64 * 2 + 16) <= smem && smem <= 160 * 1024, "LDS budget");
+  static bool attr_set = false;
+  if (!attr_set) {
+    set_smem_once(gemm_hq_kernel<AK, BKC, EPI>, smem);
+    attr_set = true;
+  }
+  gemm_hq_kernel<AK, BKC, EPI><<<tiles, 512, smem, stream>>>(g);
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
+
 // tile ids: 2 = simple 128x128, 3 = simple 64x64 (the TP shards' few-tile problems),
 //           12 = 8-phase 256x256 (two half-image wave groups, one wait per K-tile)
 //           13 = 4-phase 256x128 (three K-tiles resident)
 //           14 = 256x128 with the K-tile's two k-substeps over two wave groups (128 x 64 wave tiles)
+//           15 = 128x128 with the K-tile's two k-substeps over two wave groups (64 x 64 wave tiles,
+//                a 4-deep ring): the TP shards' few-tile problems
 //           (ids 4, 5, 8, 9 -- the simple 256x256 / 256x128 kernels and their two-substep forms --
 //           were never picked once the phased kernels existed, and the 256x256 ones spilled: dropped
 //           from the library in round 4; ids 0, 1, 6, 7, 10, 11 were pipelining experiments, measured slower and retired; so
 //           was round 2's 14: the 8-phase tile with ONE barrier per K-tile and free-running
 //           phases, 3-13 % slower on every layer shape -- the per-phase ping-pong pays for its
 //           barriers)
-constexpr int kNumTiles = 15;
-const int kTileBM[kNumTiles] = {0, 0, 128, 64, 0, 0, 0, 0, 0, 0, 0, 0, 256, 256, 256};
-const int kTileBN[kNumTiles] = {0, 0, 128, 64, 0, 0, 0, 0, 0, 0, 0, 0, 256, 128, 128};
+constexpr int kNumTiles = 16;
+const int kTileBM[kNumTiles] = {0, 0, 128, 64, 0, 0, 0, 0, 0, 0, 0, 0, 256, 256, 256, 128};
+const int kTileBN[kNumTiles] = {0, 0, 128, 64, 0, 0, 0, 0, 0, 0, 0, 0, 256, 128, 128, 128};
 
 template <bool AK, bool BKC, int EPI>
 int launch_layout(const GemmGroup& a, int tile, hipStream_t s) {
@@ -1507,6 +1690,7 @@ int launch_layout(const GemmGroup& a, int tile, hipStream_t s) {
       case 12: return launch_8ph<AK, BKC, EPI>(a, s);
       case 13: return launch_4ph<AK, BKC, EPI>(a, s);
       case 14: return launch_kh<AK, BKC, EPI>(a, s);
+      case 15: return launch_hq<AK, BKC, EPI>(a, s);
       case 2: return launch_t<128, 128, 2, 2, AK, BKC, EPI>(a, s);
       case 3: return launch_t<64, 64, 2, 2, AK, BKC, EPI>(a, s);
       default: return PT_EUNSUPPORTED;
@@ -1674,8 +1858,9 @@ bool mix_enabled() { return pt_variant(PT_VAR_GEMM_MIX) == 1; }
 // 1309 vs 1253 TF/s), equal or -4.5 % at K 2048 (o_proj forward / dX), where the half swap
 // through LDS is a larger share of a short K loop.
 bool kh_enabled(const GemmGroup& g) {
-  const int v = pt_variant(PT_VAR_GEMM_KH);
-  if (v != 2) return v == 1;
+  // 0: never (A/B); otherwise (2, default) the K >= 4096 rule -- "always" (1) measured equal to it at
+  // the step (profiles/r04/notes_r04.md) and was retired
+  if (pt_variant(PT_VAR_GEMM_KH) == 0) return false;
   for (int i = 0; i < g.nprob; ++i)
     if (g.p[i].K / (g.p[i].ksplit > 1 ? g.p[i].ksplit : 1) < 4096) return false;
   return true;

@@ -29,10 +29,13 @@ constexpr int kCUs = 256;
 // waves x 4 blocks per CU; backward 16 waves x 1 block per CU (backward + column sum 17.5-18.4 us vs
 // 19.2 with 8 x 2: one 1024-thread block per CU halves the partial rows), 4 waves for the 8-chunk
 // rows (cols > 2048: 16 waves of those would not fit the LDS row buffers and spill).
+// Below 4096 rows (the TP sequence-parallel shards: T / tp rows per rank, 512 at TP = 8) those
+// shapes leave most CUs idle -- 32 backward blocks of 16 waves for 512 rows, 10.4 us -- so the
+// blocks shrink with the rows until they cover the 256 CUs: 16 / 4 / 2 waves per backward block at
+// >= 4096 / >= 1024 / fewer rows, and 4 / 1 waves per forward block at >= 4096 / fewer rows.
 constexpr int kFwdWpb = 4, kFwdBpc = 4, kBwdBpc = 1;
-template <int NCH>
-constexpr int bwd_wpb_t() { return NCH == 8 ? 4 : 16; }
-constexpr int bwd_wpb(int nch) { return nch == 8 ? 4 : 16; }
+constexpr int fwd_wpb(int64_t rows) { return rows >= 4096 ? kFwdWpb : 1; }
+constexpr int bwd_wpb(int nch, int64_t rows) { return nch == 8 ? (rows >= 1024 ? 4 : 2) : (rows >= 4096 ? 16 : rows >= 1024 ? 4 : 2); }
 
 template <int NCH>
 __device__ __forceinline__ void load_row(const uint16_t* __restrict__ p, int lane, int nchunk, bf16x8 (&v)[NCH]) {
@@ -328,17 +331,21 @@ int grid_for(int64_t rows, int wpb, int bpc) {
 }
 
 template <int NCH>
-void launch_fwd(int grid, hipStream_t s, const uint16_t* X, const uint16_t* R, const uint16_t* W, uint16_t* Y,
+void launch_fwd(hipStream_t s, const uint16_t* X, const uint16_t* R, const uint16_t* W, uint16_t* Y,
                 uint16_t* Z, float* rstd, int64_t rows, int cols, float eps, int mode) {
-  rmsnorm_fwd_kernel<NCH, kFwdWpb><<<grid, kFwdWpb * 64, 0, s>>>(X, R, W, Y, Z, rstd, rows, cols, eps, mode);
+  if (fwd_wpb(rows) == kFwdWpb)
+    rmsnorm_fwd_kernel<NCH, kFwdWpb><<<grid_for(rows, kFwdWpb, kFwdBpc), kFwdWpb * 64, 0, s>>>(X, R, W, Y, Z, rstd,
+                                                                                              rows, cols, eps, mode);
+  else
+    rmsnorm_fwd_kernel<NCH, 1><<<grid_for(rows, 1, kFwdBpc * kFwdWpb), 64, 0, s>>>(X, R, W, Y, Z, rstd, rows, cols,
+                                                                                  eps, mode);
 }
 
 // LDS: wpb * cols * 4 (128 KiB at 16 waves x 2048 columns)
-template <int NCH, bool SPLIT = false>
-void launch_bwd(int grid, hipStream_t s, const uint16_t* DY, const uint16_t* Z, const uint16_t* W,
-                const float* rstd, const uint16_t* DR, uint16_t* DX, float* part, int64_t rows, int cols, int mode,
-                const float* P1 = nullptr) {
-  constexpr int WPB = bwd_wpb_t<NCH>();
+template <int NCH, int WPB, bool SPLIT>
+void launch_bwd_w(int grid, hipStream_t s, const uint16_t* DY, const uint16_t* Z, const uint16_t* W,
+                  const float* rstd, const uint16_t* DR, uint16_t* DX, float* part, int64_t rows, int cols, int mode,
+                  const float* P1) {
   const size_t lds = (size_t)WPB * cols * sizeof(float);
   static bool attr = false;
   if (!attr) {
@@ -349,6 +356,19 @@ void launch_bwd(int grid, hipStream_t s, const uint16_t* DY, const uint16_t* Z, 
   rmsnorm_bwd_kernel<NCH, WPB, SPLIT><<<grid, WPB * 64, lds, s>>>(DY, Z, W, rstd, DR, DX, part, rows, cols, mode, P1);
 }
 
+template <int NCH, bool SPLIT = false>
+void launch_bwd(int grid, hipStream_t s, const uint16_t* DY, const uint16_t* Z, const uint16_t* W,
+                const float* rstd, const uint16_t* DR, uint16_t* DX, float* part, int64_t rows, int cols, int mode,
+                const float* P1 = nullptr) {
+  switch (bwd_wpb(NCH, rows)) {
+    case 16:
+      if constexpr (NCH != 8) launch_bwd_w<NCH, 16, SPLIT>(grid, s, DY, Z, W, rstd, DR, DX, part, rows, cols, mode, P1);
+      break;
+    case 4: launch_bwd_w<NCH, 4, SPLIT>(grid, s, DY, Z, W, rstd, DR, DX, part, rows, cols, mode, P1); break;
+    default: launch_bwd_w<NCH, 2, SPLIT>(grid, s, DY, Z, W, rstd, DR, DX, part, rows, cols, mode, P1); break;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -356,7 +376,7 @@ extern "C" {
 int pt_rmsnorm_bwd_partials(int64_t rows, int cols) {
   const int nch = nch_for(cols);
   if (nch < 0) return PT_EUNSUPPORTED;
-  return grid_for(rows, bwd_wpb(nch), kBwdBpc);  // one partial row per bwd block
+  return grid_for(rows, bwd_wpb(nch, rows), kBwdBpc);  // one partial row per bwd block
 }
 
 int pt_rmsnorm_fwd(const void* x, const void* residual, const void* weight, void* y, void* z_out,
@@ -365,17 +385,16 @@ int pt_rmsnorm_fwd(const void* x, const void* residual, const void* weight, void
   if (residual && !z_out) return PT_EINVAL;
   if (!pt_aligned16(x) || !pt_aligned16(weight) || !pt_aligned16(y)) return PT_EALIGN;
   if (residual && (!pt_aligned16(residual) || !pt_aligned16(z_out))) return PT_EALIGN;
-  const int grid = grid_for(rows, kFwdWpb, kFwdBpc);
   const auto* X = (const uint16_t*)x;
   const auto* R = (const uint16_t*)residual;
   const auto* W = (const uint16_t*)weight;
   auto* Y = (uint16_t*)y;
   auto* Z = (uint16_t*)z_out;
   switch (nch_for((int)cols)) {
-    case 1: launch_fwd<1>(grid, stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
-    case 2: launch_fwd<2>(grid, stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
-    case 4: launch_fwd<4>(grid, stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
-    case 8: launch_fwd<8>(grid, stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
+    case 1: launch_fwd<1>(stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
+    case 2: launch_fwd<2>(stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
+    case 4: launch_fwd<4>(stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
+    case 8: launch_fwd<8>(stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
     default: return PT_EUNSUPPORTED;
   }
   PT_CHECK_LAUNCH();
@@ -393,7 +412,7 @@ int pt_rmsnorm_bwd(const void* dy, const void* z, const void* weight, const floa
   if (nch < 0) return PT_EUNSUPPORTED;
   const int nmode = mode & 3;
   if (nmode > 1 || (mode & PT_DW_ACC_BF16 && mode & PT_DW_ACC_F32)) return PT_EINVAL;
-  const int grid = grid_for(rows, bwd_wpb(nch), kBwdBpc);
+  const int grid = grid_for(rows, bwd_wpb(nch, rows), kBwdBpc);
   const auto* DY = (const uint16_t*)dy;
   const auto* Z = (const uint16_t*)z;
   const auto* W = (const uint16_t*)weight;
@@ -430,7 +449,7 @@ int pt_rmsnorm_bwd_splitk(const float* dy_p0, const float* dy_p1, const void* z,
   if (nch < 0) return PT_EUNSUPPORTED;
   const int nmode = mode & 3;
   if (nmode > 1 || (mode & PT_DW_ACC_BF16 && mode & PT_DW_ACC_F32)) return PT_EINVAL;
-  const int grid = grid_for(rows, bwd_wpb(nch), kBwdBpc);
+  const int grid = grid_for(rows, bwd_wpb(nch, rows), kBwdBpc);
   const auto* P0 = (const uint16_t*)dy_p0;  // reinterpreted as float inside the SPLIT kernel
   const auto* Z = (const uint16_t*)z;
   const auto* W = (const uint16_t*)weight;

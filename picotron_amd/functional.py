@@ -221,7 +221,11 @@ def norm_bwd(dy2, z, weight, rstd, mode, dres=None, need_dw=True, sp=None):
     if sp is not None and sp.world_size > 1:
         dx, partial = K.rmsnorm_bwd(dy2, z, weight, rstd, mode, dres=dres, defer_dw=True)
         entry = (partial, weight, torch.cuda.current_stream(z.device), sp)
-        if task == -1:   # not inside an autograd backward: sum and store now
+        sync = getattr(weight, "_pt_grad_sync", None)
+        waiting = getattr(weight, "_pt_grad_ready", None) is not None and (sync is None or sync())
+        if task == -1 or waiting:
+            # not inside an autograd backward, or an owner (a data-parallel wrapper) all-reduces this
+            # backward and waits for it at its end: sum over tp and store now (one [1, H] all-reduce)
             for part, w, st, *_ in _sp_sum_partials([entry]):
                 buf, sink = _norm_dw_sink(w)
                 K.rmsnorm_colsum_batch([(part, buf, sink)])
@@ -534,8 +538,7 @@ def attn_block_bwd(da, h2, saved, wq, wk, wv, wo, cos, sin, sh, tp, need_dx=True
         # ONE launch with the q|k|v and o_proj dW (192 + 64 tiles): 512 tiles = 2 whole rounds of the
         # 256 CUs instead of a 128-tile dX launch and a 256-tile dW launch
         return dgrad_with_wgrad(dqkv, [wq, wk, wv], [(dqkv, h2, [wq, wk, wv]), (da, o.view(sh.T, sh.wq), [wo])],
-                                keep_parts=keep_parts, split_min=1024,
-                                order=SW.qkv_dual_order if SW.qkv_dual_order >= 0 else None)
+                                keep_parts=keep_parts, split_min=1024)
     dh = handle = None
     if need_dx:
         dh = K.linear_dgrad(dqkv, [wq, wk, wv])
@@ -596,6 +599,11 @@ def _dual_gu_enabled():
     return SW.dual_gu != 0
 
 
+# the gate|up dX + dW dual launch's XCD order: 1 = every XCD its dW tiles first (+0.3 % on the step
+# over the staggered order the other dual launches keep; profiles/r04/ab_gu_order, five rounds)
+GU_DUAL_ORDER = 1
+
+
 def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True, keep_parts=False, sp=False):
     """keep_parts: the gate|up dX may come back as K.SplitKParts (its split-K halves unsummed) for a
     following rmsnorm backward to sum.  sp: the column-parallel dX is reduce-scattered onto this
@@ -619,11 +627,10 @@ def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True, keep_parts=False,
         # tp = 1): the dX as two split-K f32 halves (256 tiles: 3 whole rounds of the 256 CUs), or
         # (gu_splitk = 0) unsplit -- 128 tiles twice as long as a dW tile, beside which the other
         # CUs run four dW tiles each, and a bf16 dX for the norm backward to read.  XCD order 1
-        # (every XCD its dW tiles first; gu_dual_order): +0.3 % on the step over the staggered order
+        # (every XCD its dW tiles first, GU_DUAL_ORDER): +0.3 % on the step over the staggered order
         # the down_proj dual keeps (profiles/r04/ab_gu_order, five interleaved rounds)
         return dgrad_with_wgrad(dgu, [wg, wu], [(dgu, h2, [wg, wu])], keep_parts=keep_parts,
-                                split_min=None if split else 1 << 30,
-                                order=SW.gu_dual_order if SW.gu_dual_order >= 0 else None)
+                                split_min=None if split else 1 << 30, order=GU_DUAL_ORDER)
     if need_dx:
         dh = K.linear_dgrad(dgu, [wg, wu])
         if sp:

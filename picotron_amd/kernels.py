@@ -609,6 +609,28 @@ def fewtile_ksplit(M, N, K):
     return (s, tile) if s > 1 else (1, -1)
 
 
+def hq_form(mnks, extra_tiles=0):
+    """K-slices (1 or 2) for a group of few-tile problems [(M, N, K)] on the 128x128 k-substep tile
+    (15), or 0 when it does not apply.  It applies where the phased 256x256 tiles leave most of the 256
+    CUs idle -- fewer than 96 of them over the group: the TP shards (TP = 8 at SmolLM-1.7B: the q|k|v
+    forward 48 tiles, the o_proj dX 16, the q|k|v + o_proj dW 32, gate|up dW 64) -- and every problem
+    tiles by 128.  A 128x128 tile puts four times the workgroups on the CUs at the same K, so most
+    of these fill the chip without K-slices; 2 slices where the 128x128 tiles still fill at most half
+    a round and K >= 4096 (the q|k|v + o_proj and down_proj dW: 128 tiles).  Measured per launch
+    (tools/tp_gemm_ab.py, profiles/r05/tp_gemm_ab_r05c.log), against the 256x256 K-slice forms:
+    q|k|v forward 22.1 vs 34.4 us, o_proj dX 20.7 vs 25.8, q|k|v + o dW 34.4 vs 42.6, gate|up dW
+    40.6 vs 49.9, down_proj dW 31.6 vs 38.6."""
+    if not _ksplit_enabled() or not SW.fewtile_hq or any(m % 128 or n % 128 for m, n, _ in mnks):
+        return 0
+    t12 = sum((m // 256) * (n // 256) if m % 256 == 0 and n % 256 == 0 else (m * n) // 65536 for m, n, _ in mnks)
+    if t12 >= 96 or any(m < 2048 and k < 2048 for m, _, k in mnks):
+        return 0
+    t15 = sum((m // 128) * (n // 128) for m, n, _ in mnks) + extra_tiles
+    if t15 * 2 <= 256 and all(k >= 4096 and k % 256 == 0 for _, _, k in mnks):
+        return 2
+    return 1
+
+
 def _gemm_ksplit(A, lda, a_kcontig, Bs, ldbs, b_bounds, b_kcontig, b_seg_dim, out, M, N, K, s, tile, epilogue,
                  residual=None, ldr=0):
     """C = A . B as s K-slices into f32 partials (one grouped launch of `tile`), then the reduce
@@ -663,9 +685,10 @@ def _ksplit_launch(probs, n, a_kcontig, b_kcontig, tile, sinks, dev):
         _C.check(rc, "pt_gemm_splitk_reduce")
 
 
-def _wgrad_ksplit_run(jobs, epilogue, s):
+def _wgrad_ksplit_run(jobs, epilogue, s, tile=-1):
     """The wgrad jobs [(dy2d, x2d, outs)] as s-way split-K problems of ONE grouped launch (f32
-    partials in one workspace), then one reduce pass per job into its outs through `epilogue`."""
+    partials in one workspace; tile -1: the auto pick), then one reduce pass per job into its outs
+    through `epilogue`."""
     dev = jobs[0][0].device
     sizes = [dy.shape[1] * x.shape[1] for dy, x, _ in jobs]
     ws = torch.empty(s * sum(sizes), dtype=torch.float32, device=dev)
@@ -689,7 +712,7 @@ def _wgrad_ksplit_run(jobs, epilogue, s):
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
     sinks = [_sink(outs, _bounds([o.shape[0] for o in outs]), epilogue) for _, _, outs in jobs]
-    _ksplit_launch(probs, len(jobs), 0, 0, -1, sinks, dev)
+    _ksplit_launch(probs, len(jobs), 0, 0, tile, sinks, dev)
     if probe is not None:
         ev1.record()
         probe.records.append((ev0, ev1, flops, nbytes, sys._getframe().f_code.co_name))
@@ -700,9 +723,17 @@ def linear_wgrad_grouped(jobs, epilogue=EPI_BF16, tile=-1):
     (pt_gemm_grouped): e.g. dW of q|k|v (192 tiles) + dW of o_proj (64 tiles) fill 256 CUs.  A group
     that would leave most CUs idle (TP shards) runs split-K (wgrad_ksplit)."""
     if tile < 0 and epilogue in (EPI_BF16, EPI_BF16_ACC, EPI_F32_ACC):
-        s = wgrad_ksplit([(dy.shape[1], x.shape[1], dy.shape[0]) for dy, x, _ in jobs])
-        if s > 1 and all(_reduce_sink_ok(o) for _, _, outs in jobs for o in outs):
-            return _wgrad_ksplit_run(jobs, epilogue, s)
+        mnks = [(dy.shape[1], x.shape[1], dy.shape[0]) for dy, x, _ in jobs]
+        hq = hq_form(mnks) if all(o.shape[0] % 128 == 0 for _, _, outs in jobs for o in outs) else 0
+        sinks_ok = all(_reduce_sink_ok(o) for _, _, outs in jobs for o in outs)
+        if hq == 2 and sinks_ok:
+            return _wgrad_ksplit_run(jobs, epilogue, 2, tile=15)
+        if hq == 1:
+            tile = 15
+        else:
+            s = wgrad_ksplit(mnks)
+            if s > 1 and sinks_ok:
+                return _wgrad_ksplit_run(jobs, epilogue, s)
     probs = (_C.GemmProblem * len(jobs))()
     flops = nbytes = 0.0
     for j, (dy2d, x2d, outs) in enumerate(jobs):
@@ -748,6 +779,12 @@ def linear_fwd(x2d, weights, out=None, tile=-1, residual=None):
         h = _splitk_halves(T, N, K)
         if h is not None:
             return _linear_fwd_splitk(x2d, weights, h, y, residual)
+    hq = hq_form([(T, N, K)]) if tile < 0 and all(n % 128 == 0 for n in ns) else 0
+    if hq == 1:
+        tile = 15
+    elif hq == 2 and _reduce_sink_ok(y, residual):
+        return _gemm_ksplit(x2d, x2d.stride(0), 1, weights, [K] * len(weights), _bounds(ns), 1, 0, y, T, N, K, 2, 15,
+                            epi, residual=residual, ldr=ldr)
     if tile < 0 and _reduce_sink_ok(y, residual):
         s, t = fewtile_ksplit(T, N, K)
         if s > 1 and all(n % (256 if t == 12 else 128) == 0 for n in ns):
@@ -1005,6 +1042,12 @@ def linear_dgrad(dy2d, weights, out=None, accumulate=False, tile=-1):
                 all(n % 64 == 0 for n in ns):
             return _linear_dgrad_splitk(dy2d, weights, h, torch.empty(T, Kin, dtype=BF16, device=dy2d.device))
     dx = out if out is not None else torch.empty(T, Kin, dtype=BF16, device=dy2d.device)
+    hq = hq_form([(T, Kin, N)]) if tile < 0 and all(n % 64 == 0 for n in ns) else 0
+    if hq == 1:
+        tile = 15
+    elif hq == 2 and _reduce_sink_ok(dx):
+        return _gemm_ksplit(dy2d, dy2d.stride(0), 1, weights, [Kin] * len(weights), _bounds(ns), 0, 1, dx, T, Kin,
+                            N, 2, 15, EPI_BF16_ACC if accumulate else EPI_BF16)
     if tile < 0 and _reduce_sink_ok(dx):
         s, t = fewtile_ksplit(T, Kin, N)
         if s > 1 and all(n % 64 == 0 for n in ns):
@@ -1165,10 +1208,17 @@ def linear_wgrad(dy2d, x2d, outs, epilogue=EPI_BF16, tile=-1):
     Kin = x2d.shape[1]
     ns = [o.shape[0] for o in outs]
     _req(sum(ns) == N, "wgrad: output rows must cover dY's width")
-    if tile < 0 and epilogue in (EPI_BF16, EPI_BF16_ACC, EPI_F32_ACC) and wgrad_ksplit([(N, Kin, T)]) > 1 and \
-            all(_reduce_sink_ok(o) for o in outs):
-        _wgrad_ksplit_run([(dy2d, x2d, outs)], epilogue, wgrad_ksplit([(N, Kin, T)]))
-        return outs
+    if tile < 0 and epilogue in (EPI_BF16, EPI_BF16_ACC, EPI_F32_ACC):
+        hq = hq_form([(N, Kin, T)]) if all(n % 128 == 0 for n in ns) else 0
+        sinks_ok = all(_reduce_sink_ok(o) for o in outs)
+        if hq == 2 and sinks_ok:
+            _wgrad_ksplit_run([(dy2d, x2d, outs)], epilogue, 2, tile=15)
+            return outs
+        if hq == 1:
+            tile = 15
+        elif wgrad_ksplit([(N, Kin, T)]) > 1 and sinks_ok:
+            _wgrad_ksplit_run([(dy2d, x2d, outs)], epilogue, wgrad_ksplit([(N, Kin, T)]))
+            return outs
     _gemm(dy2d, dy2d.stride(0), 0, [x2d], [x2d.stride(0)], [0, Kin], 0, 0, outs, [o.stride(0) for o in outs],
           _bounds(ns), N, Kin, T, epilogue, tile)
     return outs

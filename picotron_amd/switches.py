@@ -16,12 +16,12 @@ DEFAULTS = {
     # functional.py: the fused epilogues (RoPE in the q|k|v GEMM and attention backward, SwiGLU in the
     # gate|up / down GEMMs), deferred norm-weight column sums, lm_head CE statistics, the q|k|v and
     # gate|up dX + dW dual launches (the latter's dX as split-K halves or unsplit)
-    "fuse": 1, "norm_defer": 1, "ce_stats": 1, "dual_qkv": 1, "dual_gu": 1, "gu_splitk": 1, "gu_dual_order": 1, "qkv_dual_order": -1,
+    "fuse": 1, "norm_defer": 1, "ce_stats": 1, "dual_qkv": 1, "dual_gu": 1, "gu_splitk": 1,
     # kernels.py: weight-gradient / few-tile forward and dX K-slices (the SwiGLU-backward dX's too), split-K dgrad halves (and their minimum K), dX + dW dual
     # launches and their XCD order, the norm backward fed by split-K halves, the attention
     # backward's fused delta, and the tile-count thresholds below which the RoPE / SwiGLU epilogues
     # run as separate kernels (TP shard widths)
-    "ksplit": 1, "fewtile": 1, "swiglu_splitk": 1, "splitk2": 1, "splitk2_min": 8192, "dual": 1, "dual_order": 2, "norm_splitk": 1,
+    "ksplit": 1, "fewtile": 1, "fewtile_hq": 1, "swiglu_splitk": 1, "splitk2": 1, "splitk2_min": 8192, "dual": 1, "dual_order": 2, "norm_splitk": 1,
     "fuse_delta": 1, "rope_fuse_min_tiles": 96, "swiglu_fuse_min_tiles": 192, "swiglu_bwd_min_tiles": 0,
     # context_parallel.py: the zig-zag (load-balanced) ring where it tiles, the residual stream kept
     # in that layout across the decoder stack, the full-mesh K|V / dK|dV exchange instead of the ring

@@ -303,7 +303,12 @@ G12_CFGS = {
                    rms_norm_eps=1e-5, max_position_embeddings=128, rope_theta=10000.0, vocab_size=49152,
                    num_hidden_layers=5),
 }
-G12_RUN = {"tiny": dict(steps=6, lr=1e-2, dtype="f32"), "smollm": dict(steps=4, lr=1e-4, dtype="bf16")}
+# "smollm_f32": the same run at config 1's literal precision (the README's --use_cpu path trains in
+# fp32) -- G12f32_smollm, which records the bf16-vs-fp32 gap as G11f32_* does for G11
+G12_CFGS["smollm_f32"] = G12_CFGS["smollm"]
+G12_RUN = {"tiny": dict(steps=6, lr=1e-2, dtype="f32"), "smollm": dict(steps=4, lr=1e-4, dtype="bf16"),
+           "smollm_f32": dict(steps=4, lr=1e-4, dtype="f32")}
+G12_NAMES = {"tiny": "G12_tiny", "smollm": "G12_smollm", "smollm_f32": "G12f32_smollm"}
 G12_GA, G12_MBS = 2, 4
 
 
@@ -391,10 +396,10 @@ def _g12_full_shape(name, p, c):
             "up_proj": (I, H), "down_proj": (H, I), "embedding": (V, H), "final_proj": (V, H)}.get(tail, tuple(p.shape))
 
 
-def g12_all(ref):
+def g12_all(ref, sizes=("tiny", "smollm", "smollm_f32")):
     import functools
-    for size in ("tiny", "smollm"):
-        _run_dist(functools.partial(g12_grid, size=size), 8, ref, f"G12_{size}")
+    for size in sizes:
+        _run_dist(functools.partial(g12_grid, size=size), 8, ref, G12_NAMES[size])
 
 
 G11_STEPS, G11_GA, G11_MBS, G11_LR = 50, 2, 2, 1e-3
@@ -506,7 +511,7 @@ def g11_all(ref, dtypes=("bf16", "f32")):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
-    ap.add_argument("--only", choices=["G11", "G11bf16", "G11s512", "G10m_pp", "G12"],
+    ap.add_argument("--only", choices=["G11", "G11bf16", "G11s512", "G10m_pp", "G12", "G12f32"],
                     help="regenerate only these fixtures")
     args = ap.parse_args()
     if args.only == "G11s512":
@@ -520,6 +525,10 @@ def main():
     if args.only == "G12":
         g12_all(args.ref)
         print("wrote G12 fixtures")
+        return
+    if args.only == "G12f32":
+        g12_all(args.ref, ("smollm_f32",))
+        print("wrote G12f32_smollm")
         return
     if args.only == "G10m_pp":
         g10m_pp_all(args.ref)

@@ -383,6 +383,12 @@ def _grid_curve(rank, world, size, out_q):
         out_q.put((size, losses, ref))
     for k, (a, b) in enumerate(zip(losses, ref)):
         assert abs(a - b) <= 0.01 * abs(b), (size, rank, k, losses, ref)   # north_star: within 1 %
+    if size == "smollm" and m.pp_is_last_stage:
+        # config 1's literal fp32 (G12f32_smollm): the bf16 HIP curve sits below it by the reference's
+        # own bf16-vs-fp32 gap (0.9 / 2.2 / 3.6 %, test_oracle_golden.py) -- within 1 % of that gap
+        f32 = torch.load(os.path.join(GOLD, "G12f32_smollm.pt"), weights_only=True)[f"rank{rank}.losses"].tolist()
+        for k, (a, b, c) in enumerate(zip(losses, ref, f32)):
+            assert abs((c - a) / c - (c - b) / c) <= 0.01, ("G12f32 gap", k, losses, ref, f32)
 
 
 @pytest.mark.parametrize("size", ["tiny", "smollm"])

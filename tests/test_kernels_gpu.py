@@ -245,7 +245,7 @@ def test_gemm_fwd_nt(M, N, K):
     assert rel_err(y, _ref_mm(x, w.t())) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [2, 3, 12, 13, 14])
+@pytest.mark.parametrize("tile", [2, 3, 12, 13, 14, 15])
 def test_gemm_every_tile_every_layout(tile):
     from picotron_amd import kernels as K_
     M, N, K = 512, 512, 256
@@ -276,12 +276,13 @@ def test_gemm_retired_tiles_are_refused():
             K_.linear_fwd(a, [b], tile=t)
 
 
-@pytest.mark.parametrize("tile", [12, 13, 14])
+@pytest.mark.parametrize("tile", [12, 13, 14, 15])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 192), (768, 512, 512), (256, 512, 2048),
                                    (512, 256, 320), (256, 256, 128)])
 def test_gemm_8phase_shapes(M, N, K, tile):
-    """the phased kernels (tile 12: 256x256, 13: 256x128, 14: 256x128 K-halves): 1-5 K-tiles (every
-    remainder of the 2- and 3-buffer loops), every layout"""
+    """the phased kernels (tile 12: 256x256, 13: 256x128, 14: 256x128 K-halves, 15: 128x128 K-halves,
+    4-deep ring): 1-5 and 8 / 32 K-tiles (every remainder of the 2-, 3- and 4-buffer loops), every
+    layout"""
     from picotron_amd import kernels as K_
     a = torch.randn(M, K).to(BF)
     b = (torch.randn(N, K) / 16).to(BF)
@@ -327,10 +328,11 @@ def test_gemm_khalves_tile_at_layer_shapes(T, N, K):
     w2 = (torch.randn(N, K, generator=g) / N ** 0.5).to(BF)
     dx = K_.linear_dgrad(dy.to(DEV), [w2.to(DEV)], tile=14)
     assert rel_err(dx, _ref_mm(dy, w2)) < 1e-2
-    with switches.override(gemm_kh=1):
-        ya = K_.linear_fwd(xd, [wd])
+    ya = K_.linear_fwd(xd, [wd])      # the auto pick: tile 14 at K >= 4096 (variant gemm_kh)
+    with switches.override(gemm_kh=0):
+        yb = K_.linear_fwd(xd, [wd])
     torch.cuda.synchronize()
-    assert rel_err(ya, ref) < 1e-2
+    assert rel_err(ya, ref) < 1e-2 and rel_err(yb, ref) < 1e-2
 
 
 def test_swiglu_dx_ksplit_beside_dw_slices():

@@ -54,3 +54,18 @@ def test_reduce_sink_alignment_decided_before_launch():
     f = torch.empty(64 * 64 + 4, dtype=torch.float32)
     assert not K._reduce_sink_ok(f[2:2 + 64 * 64].view(64, 64))              # 8-B offset f32
     assert not K._reduce_sink_ok(ok.t())                                     # column-major
+
+
+def test_hq_form_for_tp_shards():
+    """The 128x128 k-substep tile (15) for the few-tile TP-shard GEMMs, 2 K-slices where its tiles
+    fill at most half a round at K >= 4096; not for the TP = 1 shapes or the shards that already tile."""
+    assert K.hq_form([(T, 3 * H // 8, H)]) == 1                  # q|k|v forward: 192 tiles of 128x128
+    assert K.hq_form([(T, H // 8, H)]) == 1                      # o_proj dX: 64 tiles
+    assert K.hq_form([(3 * H // 8, H, T), (H, H // 8, T)]) == 2  # q|k|v + o_proj dW: 128 tiles x 2
+    assert K.hq_form([(2 * I // 8, H, T)]) == 1                  # gate|up dW: 256 tiles
+    assert K.hq_form([(T, H, H // 8)]) == 0                      # o_proj forward: 128 256x256 tiles
+    assert K.hq_form([(T, 3 * H, H)]) == 0                       # TP = 1
+    assert K.hq_form([(1024, 256, 1024)]) == 0                   # small shapes keep the old forms
+    assert K.hq_form([(T, 192, H)]) == 0                         # not on 128-column tiles
+    with switches.override(fewtile_hq=0):
+        assert K.hq_form([(T, 3 * H // 8, H)]) == 0

@@ -126,7 +126,7 @@ def _llama_body(rank, world, tp, cp, seq, zigzag, residual, cfg_over=None):
     finally:
         CP.zigzag_exchange = orig
         FN.TPContext.all_gather_rows = orig_ag
-    L, H = CFG["num_hidden_layers"], CFG["hidden_size"]
+    L, H = CFG["num_hidden_layers"], dict(CFG, **(cfg_over or {}))["hidden_size"]
     if sp_on:   # per layer 2 gathers each way, plus the exit (forward) / the entry (backward)
         assert n_ag_fwd == 2 * L + 1 and len(gathers) == 4 * L + 2, gathers
         assert all(g == (2 * s // tp, H) for g in gathers), gathers   # every gather is of T / tp rows
@@ -176,6 +176,20 @@ def test_tensor_parallel_llama_tp4(sp):
     """tp4 (4 q / 4 kv heads: one head of each per rank) against the oracle on the full model, with
     the residual stream sharded by token rows (128 of the 512 per rank) and without."""
     _dist.run(_llama, 4, 4, 1, 256, False, 1, 1, False, sp, dict(num_key_value_heads=4), device="cuda")
+
+
+def test_tensor_parallel_llama_tp8():
+    """config 3's TP degree: 8 ranks (gloo on cuda:0), one q head and one kv head each, the residual
+    stream sharded 64 token rows per rank, against the oracle on the full model."""
+    over = dict(hidden_size=512, intermediate_size=1024, num_attention_heads=8, num_key_value_heads=8)
+    _dist.run(_llama, 8, 8, 1, 256, False, 1, 1, False, 1, over, device="cuda")
+
+
+def test_context_parallel_llama_cp8():
+    """config 5's CP degree: 8 ranks (gloo on cuda:0), seq 2048 = 256 tokens per rank -- the zig-zag
+    schedule on the full mesh with the resident zig-zag residual -- against the oracle on the whole
+    sequence."""
+    _dist.run(_llama, 8, 1, 8, 2048, True, 1, 1, device="cuda")
 
 
 def test_context_parallel_llama_cp2():

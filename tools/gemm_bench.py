@@ -35,7 +35,7 @@ def tp_shapes(tp):
             ("tp.wgrad.down", H, i, T, 0, 0)]
 
 
-TILES = {0: (256, 256), 1: (256, 128), 2: (128, 128), 3: (64, 64), 4: (256, 256), 5: (256, 128), 6: (256, 256), 7: (256, 128), 8: (256, 256), 9: (128, 128), 10: (256, 256), 11: (256, 256), 12: (256, 256), 13: (256, 128), 14: (256, 128)}
+TILES = {0: (256, 256), 1: (256, 128), 2: (128, 128), 3: (64, 64), 4: (256, 256), 5: (256, 128), 6: (256, 256), 7: (256, 128), 8: (256, 256), 9: (128, 128), 10: (256, 256), 11: (256, 256), 12: (256, 256), 13: (256, 128), 14: (256, 128), 15: (128, 128)}
 
 
 def run(name, M, N, Kd, ak, bk, tile, reps=20):

@@ -6,7 +6,11 @@ KiB.  Writes profiles/<name>.json, which bench.py reads for its roofline `traffi
 GEMM launch, averaged over the GEMM launches of the sampled micro-batch like `achieved`).
 
     python tools/traffic_summary.py gpurun_out/k_pmc1/f_counter_collection.csv \
-        gpurun_out/k_pmc2/w_counter_collection.csv profiles/r01_gemm_traffic.json
+        gpurun_out/k_pmc2/w_counter_collection.csv profiles/r01_gemm_traffic.json [WORKLOAD_JSON LIB]
+
+WORKLOAD_JSON (bench.py's config keys: model, layers, micro_batch, seq_len, parallelism) and LIB (the
+library the passes loaded: its md5 is recorded) key the file: bench.py reports the measured traffic
+only on a line of the same workload run with the same library build, and `traffic: null` otherwise.
 """
 import collections
 import csv
@@ -30,7 +34,13 @@ def short(name):
 GRAD_ACC = 2
 
 
-def main(fetch, write, out):
+def lib_md5(path):
+    import hashlib
+    with open(path, "rb") as f:
+        return hashlib.md5(f.read()).hexdigest()
+
+
+def main(fetch, write, out, workload=None, lib=None):
     f, w = per_dispatch(fetch), per_dispatch(write)
     kinds = collections.defaultdict(list)
     gemm = []
@@ -45,6 +55,8 @@ def main(fetch, write, out):
             gemm.append(b)
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py --steps 1 --warmup 0 "
                      f"--grad-acc {GRAD_ACC}; bytes = 2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction)",
+           "workload": json.loads(workload) if workload else None,
+           "library_md5": lib_md5(lib) if lib else None,
            "gemm_launches": len(gemm), "gemm_avg_bytes_per_launch": sum(gemm) / max(len(gemm), 1),
            "kernels": {f"{k} [{g} WG]": {"launches": len(v), "avg_bytes": sum(v) / len(v)}
                        for (k, g), v in sorted(kinds.items(), key=lambda kv: -sum(kv[1]))[:30]}}
@@ -53,4 +65,4 @@ def main(fetch, write, out):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:6])
