@@ -295,6 +295,25 @@ int pt_attn_bwd_fused_delta(const void* q, const int64_t* q_str, const void* k, 
                             const int64_t* dv_str, int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk,
                             int64_t D, float scale, int causal, const void* rope_cos, const void* rope_sin,
                             int64_t rope_stride, int64_t lse_ld, hipStream_t stream);
+/* Few-head attention (a TP shard's heads: the regular launch -- one workgroup per causal query-block
+ * pair -- would put fewer than 128 workgroups on the 256 CUs): the same flash_attn_func forward /
+ * backward as work items of "attn_kv_chunk" K/V (Q) tiles, f32 partials in a caller-owned workspace,
+ * and a merge / reduce pass.  pt_attn_split_plan: 1 and the workspace bytes when the split forms
+ * apply to the shape (d64), else 0.  pt_attn_fwd_split = pt_attn_fwd with merge = 0 and a dense lse;
+ * pt_attn_bwd_split = pt_attn_bwd_fused_delta with a dense lse.  Results equal the regular kernels' up
+ * to the f32 summation order. */
+int pt_attn_split_plan(int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int64_t D, int causal,
+                       int backward, int64_t* ws_bytes);
+int pt_attn_fwd_split(const void* q, const int64_t* q_str, const void* k, const int64_t* k_str, const void* v,
+                      const int64_t* v_str, void* o, const int64_t* o_str, float* lse, int64_t B, int64_t H,
+                      int64_t HKV, int64_t Sq, int64_t Sk, int64_t D, float scale, int causal, void* ws,
+                      int64_t ws_bytes, hipStream_t stream);
+int pt_attn_bwd_split(const void* q, const int64_t* q_str, const void* k, const int64_t* k_str, const void* v,
+                      const int64_t* v_str, const void* o, const int64_t* o_str, const void* dout, const int64_t* do_str,
+                      const float* lse, float* delta_out, void* dq, const int64_t* dq_str, void* dk,
+                      const int64_t* dk_str, void* dv, const int64_t* dv_str, int64_t B, int64_t H, int64_t HKV,
+                      int64_t Sq, int64_t Sk, int64_t D, float scale, int causal, const void* rope_cos,
+                      const void* rope_sin, int64_t rope_stride, void* ws, int64_t ws_bytes, hipStream_t stream);
 
 /* ---- measurement variants ------------------------------------------------------------------
  * Not a reference interface: selects between kernel forms with identical results, for A/B runs and
@@ -305,6 +324,8 @@ int pt_attn_bwd_fused_delta(const void* q, const int64_t* q_str, const void* k, 
  *   "gemm_group_m" -1   GEMM tile-rows per group of the tile order (-1 = 6; n > 0: n rows)
  *   "gemm_mix"      1   q|k|v + RoPE GEMM as one mixed 256x256 / 256x128 launch
  *   "gemm_kh"       2   auto-picked 256x128 tiles as tile 14 (K-halves) when K >= 4096; 0 never
+ *   "attn_kv_chunk" 4   few-head attention (pt_attn_split_plan): K / Q tiles per work item (even;
+ *                       0 = never split)
  * Returns PT_EINVAL for an unknown name.  pt_get_variant returns the value (or PT_EINVAL). */
 int pt_set_variant(const char* name, int value);
 int pt_get_variant(const char* name);

@@ -64,6 +64,12 @@ SIGNATURES = {
     "pt_attn_bwd_fused_delta": (_i32, [_vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _vp, _vp,
                                        _i64p, _vp, _i64p, _vp, _i64p, _i64, _i64, _i64, _i64, _i64, _i64, _f32,
                                        _i32, _vp, _vp, _i64, _i64, _vp]),
+    "pt_attn_split_plan": (_i32, [_i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _vp]),
+    "pt_attn_fwd_split": (_i32, [_vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _i64, _i64, _i64, _i64, _i64,
+                                 _i64, _f32, _i32, _vp, _i64, _vp]),
+    "pt_attn_bwd_split": (_i32, [_vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _i64p, _vp, _vp, _vp, _i64p,
+                                 _vp, _i64p, _vp, _i64p, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _i32, _vp, _vp,
+                                 _i64, _vp, _i64, _vp]),
     "pt_lse_merge": (_i32, [_vp, _vp, _i32, _vp, _vp, _i32, _vp, _vp, _i64, _i64, _vp]),
     "pt_gemm_ce_stats": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp]),
     "pt_cross_entropy_fwd_stats": (_i32, [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i64, _i64, _vp, _vp]),

@@ -111,25 +111,29 @@ __global__ __launch_bounds__(256) void adamw_multi_bf16_kernel(const AdamTensor*
     const int64_t c0 = chunk_start[t], c1 = chunk_start[t + 1];
     const int64_t from = (lo > c0 ? lo : c0) - c0, to = (hi < c1 ? hi : c1) - c0;   // chunk range in t
     const int64_t full = T.n >> 3;
-    // two full chunks per thread per iteration: all 8 loads in flight before the first use
+    const int64_t end = to < full ? to : full;   // this run's full chunks in tensor t
+    // software-pipelined: the loads of a thread's next two chunks are issued before the current
+    // chunk's stores, so every wait for a load sits behind loads only -- vmcnt counts stores too,
+    // and loads issued after the previous chunk's stores waited out their write latency (5.0 TB/s)
     int64_t c = from + threadIdx.x;
-    for (; c + blockDim.x < to && c + blockDim.x < full; c += 2 * blockDim.x) {
-      const int64_t c2 = c + blockDim.x;
-      const bf16x8 p0 = ld8(T.p + c * 8), g0 = ld8(T.g + c * 8), m0 = ld8(T.m + c * 8), v0 = ld8(T.v + c * 8);
-      const bf16x8 p1 = ld8(T.p + c2 * 8), g1 = ld8(T.g + c2 * 8), m1 = ld8(T.m + c2 * 8), v1 = ld8(T.v + c2 * 8);
+    const int64_t bd = blockDim.x;
+    bf16x8 cur[4], nx1[4], nx2[4];
+    auto load4 = [&](int64_t cc, bf16x8 (&r)[4]) {
+      r[0] = ld8(T.p + cc * 8); r[1] = ld8(T.g + cc * 8); r[2] = ld8(T.m + cc * 8); r[3] = ld8(T.v + cc * 8);
+    };
+    if (c < end) load4(c, cur);
+    if (c + bd < end) load4(c + bd, nx1);
+    for (; c < end; c += bd) {
+      if (c + 2 * bd < end) load4(c + 2 * bd, nx2);
       float p[8], g[8], m[8], v[8];
-      unpack8(p0, p); unpack8(g0, g); unpack8(m0, m); unpack8(v0, v);
+      unpack8(cur[0], p); unpack8(cur[1], g); unpack8(cur[2], m); unpack8(cur[3], v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) adam_elem(p[j], g[j], m[j], v[j], s, true);
       st8(T.p + c * 8, pack8(p));
       st8(T.m + c * 8, pack8(m));
       st8(T.v + c * 8, pack8(v));
-      unpack8(p1, p); unpack8(g1, g); unpack8(m1, m); unpack8(v1, v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) adam_elem(p[j], g[j], m[j], v[j], s, true);
-      st8(T.p + c2 * 8, pack8(p));
-      st8(T.m + c2 * 8, pack8(m));
-      st8(T.v + c2 * 8, pack8(v));
+      for (int q = 0; q < 4; ++q) { cur[q] = nx1[q]; nx1[q] = nx2[q]; }
     }
     for (; c < to; c += blockDim.x) {
       if (c < full) {

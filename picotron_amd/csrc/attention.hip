@@ -30,6 +30,7 @@
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));   // v_pk_fma_f32 / v_pk_add_f32 operands
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 
 // the d64 forward: a batch of LDS operand reads stays ahead of the MFMAs that consume it (no
@@ -73,6 +74,13 @@ struct AttnArgs {
   // bwd: when set, the dQ kernel (launched first) computes D = rowsum(dO * O) of its own rows from
   // O (a.o, bf16) and writes it here for the dK/dV kernel -- no separate delta pass
   float* delta_w;
+  // few-head split forms (pt_attn_split_plan): work items of split_ck K (Q) tiles each, split_per_bh
+  // items per (batch, head) row; f32 partials [item][rows of the block][D] (split_o: O / dQ / dK,
+  // split_dv: dV) and the forward's per-row LSE [item][rows]
+  int split_ck, split_per_bh;
+  float* split_o;
+  float* split_dv;
+  float* split_lse;
 };
 
 template <int D>
@@ -293,7 +301,8 @@ constexpr int dq_stages() { return D == 64 ? 4 : 2; }
 // NWK waves per workgroup (32 query rows each): 4, or 8 at d 128 (the K/V tiles staged once for
 // twice the queries; measured 7-8 % faster at S_local 4096, equal at d 64)
 template <int D, int NWK>
-__device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_or_hk, int b) {
+__device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_or_hk, int b, int kt_lo = 0,
+                                               int kt_hi = -1, int item = -1) {
   constexpr int DT = D / 32, KS = D / 16;
   constexpr int TILE_B = KT * D * 2;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
@@ -314,7 +323,8 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
   const uint16_t* kbase = a.k + b * a.k_sb + hk * a.k_sh;
   const uint16_t* vbase = a.v + b * a.v_sb + hk * a.v_sh;
   const int kv_end = a.causal ? (qb + 1) * NWK * 32 : a.Sk;
-  const int nkt = kv_end / KT;
+  // this call's K/V tiles: all of the block's, or a split work item's [kt_lo, kt_hi)
+  const int kt0 = kt_lo, nkt = (kt_hi < 0 ? kv_end / KT : kt_hi) - kt_lo;
   const float c2 = a.scale * kLog2e;
 
   f32x16_t o[DT];
@@ -325,8 +335,8 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
   constexpr int NS = fwd_stages<D, NWK>(), OPS = 2 * (KT * D * 2 / 1024) / NWK;
   auto stage = [&](int kt, int buf) {
     lds_u8* sk = smem + buf * 2 * TILE_B;
-    stage_rows<D, NWK>(kbase + (int64_t)kt * KT * a.k_ss, a.k_ss, sk, wave, lane);
-    stage_rows<D, NWK>(vbase + (int64_t)kt * KT * a.v_ss, a.v_ss, sk + TILE_B, wave, lane);
+    stage_rows<D, NWK>(kbase + (int64_t)(kt0 + kt) * KT * a.k_ss, a.k_ss, sk, wave, lane);
+    stage_rows<D, NWK>(vbase + (int64_t)(kt0 + kt) * KT * a.v_ss, a.v_ss, sk + TILE_B, wave, lane);
   };
   const int pre = nkt < NS - 1 ? nkt : NS - 1;
   for (int t = 0; t < pre; ++t) stage(t, t);
@@ -380,15 +390,24 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
 #pragma unroll
           for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
       }
-      const float nm = -m;
+      // P = exp2(S c2 - m), summed into l: the exponent arguments as packed pairs (v_pk_fma_f32) and
+      // the row sum in four packed partial sums (v_pk_add_f32, a dependency chain of 8 instead of
+      // 32 serial adds), combined once at the end of the tile
+      const f32x2_t c22 = {c2, c2}, nm2 = {-m, -m};
+      f32x2_t ls[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(s[kh][r], c2, nm));
-          s[kh][r] = p;
-          l += p;
+        for (int r = 0; r < 16; r += 2) {
+          f32x2_t x = {s[kh][r], s[kh][r + 1]};
+          x = __builtin_elementwise_fma(x, c22, nm2);
+          const f32x2_t p = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+          s[kh][r] = p.x;
+          s[kh][r + 1] = p.y;
+          ls[(kh * 8 + r / 2) & 3] += p;
         }
+      const f32x2_t lt = (ls[0] + ls[1]) + (ls[2] + ls[3]);
+      l += lt.x + lt.y;
 #pragma unroll
       for (int half = 0; half < 2; ++half) {  // V operands of two k-steps per batch
         bf16x8_t va[2][DT];
@@ -413,7 +432,7 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
       stage(kt + NS - 1, sbuf);
       if (++sbuf == NS) sbuf = 0;
     }
-    tile(smem + buf * 2 * TILE_B, kt * KT);
+    tile(smem + buf * 2 * TILE_B, (kt0 + kt) * KT);
     if (++buf == NS) buf = 0;
     const int issued = kt + NS - 1 < nkt ? kt + NS - 1 : nkt - 1;   // the last tile issued so far
     ring_wait<OPS, NS>(issued - (kt + 1));
@@ -421,6 +440,23 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
   }
 
   l = xor32_sum(l);
+  if (item >= 0) {
+    // a split work item: its normalised partial O (f32) and LSE, merged by attn_split_merge_kernel
+    // (every query row sees at least one key of every item: split_ck is even)
+    const float inv_l = l > 0.f ? 1.0f / l : 0.f;
+    const int row = wave * 32 + (lane & 31);
+    float* orow = a.split_o + ((int64_t)item * (NWK * 32) + row) * D;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = 32 * dt + 8 * g4 + 4 * (lane >> 5);
+        *(float4*)(orow + d) = make_float4(o[dt][4 * g4] * inv_l, o[dt][4 * g4 + 1] * inv_l,
+                                           o[dt][4 * g4 + 2] * inv_l, o[dt][4 * g4 + 3] * inv_l);
+      }
+    if (lane < 32) a.split_lse[(int64_t)item * (NWK * 32) + row] = l > 0.f ? m * kLn2 + __logf(l) : -INFINITY;
+    return;
+  }
   const float inv_l = 1.0f / l;
   const float lse = m * kLn2 + __logf(l);
   float* lse_p = a.lse + ((int64_t)b * a.H + h) * a.lse_ld + myq;
@@ -463,6 +499,94 @@ __global__ __launch_bounds__(NWK * 64) void attn_fwd_kernel(AttnArgs a) {
   }
 }
 
+// ================================================================= few-head split work items
+// With few (batch, head) rows -- a TP = 8 shard of SmolLM-1.7B has 4 heads: 16 rows x 8 query blocks,
+// paired into 64 workgroups on the 256 CUs -- the forward and dQ kernels run work items of split_ck
+// K/V tiles of one query block (the dK/dV kernel: split_ck (head, Q tile) steps of one key block),
+// each writing an f32 partial that a merge / reduce pass combines.  Items per (batch, head): the
+// blocks heaviest first (query blocks descending, key blocks ascending), each cut into chunks.
+__device__ __forceinline__ int split_nq_tiles(const AttnArgs& a, int qb) {   // K tiles of query block qb
+  return a.causal ? (qb + 1) * (NW * 32 / KT) : a.Sk / KT;
+}
+__device__ __forceinline__ int split_nk_steps(const AttnArgs& a, int kb) {   // (head, Q tile) steps of key block kb
+  const int qt_begin = a.causal ? (kb * NW * 32) / KT : 0;
+  return (a.Sq / KT - qt_begin) * (a.H / a.HKV);
+}
+// work item i -> (row bh, block, chunk c); q_side: the forward / dQ enumeration, else dK/dV's
+__device__ __forceinline__ void split_item(const AttnArgs& a, int i, bool q_side, int& bh, int& blk, int& c) {
+  bh = i / a.split_per_bh;
+  int r = i - bh * a.split_per_bh;
+  const int nb = q_side ? a.Sq / (NW * 32) : a.Sk / (NW * 32);
+  for (int j = 0; j < nb; ++j) {
+    blk = q_side ? nb - 1 - j : j;
+    const int n = ((q_side ? split_nq_tiles(a, blk) : split_nk_steps(a, blk)) + a.split_ck - 1) / a.split_ck;
+    if (r < n) { c = r; return; }
+    r -= n;
+  }
+  c = 0;
+}
+// first item of (bh, blk) and its chunk count
+__device__ __forceinline__ int split_base(const AttnArgs& a, int bh, int blk, bool q_side, int& nch) {
+  int s = bh * a.split_per_bh;
+  const int nb = q_side ? a.Sq / (NW * 32) : a.Sk / (NW * 32);
+  for (int j = 0; j < nb; ++j) {
+    const int bb = q_side ? nb - 1 - j : j;
+    const int n = ((q_side ? split_nq_tiles(a, bb) : split_nk_steps(a, bb)) + a.split_ck - 1) / a.split_ck;
+    if (bb == blk) { nch = n; return s; }
+    s += n;
+  }
+  nch = 0;
+  return s;
+}
+// XCD-aware item order (attn_coords' remap on a 1-D grid): an XCD takes a contiguous item range,
+// so the items of one (batch, head) share that XCD's L2
+__device__ __forceinline__ int split_item_id() {
+  const int nwg = gridDim.x, id = blockIdx.x;
+  const int xcd = id & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
+}
+
+template <int D>
+__global__ __launch_bounds__(NW * 64) void attn_fwd_split_kernel(AttnArgs a) {
+  const int i = split_item_id();
+  int bh, qb, c;
+  split_item(a, i, true, bh, qb, c);
+  const int nqb = a.Sq / (NW * 32);
+  const int lo = c * a.split_ck, hi = min(lo + a.split_ck, split_nq_tiles(a, qb));
+  attn_fwd_block<D, NW>(a, a.causal ? nqb - 1 - qb : qb, bh % a.H, bh / a.H, lo, hi, i);
+}
+
+// O = sum_c exp(lse_c - lse) O_c, lse = log sum_c exp(lse_c): one thread per (query row, 8 columns),
+// rows in (batch, head, query) order (coalesced partial reads), bf16 O into its strided view
+__global__ __launch_bounds__(256) void attn_split_merge_kernel(AttnArgs a, int D) {
+  const int cpr = D / 8;
+  const int64_t total = (int64_t)a.B * a.H * a.Sq * cpr;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int ch = (int)(t % cpr);
+    const int64_t r = t / cpr;
+    const int q = (int)(r % a.Sq), bh = (int)(r / a.Sq);
+    const int qb = q / (NW * 32), rl = q % (NW * 32);
+    int n;
+    const int base = split_base(a, bh, qb, true, n);
+    float mx = -INFINITY;
+    for (int c = 0; c < n; ++c) mx = fmaxf(mx, a.split_lse[(int64_t)(base + c) * (NW * 32) + rl]);
+    float sum = 0.f;
+    for (int c = 0; c < n; ++c) sum += __expf(a.split_lse[(int64_t)(base + c) * (NW * 32) + rl] - mx);
+    const float lse = mx + __logf(sum);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < n; ++c) {
+      const float w = __expf(a.split_lse[(int64_t)(base + c) * (NW * 32) + rl] - lse);
+      const float* p = a.split_o + ((int64_t)(base + c) * (NW * 32) + rl) * D + ch * 8;
+      const float4 x0 = *(const float4*)p, x1 = *(const float4*)(p + 4);
+      acc[0] += w * x0.x; acc[1] += w * x0.y; acc[2] += w * x0.z; acc[3] += w * x0.w;
+      acc[4] += w * x1.x; acc[5] += w * x1.y; acc[6] += w * x1.z; acc[7] += w * x1.w;
+    }
+    const int b = bh / a.H, h = bh % a.H;
+    st8((uint16_t*)a.o + b * a.o_sb + (int64_t)q * a.o_ss + h * a.o_sh + ch * 8, pack8(acc));
+    if (ch == 0) a.lse[(int64_t)bh * a.lse_ld + q] = lse;
+  }
+}
+
 // ======================================================================= delta = rowsum(dO * O)
 // one thread per (b, h, q) row; d in 16-byte chunks.  D is passed in a.dq_sh.
 // rows in memory order (b, s, h: one row = D contiguous bf16 of the token-major layout), D/8 lanes
@@ -494,7 +618,8 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AttnArgs a, const uint1
 
 // ============================================================================ dK / dV
 template <int D>
-__device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, int h_or_hk, int b) {
+__device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, int h_or_hk, int b, int it_lo = 0,
+                                                    int it_hi = -1, int item = -1) {
   constexpr int DT = D / 32, KS = D / 16;
   constexpr int TILE_B = KT * D * 2;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
@@ -522,7 +647,8 @@ __device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, i
   const int qt_begin = a.causal ? (kb * NW * 32) / KT : 0;
   const int nqt = a.Sq / KT;
   const int nq = nqt - qt_begin;  // q tiles per query head
-  const int n_iter = nq * group;
+  // this call's (head, q tile) steps: all, or a split work item's [it_lo, it_hi)
+  const int it0 = it_lo, n_iter = (it_hi < 0 ? nq * group : it_hi) - it_lo;
   // LDS: 2 x {Q tile, dO tile, lse * log2(e) [64], delta[64]}
   constexpr int STAGE_B = 2 * TILE_B + 2 * KT * 4;
 
@@ -565,12 +691,19 @@ __device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, i
         for (int r = 0; r < 16; ++r)
           if ((r & 3) + 8 * (r >> 2) < thr) s[r] = -INFINITY;
       }
+      // P = exp2(S c2 - lse log2e), dS = P (dP - D): packed pairs of rows (v_pk_fma / v_pk_add / v_pk_mul)
+      const f32x2_t c22 = {c2, c2};
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int qi = 32 * qh + crow(r, lane);
-        const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -sl2[qi]));
-        s[r] = p;                             // P
-        dp[r] = p * (dp[r] - sdel[qi]);       // dS
+      for (int r = 0; r < 16; r += 2) {
+        const int qi = 32 * qh + crow(r, lane), qj = 32 * qh + crow(r + 1, lane);
+        f32x2_t x = {s[r], s[r + 1]};
+        x = __builtin_elementwise_fma(x, c22, (f32x2_t){-sl2[qi], -sl2[qj]});
+        const f32x2_t pp = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+        const f32x2_t ds = pp * ((f32x2_t){dp[r], dp[r + 1]} - (f32x2_t){sdel[qi], sdel[qj]});
+        s[r] = pp.x;                          // P
+        s[r + 1] = pp.y;
+        dp[r] = ds.x;                         // dS
+        dp[r + 1] = ds.y;
       }
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
@@ -585,8 +718,8 @@ __device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, i
   };
 
   // (head, tile) counters for this step and the staged one (no divisions in the loop)
-  int cur_h = hk * group, cur_t = 0, nxt_h = cur_h, nxt_t = 0;
-  if (n_iter > 0) stage(cur_h, qt_begin, 0);
+  int cur_h = hk * group + it0 / nq, cur_t = it0 % nq, nxt_h = cur_h, nxt_t = cur_t;
+  if (n_iter > 0) stage(cur_h, qt_begin + cur_t, 0);
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler: its own fragment loads are done
   if (n_iter > 0) put_lse(0);
   __syncthreads();
@@ -603,6 +736,20 @@ __device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, i
     __syncthreads();
   }
 
+  if (item >= 0) {   // a split work item: dK (scaled) and dV partials (f32), summed by attn_split_reduce_kernel
+    const int64_t ro = ((int64_t)item * (NW * 32) + wave * 32 + (lane & 31)) * D;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = 32 * dt + 8 * g4 + 4 * (lane >> 5);
+        *(float4*)(a.split_o + ro + d) = make_float4(dk[dt][4 * g4] * a.scale, dk[dt][4 * g4 + 1] * a.scale,
+                                                     dk[dt][4 * g4 + 2] * a.scale, dk[dt][4 * g4 + 3] * a.scale);
+        *(float4*)(a.split_dv + ro + d) = make_float4(dv[dt][4 * g4], dv[dt][4 * g4 + 1], dv[dt][4 * g4 + 2],
+                                                      dv[dt][4 * g4 + 3]);
+      }
+    return;
+  }
   if (!a.grad_f32) {
     uint16_t* dkr = (uint16_t*)a.dk + b * a.dk_sb + (int64_t)mykey * a.dk_ss + hk * a.dk_sh;
     uint16_t* dvr = (uint16_t*)a.dv + b * a.dv_sb + (int64_t)mykey * a.dv_ss + hk * a.dv_sh;
@@ -624,6 +771,16 @@ __device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, i
       accum_T_f32(dvr, dt, dv[dt], 1.0f, lane);
     }
   }
+}
+
+template <int D>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(D == 64 ? 2 : 1)))
+void attn_bwd_dkdv_split_kernel(AttnArgs a) {
+  const int i = split_item_id();
+  int bh, kb, c;
+  split_item(a, i, false, bh, kb, c);
+  const int lo = c * a.split_ck, hi = min(lo + a.split_ck, split_nk_steps(a, kb));
+  attn_bwd_dkdv_block<D>(a, kb, bh % a.HKV, bh / a.HKV, lo, hi, i);
 }
 
 template <int D>
@@ -873,7 +1030,8 @@ __global__ __launch_bounds__(8 * 64) void attn_bwd_dkdv_pair_kernel(AttnArgs a) 
 
 // ============================================================================ dQ
 template <int D>
-__device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int h_or_hk, int b) {
+__device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int h_or_hk, int b, int kt_lo = 0,
+                                                  int kt_hi = -1, int item = -1) {
   constexpr int DT = D / 32, KS = D / 16;
   constexpr int TILE_B = KT * D * 2;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
@@ -913,7 +1071,8 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
   const uint16_t* kbase = a.k + b * a.k_sb + hk * a.k_sh;
   const uint16_t* vbase = a.v + b * a.v_sb + hk * a.v_sh;
   const int kv_end = a.causal ? (qb + 1) * NW * 32 : a.Sk;
-  const int nkt = kv_end / KT;
+  // this call's K/V tiles: all of the block's, or a split work item's [kt_lo, kt_hi)
+  const int kt0 = kt_lo, nkt = (kt_hi < 0 ? kv_end / KT : kt_hi) - kt_lo;
   f32x16_t dq[DT];
 #pragma unroll
   for (int i = 0; i < DT; ++i) dq[i] = zero16();
@@ -921,8 +1080,8 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
   constexpr int NS = dq_stages<D>(), OPS = 2 * (KT * D * 2 / 1024) / NW;
   auto stage = [&](int kt, int buf) {
     lds_u8* sk = smem + buf * 2 * TILE_B;
-    stage_rows<D>(kbase + (int64_t)kt * KT * a.k_ss, a.k_ss, sk, wave, lane);
-    stage_rows<D>(vbase + (int64_t)kt * KT * a.v_ss, a.v_ss, sk + TILE_B, wave, lane);
+    stage_rows<D>(kbase + (int64_t)(kt0 + kt) * KT * a.k_ss, a.k_ss, sk, wave, lane);
+    stage_rows<D>(vbase + (int64_t)(kt0 + kt) * KT * a.v_ss, a.v_ss, sk + TILE_B, wave, lane);
   };
   const int pre = nkt < NS - 1 ? nkt : NS - 1;
   for (int t = 0; t < pre; ++t) stage(t, t);
@@ -934,7 +1093,8 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
 #pragma unroll
       for (int j = 0; j < 8; ++j) part += (float)dof[ks][j] * (float)of[ks][j];
     del = xor32_sum(part);
-    if (lane < 32) a.delta_w[ri] = del;
+    // (split work items: every item of the block forms D itself; the first one stores it)
+    if (lane < 32 && kt0 == 0) a.delta_w[ri] = del;
   }
   __syncthreads();
 
@@ -958,10 +1118,26 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
         for (int r = 0; r < 16; ++r)
           if ((r & 3) + 8 * (r >> 2) > thr) s[r] = -INFINITY;
       }
+      // dS = P (dP - D), P = exp2(S c2 - lse log2e): at d64 as packed pairs (v_pk_fma / v_pk_add /
+      // v_pk_mul); d128 keeps the scalar form (its 256-VGPR budget spilled the packed one)
+      if constexpr (D == 64) {
+        const f32x2_t c22 = {c2, c2}, nl2 = {nlse2, nlse2}, nd2 = {-del, -del};
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, nlse2));
-        s[r] = p * (dp[r] - del);
+        for (int r = 0; r < 16; r += 2) {
+          f32x2_t x = {s[r], s[r + 1]};
+          x = __builtin_elementwise_fma(x, c22, nl2);
+          const f32x2_t pp = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+          const f32x2_t dd = (f32x2_t){dp[r], dp[r + 1]} + nd2;
+          const f32x2_t ds = pp * dd;
+          s[r] = ds.x;
+          s[r + 1] = ds.y;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, nlse2));
+          s[r] = p * (dp[r] - del);
+        }
       }
 #pragma unroll
       for (int sh = 0; sh < 2; ++sh) {
@@ -978,13 +1154,25 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
       stage(kt + NS - 1, sbuf);
       if (++sbuf == NS) sbuf = 0;
     }
-    tile(smem + buf * 2 * TILE_B, kt * KT);
+    tile(smem + buf * 2 * TILE_B, (kt0 + kt) * KT);
     if (++buf == NS) buf = 0;
     const int issued = kt + NS - 1 < nkt ? kt + NS - 1 : nkt - 1;
     ring_wait<OPS, NS>(issued - (kt + 1));
     __syncthreads();
   }
 
+  if (item >= 0) {   // a split work item: its dQ partial (scaled, f32), summed by attn_split_reduce_kernel
+    float* prow = a.split_o + ((int64_t)item * (NW * 32) + wave * 32 + (lane & 31)) * D;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = 32 * dt + 8 * g4 + 4 * (lane >> 5);
+        *(float4*)(prow + d) = make_float4(dq[dt][4 * g4] * a.scale, dq[dt][4 * g4 + 1] * a.scale,
+                                           dq[dt][4 * g4 + 2] * a.scale, dq[dt][4 * g4 + 3] * a.scale);
+      }
+    return;
+  }
   if (!a.grad_f32) {
     // the row index re-derived behind an opaque copy: the epilogue's row pointers (and the RoPE
     // tables') are then formed here, not hoisted into the prologue and held across the loop (at d128
@@ -1014,6 +1202,70 @@ void attn_bwd_dq_kernel(AttnArgs a) {
   for (int pass = 0; pass <= a.pair; ++pass) {  // one inlined body: no register growth
     if (pass) __syncthreads();
     attn_bwd_dq_block<D>(a, pass ? nqb_of(a) - 1 - bx : bx, hh, b);
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(D == 128 ? 2 : 1)))
+void attn_bwd_dq_split_kernel(AttnArgs a) {
+  const int i = split_item_id();
+  int bh, qb, c;
+  split_item(a, i, true, bh, qb, c);
+  const int nqb = a.Sq / (NW * 32);
+  const int lo = c * a.split_ck, hi = min(lo + a.split_ck, split_nq_tiles(a, qb));
+  attn_bwd_dq_block<D>(a, a.causal ? nqb - 1 - qb : qb, bh % a.H, bh / a.H, lo, hi, i);
+}
+
+// dQ (q_side) or dK | dV of the split work items summed in item order, rounded to bf16 and stored
+// into their strided views -- dq / dk rotated back by RoPE when tables are given, with the same
+// bf16-operand arithmetic as store_T_bf16_unrope.  One thread per (row, 8 columns of each half of
+// the head: d and d + D / 2), rows in (batch, head, position) order.
+__global__ __launch_bounds__(256) void attn_split_reduce_kernel(AttnArgs a, int D, int q_side) {
+  const int hd = D / 2, cpr = hd / 8;
+  const int heads = q_side ? a.H : a.HKV, S = q_side ? a.Sq : a.Sk;
+  const int64_t total = (int64_t)a.B * heads * S * cpr;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int ch = (int)(t % cpr);
+    const int64_t r = t / cpr;
+    const int pos = (int)(r % S), bh = (int)(r / S);
+    const int blk = pos / (NW * 32), rl = pos % (NW * 32);
+    int n;
+    const int base = split_base(a, bh, blk, q_side != 0, n);
+    const int d0 = ch * 8;
+    for (int part = 0; part < (q_side ? 1 : 2); ++part) {   // dq | (dk, dv)
+      const float* src = part ? a.split_dv : a.split_o;
+      float lo[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, hi[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int c = 0; c < n; ++c) {
+        const float* p = src + ((int64_t)(base + c) * (NW * 32) + rl) * D + d0;
+        const float4 x0 = *(const float4*)p, x1 = *(const float4*)(p + 4);
+        const float4 y0 = *(const float4*)(p + hd), y1 = *(const float4*)(p + hd + 4);
+        lo[0] += x0.x; lo[1] += x0.y; lo[2] += x0.z; lo[3] += x0.w;
+        lo[4] += x1.x; lo[5] += x1.y; lo[6] += x1.z; lo[7] += x1.w;
+        hi[0] += y0.x; hi[1] += y0.y; hi[2] += y0.z; hi[3] += y0.w;
+        hi[4] += y1.x; hi[5] += y1.y; hi[6] += y1.z; hi[7] += y1.w;
+      }
+      const int b = bh / heads, h = bh % heads;
+      uint16_t* dst = part ? (uint16_t*)a.dv + b * a.dv_sb + (int64_t)pos * a.dv_ss + h * a.dv_sh
+                           : (uint16_t*)(q_side ? a.dq : a.dk) + b * (q_side ? a.dq_sb : a.dk_sb) +
+                                 (int64_t)pos * (q_side ? a.dq_ss : a.dk_ss) + h * (q_side ? a.dq_sh : a.dk_sh);
+      if (!part && a.rope_cos) {
+        float c[8], sn[8], o1[8], o2[8];
+        unpack8(ld8(a.rope_cos + (int64_t)pos * a.rope_ld + d0), c);
+        unpack8(ld8(a.rope_sin + (int64_t)pos * a.rope_ld + d0), sn);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float g1 = round_bf(lo[e]), g2 = round_bf(hi[e]);
+          const float sj = -sn[e];
+          o1[e] = fmaf(g1, c[e], -(g2 * sj));
+          o2[e] = fmaf(g2, c[e], g1 * sj);
+        }
+        st8(dst + d0, pack8(o1));
+        st8(dst + d0 + hd, pack8(o2));
+      } else {
+        st8(dst + d0, pack8(lo));
+        st8(dst + d0 + hd, pack8(hi));
+      }
+    }
   }
 }
 
@@ -1212,9 +1464,170 @@ int attn_bwd_impl(const void* q, const int64_t* q_str, const void* k, const int6
   return PT_OK;
 }
 
+// ---- few-head split forms: plan and launches
+// the work-item chunk when the split forms apply (0: they do not): d64, and the regular launch (one
+// workgroup per causal block pair) would put fewer than 128 workgroups on the 256 CUs
+int split_ck_for(int64_t B, int64_t H, int64_t Sq, int64_t Sk, int64_t D, int causal) {
+  const int ck = pt_variant(PT_VAR_ATTN_KV_CHUNK);
+  if (ck <= 0 || (ck & 1) || D != 64 || Sq % (NW * 32) || Sk % (NW * 32) || (causal && Sq != Sk)) return 0;
+  const int64_t nqb = Sq / (NW * 32);
+  const int64_t wgs = B * H * ((causal && nqb % 2 == 0) ? nqb / 2 : nqb);
+  return wgs < 128 ? ck : 0;
+}
+// items per (batch, head) row: forward / dQ (q_side) or dK / dV (per (batch, kv head))
+int64_t split_row_items(int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int causal, int ck, bool q_side) {
+  int64_t n = 0;
+  if (q_side) {
+    for (int64_t qb = 0; qb < Sq / (NW * 32); ++qb) {
+      const int64_t nt = causal ? (qb + 1) * (NW * 32 / KT) : Sk / KT;
+      n += (nt + ck - 1) / ck;
+    }
+  } else {
+    for (int64_t kb = 0; kb < Sk / (NW * 32); ++kb) {
+      const int64_t qt_begin = causal ? (kb * NW * 32) / KT : 0;
+      const int64_t steps = (Sq / KT - qt_begin) * (H / HKV);
+      n += (steps + ck - 1) / ck;
+    }
+  }
+  return n;
+}
+inline int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
 }  // namespace
 
 extern "C" {
+
+// Few-head attention (a TP shard's 4 heads): whether the split work-item forms apply to this shape and
+// the f32 workspace they need -- forward (backward = 0): partial O and LSE per item; backward: partial
+// dQ, dK, dV per item.  Returns 1 (ws_bytes set) or 0 (the regular launches; ws_bytes = 0).
+int pt_attn_split_plan(int64_t B, int64_t H, int64_t HKV, int64_t Sq, int64_t Sk, int64_t D, int causal, int backward,
+                       int64_t* ws_bytes) {
+  if (!ws_bytes || B <= 0 || H <= 0 || HKV <= 0 || H % HKV) return PT_EINVAL;
+  *ws_bytes = 0;
+  const int ck = split_ck_for(B, H, Sq, Sk, D, causal);
+  if (!ck) return 0;
+  const int64_t iq = B * H * split_row_items(H, HKV, Sq, Sk, causal, ck, true);
+  const int64_t rows = NW * 32;
+  if (!backward) {
+    *ws_bytes = align256(iq * rows * D * 4) + align256(iq * rows * 4);
+  } else {
+    const int64_t ik = B * HKV * split_row_items(H, HKV, Sq, Sk, causal, ck, false);
+    *ws_bytes = align256(iq * rows * D * 4) + 2 * align256(ik * rows * D * 4);
+  }
+  return 1;
+}
+
+// pt_attn_fwd (merge = 0, dense lse) in the split form: work items of attn_kv_chunk K/V tiles of
+// one query block, then the merge pass (O bf16 and lse)
+int pt_attn_fwd_split(const void* q, const int64_t* q_str, const void* k, const int64_t* k_str, const void* v,
+                      const int64_t* v_str, void* o, const int64_t* o_str, float* lse, int64_t B, int64_t H,
+                      int64_t HKV, int64_t Sq, int64_t Sk, int64_t D, float scale, int causal, void* ws,
+                      int64_t ws_bytes, hipStream_t stream) {
+  if (!q || !k || !v || !o || !lse || !ws) return PT_EINVAL;
+  int64_t need = 0;
+  if (pt_attn_split_plan(B, H, HKV, Sq, Sk, D, causal, 0, &need) != 1) return PT_EUNSUPPORTED;
+  if (ws_bytes < need || !pt_aligned16(ws)) return PT_EINVAL;
+  if ((o_str[0] & 7) || (o_str[1] & 7) || (o_str[2] & 7) || !pt_aligned16(o)) return PT_EALIGN;
+  AttnArgs a{};
+  a.lse_ld = Sq;
+  a.q = (const uint16_t*)q; a.q_sb = q_str[0]; a.q_ss = q_str[1]; a.q_sh = q_str[2];
+  a.k = (const uint16_t*)k; a.k_sb = k_str[0]; a.k_ss = k_str[1]; a.k_sh = k_str[2];
+  a.v = (const uint16_t*)v; a.v_sb = v_str[0]; a.v_ss = v_str[1]; a.v_sh = v_str[2];
+  a.o = o; a.o_sb = o_str[0]; a.o_ss = o_str[1]; a.o_sh = o_str[2];
+  a.lse = lse;
+  a.B = (int)B; a.H = (int)H; a.HKV = (int)HKV; a.Sq = (int)Sq; a.Sk = (int)Sk;
+  a.scale = scale; a.causal = causal;
+  int rc = check_common(a, (int)D);
+  if (rc) return rc;
+  a.split_ck = split_ck_for(B, H, Sq, Sk, D, causal);
+  a.split_per_bh = (int)split_row_items(H, HKV, Sq, Sk, causal, a.split_ck, true);
+  const int64_t items = B * H * a.split_per_bh;
+  a.split_o = (float*)ws;
+  a.split_lse = (float*)((char*)ws + align256(items * NW * 32 * D * 4));
+  const int smem = fwd_stages<64, NW>() * 2 * KT * 64 * 2;
+  set_smem(attn_fwd_split_kernel<64>, smem);
+  attn_fwd_split_kernel<64><<<(unsigned)items, NW * 64, smem, stream>>>(a);
+  PT_CHECK_LAUNCH();
+  const int64_t total = B * H * Sq * (D / 8);
+  int64_t g = (total + 255) / 256;
+  if (g > 4 * PT_STREAM_GRID_CAP) g = 4 * PT_STREAM_GRID_CAP;
+  attn_split_merge_kernel<<<(unsigned)g, 256, 0, stream>>>(a, (int)D);
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
+
+// pt_attn_bwd_fused_delta in the split form: dQ items (each forms D from O; the first of a block
+// stores it), then dK/dV items of attn_kv_chunk (head, Q tile) steps, then one reduce pass each
+int pt_attn_bwd_split(const void* q, const int64_t* q_str, const void* k, const int64_t* k_str, const void* v,
+                      const int64_t* v_str, const void* o, const int64_t* o_str, const void* dout, const int64_t* do_str,
+                      const float* lse, float* delta_out, void* dq, const int64_t* dq_str, void* dk,
+                      const int64_t* dk_str, void* dv, const int64_t* dv_str, int64_t B, int64_t H, int64_t HKV,
+                      int64_t Sq, int64_t Sk, int64_t D, float scale, int causal, const void* rope_cos,
+                      const void* rope_sin, int64_t rope_stride, void* ws, int64_t ws_bytes, hipStream_t stream) {
+  if (!q || !k || !v || !o || !dout || !lse || !delta_out || !dq || !dk || !dv || !ws) return PT_EINVAL;
+  int64_t need = 0;
+  if (pt_attn_split_plan(B, H, HKV, Sq, Sk, D, causal, 1, &need) != 1) return PT_EUNSUPPORTED;
+  if (ws_bytes < need || !pt_aligned16(ws)) return PT_EINVAL;
+  if (!pt_aligned16(o) || (o_str[0] & 7) || (o_str[1] & 7) || (o_str[2] & 7)) return PT_EALIGN;
+  for (const int64_t* st : {dq_str, dk_str, dv_str})
+    if ((st[0] & 7) || (st[1] & 7) || (st[2] & 7)) return PT_EALIGN;
+  if (!pt_aligned16(dq) || !pt_aligned16(dk) || !pt_aligned16(dv)) return PT_EALIGN;
+  if (rope_cos && (!rope_sin || Sq != Sk || (rope_stride & 7) || !pt_aligned16(rope_cos) || !pt_aligned16(rope_sin)))
+    return PT_EINVAL;
+  AttnArgs a{};
+  a.q = (const uint16_t*)q; a.q_sb = q_str[0]; a.q_ss = q_str[1]; a.q_sh = q_str[2];
+  a.k = (const uint16_t*)k; a.k_sb = k_str[0]; a.k_ss = k_str[1]; a.k_sh = k_str[2];
+  a.v = (const uint16_t*)v; a.v_sb = v_str[0]; a.v_ss = v_str[1]; a.v_sh = v_str[2];
+  a.dout = (const uint16_t*)dout; a.do_sb = do_str[0]; a.do_ss = do_str[1]; a.do_sh = do_str[2];
+  a.o = const_cast<void*>(o); a.o_sb = o_str[0]; a.o_ss = o_str[1]; a.o_sh = o_str[2];
+  a.lse = (float*)lse; a.lse_ld = Sq;
+  a.delta_w = delta_out;
+  a.dq = dq; a.dq_sb = dq_str[0]; a.dq_ss = dq_str[1]; a.dq_sh = dq_str[2];
+  a.dk = dk; a.dk_sb = dk_str[0]; a.dk_ss = dk_str[1]; a.dk_sh = dk_str[2];
+  a.dv = dv; a.dv_sb = dv_str[0]; a.dv_ss = dv_str[1]; a.dv_sh = dv_str[2];
+  a.B = (int)B; a.H = (int)H; a.HKV = (int)HKV; a.Sq = (int)Sq; a.Sk = (int)Sk;
+  a.scale = scale; a.causal = causal;
+  a.rope_cos = (const uint16_t*)rope_cos; a.rope_sin = (const uint16_t*)rope_sin; a.rope_ld = rope_stride;
+  int rc = check_common(a, (int)D);
+  if (rc) return rc;
+  const int ck = split_ck_for(B, H, Sq, Sk, D, causal);
+  const int64_t per_q = split_row_items(H, HKV, Sq, Sk, causal, ck, true);
+  const int64_t per_k = split_row_items(H, HKV, Sq, Sk, causal, ck, false);
+  const int64_t iq = B * H * per_q, ik = B * HKV * per_k;
+  char* w = (char*)ws;
+  float* pdq = (float*)w;
+  float* pdk = (float*)(w + align256(iq * NW * 32 * D * 4));
+  float* pdv = (float*)((char*)pdk + align256(ik * NW * 32 * D * 4));
+  a.split_ck = ck;
+  // dQ items
+  a.split_per_bh = (int)per_q;
+  a.split_o = pdq;
+  const int smem_kv = dq_stages<64>() * 2 * KT * 64 * 2;
+  set_smem(attn_bwd_dq_split_kernel<64>, smem_kv);
+  attn_bwd_dq_split_kernel<64><<<(unsigned)iq, NW * 64, smem_kv, stream>>>(a);
+  PT_CHECK_LAUNCH();
+  const int64_t tq = B * H * Sq * (D / 16);
+  int64_t g = (tq + 255) / 256;
+  if (g > 4 * PT_STREAM_GRID_CAP) g = 4 * PT_STREAM_GRID_CAP;
+  attn_split_reduce_kernel<<<(unsigned)g, 256, 0, stream>>>(a, (int)D, 1);
+  PT_CHECK_LAUNCH();
+  // dK / dV items read the D the dQ items stored
+  a.delta = delta_out;
+  a.delta_w = nullptr;
+  a.split_per_bh = (int)per_k;
+  a.split_o = pdk;
+  a.split_dv = pdv;
+  const int smem_q = 2 * (2 * KT * 64 * 2 + 2 * KT * 4);
+  set_smem(attn_bwd_dkdv_split_kernel<64>, smem_q);
+  attn_bwd_dkdv_split_kernel<64><<<(unsigned)ik, NW * 64, smem_q, stream>>>(a);
+  PT_CHECK_LAUNCH();
+  const int64_t tk = B * HKV * Sk * (D / 16);
+  g = (tk + 255) / 256;
+  if (g > 4 * PT_STREAM_GRID_CAP) g = 4 * PT_STREAM_GRID_CAP;
+  attn_split_reduce_kernel<<<(unsigned)g, 256, 0, stream>>>(a, (int)D, 0);
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
 
 // pt_attn_bwd computing only dQ (parts 1) or only dK / dV (parts 2): the full-mesh context-parallel
 // backward runs each rank's dQ against the visiting K / V and its own keys' dK / dV against the

@@ -1270,11 +1270,26 @@ def attn_fwd(q, k, v, scale, causal, out=None, lse=None, merge=False):
     if lse is None:
         lse = torch.empty(B, H, Sq, dtype=torch.float32, device=q.device)
     ld = _lse_ld(lse, B, H, Sq)
+    ws = _attn_split_ws(B, H, HKV, Sq, Sk, D, causal, 0, q.device) if (not merge and ld == Sq) else None
+    if ws is not None:   # few heads (a TP shard): split work items + merge (pt_attn_split_plan)
+        rc = _C.lib().pt_attn_fwd_split(_ptr(q), _str3(q), _ptr(k), _str3(k), _ptr(v), _str3(v), _ptr(out),
+                                        _str3(out), _ptr(lse), B, H, HKV, Sq, Sk, D, float(scale), int(bool(causal)),
+                                        _ptr(ws), ws.numel(), _C.stream_ptr(q.device))
+        _C.check(rc, "pt_attn_fwd_split")
+        return out, lse
     rc = _C.lib().pt_attn_fwd(_ptr(q), _str3(q), _ptr(k), _str3(k), _ptr(v), _str3(v), _ptr(out), _str3(out),
                               _ptr(lse), B, H, HKV, Sq, Sk, D, float(scale), int(bool(causal)), int(bool(merge)),
                               ld, _C.stream_ptr(q.device))
     _C.check(rc, "pt_attn_fwd")
     return out, lse
+
+
+def _attn_split_ws(B, H, HKV, Sq, Sk, D, causal, backward, device):
+    """The workspace (uint8) of the few-head split forms when they apply to this shape, else None."""
+    nb = ctypes.c_int64(0)
+    rc = _C.lib().pt_attn_split_plan(B, H, HKV, Sq, Sk, D, int(bool(causal)), int(backward), ctypes.byref(nb))
+    _C.check(min(rc, 0), "pt_attn_split_plan")
+    return torch.empty(nb.value, dtype=torch.uint8, device=device) if rc == 1 else None
 
 
 def attn_delta(dout, out, delta=None):
@@ -1343,6 +1358,15 @@ def attn_bwd(dout, q, k, v, out, lse, scale, causal, dq=None, dk=None, dv=None, 
         _req(out.shape == q.shape, "attn_bwd: out must be [B, Sq, H, D]")
         _req(ld == Sq, "attn_bwd: the fused-delta form takes a dense lse")
         delta = torch.empty(B, H, Sq, dtype=torch.float32, device=q.device)
+        ws = _attn_split_ws(B, H, HKV, Sq, Sk, D, causal, 1, q.device)
+        if ws is not None:   # few heads (a TP shard): split work items + reduce passes
+            rc = lib.pt_attn_bwd_split(_ptr(q), _str3(q), _ptr(k), _str3(k), _ptr(v), _str3(v), _ptr(out), _str3(out),
+                                       _ptr(dout), _str3(dout), _ptr(lse), _ptr(delta), _ptr(dq), _str3(dq), _ptr(dk),
+                                       _str3(dk), _ptr(dv), _str3(dv), B, H, HKV, Sq, Sk, D, float(scale),
+                                       int(bool(causal)), _ptr(rc_cos), _ptr(rc_sin), rstride, _ptr(ws), ws.numel(),
+                                       _C.stream_ptr(q.device))
+            _C.check(rc, "pt_attn_bwd_split")
+            return dq, dk, dv, delta
         rc = lib.pt_attn_bwd_fused_delta(_ptr(q), _str3(q), _ptr(k), _str3(k), _ptr(v), _str3(v), _ptr(out), _str3(out),
                                          _ptr(dout), _str3(dout), _ptr(lse), _ptr(delta), _ptr(dq), _str3(dq), _ptr(dk),
                                          _str3(dk), _ptr(dv), _str3(dv), B, H, HKV, Sq, Sk, D, float(scale),

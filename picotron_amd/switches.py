@@ -29,9 +29,9 @@ DEFAULTS = {
     # tensor_parallel/sequence_parallel.py: the residual stream sharded by token rows over the tp group
     "tp_sp": 1,
     # native (libpicotron_hip.so, pt_set_variant)
-    "attn_pair": 1, "attn_split": 2, "gemm_group_m": -1, "gemm_mix": 1, "gemm_kh": 2,
+    "attn_pair": 1, "attn_split": 2, "gemm_group_m": -1, "gemm_mix": 1, "gemm_kh": 2, "attn_kv_chunk": 4,
 }
-NATIVE = ("attn_pair", "attn_split", "gemm_group_m", "gemm_mix", "gemm_kh")
+NATIVE = ("attn_pair", "attn_split", "gemm_group_m", "gemm_mix", "gemm_kh", "attn_kv_chunk")
 
 
 class _Switches:

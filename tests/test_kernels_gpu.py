@@ -1002,3 +1002,42 @@ def test_fewtile_splitk_matches_single_pass(monkeypatch, M, N, K, kind, residual
     torch.cuda.synchronize()
     assert rel_err(y, ref) < 4e-3
     assert maxabs(y, y1) <= 2 * y1.float().abs().max().item() * 2 ** -8
+
+
+@pytest.mark.parametrize("B,S,H,HKV,causal,rope", [(4, 1024, 4, 4, True, True), (2, 1024, 4, 2, True, False),
+                                                   (1, 512, 2, 2, False, False), (4, 1024, 4, 4, True, False)])
+@pytest.mark.parametrize("chunk", [2, 4, 6])
+def test_attention_few_head_split_forms(B, S, H, HKV, causal, rope, chunk):
+    """The few-head split forms (pt_attn_split_plan: the regular launch would put < 128 workgroups on
+    the 256 CUs -- a TP = 8 shard of SmolLM-1.7B is B 4 x 4 heads): forward work items of `chunk`
+    K/V tiles + the LSE merge, backward dQ / dK|dV items + reduce passes (the RoPE backward in the
+    reduce), against the regular kernels (attn_kv_chunk = 0) to f32-summation-order rounding and
+    against the fp32 oracle at bf16 tolerance."""
+    from picotron_amd import kernels as K_
+    D = 64
+    q, k, v = _qkv(B, S, H, HKV, D)
+    scale = 1 / math.sqrt(D)
+    do = torch.randn(B, S, H, D).to(BF).to(DEV)
+    rp = tuple(t.to(DEV) for t in O.get_cos_sin(S, D, base=10000.0)) if rope else None
+    res = {}
+    for ck in (0, chunk):
+        with switches.override(attn_kv_chunk=ck):
+            assert (K_._attn_split_ws(B, H, HKV, S, S, D, causal, 0, DEV) is not None) == (ck > 0)
+            o, lse = K_.attn_fwd(q, k, v, scale, causal)
+            dq, dk, dv, delta = K_.attn_bwd(do, q, k, v, o, lse, scale, causal, rope=rp)
+        torch.cuda.synchronize()
+        res[ck] = [t.clone() for t in (o, lse, dq, dk, dv, delta)]
+    for name, a, b in zip(("o", "lse", "dq", "dk", "dv", "delta"), res[chunk], res[0]):
+        assert torch.isfinite(a.float()).all(), name
+        assert rel_err(a, b.float().cpu()) < 4e-3, name      # f32 summation order, then bf16 rounding
+    qq, kk, vv = _ref_attn(q, k, v, causal, scale)
+    qq.requires_grad_(True); kk.requires_grad_(True); vv.requires_grad_(True)
+    o_ref, lse_ref = O.attention_lse(qq, kk, vv, scale, causal)
+    o, lse, dq, dk, dv, _ = res[chunk]
+    assert rel_err(o, o_ref.transpose(1, 2)) < 1e-2 and maxabs(lse, lse_ref) < 1e-2
+    if not rope:
+        (o_ref * do.float().cpu().transpose(1, 2)).sum().backward()
+        rep = H // HKV
+        assert rel_err(dq, qq.grad.transpose(1, 2)) < 2e-2
+        assert rel_err(dk, kk.grad.view(B, HKV, rep, S, D).sum(2).transpose(1, 2)) < 2e-2
+        assert rel_err(dv, vv.grad.view(B, HKV, rep, S, D).sum(2).transpose(1, 2)) < 2e-2

@@ -86,12 +86,15 @@ def main():
             variants[f"{var}={val}"] = {var: val}
     defaults = {}
     outs = {}
+    split_ws = K._attn_split_ws
     med = {name: {"fwd": [], "bwd": []} for name in libs}
     for rnd in range(a.rounds):
         order = list(libs.items())
         order = order[rnd % len(order):] + order[:rnd % len(order)]   # rotate who goes first
         for name, lib in order:
             _C._lib = lib
+            # builds from before the few-head split forms lack pt_attn_split_plan: the unsplit kernels
+            K._attn_split_ws = split_ws if hasattr(lib, "pt_attn_split_plan") else (lambda *args: None)
             for var, val in variants[name].items():
                 if var not in defaults:
                     defaults[var] = lib.pt_get_variant(var.encode())
@@ -126,6 +129,7 @@ def main():
                               "bwd_us": round(t_bwd, 1), "bwd_tflops": round(5 * unit / t_bwd / 1e6, 1),
                               "bwd_kernel_flop_tflops": round(7 * unit / t_bwd / 1e6, 1)}), flush=True)
     _C._lib = libs["new"]
+    K._attn_split_ws = split_ws
     for name, m in med.items():
         f, b = sorted(m["fwd"])[len(m["fwd"]) // 2], sorted(m["bwd"])[len(m["bwd"]) // 2]
         print(json.dumps({"median": name, "fwd_us": round(f, 1), "bwd_us": round(b, 1)}), flush=True)
