@@ -114,8 +114,9 @@ def tp_proxy(args, base, layers):
     """One TP rank's compute for a micro-batch (no collectives): `layers` decoder layers with the
     shard widths (heads / tp, I / tp; the layer kernels read shards exactly like this inside the
     TP model) and the launch forms of a tp > 1 group (its all-reduces no-ops), the embedding lookup
-    and the lm_head's vocab shard (ColumnParallel, V / tp) plus the cross-entropy over the gathered
-    vocabulary, fwd + bwd.  Returns the JSON line."""
+    and the lm_head's vocab shard (ColumnParallel, V / tp) plus the cross-entropy -- on the vocab
+    shard (functional.VocabParallelCEFunction, the shipped form) or, with PICOTRON_VP_CE=0, over the
+    gathered vocabulary as the reference -- fwd + bwd.  Returns the JSON line."""
     import math
     from picotron_amd import functional as FN
     from picotron_amd import kernels as K
@@ -156,6 +157,7 @@ def tp_proxy(args, base, layers):
 
     from picotron_amd.switches import S as SW
     sp = tp > 1 and SW.tp_sp != 0 and args.seq % tp == 0   # sequence parallelism (sequence_parallel.py)
+    vp = tp > 1 and FN.vp_ce_shape_ok(T, V // tp, H)          # the lm_head's vocab-parallel CE
 
     def micro_batch():
         x = FN.embedding(ids, emb)
@@ -165,8 +167,12 @@ def tp_proxy(args, base, layers):
             x = FN.DecoderLayerFunction.apply(x, *w, cos, sin, cfg.rms_norm_eps, 0, nh, nkv, d, False, sp)
         if sp:   # the exit hook's all-gather before the final norm
             x = _TPNoComm(None, tp, 0).all_gather_rows(x.reshape(T // tp, H))
-        lg = FN.linear(x.view(T, H), head)                         # this rank's vocab shard
-        full = _GatherStandIn.apply(lg) if tp > 1 else lg           # stands in for the all-gather
+        if vp:   # the vocab-parallel CE (functional.VocabParallelCEFunction): no logits gather
+            lg, stats = FN.lm_head_shard(x.view(T, H), head)
+            full = FN.vp_logits(lg, stats, 0, V, lambda: _GatherStandIn.apply(lg))
+        else:
+            lg = FN.linear(x.view(T, H), head)                     # this rank's vocab shard
+            full = _GatherStandIn.apply(lg) if tp > 1 else lg       # stands in for the all-gather
         FN.cross_entropy(full, tgt).backward()
     # the layers see a tp group of `tp` ranks whose all-reduces are no-ops, so they take the TP
     # launch forms (dX and dW as separate launches around the dX all-reduce), not tp = 1's duals
@@ -210,7 +216,7 @@ def tp_proxy(args, base, layers):
             "mfu_upper_bound": tok_gpu * (fpt_rank * tp) / MI355X_BF16_DENSE_PEAK,
             "config": {"model": cfg_name(base), "layers": layers, "micro_batch": args.mbs, "seq_len": args.seq,
                        "shard": {"q|k|v": 3 * nh * d, "I": I, "heads": nh, "vocab": V // tp},
-                       "sequence_parallel": sp},
+                       "sequence_parallel": sp, "vocab_parallel_ce": vp},
             "roofline": {"bound": "mfma", "kernel": "gemm (every GEMM launch of one micro-batch)", "achieved": ach,
                          "peak": MI355X_BF16_DENSE_PEAK / 1e12, "unit": "TFLOP/s",
                          "frac": ach / (MI355X_BF16_DENSE_PEAK / 1e12), "launches": s["launches"],

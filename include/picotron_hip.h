@@ -111,6 +111,24 @@ int pt_cross_entropy_fwd_stats(const void* logits, int64_t logits_stride, const 
                                const float* stats, int64_t nblk, float* row_loss, float* row_lse, int64_t rows,
                                int64_t vocab, int64_t ignore_index, int* status, hipStream_t stream);
 
+/* Vocab-parallel form (the lm_head as ColumnParallelLinear(gather_output=True), tensor_parallel.py:
+ * 50 + tp_communications.py:51-72, whose logits all-gather it replaces): each tp rank reduces its
+ * shard logits [rows, vocab_shard] (global columns vocab_lo ..) with the GEMM statistics to a float4
+ * part[row] = (max, sum exp(x - max), x[target] if target in the shard else 0, 1 / 0); the caller
+ * all-gathers the parts [tp][rows][4] and combines them (rank order) into row_loss / row_lse as
+ * pt_cross_entropy_fwd_stats returns them for the whole vocabulary (same range check against
+ * `vocab`).  The backward on the shard: pt_cross_entropy_bwd_lse with the one-hot at target - vocab_lo. */
+int pt_cross_entropy_vp_partial(const void* logits, int64_t logits_stride, const int64_t* targets,
+                                const float* stats, int64_t nblk, float* part, int64_t rows, int64_t vocab_shard,
+                                int64_t vocab_lo, hipStream_t stream);
+int pt_cross_entropy_vp_combine(const float* parts, int64_t tp, const int64_t* targets, float* row_loss,
+                                float* row_lse, int64_t rows, int64_t vocab, int64_t ignore_index, int* status,
+                                hipStream_t stream);
+int pt_cross_entropy_bwd_lse_shard(const void* logits, int64_t logits_stride, const int64_t* targets,
+                                   const float* row_lse, void* dlogits, int64_t dlogits_stride, int64_t rows,
+                                   int64_t vocab_shard, int64_t vocab_lo, const float* scale, int64_t scale_stride,
+                                   int64_t ignore_index, hipStream_t stream);
+
 /* train.py:49's reduction='mean' over the per-row losses: loss = sum(row_loss) / #(target !=
  * ignore_index) in one deterministic launch; inv_count = 1 / #valid (the backward's scale);
  * reduce_sum != 0: reduction='sum' (loss = sum(row_loss), inv_count = 1);

@@ -74,6 +74,10 @@ SIGNATURES = {
     "pt_gemm_ce_stats": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp]),
     "pt_cross_entropy_fwd_stats": (_i32, [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i64, _i64, _vp, _vp]),
     "pt_cross_entropy_mean": (_i32, [_vp, _vp, _i64, _i64, _vp, _vp, _vp, _i32, _i32, _vp]),
+    "pt_cross_entropy_vp_partial": (_i32, [_vp, _i64, _vp, _vp, _i64, _vp, _i64, _i64, _i64, _vp]),
+    "pt_cross_entropy_vp_combine": (_i32, [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp]),
+    "pt_cross_entropy_bwd_lse_shard": (_i32, [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp, _i64, _i64,
+                                              _vp]),
     "pt_embedding_sort": (_i32, [_vp, _i64, _i64, _i64, _i32, _i64, _vp, _vp, _vp]),
     "pt_set_variant": (_i32, [ctypes.c_char_p, _i32]),
     "pt_get_variant": (_i32, [ctypes.c_char_p]),

@@ -27,6 +27,8 @@
 
 #include <stdlib.h>
 
+#include <type_traits>
+
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
@@ -289,6 +291,25 @@ __device__ __forceinline__ void ring_wait(int younger) {
   vm_wait<0>();
 }
 
+// A wave's tiles [0, nkt) in three loops -- below the causal diagonal (kind 0), on it (1), past it
+// (2: only the ring's refill / wait / barrier) -- so no per-tile branch joins two versions of the
+// accumulators (such a join cost 16-32 register copies on every tile) and the diagonal mask is
+// compiled into its own loop only.
+template <typename Step>
+__device__ __forceinline__ void tile_loops(int n_nd, int n_c, int nkt, Step&& step) {
+  for (int kt = 0; kt < n_nd; ++kt) step(std::integral_constant<int, 0>{}, kt);
+  for (int kt = n_nd; kt < n_c; ++kt) step(std::integral_constant<int, 1>{}, kt);
+  for (int kt = n_c; kt < nkt; ++kt) step(std::integral_constant<int, 2>{}, kt);
+}
+
+// the loop bounds for a wave whose 32 query rows start at q0, over key tiles kt0 .. kt0 + nkt - 1:
+// n_c tiles hold a key <= q0 + 31, the first n_nd of them only keys <= q0
+__device__ __forceinline__ void causal_split(bool causal, int q0, int kt0, int nkt, int& n_nd, int& n_c) {
+  if (!causal) { n_nd = n_c = nkt; return; }
+  n_c = min(nkt, max(0, (q0 + 31) / KT - kt0 + 1));
+  n_nd = min(n_c, max(0, (q0 + 1) / KT - kt0));
+}
+
 // ring depth per kernel and head dim (LDS: a d64 K|V stage is 16 KiB, d128 32 KiB).  Measured
 // (tools/attn_bench.py, in-process A/B): d64 forward 4 stages 36.0 -> 35.1 us with the widened stores
 // (ring alone -2 %); the d128 forward slower with 3 (138.5 vs 145.8 us), so it keeps 2.
@@ -343,10 +364,11 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler: its own fragment loads are done
   __syncthreads();
 
-  // one K/V tile (a lambda, not a loop body: the causal skip is an early return)
-  auto tile = [&](const lds_u8* sk, int kv0) {
+  // one K/V tile (a lambda, not a loop body: the causal skip is an early return).  The diagonal
+  // tile's mask is a separate instantiation (dg): as a runtime branch the compiler if-converted it,
+  // 60 compares / selects on every tile
+  auto tile = [&](auto dg, const lds_u8* sk, int kv0) {
     const lds_u8* sv = sk + TILE_B;
-    if (a.causal && kv0 > q0 + 31) return;  // wave-uniform: skip tiles fully above the diagonal
     {
       f32x16_t s[2];
       // the tile's K operands in one batch of LDS reads ahead of the MFMAs (left to itself the
@@ -364,7 +386,7 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
         for (int ks = 0; ks < KS; ++ks) s[kh] = mfma(ka[kh][ks], qf[ks], s[kh]);
       }
       // causal mask, diagonal tiles only: key row 32 kh + crow(r) visible iff <= thr
-      if (a.causal && (kv0 + KT - 1 > q0)) {
+      if constexpr (decltype(dg)::value == 1) {
         const int thr = myq - kv0 - 4 * (lane >> 5);
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh)
@@ -380,8 +402,10 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
       mt = xor32_max(mt) * c2;  // log2 units (c2 > 0)
       // lazy rescale (FA-style deferred max): only when some query's max grew by > 2^8; P may then
       // exceed 1 by at most 2^8, harmless in f32 accumulation and in bf16 (relative precision)
-      if (__any(mt > m + kRescaleLog2)) {
-        const float mn = fmaxf(m, mt);
+      // branch-free: alpha = exp2(0) = 1 exactly when no row grew, and x * 1 = x, so the result is
+      // the lazy form's; as a branch the two paths' copies of O cost 16 v_mov_b64 per tile
+      {
+        const float mn = __any(mt > m + kRescaleLog2) ? fmaxf(m, mt) : m;
         const float alpha = __builtin_amdgcn_exp2f(m - mn);
         m = mn;
         l *= alpha;
@@ -394,7 +418,7 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
       // the row sum in four packed partial sums (v_pk_add_f32, a dependency chain of 8 instead of
       // 32 serial adds), combined once at the end of the tile
       const f32x2_t c22 = {c2, c2}, nm2 = {-m, -m};
-      f32x2_t ls[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+      f32x2_t ls[4];   // each partial starts as its first pair (= 0 + p: exp2 is never -0)
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
@@ -404,7 +428,8 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
           const f32x2_t p = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
           s[kh][r] = p.x;
           s[kh][r + 1] = p.y;
-          ls[(kh * 8 + r / 2) & 3] += p;
+          if (kh == 0 && r < 8) ls[r / 2] = p;
+          else ls[(kh * 8 + r / 2) & 3] += p;
         }
       const f32x2_t lt = (ls[0] + ls[1]) + (ls[2] + ls[3]);
       l += lt.x + lt.y;
@@ -426,18 +451,16 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
     }
   };
 
-  const int nkt_run = nkt;
-  for (int kt = 0, buf = 0, sbuf = pre % NS; kt < nkt_run; ++kt) {
-    if (kt + NS - 1 < nkt) {  // into the stage tile kt - 1 used (every wave passed its barrier)
-      stage(kt + NS - 1, sbuf);
-      if (++sbuf == NS) sbuf = 0;
-    }
-    tile(smem + buf * 2 * TILE_B, (kt0 + kt) * KT);
-    if (++buf == NS) buf = 0;
+  int n_nd, n_c;
+  causal_split(a.causal, q0, kt0, nkt, n_nd, n_c);
+  tile_loops(n_nd, n_c, nkt, [&](auto kind, int kt) {
+    if (kt + NS - 1 < nkt)  // into the stage tile kt - 1 used (every wave passed its barrier)
+      stage(kt + NS - 1, (kt + NS - 1) % NS);
+    if constexpr (decltype(kind)::value != 2) tile(kind, smem + (kt % NS) * 2 * TILE_B, (kt0 + kt) * KT);
     const int issued = kt + NS - 1 < nkt ? kt + NS - 1 : nkt - 1;   // the last tile issued so far
     ring_wait<OPS, NS>(issued - (kt + 1));
     __syncthreads();
-  }
+  });
 
   l = xor32_sum(l);
   if (item >= 0) {
@@ -496,6 +519,220 @@ __global__ __launch_bounds__(NWK * 64) void attn_fwd_kernel(AttnArgs a) {
   for (int pass = 0; pass <= a.pair; ++pass) {  // one inlined body: no register growth
     if (pass) __syncthreads();
     attn_fwd_block<D, NWK>(a, pass ? a.Sq / (NWK * 32) - 1 - bx : bx, hh, b);
+  }
+}
+
+// ===================================================== d64 forward: two query slices per wave
+// attn_fwd_block at d 64 runs two 4-wave workgroups per CU, each wave one 32-row chain
+// (QK^T -> max -> exp -> PV) whose softmax VALU the matrix pipe waits on (PMC: 13.5 VALU per MFMA,
+// 18 % MFMA busy).  Here one workgroup per CU (4 waves, one per SIMD) takes 256 query rows and each
+// wave TWO independent 32-row slices, A = rows 32 w and B = rows 128 + 32 w of the block (interleaved
+// so the causal diagonal spreads over the waves).  Per K|V tile the two chains are offset by half a
+// tile, so one slice's softmax issues beside the other's MFMAs inside the same wave:
+//   segment 1:  PV_B(t - 1) MFMAs || row max of A(t)   |  S_B(t)     MFMAs || exp / sums of A(t)
+//   segment 2:  PV_A(t)     MFMAs || row max of B(t)   |  S_A(t + 1) MFMAs || exp / sums of B(t)
+// Q arrives by LDS-DMA with the first K|V tiles (no compiler-tracked load to drain the ring).  Every
+// row's arithmetic is attn_fwd_block's, op for op (score chain, lazy rescale, exponent fma, the eight
+// partial row sums, PV order), so O and LSE are bit-identical to it (tests/test_kernels_gpu.py).
+constexpr int FD_ROWS = 256;  // query rows per workgroup
+constexpr int FD_NS = 6;      // K|V ring stages (16 KiB each) + the 32 KiB Q image: 128 KiB of LDS
+
+// `younger` tiles of OPS pieces each may stay in flight
+template <int OPS, int MAXY>
+__device__ __forceinline__ void vm_wait_tiles(int younger) {
+  if constexpr (MAXY >= 4) { if (younger >= 4) { vm_wait<4 * OPS>(); return; } }
+  if constexpr (MAXY >= 3) { if (younger >= 3) { vm_wait<3 * OPS>(); return; } }
+  if constexpr (MAXY >= 2) { if (younger >= 2) { vm_wait<2 * OPS>(); return; } }
+  if constexpr (MAXY >= 1) { if (younger >= 1) { vm_wait<OPS>(); return; } }
+  vm_wait<0>();
+}
+
+// S^T = K Q^T of one slice against the 64 keys of a tile (key on the row, as attn_fwd_block); the
+// slice's Q operands are re-read from the block's resident Q image (32 VGPRs fewer per wave)
+__device__ __forceinline__ void fd_qk(const lds_u8* sk, const lds_u8* qi, int qrow0, f32x16_t (&s)[2], int lane) {
+  bf16x8_t qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) qf[ks] = rd_row<64>(qi, qrow0, ks, lane);
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh) {
+    bf16x8_t ka[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) ka[ks] = rd_row<64>(sk, 32 * kh, ks, lane);
+    s[kh] = zero16();
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) s[kh] = mfma(ka[ks], qf[ks], s[kh]);
+  }
+}
+
+// O^T += V^T P^T of one slice (P = the four bf16 B operands of fd_exp)
+__device__ __forceinline__ void fd_pv(const lds_u8* sv, const bf16x8_t (&p)[4], f32x16_t (&o)[2], int lane) {
+#pragma unroll
+  for (int st = 0; st < 4; ++st)
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) o[dt] = mfma(rd_tr<64>(sv, st, dt, lane), p[st], o[dt]);
+}
+
+// first half of a slice's softmax: diagonal mask, tile max, lazy rescale of (l, O)
+template <bool DIAG>
+__device__ __forceinline__ void fd_max(f32x16_t (&s)[2], int thr, float c2, float& m, float& l, f32x16_t (&o)[2]) {
+  if constexpr (DIAG) {
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (32 * kh + (r & 3) + 8 * (r >> 2) > thr) s[kh][r] = -INFINITY;
+  }
+  float mt = -INFINITY;
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[kh][r]);
+  mt = xor32_max(mt) * c2;
+  {   // branch-free lazy rescale (attn_fwd_block)
+    const float mn = __any(mt > m + kRescaleLog2) ? fmaxf(m, mt) : m;
+    const float alpha = __builtin_amdgcn_exp2f(m - mn);
+    m = mn;
+    l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+  }
+}
+
+// second half: P = exp2(S c2 - m) as bf16 B operands, row sum into l (attn_fwd_block's eight partials,
+// each fed in its order: k-steps st = 0..3 are (kh, r) = (0, 0-7), (0, 8-15), (1, 0-7), (1, 8-15))
+__device__ __forceinline__ void fd_exp(const f32x16_t (&s)[2], float c2, float m, float& l, bf16x8_t (&p)[4]) {
+  float lx[4], ly[4];   // each partial starts as its first term (= 0 + e: exp2 is never -0)
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    bf16x8_t v;
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const int r = 8 * (st & 1) + j;
+      const float e0 = __builtin_amdgcn_exp2f(fmaf(s[st >> 1][r], c2, -m));
+      const float e1 = __builtin_amdgcn_exp2f(fmaf(s[st >> 1][r + 1], c2, -m));
+      if (st == 0) { lx[r / 2] = e0; ly[r / 2] = e1; }
+      else { lx[(r / 2) & 3] += e0; ly[(r / 2) & 3] += e1; }
+      v[j] = (__bf16)e0;
+      v[j + 1] = (__bf16)e1;
+    }
+    p[st] = v;
+  }
+  l += ((lx[0] + lx[1]) + (lx[2] + lx[3])) + ((ly[0] + ly[1]) + (ly[2] + ly[3]));
+}
+
+// one 256-row query block; `nT` K|V tiles for the workgroup, nA / nB for the wave's slices
+__device__ __forceinline__ void attn_fwd_dual_block(const AttnArgs& a, int blk, int h, int b) {
+  constexpr int D = 64, TILE_B = KT * D * 2, NS = FD_NS, OPS = 2 * TILE_B / 1024 / NW;
+  constexpr int QOPS = FD_ROWS * D * 2 / 1024 / NW;   // Q image pieces per wave
+  static_assert(QOPS == 2 * OPS, "the prologue wait counts Q as two tiles");
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+  lds_u8* qimg = (lds_u8*)smem_raw;                 // [4][64 rows][64] swizzled, 32 KiB
+  lds_u8* ring = qimg + FD_ROWS * D * 2;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int hk = h / (a.H / a.HKV);
+  const int qA = blk * FD_ROWS + 32 * wave, qB = qA + 128;
+  const int nT = a.causal ? (blk + 1) * (FD_ROWS / KT) : a.Sk / KT;
+  const int nA = a.causal ? (qA + 95) / KT : nT, nB = a.causal ? (qB + 95) / KT : nT;
+  const float c2 = a.scale * kLog2e;
+  const uint16_t* kbase = a.k + b * a.k_sb + hk * a.k_sh;
+  const uint16_t* vbase = a.v + b * a.v_sb + hk * a.v_sh;
+  auto stage = [&](int kt, int buf) {
+    lds_u8* sk = ring + buf * 2 * TILE_B;
+    stage_rows<D, NW>(kbase + (int64_t)kt * KT * a.k_ss, a.k_ss, sk, wave, lane);
+    stage_rows<D, NW>(vbase + (int64_t)kt * KT * a.v_ss, a.v_ss, sk + TILE_B, wave, lane);
+  };
+  const uint16_t* qbase = a.q + b * a.q_sb + h * a.q_sh + (int64_t)blk * FD_ROWS * a.q_ss;
+#pragma unroll
+  for (int i = 0; i < FD_ROWS / KT; ++i)
+    stage_rows<D, NW>(qbase + (int64_t)i * KT * a.q_ss, a.q_ss, qimg + i * TILE_B, wave, lane);
+  const int pre = nT < NS - 1 ? nT : NS - 1;
+  for (int t = 0; t < pre; ++t) stage(t, t);
+  vm_wait_tiles<OPS, NS - 2>(pre - 1);   // Q and tile 0 landed
+  __syncthreads();
+
+  const lds_u8* qiA = qimg + (wave >> 1) * TILE_B;        // rows 32 w .. of the block: image w / 2
+  const lds_u8* qiB = qimg + (2 + (wave >> 1)) * TILE_B;  // rows 128 + 32 w ..: image 2 + w / 2
+  const int qr0 = 32 * (wave & 1);
+  f32x16_t oA[2] = {zero16(), zero16()}, oB[2] = {zero16(), zero16()};
+  float mA = -INFINITY, lA = 0.f, mB = -INFINITY, lB = 0.f;
+  f32x16_t sA[2], sB[2];
+  bf16x8_t pA[4], pB[4];
+  const int thrA = qA + (lane & 31) - 4 * (lane >> 5), thrB = thrA + 128;   // + kv0 offsets below
+  auto tile_at = [&](int t) -> lds_u8* { return ring + (t % NS) * 2 * TILE_B; };
+
+  // one iteration t, its parts fixed at compile time (each kind of iteration is its own straight-line
+  // code, run by its own loop or call: no runtime branch joins two versions of the accumulators)
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  auto iter = [&](auto pvb, auto qkb, auto sma, auto pva, auto qka, auto smb, int t) {
+    lds_u8* cur = tile_at(t);
+    const int kv0 = t * KT;
+    // ---- segment 1: PV_B(t - 1), S_B(t) || softmax A(t)   (sma: 0 none, 1 plain, 2 diagonal)
+    if constexpr (decltype(pvb)::value) fd_pv(tile_at(t - 1) + TILE_B, pB, oB, lane);
+    if constexpr (decltype(sma)::value) fd_max<decltype(sma)::value == 2>(sA, thrA - kv0, c2, mA, lA, oA);
+    if constexpr (decltype(qkb)::value) fd_qk(cur, qiB, qr0, sB, lane);
+    if constexpr (decltype(sma)::value) fd_exp(sA, c2, mA, lA, pA);
+    // ---- ring: tile t + 1 landed, everyone is past tile t - 1 -> refill its stage
+    if (t + 1 < nT) {
+      const int issued = t + NS - 2 < nT - 1 ? t + NS - 2 : nT - 1;
+      vm_wait_tiles<OPS, NS - 3>(issued - (t + 1));
+    }
+    __syncthreads();
+    if (t + NS - 1 < nT) stage(t + NS - 1, (t + NS - 1) % NS);
+    // ---- segment 2: PV_A(t), S_A(t + 1) || softmax B(t)
+    if constexpr (decltype(pva)::value) fd_pv(cur + TILE_B, pA, oA, lane);
+    if constexpr (decltype(smb)::value) fd_max<decltype(smb)::value == 2>(sB, thrB - kv0, c2, mB, lB, oB);
+    if constexpr (decltype(qka)::value) fd_qk(tile_at(t + 1), qiA, qr0, sA, lane);
+    if constexpr (decltype(smb)::value) fd_exp(sB, c2, mB, lB, pB);
+  };
+
+  fd_qk(tile_at(0), qiA, qr0, sA, lane);
+  if (a.causal) {
+    // nB = nA + 2 <= nT; A's last tile and B's last tile are the slices' diagonal tiles
+    if (nA == 1) iter(I0{}, I1{}, I2{}, I1{}, I0{}, I1{}, 0);
+    else iter(I0{}, I1{}, I1{}, I1{}, I1{}, I1{}, 0);
+    for (int t = 1; t < nA - 1; ++t) iter(I1{}, I1{}, I1{}, I1{}, I1{}, I1{}, t);   // steady state
+    if (nA >= 2) iter(I1{}, I1{}, I2{}, I1{}, I0{}, I1{}, nA - 1);
+    iter(I1{}, I1{}, I0{}, I0{}, I0{}, I1{}, nA);
+    iter(I1{}, I1{}, I0{}, I0{}, I0{}, I2{}, nA + 1);
+    for (int t = nB; t < nT; ++t) {   // PV_B(nB - 1), then only the ring
+      if (t == nB) iter(I1{}, I0{}, I0{}, I0{}, I0{}, I0{}, t);
+      else iter(I0{}, I0{}, I0{}, I0{}, I0{}, I0{}, t);
+    }
+  } else {
+    if (nT == 1) iter(I0{}, I1{}, I1{}, I1{}, I0{}, I1{}, 0);
+    else iter(I0{}, I1{}, I1{}, I1{}, I1{}, I1{}, 0);
+    for (int t = 1; t < nT - 1; ++t) iter(I1{}, I1{}, I1{}, I1{}, I1{}, I1{}, t);
+    if (nT >= 2) iter(I1{}, I1{}, I1{}, I1{}, I0{}, I1{}, nT - 1);
+  }
+  if (nB == nT) fd_pv(tile_at(nT - 1) + TILE_B, pB, oB, lane);
+
+  // ---- epilogue: normalise, bf16 O rows and the LSE (attn_fwd_block's non-merge store)
+  auto finish = [&](const f32x16_t (&o)[2], float m, float l, int q0) {
+    l = xor32_sum(l);
+    const float inv_l = 1.0f / l;
+    const int myq = q0 + (lane & 31);
+    uint16_t* orow = (uint16_t*)a.o + b * a.o_sb + (int64_t)myq * a.o_ss + h * a.o_sh;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) store_T_bf16(orow, dt, o[dt], inv_l, lane);
+    if (lane < 32) a.lse[((int64_t)b * a.H + h) * a.lse_ld + myq] = m * kLn2 + __logf(l);
+  };
+  finish(oA, mA, lA, qA);
+  finish(oB, mB, lB, qB);
+}
+
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1)))
+void attn_fwd_dual_kernel(AttnArgs a) {
+  int bx, hh, b;
+  attn_coords(a, bx, hh, b);
+  const int nq = a.Sq / FD_ROWS;
+  for (int pass = 0; pass <= a.pair; ++pass) {   // causal: the heavy block first (attn_fwd_block's order)
+    if (pass) __syncthreads();   // the first block's LDS reads are done before the next block's DMA
+    const int x = pass ? nq - 1 - bx : bx;
+    attn_fwd_dual_block(a, a.causal ? nq - 1 - x : x, hh, b);
   }
 }
 
@@ -669,15 +906,17 @@ __device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, i
     if (wave == 0) ((__attribute__((address_space(3))) float*)(smem + buf * STAGE_B + 2 * TILE_B))[lane] = lse_next * kLog2e;
   };
 
-  // one (query head, q tile) step
-  auto tile = [&](const lds_u8* sq, int qt) {
+  // one (query head, q tile) step; edge (the causal block's first NW * 32 / KT q tiles of a head: halves
+  // before my keys skipped, the diagonal one masked) and full steps are separate instantiations, run
+  // by separate loops below (as the forward's tile_loops)
+  auto tile = [&](auto edge, const lds_u8* sq, int qt) {
     const lds_u8* sdo = sq + TILE_B;
     const float* sl2 = (const float*)(sq + 2 * TILE_B);
     const float* sdel = sl2 + KT;
 #pragma unroll
     for (int qh = 0; qh < 2; ++qh) {
       const int qs = qt * KT + 32 * qh;
-      if (a.causal && qs + 31 < k0) continue;  // wave-uniform: all these queries precede my keys
+      if (decltype(edge)::value && a.causal && qs + 31 < k0) continue;  // wave-uniform: all these queries precede my keys
       // S = Q K^T and dP = dO V^T  (C layout: col = key = lane, row = query)
       f32x16_t s = zero16(), dp = zero16();
 #pragma unroll
@@ -685,7 +924,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, i
         s = mfma(rd_row<D>(sq, 32 * qh, ks, lane), kf[ks], s);
         dp = mfma(rd_row<D>(sdo, 32 * qh, ks, lane), vf[ks], dp);
       }
-      if (a.causal && (qs < k0 + 31)) {  // diagonal: query row crow(r) sees my key iff >= thr
+      if (decltype(edge)::value && a.causal && (qs < k0 + 31)) {  // diagonal: query row crow(r) sees my key iff >= thr
         const int thr = mykey - qs - 4 * (lane >> 5);
 #pragma unroll
         for (int r = 0; r < 16; ++r)
@@ -724,16 +963,23 @@ __device__ __forceinline__ void attn_bwd_dkdv_block(const AttnArgs& a, int bx, i
   if (n_iter > 0) put_lse(0);
   __syncthreads();
 
-  for (int it = 0; it < n_iter; ++it) {
+  auto step = [&](auto edge, int it) {
     const int buf = it & 1;
     if (++nxt_t == nq) { nxt_t = 0; ++nxt_h; }
     if (it + 1 < n_iter) stage(nxt_h, qt_begin + nxt_t, buf ^ 1);
     const lds_u8* sq = smem + buf * STAGE_B;
-    tile(sq, qt_begin + cur_t);
+    tile(edge, sq, qt_begin + cur_t);
     cur_h = nxt_h; cur_t = nxt_t;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (it + 1 < n_iter) put_lse(buf ^ 1);
     __syncthreads();
+  };
+  const int n_edge = a.causal ? NW * 32 / KT : 0;   // q tiles of a head that reach the diagonal
+  for (int it = 0; it < n_iter;) {   // per query head: its edge steps, then its full ones
+    const int h_end = min(n_iter, it + (nq - cur_t));   // this head's last step + 1
+    const int e_end = min(h_end, it + max(0, n_edge - cur_t));
+    for (; it < e_end; ++it) step(std::true_type{}, it);
+    for (; it < h_end; ++it) step(std::false_type{}, it);
   }
 
   if (item >= 0) {   // a split work item: dK (scaled) and dV partials (f32), summed by attn_split_reduce_kernel
@@ -1098,10 +1344,13 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
   }
   __syncthreads();
 
-  // one K/V tile
-  auto tile = [&](const lds_u8* sk, int kv0) {
+  // one K/V tile; the diagonal tile's mask is its own instantiation (dg 1), as in the forward, at d64;
+  // d128 keeps one body with the skip and the mask as runtime branches (dg 3: its 256-VGPR budget
+  // spilled the split loops)
+  auto tile = [&](auto dg, const lds_u8* sk, int kv0) {
     const lds_u8* sv = sk + TILE_B;
-    if (a.causal && kv0 > q0 + 31) return;  // wave-uniform: every key of the tile is after my queries
+    if constexpr (decltype(dg)::value == 3)
+      if (a.causal && kv0 > q0 + 31) return;  // wave-uniform: every key of the tile is after my queries
     // each 32-key half's dS feeds its two dQ k-steps right away: one dS tile live, not two
     // (16 VGPRs: d128's dQ kernel fits 2 waves per SIMD)
 #pragma unroll
@@ -1112,7 +1361,8 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
         s = mfma(rd_row<D>(sk, 32 * kh, ks, lane), qf[ks], s);
         dp = mfma(rd_row<D>(sv, 32 * kh, ks, lane), dof[ks], dp);
       }
-      if (a.causal && kv0 + KT - 1 > q0) {  // key row 32 kh + crow(r) visible iff <= thr
+      if (decltype(dg)::value == 1 || (decltype(dg)::value == 3 && a.causal && kv0 + KT - 1 > q0)) {
+        // key row 32 kh + crow(r) visible iff <= thr
         const int thr = myq - kv0 - 32 * kh - 4 * (lane >> 5);
 #pragma unroll
         for (int r = 0; r < 16; ++r)
@@ -1149,16 +1399,19 @@ __device__ __forceinline__ void attn_bwd_dq_block(const AttnArgs& a, int bx, int
     }
   };
 
-  for (int kt = 0, buf = 0, sbuf = pre % NS; kt < nkt; ++kt) {   // the forward's ring (ring_wait)
-    if (kt + NS - 1 < nkt) {
-      stage(kt + NS - 1, sbuf);
-      if (++sbuf == NS) sbuf = 0;
-    }
-    tile(smem + buf * 2 * TILE_B, (kt0 + kt) * KT);
-    if (++buf == NS) buf = 0;
+  int n_nd, n_c;   // the forward's ring (ring_wait) and loop split (tile_loops)
+  causal_split(a.causal, q0, kt0, nkt, n_nd, n_c);
+  auto step = [&](auto kind, int kt) {
+    if (kt + NS - 1 < nkt) stage(kt + NS - 1, (kt + NS - 1) % NS);
+    if constexpr (decltype(kind)::value != 2) tile(kind, smem + (kt % NS) * 2 * TILE_B, (kt0 + kt) * KT);
     const int issued = kt + NS - 1 < nkt ? kt + NS - 1 : nkt - 1;
     ring_wait<OPS, NS>(issued - (kt + 1));
     __syncthreads();
+  };
+  if constexpr (D == 64) {
+    tile_loops(n_nd, n_c, nkt, step);
+  } else {   // one loop: at d128 the three loops' extra copies of the body spilled (256-VGPR budget)
+    for (int kt = 0; kt < nkt; ++kt) step(std::integral_constant<int, 3>{}, kt);
   }
 
   if (item >= 0) {   // a split work item: its dQ partial (scaled, f32), summed by attn_split_reduce_kernel
@@ -1326,7 +1579,14 @@ int pt_attn_fwd(const void* q, const int64_t* q_str, const void* k, const int64_
   a.pair = causal && nqb % 2 == 0 && pair_enabled();
   const dim3 grid((unsigned)(a.pair ? nqb / 2 : nqb), (unsigned)H, (unsigned)B);
   const int stage_b = 2 * KT * (int)D * 2;
-  if (D == 64) {
+  if (D == 64 && !merge && Sq % FD_ROWS == 0 && pt_variant(PT_VAR_ATTN_FWD_DUAL) == 1) {
+    const int nq = (int)(Sq / FD_ROWS);
+    a.pair = causal && nq % 2 == 0 && pair_enabled();
+    const dim3 g((unsigned)(a.pair ? nq / 2 : nq), (unsigned)H, (unsigned)B);
+    const int smem = FD_ROWS * 64 * 2 + FD_NS * stage_b;
+    set_smem(attn_fwd_dual_kernel, smem);
+    attn_fwd_dual_kernel<<<g, NW * 64, smem, stream>>>(a);
+  } else if (D == 64) {
     const int smem = fwd_stages<64, NW>() * stage_b;
     set_smem(attn_fwd_kernel<64, NW>, smem);
     attn_fwd_kernel<64, NW><<<grid, NW * 64, smem, stream>>>(a);

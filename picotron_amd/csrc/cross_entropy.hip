@@ -319,14 +319,15 @@ __global__ __launch_bounds__(kThreads) void ce_bwd_stream_kernel(const uint16_t*
                                                                  const float* __restrict__ row_lse,
                                                                  uint16_t* __restrict__ dl, int64_t ds, int V,
                                                                  const float* __restrict__ scale_dev,
-                                                                 int64_t scale_stride, int64_t ignore_index) {
+                                                                 int64_t scale_stride, int64_t ignore_index,
+                                                                 int64_t vocab_lo) {
   const int64_t row = blockIdx.x;
   const uint16_t* x = logits + row * ls;
   uint16_t* d = dl + row * ds;
   const int nch = V >> 3;
-  const int64_t t = tgt[row];
+  const int64_t t = tgt[row] - vocab_lo;   // a vocab shard [vocab_lo, vocab_lo + V): its own columns
   const float nl2 = -row_lse[row] * kLog2e;   // exp(x - lse) = exp2(x log2e - lse log2e)
-  const float g = t != ignore_index ? scale_dev[row * scale_stride] : 0.f;
+  const float g = tgt[row] != ignore_index ? scale_dev[row * scale_stride] : 0.f;
   for (int c0 = threadIdx.x; c0 < nch; c0 += kThreads * kUnroll) {
     bf16x8 v[kUnroll];
 #pragma unroll
@@ -349,7 +350,111 @@ __global__ __launch_bounds__(kThreads) void ce_bwd_stream_kernel(const uint16_t*
   }
 }
 
+// ---- vocab-parallel cross-entropy (the lm_head as a ColumnParallelLinear over tp ranks, each holding
+// the logits of vocab columns [vocab_lo, vocab_lo + Vs)): instead of gathering the [rows, V] logits
+// (tp_communications.py:51-72, 7/8 of them crossing xGMI at tp 8) every rank reduces its shard to a
+// per-row float4 (m, s = sum exp(x - m), x[target] if the target is in the shard else 0, 1 / 0 flag),
+// the tp group all-gathers those 16 bytes per row, and every rank combines them in rank order.
+__global__ __launch_bounds__(kStatRows * kStatGroups) void ce_vp_partial_kernel(
+    const uint16_t* __restrict__ logits, int64_t ls, const int64_t* __restrict__ tgt,
+    const float2* __restrict__ stats, int nblk, float4* __restrict__ part_out, int64_t rows, int Vs,
+    int64_t vocab_lo) {
+  __shared__ float2 part[kStatGroups][kStatRows];
+  const int r = threadIdx.x % kStatRows, grp = threadIdx.x / kStatRows;
+  const int64_t row = (int64_t)blockIdx.x * kStatRows + r;
+  float m = -INFINITY, s = 0.f;
+  if (row < rows) {
+    for (int b = grp; b < nblk; b += kStatGroups) {   // ce_fwd_stats_kernel's merge
+      const float2 p = stats[(int64_t)b * rows + row];
+      const float nm = fmaxf(m, p.x);
+      s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (p.x == -INFINITY ? 0.f : p.y * __expf(p.x - nm));
+      m = nm;
+    }
+  }
+  part[grp][r] = make_float2(m, s);
+  __syncthreads();
+  if (grp == 0 && row < rows) {
+    for (int g = 1; g < kStatGroups; ++g) {
+      const float2 p = part[g][r];
+      const float nm = fmaxf(m, p.x);
+      s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (p.x == -INFINITY ? 0.f : p.y * __expf(p.x - nm));
+      m = nm;
+    }
+    const int64_t t = tgt[row] - vocab_lo;
+    const bool own = t >= 0 && t < Vs;
+    part_out[row] = make_float4(m, s, own ? bf2f(logits[row * ls + t]) : 0.f, own ? 1.f : 0.f);
+  }
+}
+
+// every rank's partials [tp][rows] -> row_lse, row_loss (lse - x[target]); the range check of
+// ce_fwd_stats_kernel against the global vocab (NaN row + PT_STATUS_BAD_TARGET)
+__global__ __launch_bounds__(256) void ce_vp_combine_kernel(const float4* __restrict__ parts, int tp,
+                                                            const int64_t* __restrict__ tgt, float* __restrict__ row_loss,
+                                                            float* __restrict__ row_lse, int64_t rows, int64_t V,
+                                                            int64_t ignore_index, int* __restrict__ status) {
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= rows) return;
+  float m = -INFINITY, s = 0.f, xt = 0.f;
+  for (int q = 0; q < tp; ++q) {
+    const float4 p = parts[(int64_t)q * rows + row];
+    const float nm = fmaxf(m, p.x);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (p.x == -INFINITY ? 0.f : p.y * __expf(p.x - nm));
+    m = nm;
+    xt += p.z;
+  }
+  const int64_t t = tgt[row];
+  const bool valid = t != ignore_index;
+  const bool bad = valid && (t < 0 || t >= V);
+  const float lse = bad ? __builtin_nanf("") : m + __logf(s);
+  row_lse[row] = lse;
+  row_loss[row] = valid ? lse - xt : 0.f;
+  if (bad && status) status[0] = PT_STATUS_BAD_TARGET;
+}
+
 }  // namespace
+
+extern "C" int pt_cross_entropy_vp_partial(const void* logits, int64_t logits_stride, const int64_t* targets,
+                                           const float* stats, int64_t nblk, float* part, int64_t rows,
+                                           int64_t vocab_shard, int64_t vocab_lo, hipStream_t stream) {
+  if (!logits || !targets || !stats || !part || rows <= 0 || vocab_shard <= 0 || nblk <= 0) return PT_EINVAL;
+  if (vocab_shard % nblk || !pt_aligned16(stats) || !pt_aligned16(part)) return PT_EINVAL;
+  if (rows > INT32_MAX || vocab_shard > INT32_MAX) return PT_EUNSUPPORTED;
+  const unsigned grid = (unsigned)((rows + kStatRows - 1) / kStatRows);
+  ce_vp_partial_kernel<<<grid, kStatRows * kStatGroups, 0, stream>>>((const uint16_t*)logits, logits_stride, targets,
+                                                                   (const float2*)stats, (int)nblk, (float4*)part,
+                                                                   rows, (int)vocab_shard, vocab_lo);
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
+
+extern "C" int pt_cross_entropy_vp_combine(const float* parts, int64_t tp, const int64_t* targets, float* row_loss,
+                                           float* row_lse, int64_t rows, int64_t vocab, int64_t ignore_index,
+                                           int* status, hipStream_t stream) {
+  if (!parts || !targets || !row_loss || !row_lse || rows <= 0 || vocab <= 0 || tp <= 0) return PT_EINVAL;
+  if (!pt_aligned16(parts)) return PT_EALIGN;
+  ce_vp_combine_kernel<<<(unsigned)((rows + 255) / 256), 256, 0, stream>>>((const float4*)parts, (int)tp, targets,
+                                                                          row_loss, row_lse, rows, vocab,
+                                                                          ignore_index, status);
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
+
+extern "C" int pt_cross_entropy_bwd_lse_shard(const void* logits, int64_t logits_stride, const int64_t* targets,
+                                              const float* row_lse, void* dlogits, int64_t dlogits_stride,
+                                              int64_t rows, int64_t vocab_shard, int64_t vocab_lo, const float* scale,
+                                              int64_t scale_stride, int64_t ignore_index, hipStream_t stream) {
+  if (!logits || !targets || !row_lse || !dlogits || !scale || rows <= 0 || vocab_shard <= 0) return PT_EINVAL;
+  if (scale_stride != 0 && scale_stride != 1) return PT_EINVAL;
+  if ((vocab_shard & 7) || (logits_stride & 7) || (dlogits_stride & 7)) return PT_EALIGN;
+  if (!pt_aligned16(logits) || !pt_aligned16(dlogits)) return PT_EALIGN;
+  if (rows > INT32_MAX || vocab_shard > INT32_MAX) return PT_EUNSUPPORTED;
+  ce_bwd_stream_kernel<<<(unsigned)rows, kThreads, 0, stream>>>((const uint16_t*)logits, logits_stride, targets,
+                                                               row_lse, (uint16_t*)dlogits, dlogits_stride,
+                                                               (int)vocab_shard, scale, scale_stride, ignore_index,
+                                                               vocab_lo);
+  PT_CHECK_LAUNCH();
+  return PT_OK;
+}
 
 extern "C" int pt_cross_entropy_fwd_lse(const void* logits, int64_t logits_stride, const int64_t* targets,
                                         float* row_loss, float* row_lse, int64_t rows, int64_t vocab,
@@ -374,7 +479,7 @@ extern "C" int pt_cross_entropy_bwd_lse(const void* logits, int64_t logits_strid
   if (rows > INT32_MAX || vocab > INT32_MAX) return PT_EUNSUPPORTED;
   ce_bwd_stream_kernel<<<(unsigned)rows, kThreads, 0, stream>>>((const uint16_t*)logits, logits_stride, targets,
                                                                row_lse, (uint16_t*)dlogits, dlogits_stride,
-                                                               (int)vocab, scale, scale_stride, ignore_index);
+                                                               (int)vocab, scale, scale_stride, ignore_index, 0);
   PT_CHECK_LAUNCH();
   return PT_OK;
 }

@@ -423,22 +423,28 @@ class LMHeadFunction(torch.autograd.Function):
     backward is LinearFunction's."""
 
     @staticmethod
-    def forward(ctx, x, weight):
+    def forward(ctx, x, weight, tp_reduce_bwd):
         x2 = _contig2d(x)
         y, stats = K.linear_ce_stats(x2, weight)
         _stash_ce_stats(y, stats)
         ctx.save_for_backward(x2, weight)
-        ctx.xshape = x.shape
+        ctx.xshape, ctx.tp_reduce_bwd = x.shape, tp_reduce_bwd
         return y.view(*x.shape[:-1], weight.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
         x2, weight = ctx.saved_tensors
         dy2 = _contig2d(dy)
-        dx = K.linear_dgrad(dy2, [weight]) if ctx.needs_input_grad[0] else None
+        dx = handle = None
+        if ctx.needs_input_grad[0]:
+            dx = K.linear_dgrad(dy2, [weight])
+            if ctx.tp_reduce_bwd:   # a vocab shard (ColumnParallelLinear): sum dX over tp beside the dW GEMM
+                handle = TPContext.current().all_reduce(dx, async_op=True)
         if ctx.needs_input_grad[1]:
             wgrad(dy2, x2, [weight])
-        return (dx.view(ctx.xshape) if dx is not None else None), None
+        if handle is not None:
+            handle.wait()
+        return (dx.view(ctx.xshape) if dx is not None else None), None, None
 
 
 def lm_head_linear(x, weight):
@@ -446,8 +452,120 @@ def lm_head_linear(x, weight):
     T = x.numel() // x.shape[-1]
     if (ce_stats_enabled() and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
             and K.ce_stats_fusable(T, weight.shape[0]) and x.shape[-1] % 64 == 0):
-        return LMHeadFunction.apply(x, weight)
+        return LMHeadFunction.apply(x, weight, False)
     return linear(x, weight)
+
+
+# ------------------------------------------------------------------------ vocab-parallel CE
+# The reference's apply_tensor_parallel makes the lm_head ColumnParallelLinear(gather_output=True)
+# (tensor_parallel.py:50): every rank all-gathers the [T, V] logits (tp_communications.py:51-72; at
+# tp 8 and T 4096, 336 MiB into every rank per micro-batch) for F.cross_entropy (train.py:49).  Here
+# that layer returns a stand-in of the gathered logits (same shape and dtype, no storage) carrying
+# the vocab shards: F.cross_entropy on it -- or on its view(-1, V) / transpose(1, 2), the
+# reference's two call sites -- reduces each shard to 16 bytes per row with the lm_head GEMM's
+# statistics, all-gathers those, and differentiates the shard only (VocabParallelCEFunction); any
+# other use gathers the logits exactly as the reference does, once, and runs on them.
+def vp_ce_shape_ok(T, vocab_shard, K_in):
+    return SW.vp_ce != 0 and K.ce_stats_fusable(T, vocab_shard) and K_in % 64 == 0
+
+
+def lm_head_shard(x, weight):
+    """The vocab shard's logits (ColumnParallelLinear's GEMM, dX summed over tp in its backward) and
+    their per-tile CE statistics."""
+    y = LMHeadFunction.apply(x, weight, True)
+    return y, _take_ce_stats(_contig2d(y))
+
+
+class _VPInfo:
+    def __init__(self, shard, stats, vocab_lo, vocab, materialize):
+        self.shard, self.stats, self.vocab_lo, self.vocab = shard, stats, vocab_lo, vocab
+        self.materialize, self.full = materialize, None
+
+    def gathered(self):
+        if self.full is None:
+            self.full = self.materialize()
+        return self.full
+
+
+def vp_logits(shard, stats, vocab_lo, vocab, materialize):
+    """The stand-in for the gathered [..., vocab] logits of the vocab shard `shard` [..., Vs]
+    (columns vocab_lo ..); `materialize()` gathers the real logits (GatherFromModelParallelRegion)."""
+    ph = torch.empty((), dtype=shard.dtype, device=shard.device).expand(*shard.shape[:-1], vocab)
+    out = ph.as_subclass(HipLogits)
+    out._pt_vp, out._pt_vp_path = _VPInfo(shard, stats, vocab_lo, vocab, materialize), ()
+    return out
+
+
+def _vp_real(t):
+    """A vocab-parallel stand-in (or a view of one) as the real gathered logits (same view)."""
+    real = t._pt_vp.gathered()
+    with torch._C.DisableTorchFunctionSubclass():
+        for f, a, kw in t._pt_vp_path:
+            real = f(real, *a, **kw)
+    return real.as_subclass(HipLogits)
+
+
+def _is_vp(t):
+    return isinstance(t, HipLogits) and getattr(t, "_pt_vp", None) is not None
+
+
+# metadata reads that are safe on the stand-in (no data)
+_VP_META = frozenset([torch.Tensor.dim, torch.Tensor.size, torch.Tensor.numel, torch.Tensor.__len__])
+
+
+class VocabParallelCEFunction(torch.autograd.Function):
+    """F.cross_entropy(gathered logits, targets) from the vocab shards: per-row (max, sum-exp,
+    target logit) of this rank's shard (pt_cross_entropy_vp_partial, from the lm_head GEMM's
+    statistics), all-gathered over tp (16 B per row), combined in rank order
+    (pt_cross_entropy_vp_combine) -- the same loss on every rank.  Backward: the shard's
+    (exp(x - lse) - onehot) * scale, the columns of the gathered logits' gradient this rank's
+    GatherFromModelParallelRegion backward (tp_communications.py:69-72) would keep."""
+
+    @staticmethod
+    def forward(ctx, shard, targets, stats, vocab_lo, vocab, ignore_index, reduction):
+        lg = _contig2d(shard)
+        tg = targets.reshape(-1)
+        tp = TPContext.current()
+        part = K.cross_entropy_vp_partial(lg, tg, stats, vocab_lo)
+        parts = tp.all_gather_rows(part).view(tp.world_size, lg.shape[0], 4)
+        odt = shard.dtype if shard.dtype in (torch.bfloat16, torch.float32) else torch.float32
+        loss, inv_count, row_lse = K.cross_entropy_vp_combine(parts, tg, vocab, ignore_index, out_dtype=odt,
+                                                              reduction=reduction)
+        ctx.save_for_backward(lg, tg, row_lse, *([inv_count] if inv_count is not None else []))
+        ctx.vocab_lo, ctx.ignore_index, ctx.shape, ctx.reduction = vocab_lo, ignore_index, shard.shape, reduction
+        return loss if loss.dtype == shard.dtype else loss.to(shard.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        lg, tg, row_lse, *inv = ctx.saved_tensors
+        if ctx.reduction == "none":
+            scale = g.float().reshape(-1).contiguous()
+        elif ctx.reduction == "sum":
+            scale = g.float().reshape(1)
+        else:
+            scale = g.float().reshape(1) * inv[0]
+        dl = K.cross_entropy_grad_lse_shard(lg, tg, row_lse, scale, ctx.vocab_lo, ctx.ignore_index)
+        return dl.view(ctx.shape), None, None, None, None, None, None
+
+
+def _vp_cross_entropy(input, target, reduction, ignore_index):
+    """cross_entropy on a stand-in in one of the reference's two forms -- [N, V] rows (train.py:49)
+    or [B, V, S] = transpose(1, 2) of [B, S, V] (pipeline_parallel.py:103,153) -- else None."""
+    info = input._pt_vp
+    shard, V = info.shard, info.vocab
+    lead = tuple(shard.shape[:-1])
+    rows = shard.numel() // shard.shape[-1]
+    target = _plain(target)
+    if input.dim() == 2 and tuple(input.shape) == (rows, V) and target.dim() == 1 and target.numel() == rows:
+        out_shape = (rows,)
+    elif input.dim() == 3 and len(lead) == 2 and tuple(input.shape) == (lead[0], V, lead[1]) and \
+            tuple(target.shape) == lead:
+        out_shape = lead
+    else:
+        return None
+    out = VocabParallelCEFunction.apply(shard, target.reshape(-1), info.stats, info.vocab_lo, V, ignore_index,
+                                        reduction)
+    return out.view(out_shape) if reduction == "none" else out
 
 
 # ------------------------------------------------------------------------ attention block
@@ -829,6 +947,8 @@ class CrossEntropyFunction(torch.autograd.Function):
 
 
 def _plain(t):
+    if isinstance(t, HipLogits) and getattr(t, "_pt_vp", None) is not None:
+        t = _vp_real(t)   # a vocab-parallel stand-in has no data of its own: the gathered logits
     return t.as_subclass(torch.Tensor) if isinstance(t, (HipLogits, HipHidden)) else t
 
 
@@ -848,6 +968,19 @@ class HipLogits(torch.Tensor):
         kwargs = kwargs or {}
         if func is torch.nn.functional.cross_entropy:
             return _dispatch_cross_entropy(*args, **kwargs)
+        if args and _is_vp(args[0]) and (func in cls._KEEP or func in _VP_META or
+                                         getattr(func, "__name__", "") == "__get__"):
+            # a view of the vocab-parallel stand-in stays one (its path replayed on a gather, if ever);
+            # shape / dtype / device reads need no data
+            out = super().__torch_function__(func, types, args, kwargs)
+            if func in cls._KEEP and isinstance(out, HipLogits):
+                out._pt_vp = args[0]._pt_vp
+                out._pt_vp_path = args[0]._pt_vp_path + ((func, tuple(args[1:]), dict(kwargs)),)
+            return out
+        if any(_is_vp(a) for a in args) or any(_is_vp(v) for v in kwargs.values()):
+            args = tuple(_vp_real(a) if _is_vp(a) else a for a in args)
+            kwargs = {k: (_vp_real(v) if _is_vp(v) else v) for k, v in kwargs.items()}
+            return HipLogits.__torch_function__(func, types, args, kwargs)
         if func in cls._KEEP:
             return super().__torch_function__(func, types, args, kwargs)
         with torch._C.DisableTorchFunctionSubclass():
@@ -889,16 +1022,24 @@ def _dispatch_cross_entropy(input, target, weight=None, size_average=None, ignor
             reduction not in ("mean", "sum", "none"):
         # not on picotron's path (train.py:49 / pipeline_parallel.py:103,153 call the plain form): class
         # weights, label smoothing and the legacy reduction flags are torch's own op on the same tensors
+        if _is_vp(input):
+            input = _vp_real(input)
         return torch.nn.functional.cross_entropy(_plain(input), _plain(target), weight=weight,
                                                  size_average=size_average, ignore_index=ignore_index,
                                                  reduce=reduce, reduction=reduction,
                                                  label_smoothing=label_smoothing)
+    if _is_vp(input):   # the TP lm_head's stand-in (vp_logits)
+        out = _vp_cross_entropy(input, target, reduction, ignore_index)
+        if out is not None:
+            return out
     return cross_entropy(_plain(input), _plain(target), reduction=reduction, ignore_index=ignore_index)
 
 
 def as_logits(t):
-    """Tag an lm_head output so F.cross_entropy on it (or on its views) takes the HIP kernel."""
-    return t.as_subclass(HipLogits)
+    """Tag an lm_head output so F.cross_entropy on it (or on its views) takes the HIP kernel.
+    (Tensor.as_subclass is not dispatched to __torch_function__: a HipLogits -- a vocab-parallel
+    stand-in among them -- is returned as it is.)"""
+    return t if isinstance(t, HipLogits) else t.as_subclass(HipLogits)
 
 
 def cross_entropy(input, target, reduction="mean", ignore_index=-100):
@@ -912,6 +1053,11 @@ def cross_entropy(input, target, reduction="mean", ignore_index=-100):
     (per-row losses shaped like target, 0 at ignored rows) follow torch."""
     if reduction not in ("mean", "sum", "none"):
         raise ValueError(f"cross_entropy: reduction must be 'mean', 'sum' or 'none', got {reduction!r}")
+    if _is_vp(input):   # the TP lm_head's stand-in: on the vocab shards, else on the gathered logits
+        out = _vp_cross_entropy(input, target, reduction, ignore_index)
+        if out is not None:
+            return out
+        input = _vp_real(input)
     input, target = _plain(input), _plain(target)
     if input.dim() == 3:
         B, V, S = input.shape

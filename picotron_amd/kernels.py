@@ -903,6 +903,61 @@ def cross_entropy_loss_lse_stats(logits, targets, stats, ignore_index=-100, out_
     return loss, inv_count, row_lse
 
 
+def cross_entropy_vp_partial(logits_shard, targets, stats, vocab_lo):
+    """One tp rank's share of the vocab-parallel CE: per row float4 (max, sum exp(x - max), x[target]
+    or 0, 1 or 0: the target in this shard) of the shard logits [rows, Vs] (columns vocab_lo ..), from
+    the lm_head GEMM's statistics (linear_ce_stats) -- the logits are read at x[target] only."""
+    _bf16_rowmajor(logits_shard, "logits")
+    rows, vs = logits_shard.shape
+    _req(targets.dtype == torch.int64 and targets.numel() == rows, "targets: int64 [rows]")
+    _req(stats.dtype == torch.float32 and stats.is_contiguous() and stats.dim() == 3 and stats.shape[1:] == (rows, 2)
+         and vs % stats.shape[0] == 0, "stats: f32 [nblk, rows, 2]")
+    targets = targets.contiguous()
+    part = torch.empty(rows, 4, dtype=torch.float32, device=logits_shard.device)
+    rc = _C.lib().pt_cross_entropy_vp_partial(_ptr(logits_shard), logits_shard.stride(0), _ptr(targets), _ptr(stats),
+                                              stats.shape[0], _ptr(part), rows, vs, int(vocab_lo),
+                                              _C.stream_ptr(logits_shard.device))
+    _C.check(rc, "pt_cross_entropy_vp_partial")
+    return part
+
+
+def cross_entropy_vp_combine(parts, targets, vocab, ignore_index=-100, out_dtype=torch.float32, reduction="mean"):
+    """Every tp rank's partials [tp, rows, 4] (rank order) -> (loss, inv_count, row_lse) as
+    cross_entropy_loss_lse_stats returns them for the whole [rows, vocab] logits."""
+    _req(parts.dtype == torch.float32 and parts.is_contiguous() and parts.dim() == 3 and parts.shape[2] == 4,
+         "parts: f32 [tp, rows, 4]")
+    tp, rows = parts.shape[0], parts.shape[1]
+    _req(targets.dtype == torch.int64 and targets.numel() == rows, "targets: int64 [rows]")
+    targets = targets.contiguous()
+    row_loss = torch.empty(rows, dtype=torch.float32, device=parts.device)
+    row_lse = torch.empty(rows, dtype=torch.float32, device=parts.device)
+    rc = _C.lib().pt_cross_entropy_vp_combine(_ptr(parts), tp, _ptr(targets), _ptr(row_loss), _ptr(row_lse), rows,
+                                              int(vocab), int(ignore_index), _ptr(status_word(parts.device)),
+                                              _C.stream_ptr(parts.device))
+    _C.check(rc, "pt_cross_entropy_vp_combine")
+    _status_posted(parts.device)
+    loss, inv_count = _ce_reduce(row_loss, targets, ignore_index, out_dtype, reduction)
+    return loss, inv_count, row_lse
+
+
+def cross_entropy_grad_lse_shard(logits_shard, targets, row_lse, scale_dev, vocab_lo, ignore_index=-100):
+    """cross_entropy_grad_lse on a vocab shard (columns vocab_lo ..): the one-hot only where the
+    target falls in the shard; row_lse is the whole vocabulary's."""
+    _bf16_rowmajor(logits_shard, "logits")
+    rows, vs = logits_shard.shape
+    targets = targets.contiguous()
+    _req(scale_dev.dtype == torch.float32 and scale_dev.numel() in (1, rows), "scale: f32 device scalar or [rows]")
+    _req(row_lse.dtype == torch.float32 and row_lse.is_contiguous() and row_lse.numel() == rows, "row_lse: f32 [rows]")
+    scale_dev = scale_dev.contiguous()
+    dl = torch.empty(rows, vs, dtype=BF16, device=logits_shard.device)
+    rc = _C.lib().pt_cross_entropy_bwd_lse_shard(_ptr(logits_shard), logits_shard.stride(0), _ptr(targets),
+                                                 _ptr(row_lse), _ptr(dl), dl.stride(0), rows, vs, int(vocab_lo),
+                                                 _ptr(scale_dev), int(scale_dev.numel() != 1), int(ignore_index),
+                                                 _C.stream_ptr(logits_shard.device))
+    _C.check(rc, "pt_cross_entropy_bwd_lse_shard")
+    return dl
+
+
 def swiglu_fusable(T, I, backward=False):
     """Shapes the SwiGLU-fused projections tile (8-phase kernel: T % 256, I % 128 (fwd) / 256 (bwd))."""
     return T % 256 == 0 and I % (256 if backward else 128) == 0

@@ -5,12 +5,13 @@ split-K vs one pass, one launch vs two); the defaults are the production path, a
 hot path reads the environment again.  `PICOTRON_<NAME>` (upper case) sets a switch for a whole
 process (an A/B run); tests and tools change one for a block with `override(name=value)`.
 
-The four native switches (attention causal pairing and dK/dV kernel form, GEMM tile-row grouping,
-the mixed-tile q|k|v launch) live in the library; `apply_native` pushes them through
+The native switches (attention causal pairing, dK/dV kernel form, few-head split chunk and two-slice
+d64 forward; GEMM tile-row grouping, mixed-tile q|k|v launch, K-halves tile) live in the library; `apply_native` pushes them through
 `pt_set_variant` when the library is loaded, and `override` pushes a changed one at once.
 """
 import contextlib
 import os
+import sys
 
 DEFAULTS = {
     # functional.py: the fused epilogues (RoPE in the q|k|v GEMM and attention backward, SwiGLU in the
@@ -28,10 +29,12 @@ DEFAULTS = {
     "ring_zigzag": 1, "zigzag_residual": 1, "ring_mesh": 1,
     # tensor_parallel/sequence_parallel.py: the residual stream sharded by token rows over the tp group
     "tp_sp": 1,
+    # functional.py: the TP lm_head's F.cross_entropy on the vocab shards (no logits all-gather)
+    "vp_ce": 1,
     # native (libpicotron_hip.so, pt_set_variant)
-    "attn_pair": 1, "attn_split": 2, "gemm_group_m": -1, "gemm_mix": 1, "gemm_kh": 2, "attn_kv_chunk": 4,
+    "attn_pair": 1, "attn_split": 2, "gemm_group_m": -1, "gemm_mix": 1, "gemm_kh": 2, "attn_kv_chunk": 4, "attn_fwd_dual": 0,
 }
-NATIVE = ("attn_pair", "attn_split", "gemm_group_m", "gemm_mix", "gemm_kh", "attn_kv_chunk")
+NATIVE = ("attn_pair", "attn_split", "gemm_group_m", "gemm_mix", "gemm_kh", "attn_kv_chunk", "attn_fwd_dual")
 
 
 class _Switches:
@@ -52,6 +55,12 @@ def apply_native(lib):
     for k in NATIVE:
         rc = lib.pt_set_variant(k.encode(), int(getattr(S, k)))
         if rc != 0:
+            # an older build (whole-step A/B of library builds) without this variant runs the form
+            # its default names; any other value is an error
+            if lib.pt_get_variant(k.encode()) < 0 and getattr(S, k) == DEFAULTS[k]:
+                print(f"[picotron_amd] library has no variant {k!r}; its default ({DEFAULTS[k]}) form assumed",
+                      file=sys.stderr)
+                continue
             raise RuntimeError(f"pt_set_variant({k!r}, {getattr(S, k)}) failed: {rc}")
 
 

@@ -89,6 +89,16 @@ class ColumnParallelLinear(torch.nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x = FN._plain(x)
+        if (self.gather_output and getattr(self, "_pt_lm_head", False) and self.tp_world_size > 1
+                and self.bias is None and x.dtype == torch.bfloat16 and self.weight.dtype == torch.bfloat16
+                and FN.vp_ce_shape_ok(x.numel() // x.shape[-1], self.output_size_per_partition, x.shape[-1])):
+            # the lm_head: F.cross_entropy on the vocab shards, the logits gathered only if something
+            # else reads them (functional.vp_logits)
+            y, stats = FN.lm_head_shard(x, self.weight)
+            if stats is not None:
+                return FN.vp_logits(y, stats, self.tp_rank * self.output_size_per_partition, self.out_features,
+                                    lambda: GatherFromModelParallelRegion.apply(y))
+            return FN.as_logits(GatherFromModelParallelRegion.apply(y))
         if self.async_all_reduce:
             output = linear_with_async_all_reduce(x, self.weight, self.bias)
         else:

@@ -127,6 +127,10 @@ def _llama_body(rank, world, tp, cp, seq, zigzag, residual, cfg_over=None):
         CP.zigzag_exchange = orig
         FN.TPContext.all_gather_rows = orig_ag
     L, H = CFG["num_hidden_layers"], dict(CFG, **(cfg_over or {}))["hidden_size"]
+    # the vocab-parallel CE (functional.VocabParallelCEFunction): one gather of 16 B per row at tp > 1
+    vp = [g for g in gathers if g == (2 * s, 4)]
+    assert len(vp) == (1 if tp > 1 else 0), gathers
+    gathers = [g for g in gathers if g != (2 * s, 4)]
     if sp_on:   # per layer 2 gathers each way, plus the exit (forward) / the entry (backward)
         assert n_ag_fwd == 2 * L + 1 and len(gathers) == 4 * L + 2, gathers
         assert all(g == (2 * s // tp, H) for g in gathers), gathers   # every gather is of T / tp rows
@@ -418,3 +422,56 @@ def _dp_overlap(rank, world):
 
 def test_dp_bucket_allreduce_overlaps_last_backward():
     _dist.run(_dp_overlap, 2, device="cuda")
+
+
+def _vp_ce(rank, world):
+    """The TP lm_head's F.cross_entropy on the vocab shards (functional.VocabParallelCEFunction, no
+    logits all-gather) against the reference's gathered logits (vp_ce = 0) and the fp32 loss: the
+    reference's two call forms, reductions, ignore_index rows, and a stand-in read by another op."""
+    from picotron_amd import functional as FN
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd import switches
+    from picotron_amd.tensor_parallel.tensor_parallel import ColumnParallelLinear
+    torch.cuda.set_device(0)
+    m = pgm.setup_process_group_manager(tp_size=world, cp_size=1, pp_size=1, dp_size=1)
+    B, S, H, V = 2, 256, 128, 1024
+    g = torch.Generator().manual_seed(5)
+    w_full = (torch.randn(V, H, generator=g) * 0.05).to(torch.bfloat16)
+    x_full = torch.randn(B, S, H, generator=g).to(torch.bfloat16)
+    tgt = torch.randint(0, V, (B, S), generator=g)
+    tgt[0, :7] = -100                                   # ignore_index rows
+    lin = ColumnParallelLinear(H, V, bias=False, gather_output=True).cuda().to(torch.bfloat16)
+    lin._pt_lm_head = True
+    with torch.no_grad():
+        lin.weight.copy_(w_full.narrow(0, m.tp_rank * (V // world), V // world))
+    ref_loss = F.cross_entropy(x_full.float().reshape(-1, H) @ w_full.float().t(), tgt.reshape(-1))
+    res = {}
+    for vp in (1, 0):
+        for form in ("rows", "bvs"):
+            for red in ("mean", "sum", "none"):
+                with switches.override(vp_ce=vp):
+                    x = x_full.cuda().requires_grad_(True)
+                    lin.weight.grad = None
+                    logits = lin(x)
+                    assert FN._is_vp(logits) == bool(vp) and logits.shape == (B, S, V)
+                    if form == "rows":
+                        loss = F.cross_entropy(logits.view(-1, V), tgt.reshape(-1).cuda(), reduction=red)
+                    else:
+                        loss = F.cross_entropy(logits.transpose(1, 2), tgt.cuda(), reduction=red)
+                    (loss.float().sum() if red == "none" else loss.float()).backward()
+                    torch.cuda.synchronize()
+                    res[(vp, form, red)] = (loss.detach().float().cpu(), x.grad.float().cpu(),
+                                            lin.weight.grad.float().cpu())
+    for key, (l1, gx1, gw1) in res.items():
+        l0, gx0, gw0 = res[(0,) + key[1:]]
+        assert _rel(l1, l0) < 1e-2 and _rel(gx1, gx0) < 1e-2 and _rel(gw1, gw0) < 1e-2, key
+    assert abs(res[(1, "rows", "mean")][0].item() - ref_loss.item()) < TOL * abs(ref_loss.item())
+    # another op on the stand-in gathers the logits (as GatherFromModelParallelRegion) and runs on them
+    with switches.override(vp_ce=1):
+        logits = lin(x_full.cuda())
+        full = (x_full.float().reshape(-1, H) @ w_full.float().t()).view(B, S, V)
+        assert _rel(logits.float(), full) < 1e-2 and _rel(logits.view(-1, V)[3], full.view(-1, V)[3]) < 1e-2
+
+
+def test_vocab_parallel_cross_entropy_tp2():
+    _dist.run(_vp_ce, 2, device="cuda")
