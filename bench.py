@@ -155,6 +155,19 @@ def tp_proxy(args, base, layers):
         def backward(ctx, g):
             return g[:, :g.shape[1] // tp]
 
+    class _RowGatherStandIn(torch.autograd.Function):
+        """sequence_parallel.GatherFromSequenceRegion (the exit all-gather) as one rank sees it:
+        forward a [T, H] buffer (the no-op collective's, filled once), backward this rank's rows of
+        the gradient -- the autograd edge back into the layers must stay."""
+
+        @staticmethod
+        def forward(ctx, x):
+            return _TPNoComm(None, tp, 0).all_gather_rows(x).clone()
+
+        @staticmethod
+        def backward(ctx, g):
+            return g[:g.shape[0] // tp]
+
     from picotron_amd.switches import S as SW
     sp = tp > 1 and SW.tp_sp != 0 and args.seq % tp == 0   # sequence parallelism (sequence_parallel.py)
     vp = tp > 1 and FN.vp_ce_shape_ok(T, V // tp, H)          # the lm_head's vocab-parallel CE
@@ -166,7 +179,7 @@ def tp_proxy(args, base, layers):
         for w in stack:
             x = FN.DecoderLayerFunction.apply(x, *w, cos, sin, cfg.rms_norm_eps, 0, nh, nkv, d, False, sp)
         if sp:   # the exit hook's all-gather before the final norm
-            x = _TPNoComm(None, tp, 0).all_gather_rows(x.reshape(T // tp, H))
+            x = _RowGatherStandIn.apply(x.reshape(T // tp, H))
         if vp:   # the vocab-parallel CE (functional.VocabParallelCEFunction): no logits gather
             lg, stats = FN.lm_head_shard(x.view(T, H), head)
             full = FN.vp_logits(lg, stats, 0, V, lambda: _GatherStandIn.apply(lg))
@@ -201,6 +214,8 @@ def tp_proxy(args, base, layers):
         for _ in range(args.warmup + 1):
             micro_batch()
         torch.cuda.synchronize()
+        # the backward reached every layer's weights (a stand-in off the autograd graph would cut it)
+        assert all(p.grad is not None for w in stack for p in w) and emb.grad is not None, "proxy backward incomplete"
         t = _events_time(micro_batch, args.steps)
         with probe:
             micro_batch()

@@ -364,11 +364,14 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler: its own fragment loads are done
   __syncthreads();
 
-  // one K/V tile (a lambda, not a loop body: the causal skip is an early return).  The diagonal
-  // tile's mask is a separate instantiation (dg): as a runtime branch the compiler if-converted it,
-  // 60 compares / selects on every tile
+  // one K/V tile.  d64: the diagonal tile's mask is a separate instantiation (dg 1), run by its own
+  // loop (tile_loops) -- as a runtime branch the compiler if-converted it (60 compares / selects on
+  // every tile) and the join copied the accumulators; d128 keeps one body with the skip and the mask
+  // as runtime branches (dg 3: its split loops measured 5 % slower)
   auto tile = [&](auto dg, const lds_u8* sk, int kv0) {
     const lds_u8* sv = sk + TILE_B;
+    if constexpr (decltype(dg)::value == 3)
+      if (a.causal && kv0 > q0 + 31) return;  // wave-uniform: skip tiles fully above the diagonal
     {
       f32x16_t s[2];
       // the tile's K operands in one batch of LDS reads ahead of the MFMAs (left to itself the
@@ -386,7 +389,7 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
         for (int ks = 0; ks < KS; ++ks) s[kh] = mfma(ka[kh][ks], qf[ks], s[kh]);
       }
       // causal mask, diagonal tiles only: key row 32 kh + crow(r) visible iff <= thr
-      if constexpr (decltype(dg)::value == 1) {
+      if (decltype(dg)::value == 1 || (decltype(dg)::value == 3 && a.causal && kv0 + KT - 1 > q0)) {
         const int thr = myq - kv0 - 4 * (lane >> 5);
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh)
@@ -402,9 +405,11 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
       mt = xor32_max(mt) * c2;  // log2 units (c2 > 0)
       // lazy rescale (FA-style deferred max): only when some query's max grew by > 2^8; P may then
       // exceed 1 by at most 2^8, harmless in f32 accumulation and in bf16 (relative precision)
-      // branch-free: alpha = exp2(0) = 1 exactly when no row grew, and x * 1 = x, so the result is
-      // the lazy form's; as a branch the two paths' copies of O cost 16 v_mov_b64 per tile
-      {
+      // d64 branch-free: alpha = exp2(0) = 1 exactly when no row grew, and x * 1 = x, so the result
+      // is the lazy form's; as a branch the two paths' copies of O cost 16 v_mov_b64 per tile.  d128
+      // (64 O registers, 8-wave workgroups) keeps the branch: its unconditional multiply measured 6 %
+      // slower
+      if (D == 64 || __any(mt > m + kRescaleLog2)) {
         const float mn = __any(mt > m + kRescaleLog2) ? fmaxf(m, mt) : m;
         const float alpha = __builtin_amdgcn_exp2f(m - mn);
         m = mn;
@@ -453,14 +458,16 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
 
   int n_nd, n_c;
   causal_split(a.causal, q0, kt0, nkt, n_nd, n_c);
-  tile_loops(n_nd, n_c, nkt, [&](auto kind, int kt) {
+  auto step = [&](auto kind, int kt) {
     if (kt + NS - 1 < nkt)  // into the stage tile kt - 1 used (every wave passed its barrier)
       stage(kt + NS - 1, (kt + NS - 1) % NS);
     if constexpr (decltype(kind)::value != 2) tile(kind, smem + (kt % NS) * 2 * TILE_B, (kt0 + kt) * KT);
     const int issued = kt + NS - 1 < nkt ? kt + NS - 1 : nkt - 1;   // the last tile issued so far
     ring_wait<OPS, NS>(issued - (kt + 1));
     __syncthreads();
-  });
+  };
+  if constexpr (D == 64) tile_loops(n_nd, n_c, nkt, step);
+  else for (int kt = 0; kt < nkt; ++kt) step(std::integral_constant<int, 3>{}, kt);
 
   l = xor32_sum(l);
   if (item >= 0) {
@@ -519,220 +526,6 @@ __global__ __launch_bounds__(NWK * 64) void attn_fwd_kernel(AttnArgs a) {
   for (int pass = 0; pass <= a.pair; ++pass) {  // one inlined body: no register growth
     if (pass) __syncthreads();
     attn_fwd_block<D, NWK>(a, pass ? a.Sq / (NWK * 32) - 1 - bx : bx, hh, b);
-  }
-}
-
-// ===================================================== d64 forward: two query slices per wave
-// attn_fwd_block at d 64 runs two 4-wave workgroups per CU, each wave one 32-row chain
-// (QK^T -> max -> exp -> PV) whose softmax VALU the matrix pipe waits on (PMC: 13.5 VALU per MFMA,
-// 18 % MFMA busy).  Here one workgroup per CU (4 waves, one per SIMD) takes 256 query rows and each
-// wave TWO independent 32-row slices, A = rows 32 w and B = rows 128 + 32 w of the block (interleaved
-// so the causal diagonal spreads over the waves).  Per K|V tile the two chains are offset by half a
-// tile, so one slice's softmax issues beside the other's MFMAs inside the same wave:
-//   segment 1:  PV_B(t - 1) MFMAs || row max of A(t)   |  S_B(t)     MFMAs || exp / sums of A(t)
-//   segment 2:  PV_A(t)     MFMAs || row max of B(t)   |  S_A(t + 1) MFMAs || exp / sums of B(t)
-// Q arrives by LDS-DMA with the first K|V tiles (no compiler-tracked load to drain the ring).  Every
-// row's arithmetic is attn_fwd_block's, op for op (score chain, lazy rescale, exponent fma, the eight
-// partial row sums, PV order), so O and LSE are bit-identical to it (tests/test_kernels_gpu.py).
-constexpr int FD_ROWS = 256;  // query rows per workgroup
-constexpr int FD_NS = 6;      // K|V ring stages (16 KiB each) + the 32 KiB Q image: 128 KiB of LDS
-
-// `younger` tiles of OPS pieces each may stay in flight
-template <int OPS, int MAXY>
-__device__ __forceinline__ void vm_wait_tiles(int younger) {
-  if constexpr (MAXY >= 4) { if (younger >= 4) { vm_wait<4 * OPS>(); return; } }
-  if constexpr (MAXY >= 3) { if (younger >= 3) { vm_wait<3 * OPS>(); return; } }
-  if constexpr (MAXY >= 2) { if (younger >= 2) { vm_wait<2 * OPS>(); return; } }
-  if constexpr (MAXY >= 1) { if (younger >= 1) { vm_wait<OPS>(); return; } }
-  vm_wait<0>();
-}
-
-// S^T = K Q^T of one slice against the 64 keys of a tile (key on the row, as attn_fwd_block); the
-// slice's Q operands are re-read from the block's resident Q image (32 VGPRs fewer per wave)
-__device__ __forceinline__ void fd_qk(const lds_u8* sk, const lds_u8* qi, int qrow0, f32x16_t (&s)[2], int lane) {
-  bf16x8_t qf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) qf[ks] = rd_row<64>(qi, qrow0, ks, lane);
-#pragma unroll
-  for (int kh = 0; kh < 2; ++kh) {
-    bf16x8_t ka[4];
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) ka[ks] = rd_row<64>(sk, 32 * kh, ks, lane);
-    s[kh] = zero16();
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) s[kh] = mfma(ka[ks], qf[ks], s[kh]);
-  }
-}
-
-// O^T += V^T P^T of one slice (P = the four bf16 B operands of fd_exp)
-__device__ __forceinline__ void fd_pv(const lds_u8* sv, const bf16x8_t (&p)[4], f32x16_t (&o)[2], int lane) {
-#pragma unroll
-  for (int st = 0; st < 4; ++st)
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt) o[dt] = mfma(rd_tr<64>(sv, st, dt, lane), p[st], o[dt]);
-}
-
-// first half of a slice's softmax: diagonal mask, tile max, lazy rescale of (l, O)
-template <bool DIAG>
-__device__ __forceinline__ void fd_max(f32x16_t (&s)[2], int thr, float c2, float& m, float& l, f32x16_t (&o)[2]) {
-  if constexpr (DIAG) {
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (32 * kh + (r & 3) + 8 * (r >> 2) > thr) s[kh][r] = -INFINITY;
-  }
-  float mt = -INFINITY;
-#pragma unroll
-  for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[kh][r]);
-  mt = xor32_max(mt) * c2;
-  {   // branch-free lazy rescale (attn_fwd_block)
-    const float mn = __any(mt > m + kRescaleLog2) ? fmaxf(m, mt) : m;
-    const float alpha = __builtin_amdgcn_exp2f(m - mn);
-    m = mn;
-    l *= alpha;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
-  }
-}
-
-// second half: P = exp2(S c2 - m) as bf16 B operands, row sum into l (attn_fwd_block's eight partials,
-// each fed in its order: k-steps st = 0..3 are (kh, r) = (0, 0-7), (0, 8-15), (1, 0-7), (1, 8-15))
-__device__ __forceinline__ void fd_exp(const f32x16_t (&s)[2], float c2, float m, float& l, bf16x8_t (&p)[4]) {
-  float lx[4], ly[4];   // each partial starts as its first term (= 0 + e: exp2 is never -0)
-#pragma unroll
-  for (int st = 0; st < 4; ++st) {
-    bf16x8_t v;
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      const int r = 8 * (st & 1) + j;
-      const float e0 = __builtin_amdgcn_exp2f(fmaf(s[st >> 1][r], c2, -m));
-      const float e1 = __builtin_amdgcn_exp2f(fmaf(s[st >> 1][r + 1], c2, -m));
-      if (st == 0) { lx[r / 2] = e0; ly[r / 2] = e1; }
-      else { lx[(r / 2) & 3] += e0; ly[(r / 2) & 3] += e1; }
-      v[j] = (__bf16)e0;
-      v[j + 1] = (__bf16)e1;
-    }
-    p[st] = v;
-  }
-  l += ((lx[0] + lx[1]) + (lx[2] + lx[3])) + ((ly[0] + ly[1]) + (ly[2] + ly[3]));
-}
-
-// one 256-row query block; `nT` K|V tiles for the workgroup, nA / nB for the wave's slices
-__device__ __forceinline__ void attn_fwd_dual_block(const AttnArgs& a, int blk, int h, int b) {
-  constexpr int D = 64, TILE_B = KT * D * 2, NS = FD_NS, OPS = 2 * TILE_B / 1024 / NW;
-  constexpr int QOPS = FD_ROWS * D * 2 / 1024 / NW;   // Q image pieces per wave
-  static_assert(QOPS == 2 * OPS, "the prologue wait counts Q as two tiles");
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
-  lds_u8* qimg = (lds_u8*)smem_raw;                 // [4][64 rows][64] swizzled, 32 KiB
-  lds_u8* ring = qimg + FD_ROWS * D * 2;
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int hk = h / (a.H / a.HKV);
-  const int qA = blk * FD_ROWS + 32 * wave, qB = qA + 128;
-  const int nT = a.causal ? (blk + 1) * (FD_ROWS / KT) : a.Sk / KT;
-  const int nA = a.causal ? (qA + 95) / KT : nT, nB = a.causal ? (qB + 95) / KT : nT;
-  const float c2 = a.scale * kLog2e;
-  const uint16_t* kbase = a.k + b * a.k_sb + hk * a.k_sh;
-  const uint16_t* vbase = a.v + b * a.v_sb + hk * a.v_sh;
-  auto stage = [&](int kt, int buf) {
-    lds_u8* sk = ring + buf * 2 * TILE_B;
-    stage_rows<D, NW>(kbase + (int64_t)kt * KT * a.k_ss, a.k_ss, sk, wave, lane);
-    stage_rows<D, NW>(vbase + (int64_t)kt * KT * a.v_ss, a.v_ss, sk + TILE_B, wave, lane);
-  };
-  const uint16_t* qbase = a.q + b * a.q_sb + h * a.q_sh + (int64_t)blk * FD_ROWS * a.q_ss;
-#pragma unroll
-  for (int i = 0; i < FD_ROWS / KT; ++i)
-    stage_rows<D, NW>(qbase + (int64_t)i * KT * a.q_ss, a.q_ss, qimg + i * TILE_B, wave, lane);
-  const int pre = nT < NS - 1 ? nT : NS - 1;
-  for (int t = 0; t < pre; ++t) stage(t, t);
-  vm_wait_tiles<OPS, NS - 2>(pre - 1);   // Q and tile 0 landed
-  __syncthreads();
-
-  const lds_u8* qiA = qimg + (wave >> 1) * TILE_B;        // rows 32 w .. of the block: image w / 2
-  const lds_u8* qiB = qimg + (2 + (wave >> 1)) * TILE_B;  // rows 128 + 32 w ..: image 2 + w / 2
-  const int qr0 = 32 * (wave & 1);
-  f32x16_t oA[2] = {zero16(), zero16()}, oB[2] = {zero16(), zero16()};
-  float mA = -INFINITY, lA = 0.f, mB = -INFINITY, lB = 0.f;
-  f32x16_t sA[2], sB[2];
-  bf16x8_t pA[4], pB[4];
-  const int thrA = qA + (lane & 31) - 4 * (lane >> 5), thrB = thrA + 128;   // + kv0 offsets below
-  auto tile_at = [&](int t) -> lds_u8* { return ring + (t % NS) * 2 * TILE_B; };
-
-  // one iteration t, its parts fixed at compile time (each kind of iteration is its own straight-line
-  // code, run by its own loop or call: no runtime branch joins two versions of the accumulators)
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  auto iter = [&](auto pvb, auto qkb, auto sma, auto pva, auto qka, auto smb, int t) {
-    lds_u8* cur = tile_at(t);
-    const int kv0 = t * KT;
-    // ---- segment 1: PV_B(t - 1), S_B(t) || softmax A(t)   (sma: 0 none, 1 plain, 2 diagonal)
-    if constexpr (decltype(pvb)::value) fd_pv(tile_at(t - 1) + TILE_B, pB, oB, lane);
-    if constexpr (decltype(sma)::value) fd_max<decltype(sma)::value == 2>(sA, thrA - kv0, c2, mA, lA, oA);
-    if constexpr (decltype(qkb)::value) fd_qk(cur, qiB, qr0, sB, lane);
-    if constexpr (decltype(sma)::value) fd_exp(sA, c2, mA, lA, pA);
-    // ---- ring: tile t + 1 landed, everyone is past tile t - 1 -> refill its stage
-    if (t + 1 < nT) {
-      const int issued = t + NS - 2 < nT - 1 ? t + NS - 2 : nT - 1;
-      vm_wait_tiles<OPS, NS - 3>(issued - (t + 1));
-    }
-    __syncthreads();
-    if (t + NS - 1 < nT) stage(t + NS - 1, (t + NS - 1) % NS);
-    // ---- segment 2: PV_A(t), S_A(t + 1) || softmax B(t)
-    if constexpr (decltype(pva)::value) fd_pv(cur + TILE_B, pA, oA, lane);
-    if constexpr (decltype(smb)::value) fd_max<decltype(smb)::value == 2>(sB, thrB - kv0, c2, mB, lB, oB);
-    if constexpr (decltype(qka)::value) fd_qk(tile_at(t + 1), qiA, qr0, sA, lane);
-    if constexpr (decltype(smb)::value) fd_exp(sB, c2, mB, lB, pB);
-  };
-
-  fd_qk(tile_at(0), qiA, qr0, sA, lane);
-  if (a.causal) {
-    // nB = nA + 2 <= nT; A's last tile and B's last tile are the slices' diagonal tiles
-    if (nA == 1) iter(I0{}, I1{}, I2{}, I1{}, I0{}, I1{}, 0);
-    else iter(I0{}, I1{}, I1{}, I1{}, I1{}, I1{}, 0);
-    for (int t = 1; t < nA - 1; ++t) iter(I1{}, I1{}, I1{}, I1{}, I1{}, I1{}, t);   // steady state
-    if (nA >= 2) iter(I1{}, I1{}, I2{}, I1{}, I0{}, I1{}, nA - 1);
-    iter(I1{}, I1{}, I0{}, I0{}, I0{}, I1{}, nA);
-    iter(I1{}, I1{}, I0{}, I0{}, I0{}, I2{}, nA + 1);
-    for (int t = nB; t < nT; ++t) {   // PV_B(nB - 1), then only the ring
-      if (t == nB) iter(I1{}, I0{}, I0{}, I0{}, I0{}, I0{}, t);
-      else iter(I0{}, I0{}, I0{}, I0{}, I0{}, I0{}, t);
-    }
-  } else {
-    if (nT == 1) iter(I0{}, I1{}, I1{}, I1{}, I0{}, I1{}, 0);
-    else iter(I0{}, I1{}, I1{}, I1{}, I1{}, I1{}, 0);
-    for (int t = 1; t < nT - 1; ++t) iter(I1{}, I1{}, I1{}, I1{}, I1{}, I1{}, t);
-    if (nT >= 2) iter(I1{}, I1{}, I1{}, I1{}, I0{}, I1{}, nT - 1);
-  }
-  if (nB == nT) fd_pv(tile_at(nT - 1) + TILE_B, pB, oB, lane);
-
-  // ---- epilogue: normalise, bf16 O rows and the LSE (attn_fwd_block's non-merge store)
-  auto finish = [&](const f32x16_t (&o)[2], float m, float l, int q0) {
-    l = xor32_sum(l);
-    const float inv_l = 1.0f / l;
-    const int myq = q0 + (lane & 31);
-    uint16_t* orow = (uint16_t*)a.o + b * a.o_sb + (int64_t)myq * a.o_ss + h * a.o_sh;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt) store_T_bf16(orow, dt, o[dt], inv_l, lane);
-    if (lane < 32) a.lse[((int64_t)b * a.H + h) * a.lse_ld + myq] = m * kLn2 + __logf(l);
-  };
-  finish(oA, mA, lA, qA);
-  finish(oB, mB, lB, qB);
-}
-
-__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1)))
-void attn_fwd_dual_kernel(AttnArgs a) {
-  int bx, hh, b;
-  attn_coords(a, bx, hh, b);
-  const int nq = a.Sq / FD_ROWS;
-  for (int pass = 0; pass <= a.pair; ++pass) {   // causal: the heavy block first (attn_fwd_block's order)
-    if (pass) __syncthreads();   // the first block's LDS reads are done before the next block's DMA
-    const int x = pass ? nq - 1 - bx : bx;
-    attn_fwd_dual_block(a, a.causal ? nq - 1 - x : x, hh, b);
   }
 }
 
@@ -1579,14 +1372,7 @@ int pt_attn_fwd(const void* q, const int64_t* q_str, const void* k, const int64_
   a.pair = causal && nqb % 2 == 0 && pair_enabled();
   const dim3 grid((unsigned)(a.pair ? nqb / 2 : nqb), (unsigned)H, (unsigned)B);
   const int stage_b = 2 * KT * (int)D * 2;
-  if (D == 64 && !merge && Sq % FD_ROWS == 0 && pt_variant(PT_VAR_ATTN_FWD_DUAL) == 1) {
-    const int nq = (int)(Sq / FD_ROWS);
-    a.pair = causal && nq % 2 == 0 && pair_enabled();
-    const dim3 g((unsigned)(a.pair ? nq / 2 : nq), (unsigned)H, (unsigned)B);
-    const int smem = FD_ROWS * 64 * 2 + FD_NS * stage_b;
-    set_smem(attn_fwd_dual_kernel, smem);
-    attn_fwd_dual_kernel<<<g, NW * 64, smem, stream>>>(a);
-  } else if (D == 64) {
+  if (D == 64) {
     const int smem = fwd_stages<64, NW>() * stage_b;
     set_smem(attn_fwd_kernel<64, NW>, smem);
     attn_fwd_kernel<64, NW><<<grid, NW * 64, smem, stream>>>(a);

@@ -5,9 +5,9 @@ split-K vs one pass, one launch vs two); the defaults are the production path, a
 hot path reads the environment again.  `PICOTRON_<NAME>` (upper case) sets a switch for a whole
 process (an A/B run); tests and tools change one for a block with `override(name=value)`.
 
-The native switches (attention causal pairing, dK/dV kernel form, few-head split chunk and two-slice
-d64 forward; GEMM tile-row grouping, mixed-tile q|k|v launch, K-halves tile) live in the library; `apply_native` pushes them through
-`pt_set_variant` when the library is loaded, and `override` pushes a changed one at once.
+The native switches (attention causal pairing, dK/dV kernel form, few-head split chunk; GEMM
+tile-row grouping, mixed-tile q|k|v launch, K-halves tile) live in the library; `apply_native`
+pushes them through `pt_set_variant` when the library is loaded, and `override` pushes a changed one at once.
 """
 import contextlib
 import os
@@ -32,9 +32,9 @@ DEFAULTS = {
     # functional.py: the TP lm_head's F.cross_entropy on the vocab shards (no logits all-gather)
     "vp_ce": 1,
     # native (libpicotron_hip.so, pt_set_variant)
-    "attn_pair": 1, "attn_split": 2, "gemm_group_m": -1, "gemm_mix": 1, "gemm_kh": 2, "attn_kv_chunk": 4, "attn_fwd_dual": 0,
+    "attn_pair": 1, "attn_split": 2, "gemm_group_m": -1, "gemm_mix": 1, "gemm_kh": 2, "attn_kv_chunk": 4,
 }
-NATIVE = ("attn_pair", "attn_split", "gemm_group_m", "gemm_mix", "gemm_kh", "attn_kv_chunk", "attn_fwd_dual")
+NATIVE = ("attn_pair", "attn_split", "gemm_group_m", "gemm_mix", "gemm_kh", "attn_kv_chunk")
 
 
 class _Switches:

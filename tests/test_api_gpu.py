@@ -381,7 +381,7 @@ def test_cross_entropy_stats_bad_target():
     K.device_status(torch.device("cuda"))
     x = torch.randn(256, 128, device="cuda").to(BF)
     w = (torch.randn(1024, 128, device="cuda") * 0.1).to(BF)
-    y = FN.LMHeadFunction.apply(x, w)
+    y = FN.LMHeadFunction.apply(x, w, False)
     tgt = torch.randint(0, 1024, (256,), device="cuda")
     tgt[3] = 5000
     loss = FN.cross_entropy(y, tgt)

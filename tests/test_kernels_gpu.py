@@ -1042,26 +1042,3 @@ def test_attention_few_head_split_forms(B, S, H, HKV, causal, rope, chunk):
         assert rel_err(dk, kk.grad.view(B, HKV, rep, S, D).sum(2).transpose(1, 2)) < 2e-2
         assert rel_err(dv, vv.grad.view(B, HKV, rep, S, D).sum(2).transpose(1, 2)) < 2e-2
 
-
-@pytest.mark.parametrize("B,S,H,HKV,causal", [(1, 256, 2, 2, True), (2, 512, 4, 2, True), (1, 1024, 4, 4, False),
-                                               (2, 1024, 8, 8, True), (1, 768, 2, 1, True)])
-def test_attention_fwd_dual_bit_identical(B, S, H, HKV, causal):
-    """The d64 forward with two query slices per wave (attn_fwd_dual_kernel: one workgroup per CU,
-    256 rows, Q by LDS-DMA) performs every row's arithmetic in attn_fwd_block's order, so O and the
-    LSE are bit-identical to the one-slice kernel (attn_fwd_dual = 0), pairing on and off."""
-    from picotron_amd import kernels as K_
-    D = 64
-    q, k, v = _qkv(B, S, H, HKV, D)
-    scale = 1 / math.sqrt(D)
-    res = {}
-    for dual in (0, 1):
-        for pair in (1, 0):
-            with switches.override(attn_fwd_dual=dual, attn_pair=pair, attn_kv_chunk=0):
-                o, lse = K_.attn_fwd(q, k, v, scale, causal)
-            torch.cuda.synchronize()
-            res[(dual, pair)] = (o.clone(), lse.clone())
-    for key, (o, lse) in res.items():
-        assert torch.equal(o, res[(0, 1)][0]) and torch.equal(lse, res[(0, 1)][1]), key
-    qq, kk, vv = _ref_attn(q, k, v, causal, scale)
-    o_ref, lse_ref = O.attention_lse(qq, kk, vv, scale, causal)
-    assert rel_err(res[(1, 1)][0], o_ref.transpose(1, 2)) < 1e-2 and maxabs(res[(1, 1)][1], lse_ref) < 1e-2
