@@ -216,7 +216,25 @@ def tp_proxy(args, base, layers):
         torch.cuda.synchronize()
         # the backward reached every layer's weights (a stand-in off the autograd graph would cut it)
         assert all(p.grad is not None for w in stack for p in w) and emb.grad is not None, "proxy backward incomplete"
-        t = _events_time(micro_batch, args.steps)
+        t = t_eager = _events_time(micro_batch, args.steps)
+        graph_note = None
+        if args.graph:
+            # at the shard widths the ~425 launches of a micro-batch outrun their kernels on the host
+            # (Python + autograd + ctypes per launch): capture the micro-batch (fwd, CE, bwd) as one
+            # HIP graph and replay it -- how a TP deployment issues this fixed sequence
+            try:
+                side = torch.cuda.Stream()
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    micro_batch()
+                torch.cuda.current_stream().wait_stream(side)
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    micro_batch()
+                t = _events_time(graph.replay, args.steps)
+            except Exception as e:   # a capture the stack refuses: report it, keep the eager timing
+                graph_note = f"graph capture failed: {type(e).__name__}: {e}"[:300]
+                torch.cuda.synchronize()
         with probe:
             micro_batch()
         s = probe.summary()
@@ -228,6 +246,8 @@ def tp_proxy(args, base, layers):
     from picotron_amd.train import SMOLLM_1_7B  # noqa: F401
     return {"metric": f"TP={tp} per-rank compute proxy (1 GPU, no collectives)", "value": tok_gpu,
             "unit": "tokens/s/GPU (compute-only upper bound)", "ms_per_microbatch": t * 1e3,
+            "launch": "hip graph replay" if (args.graph and graph_note is None) else "eager",
+            "eager_ms_per_microbatch": t_eager * 1e3, **({"graph_note": graph_note} if graph_note else {}),
             "mfu_upper_bound": tok_gpu * (fpt_rank * tp) / MI355X_BF16_DENSE_PEAK,
             "config": {"model": cfg_name(base), "layers": layers, "micro_batch": args.mbs, "seq_len": args.seq,
                        "shard": {"q|k|v": 3 * nh * d, "I": I, "heads": nh, "vocab": V // tp},
@@ -375,7 +395,9 @@ def cp_proxy(args, base, layers):
             "mesh": {"comm_bytes_per_layer": (C - 1) * (kv_b / 2 + kv_b + qdo_b) + (C - 1 - crit_m) * kv_b / 2,
                      "link_time_ms": ((kv_b if crit_m < C - 1 else kv_b / 2) + kv_b + qdo_b) / bw * 1e3,
                      "links": C - 1,
-                     "exposed_ms": (mesh_f + mesh_b) * 1e3},
+                     "exposed_ms": (mesh_f + mesh_b) * 1e3,
+                     # the backward's receive buffers, all peers' at once (mesh_backward), vs the ring's two
+                     "recv_buffer_bytes": (C - 1) * (kv_b + qdo_b), "ring_recv_buffer_bytes": 2 * (kv_b + dkv_b)},
             "relayout": {"comm_bytes_per_pass": relay_b, "per_layer_ms": relay_t * 1e3}}
     t_mesh = t_layer + mesh_c + mesh_f + mesh_b + relay_t
     t_ring_zz = t_zz + ring_f + ring_b + relay_t
@@ -513,6 +535,8 @@ def build_parser():
     ap.add_argument("--pp-engine", choices=["1f1b", "afab"], default="1f1b", help="pipeline schedule (train.py:222-225)")
     ap.add_argument("--tp-proxy", type=int, default=0, help="1 GPU: one TP rank's compute at this degree")
     ap.add_argument("--cp-proxy", type=int, default=0, help="1 GPU: the CP ring's critical rank at this degree")
+    ap.add_argument("--graph", type=int, default=1, help="--tp-proxy: time the micro-batch as a captured HIP graph "
+                                                         "(0: eager launches only)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo: rehearse an N-rank grid with every rank on cuda:0 (one-GPU box); timing meaningless")
     ap.add_argument("--mbs", type=int, default=4)
