@@ -119,7 +119,8 @@ __global__ __launch_bounds__(256) void adamw_multi_bf16_kernel(const AdamTensor*
     const int64_t bd = blockDim.x;
     bf16x8 cur[4], nx1[4], nx2[4];
     auto load4 = [&](int64_t cc, bf16x8 (&r)[4]) {
-      r[0] = ld8(T.p + cc * 8); r[1] = ld8(T.g + cc * 8); r[2] = ld8(T.m + cc * 8); r[3] = ld8(T.v + cc * 8);
+      r[0] = ld8_nt(T.p + cc * 8); r[1] = ld8_nt(T.g + cc * 8); r[2] = ld8_nt(T.m + cc * 8);
+      r[3] = ld8_nt(T.v + cc * 8);
     };
     if (c < end) load4(c, cur);
     if (c + bd < end) load4(c + bd, nx1);
@@ -129,9 +130,9 @@ __global__ __launch_bounds__(256) void adamw_multi_bf16_kernel(const AdamTensor*
       unpack8(cur[0], p); unpack8(cur[1], g); unpack8(cur[2], m); unpack8(cur[3], v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) adam_elem(p[j], g[j], m[j], v[j], s, true);
-      st8(T.p + c * 8, pack8(p));
-      st8(T.m + c * 8, pack8(m));
-      st8(T.v + c * 8, pack8(v));
+      st8_nt(T.p + c * 8, pack8(p));
+      st8_nt(T.m + c * 8, pack8(m));
+      st8_nt(T.v + c * 8, pack8(v));
 #pragma unroll
       for (int q = 0; q < 4; ++q) { cur[q] = nx1[q]; nx1[q] = nx2[q]; }
     }

@@ -336,10 +336,12 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
   const int q0 = qb * NWK * 32 + wave * 32;
   const int myq = q0 + (lane & 31);
 
-  const uint16_t* qrow = a.q + b * a.q_sb + (int64_t)myq * a.q_ss + h * a.q_sh;
   bf16x8_t qf[KS];
+  if constexpr (D != 64) {
+    const uint16_t* qrow = a.q + b * a.q_sb + (int64_t)myq * a.q_ss + h * a.q_sh;
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) qf[ks] = ld_row_frag(qrow, ks, lane);
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = ld_row_frag(qrow, ks, lane);
+  }
 
   const uint16_t* kbase = a.k + b * a.k_sb + hk * a.k_sh;
   const uint16_t* vbase = a.v + b * a.v_sb + hk * a.v_sh;
@@ -360,9 +362,28 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
     stage_rows<D, NWK>(vbase + (int64_t)(kt0 + kt) * KT * a.v_ss, a.v_ss, sk + TILE_B, wave, lane);
   };
   const int pre = nkt < NS - 1 ? nkt : NS - 1;
-  for (int t = 0; t < pre; ++t) stage(t, t);
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler: its own fragment loads are done
-  __syncthreads();
+  if constexpr (D == 64) {
+    // the block's Q rows by LDS-DMA too, into the ring stage tile NS - 1 will use, so the prologue
+    // waits for Q and tile 0 only -- with Q as compiler-tracked loads its vmcnt(0) drained all NS - 1
+    // prefetched tiles
+    static_assert(NWK * 32 == 2 * KT, "two 64-row Q images: one K|V stage");
+    lds_u8* qimg = smem + (NS - 1) * 2 * TILE_B;
+    const uint16_t* qbase = a.q + b * a.q_sb + h * a.q_sh + (int64_t)qb * NWK * 32 * a.q_ss;
+    stage_rows<D, NWK>(qbase, a.q_ss, qimg, wave, lane);
+    stage_rows<D, NWK>(qbase + (int64_t)KT * a.q_ss, a.q_ss, qimg + TILE_B, wave, lane);
+    for (int t = 0; t < pre; ++t) stage(t, t);
+    if (pre >= 3) vm_wait<2 * OPS>();   // the younger tiles 1 .. pre - 1 may stay in flight
+    else if (pre == 2) vm_wait<OPS>();
+    else vm_wait<0>();
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = rd_row<D>(qimg + (wave >> 1) * TILE_B, 32 * (wave & 1), ks, lane);
+    __syncthreads();   // every wave has its Q fragments before tile NS - 1's DMA reuses the stage
+  } else {
+    for (int t = 0; t < pre; ++t) stage(t, t);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler: its own fragment loads are done
+    __syncthreads();
+  }
 
   // one K/V tile.  d64: the diagonal tile's mask is a separate instantiation (dg 1), run by its own
   // loop (tile_loops) -- as a runtime branch the compiler if-converted it (60 compares / selects on
@@ -1373,7 +1394,7 @@ int pt_attn_fwd(const void* q, const int64_t* q_str, const void* k, const int64_
   const dim3 grid((unsigned)(a.pair ? nqb / 2 : nqb), (unsigned)H, (unsigned)B);
   const int stage_b = 2 * KT * (int)D * 2;
   if (D == 64) {
-    const int smem = fwd_stages<64, NW>() * stage_b;
+    const int smem = fwd_stages<64, NW>() * stage_b;   // the Q image shares the last stage
     set_smem(attn_fwd_kernel<64, NW>, smem);
     attn_fwd_kernel<64, NW><<<grid, NW * 64, smem, stream>>>(a);
   } else if (nwk == 8) {
@@ -1590,7 +1611,7 @@ int pt_attn_fwd_split(const void* q, const int64_t* q_str, const void* k, const 
   const int64_t items = B * H * a.split_per_bh;
   a.split_o = (float*)ws;
   a.split_lse = (float*)((char*)ws + align256(items * NW * 32 * D * 4));
-  const int smem = fwd_stages<64, NW>() * 2 * KT * 64 * 2;
+  const int smem = fwd_stages<64, NW>() * 2 * KT * 64 * 2;   // the Q image shares the last stage
   set_smem(attn_fwd_split_kernel<64>, smem);
   attn_fwd_split_kernel<64><<<(unsigned)items, NW * 64, smem, stream>>>(a);
   PT_CHECK_LAUNCH();
