@@ -340,9 +340,13 @@ __device__ __forceinline__ void f32_acc_tail(const f32x4_t (&acc)[TM / 16][TN / 
   const uint32_t coff = (uint32_t)(lrow * ldc + ch * 4) * 4u;
   const int64_t rstep = (int64_t)RPI * ldc * 4;
   f32x4_t old[NP][NIT];
+  // the f32 main_grad is read-modify-written once per micro-batch, nothing re-reads it soon: non-
+  // temporal loads / stores, so it does not push the GEMMs' operand panels out of L2 / Infinity Cache
+  typedef __attribute__((address_space(1))) f32x4_t g_f32x4_t;
   auto load_pass = [&](int p) {
 #pragma unroll
-    for (int q = 0; q < NIT; ++q) old[p][q] = *(const f32x4_t*)(cbase + (p * NIT + q) * rstep + coff);
+    for (int q = 0; q < NIT; ++q)
+      old[p][q] = __builtin_nontemporal_load((const g_f32x4_t*)(cbase + (p * NIT + q) * rstep + coff));
   };
   auto stage_pass = [&](int p) {
 #pragma unroll
@@ -368,7 +372,7 @@ __device__ __forceinline__ void f32_acc_tail(const f32x4_t (&acc)[TM / 16][TN / 
       const f32x4_t v = *(const __attribute__((address_space(3))) f32x4_t*)(st + (q * RPI + lrow) * ROWB + ch * 16);
       if (ACC) {
         asm volatile("" : "+v"(old[p][q]));
-        *(f32x4_t*)(cbase + (p * NIT + q) * rstep + coff) = old[p][q] + v;
+        __builtin_nontemporal_store(old[p][q] + v, (g_f32x4_t*)(cbase + (p * NIT + q) * rstep + coff));
       } else {
         *(f32x4_t*)(cbase + (p * NIT + q) * rstep + coff) = v;
       }
@@ -470,7 +474,9 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
           const int row = (g0 + q) * RPI + lane / CPR, ch = lane % CPR;
           const uint16_t* src = EPI == EPI_BF16_ACC ? C + (mrow0 + row) * ldc + ncol0 + ch * 8
                                                     : a.R + (mrow0 + row) * a.ldr + ncol0 + ch * 8;
-          pre[q][0] = ld8(src);
+          // the accumulated weight gradient (.grad): read-modify-written once per micro-batch,
+          // non-temporal (as the f32 main_grad in f32_acc_tail)
+          pre[q][0] = EPI == EPI_BF16_ACC ? ld8_nt(src) : ld8(src);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -507,7 +513,8 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
           for (int e = 0; e < 8; ++e) o[e] += f[e];
           v = pack8(o);
         }
-        st8(dst, v);
+        if constexpr (EPI == EPI_BF16_ACC) st8_nt(dst, v);
+        else st8(dst, v);
       }
     }
   } else {
