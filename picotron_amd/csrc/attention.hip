@@ -363,22 +363,26 @@ __device__ __forceinline__ void attn_fwd_block(const AttnArgs& a, int bx, int h_
   };
   const int pre = nkt < NS - 1 ? nkt : NS - 1;
   if constexpr (D == 64) {
-    // the block's Q rows by LDS-DMA too, into the ring stage tile NS - 1 will use, so the prologue
-    // waits for Q and tile 0 only -- with Q as compiler-tracked loads its vmcnt(0) drained all NS - 1
-    // prefetched tiles
-    static_assert(NWK * 32 == 2 * KT, "two 64-row Q images: one K|V stage");
-    lds_u8* qimg = smem + (NS - 1) * 2 * TILE_B;
+    // the block's Q rows by LDS-DMA too, into the ring stages the last prefetched tiles would use
+    // (one stage at 4 waves, two at 8), so the prologue waits for Q and tile 0 only -- with Q as
+    // compiler-tracked loads its vmcnt(0) drained every prefetched tile; those stages' tiles are
+    // issued once every wave holds its Q fragments
+    constexpr int QI = NWK * 32 / KT, QS = QI / 2;   // 64-row Q images, K|V stages they take
+    static_assert(QI % 2 == 0 && QS < NS, "Q images fill whole K|V stages");
+    lds_u8* qimg = smem + (NS - QS) * 2 * TILE_B;
     const uint16_t* qbase = a.q + b * a.q_sb + h * a.q_sh + (int64_t)qb * NWK * 32 * a.q_ss;
-    stage_rows<D, NWK>(qbase, a.q_ss, qimg, wave, lane);
-    stage_rows<D, NWK>(qbase + (int64_t)KT * a.q_ss, a.q_ss, qimg + TILE_B, wave, lane);
-    for (int t = 0; t < pre; ++t) stage(t, t);
-    if (pre >= 3) vm_wait<2 * OPS>();   // the younger tiles 1 .. pre - 1 may stay in flight
-    else if (pre == 2) vm_wait<OPS>();
+#pragma unroll
+    for (int i = 0; i < QI; ++i) stage_rows<D, NWK>(qbase + (int64_t)i * KT * a.q_ss, a.q_ss, qimg + i * TILE_B, wave, lane);
+    const int pre0 = nkt < NS - QS ? nkt : NS - QS;   // tiles in flight beside Q
+    for (int t = 0; t < pre0; ++t) stage(t, t);
+    if (pre0 >= 3) vm_wait<2 * OPS>();   // the younger tiles 1 .. pre0 - 1 may stay in flight
+    else if (pre0 == 2) vm_wait<OPS>();
     else vm_wait<0>();
     __syncthreads();
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) qf[ks] = rd_row<D>(qimg + (wave >> 1) * TILE_B, 32 * (wave & 1), ks, lane);
-    __syncthreads();   // every wave has its Q fragments before tile NS - 1's DMA reuses the stage
+    __syncthreads();   // every wave has its Q fragments before the tiles' DMA reuses those stages
+    for (int t = pre0; t < pre; ++t) stage(t, t);
   } else {
     for (int t = 0; t < pre; ++t) stage(t, t);
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler: its own fragment loads are done
@@ -1388,6 +1392,8 @@ int pt_attn_fwd(const void* q, const int64_t* q_str, const void* k, const int64_
   a.scale = scale; a.causal = causal; a.merge = merge;
   int rc = check_common(a, (int)D);
   if (rc) return rc;
+  // 8-wave workgroups (the K|V tiles staged once for 256 queries) at d128; at d64 measured equal or
+  // slower (round 5: 35.6 vs 34.8 us, bit-identical), so 4
   const int nwk = (D == 128 && Sq % (8 * 32) == 0) ? 8 : NW;
   const int nqb = (int)(Sq / (nwk * 32));
   a.pair = causal && nqb % 2 == 0 && pair_enabled();

@@ -1042,3 +1042,4 @@ def test_attention_few_head_split_forms(B, S, H, HKV, causal, rope, chunk):
         assert rel_err(dk, kk.grad.view(B, HKV, rep, S, D).sum(2).transpose(1, 2)) < 2e-2
         assert rel_err(dv, vv.grad.view(B, HKV, rep, S, D).sum(2).transpose(1, 2)) < 2e-2
 
+
