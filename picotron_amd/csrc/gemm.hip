@@ -295,8 +295,10 @@ __device__ __forceinline__ void swiglu_bwd_tail(const GemmArgs& a, const lds_u8*
     bf16x8 g[SG], u[SG];
 #pragma unroll
     for (int k = 0; k < SG; ++k) {
-      g[k] = ld8((const uint16_t*)(gbase + (q0 + k) * rstep + roff));
-      u[k] = ld8((const uint16_t*)(gbase + (q0 + k) * rstep + ustep + roff));
+      // g|u: the forward's activations, read once here -- non-temporal, beside the dual launch's
+      // weight-gradient tiles and their operand panels
+      g[k] = ld8_nt((const uint16_t*)(gbase + (q0 + k) * rstep + roff));
+      u[k] = ld8_nt((const uint16_t*)(gbase + (q0 + k) * rstep + ustep + roff));
     }
 #pragma unroll
     for (int k = 0; k < SG; ++k) {
@@ -475,8 +477,8 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, const f32x4_t (&acc)
           const uint16_t* src = EPI == EPI_BF16_ACC ? C + (mrow0 + row) * ldc + ncol0 + ch * 8
                                                     : a.R + (mrow0 + row) * a.ldr + ncol0 + ch * 8;
           // the accumulated weight gradient (.grad): read-modify-written once per micro-batch,
-          // non-temporal (as the f32 main_grad in f32_acc_tail)
-          pre[q][0] = EPI == EPI_BF16_ACC ? ld8_nt(src) : ld8(src);
+          // non-temporal (as the f32 main_grad in f32_acc_tail); the residual: read once, too
+          pre[q][0] = ld8_nt(src);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
