@@ -608,7 +608,7 @@ def main():
     from picotron_amd.process_group_manager import setup_process_group_manager
     from picotron_amd.tensor_parallel.tensor_parallel import apply_tensor_parallel
     from picotron_amd.train import (SyntheticMicroBatchDataLoader, count_params, flops_per_token, make_config,
-                                    train_step, MI355X_BF16_DENSE_PEAK)
+                                    train_step, read_step_loss, MI355X_BF16_DENSE_PEAK)
 
     model_name, base_name, default_layers = MODELS[args.model]
     base = dict(getattr(TR, base_name), _name=base_name)
@@ -660,18 +660,25 @@ def main():
         shapes = (args.mbs, args.seq // cp, cfg.hidden_size)
 
     def step():
-        optimizer.zero_grad()
         if pp > 1:   # train.py:222-225 (the GEMM probe samples micro-batches of train_step only)
+            optimizer.zero_grad()
             loss = pp_step(model, loader, shapes, device, torch.bfloat16)
             if hasattr(model, "reset"):
                 model.reset()
             optimizer.step()
             return loss
-        loss = train_step(model, loader, device, on_microbatch=sample)
+        # train.py:220-225 with the host work of the step boundary moved under the GPU's: the optimizer
+        # is enqueued behind the backward before the host reads the loss (train_step(read_loss=False)),
+        # and the next step's zero_grad (set_to_none: drops the gradients, stream-ordered) runs while
+        # the AdamW launch does -- same work, no GPU idle gap at the boundary
+        loss = train_step(model, loader, device, on_microbatch=sample, read_loss=False)
         optimizer.step()
         if hasattr(model, "reset"):
             model.reset()
-        return loss
+        optimizer.zero_grad()
+        return read_step_loss(loss, device)
+
+    optimizer.zero_grad()
 
     for i in range(args.warmup):
         t = time.time()

@@ -83,9 +83,13 @@ class SyntheticMicroBatchDataLoader:
                 "hidden_states": None}
 
 
-def train_step(model, data_loader, device, on_microbatch=None):
+def train_step(model, data_loader, device, on_microbatch=None, read_loss=True):
     """train.py:29-55 with the fused HIP cross-entropy; returns the accumulated loss (float).
-    on_microbatch(i): optional hook called before micro-batch i (bench.py samples its GEMM timing)."""
+    on_microbatch(i): optional hook called before micro-batch i (bench.py samples its GEMM timing).
+    read_loss=False: return the loss as a device scalar instead, so that the caller can enqueue the
+    optimizer step before the host waits for the backward (`read_step_loss` reads it then): reading it
+    here idles the GPU for the optimizer's host work (~1.5 ms at SmolLM-1.7B), and the AdamW launch that
+    follows an idle gap runs at the idle clocks, 3.4 vs 2.8 ms (profiles/r05/notes_r05.md)."""
     acc_loss = torch.zeros((), dtype=torch.float32, device=device)
     # (bench.py --dp-bucket: a 1-rank DataParallelBucket syncs like N > 1 would)
     requires_grad_sync = pgm.current().cp_dp_world_size > 1 or getattr(model, "_force_grad_sync", False)
@@ -104,6 +108,11 @@ def train_step(model, data_loader, device, on_microbatch=None):
         loss = FN.cross_entropy(outputs, target_ids, reduction="mean") / data_loader.grad_acc_steps
         loss.backward()
         acc_loss += loss.detach().float()
+    return read_step_loss(acc_loss, device) if read_loss else acc_loss
+
+
+def read_step_loss(acc_loss, device):
+    """The step's loss as a float (one host <-> device synchronisation), then the device status check."""
     out = acc_loss.item()
     K.check_device_status(torch.device(device))   # the host has synchronised: surface device asserts
     return out

@@ -100,9 +100,14 @@ def test_bench_assembles_the_8_rank_dp2_tp2_pp2_grid_on_cpu():
     any GPU run -- here config 4's dp2 tp2 pp2 (process_group_manager.py:13's view(dp, pp, cp, tp)):
     every grid coordinate once, each pipeline stage's shard the same size on all of its ranks, the
     stages' layers covering the model, the embedding on stage 0 and the lm_head on the last stage."""
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--backend", "gloo",
-                        "--assemble-only", "--tp", "2", "--pp", "2", "--layers", "2", "--seq", "256"],
-                       capture_output=True, text=True, timeout=600, env=_env(OMP_NUM_THREADS="1"))
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--backend", "gloo",
+           "--assemble-only", "--tp", "2", "--pp", "2", "--layers", "2", "--seq", "256"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=_env(OMP_NUM_THREADS="1"))
+    if r.returncode != 0 and "Signal 6 (SIGABRT)" in r.stderr:
+        # once in ~15 runs one of the 8 gloo ranks on this 8-CPU container has died of SIGABRT inside
+        # the gloo transport during rendezvous (not reproduced in isolation); one fresh launch
+        sys.stderr.write(r.stderr[-3000:])
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=_env(OMP_NUM_THREADS="1"))
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, r.stdout
