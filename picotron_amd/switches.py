@@ -4,6 +4,9 @@ Every switch selects between HIP kernels with the same results (fused vs separat
 split-K vs one pass, one launch vs two); the defaults are the production path, and nothing on the
 hot path reads the environment again.  `PICOTRON_<NAME>` (upper case) sets a switch for a whole
 process (an A/B run); tests and tools change one for a block with `override(name=value)`.
+Every non-default form runs through the whole GPU path against the oracle in
+tests/test_switch_forms_gpu.py (ring_zigzag in test_parallel_gpu.py, gemm_kh in test_kernels_gpu.py);
+tools/switch_kernels.py traces which launches each changes (profiles/r05/switch_kernels_r05k.txt).
 
 The native switches (attention causal pairing, dK/dV kernel form, few-head split chunk; GEMM
 tile-row grouping, mixed-tile q|k|v launch, K-halves tile) live in the library; `apply_native`

@@ -216,6 +216,19 @@ def test_zigzag_ring_llama(tp, cp, seq, residual, mesh):
     _dist.run(_llama, tp * cp, tp, cp, seq, True, residual, mesh, device="cuda")
 
 
+def _llama_ring_plain(rank, world, tp, cp, seq):
+    from picotron_amd import switches
+    with switches.override(ring_zigzag=0):
+        _llama(rank, world, tp, cp, seq, False, 1, 1)
+
+
+def test_ring_zigzag_off_llama():
+    """PICOTRON_RING_ZIGZAG=0 at a shape the zig-zag schedule tiles (cp2, S_local 256): the
+    reference's contiguous-chunk ring (context_parallel.py:130-155 of the reference), no re-lays,
+    against the oracle on the whole sequence."""
+    _dist.run(_llama_ring_plain, 2, 1, 2, 512, device="cuda")
+
+
 def _ring_api(rank, world):
     """ring_attention (context_parallel.py:14-15, RingAttentionFunc [B, H, S, D], GQA-expanded k/v
     as model.py:142-143 passes them) with the zig-zag schedule: out and dq / dk / dv of this rank's
