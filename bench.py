@@ -46,7 +46,7 @@ if ROOT not in sys.path:
 
 # HBM bytes per GEMM launch from rocprofv3 PMC passes (tools/gpu.sh counters: bench.py --grad-acc 2, then
 # tools/traffic_summary.py); read for the roofline's `traffic`
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r05", "gemm_traffic_r05z.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r05", "gemm_traffic_r05e3.json")
 
 
 def log(*a):

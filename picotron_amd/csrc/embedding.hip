@@ -81,21 +81,23 @@ __global__ __launch_bounds__(256) void embedding_bwd_kernel(const int64_t* __res
 
 // The backward's key preparation + stable sort in ONE single-workgroup launch (T <= 16384): key =
 // 0 for a skipped token (outside [lo, hi) or padding_idx), id - lo + 1 otherwise, carried with its
-// position as (key << 32 | position).  LSD radix sort, one key bit per pass (bits = bit length of
-// hi - lo): each pass is a stable split -- zeros keep their order ahead of the ones -- ranked by
-// wave ballots and one 64-entry prefix over (round, wave), scattered through LDS.  Stable by
-// construction, so equal ids keep ascending positions (== torch.sort(stable=True) of the keyed ids;
-// the backward's fixed summation order).  Element i = r * 1024 + tid lives in thread tid's
-// register r.  Writes sorted_ids (-1 = skip, first) and perm as int64.
-constexpr int kSortThreads = 1024, kSortMax = 16384, kSortRounds = kSortMax / kSortThreads;
+// position as (key << 32 | position).  LSD radix sort, 4 key bits per pass (passes = bit length of
+// hi - lo, rounded up to 4): each pass is a stable 16-way split, an element's destination = the
+// elements of smaller digits + those of its digit in earlier (round, wave) slots + those before it in
+// its wave (4 ballots of the digit bits give each digit's lane mask), one block-wide exclusive scan
+// over the (digit, round, wave) counts, scattered through LDS.  Stable by construction, so equal ids
+// keep ascending positions (== torch.sort(stable=True) of the keyed ids; the backward's fixed
+// summation order).  Element i = r * 1024 + tid lives in thread tid's register r.  Writes sorted_ids
+// (-1 = skip, first) and perm as int64.  (One bit per pass: 16 passes, 35 us at T 4096.)
+constexpr int kSortThreads = 1024, kSortMax = 16384, kSortRounds = kSortMax / kSortThreads, kSortDigits = 16;
 __global__ __launch_bounds__(kSortThreads) void embedding_sort_kernel(const int64_t* __restrict__ ids, int T,
                                                                       int rounds, int bits, int64_t lo, int64_t hi,
                                                                       int has_pad, int64_t pad,
                                                                       int64_t* __restrict__ sorted_ids,
                                                                       int64_t* __restrict__ perm) {
-  extern __shared__ uint64_t buf[];             // [rounds * 1024]
-  __shared__ int zc[kSortRounds * 16];          // zeros per (round, wave), then their exclusive prefix
-  __shared__ int ztotal;
+  extern __shared__ uint64_t buf[];                          // [rounds * 1024]
+  __shared__ int cnt[kSortDigits * kSortRounds * 16];        // (digit, round, wave) counts -> offsets
+  __shared__ int wsum[16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t lt_mask = (1ull << lane) - 1;
   uint64_t c[kSortRounds];
@@ -109,43 +111,56 @@ __global__ __launch_bounds__(kSortThreads) void embedding_sort_kernel(const int6
       c[r] = ((uint64_t)(skip ? 0 : (uint32_t)(id - lo + 1)) << 32) | (uint32_t)i;
     }
   }
-  for (int b = 0; b < bits; ++b) {
-    int zr[kSortRounds];
+  const int n = kSortDigits * rounds * 16;   // scan entries, (digit, round, wave) order
+  for (int shift = 0; shift < bits; shift += 4) {
+    int rk[kSortRounds];
 #pragma unroll
     for (int r = 0; r < kSortRounds; ++r) {
       if (r < rounds) {
-        const bool zero = ((c[r] >> (32 + b)) & 1) == 0;
-        const uint64_t m = __ballot(zero);
-        zr[r] = __popcll(m & lt_mask);          // zeros before this lane in its wave-round
-        if (lane == 0) zc[r * 16 + wave] = __popcll(m);
+        const int dg = (int)(c[r] >> (32 + shift)) & 15;
+        const uint64_t b0 = __ballot(dg & 1), b1 = __ballot(dg & 2), b2 = __ballot(dg & 4), b3 = __ballot(dg & 8);
+        // the lanes holding digit d: per lane, from the four bit masks (own digit: rank; lane < 16:
+        // that digit's count in the wave)
+        auto lanes_of = [&](int d) {
+          return ((d & 1) ? b0 : ~b0) & ((d & 2) ? b1 : ~b1) & ((d & 4) ? b2 : ~b2) & ((d & 8) ? b3 : ~b3);
+        };
+        rk[r] = __popcll(lanes_of(dg) & lt_mask);
+        if (lane < kSortDigits) cnt[(lane * rounds + r) * 16 + wave] = __popcll(lanes_of(lane));
       }
     }
     __syncthreads();
-    if (wave == 0) {  // exclusive prefix of the zero counts in (round, wave) order: <= 256 entries
-      const int n = rounds * 16;
-      int carry = 0;
-      for (int base = 0; base < n; base += 64) {
-        const int v = base + lane < n ? zc[base + lane] : 0;
-        int x = v;
+    {  // block-wide exclusive scan of cnt[0, n): 4 consecutive entries per thread
+      int v4[4], run = 0;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const int y = __shfl_up(x, o, 64);
-          if (lane >= o) x += y;
-        }
-        if (base + lane < n) zc[base + lane] = carry + x - v;
-        carry += __shfl(x, 63, 64);
+      for (int k = 0; k < 4; ++k) {
+        const int e = tid * 4 + k;
+        v4[k] = e < n ? cnt[e] : 0;
+        run += v4[k];
       }
-      if (lane == 0) ztotal = carry;
+      int x = run;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      if (lane == 63) wsum[wave] = x;
+      __syncthreads();
+      int before = 0;
+      for (int w = 0; w < wave; ++w) before += wsum[w];
+      int acc = before + x - run;   // exclusive prefix of this thread's first entry
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = tid * 4 + k;
+        if (e < n) cnt[e] = acc;
+        acc += v4[k];
+      }
     }
     __syncthreads();
-    const int Z = ztotal;
 #pragma unroll
     for (int r = 0; r < kSortRounds; ++r) {
       if (r < rounds) {
-        const int zb = zc[r * 16 + wave] + zr[r];  // zeros before this element
-        const int i = r * kSortThreads + tid;
-        const bool zero = ((c[r] >> (32 + b)) & 1) == 0;
-        buf[zero ? zb : Z + (i - zb)] = c[r];
+        const int dg = (int)(c[r] >> (32 + shift)) & 15;
+        buf[cnt[(dg * rounds + r) * 16 + wave] + rk[r]] = c[r];
       }
     }
     __syncthreads();

@@ -933,10 +933,12 @@ def test_dgrad_k_segmented(ns, T, Kin, acc):
 
 
 @pytest.mark.parametrize("T,lo,hi,pad", [(4096, 0, 49152, None), (1000, 100, 300, 150), (17, 0, 8, 3),
-                                         (20000, 0, 512, None)])
+                                         (16384, 0, 49152, 7), (5000, 0, 70000, None), (20000, 0, 512, None)])
 def test_embedding_sort_equals_torch_stable_sort(T, lo, hi, pad):
-    """pt_embedding_sort (one-workgroup LDS bitonic sort of (key, position)) == torch.sort(stable) of
-    the keyed ids, bit for bit; T > 16384 takes torch's device sort (same result by construction)."""
+    """pt_embedding_sort (one-workgroup LSD radix sort of (key, position), 4 key bits per pass) ==
+    torch.sort(stable) of the keyed ids, bit for bit -- at the most tokens it holds (16384) and with a
+    key width that is not a multiple of 4 bits (hi 70000: 17 bits); T > 16384 takes torch's device
+    sort (same result by construction)."""
     from picotron_amd import _C
     from picotron_amd import kernels as K
     g = torch.Generator().manual_seed(T)
