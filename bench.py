@@ -110,17 +110,76 @@ def _events_time(fn, reps):
     return e0.elapsed_time(e1) / reps * 1e-3
 
 
+class OneRankTP:
+    """A tp group of `world` ranks as one of its ranks sees it, with every collective a REAL RCCL
+    launch on a ONE-rank group (functional.TPContext's interface): an all-gather moves this rank's
+    rows through RCCL into its slot (the other ranks' slots are filled with copies of them on the
+    compute stream, so values stay finite and deterministic), a reduce-scatter reduces this rank's
+    share of the rows, an all-reduce the whole tensor -- on RCCL's stream, async where the layer
+    issues them async, captured into a HIP graph with the rest.  What one rank of a tp group launches
+    and waits on, minus the xGMI transfer time (bench.py --tp-proxy; tests/test_graph_gpu.py)."""
+
+    _cls = None
+
+    def __new__(cls, group, world):
+        if cls._cls is None:
+            cls._cls = cls._make()
+        return cls._cls(group, world, 0)
+
+    @staticmethod
+    def _make():
+        from picotron_amd import functional as FN
+
+        class _OneRankTP(FN.TPContext):
+            def _nccl(self):
+                return True
+
+            def all_reduce(self, t, async_op=False):
+                return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+
+            def all_gather_rows_into(self, out, t, async_op=False):
+                n = t.shape[0]
+                t = t.contiguous()
+                rest = out[n:].view(self.world_size - 1, *t.shape)
+                rest.copy_(t.unsqueeze(0).expand_as(rest))
+                return dist.all_gather_into_tensor(out[:n], t, group=self.group, async_op=async_op)
+
+            def reduce_scatter_rows_into(self, out, t, async_op=False):
+                return dist.reduce_scatter_tensor(out, t[:out.shape[0]].contiguous(), op=dist.ReduceOp.SUM,
+                                                  group=self.group, async_op=async_op)
+
+            def reduce_scatter_rows(self, t, async_op=False):
+                out = torch.empty((t.shape[0] // self.world_size,) + tuple(t.shape[1:]), dtype=t.dtype,
+                                  device=t.device)
+                return out, self.reduce_scatter_rows_into(out, t, async_op)
+        return _OneRankTP
+
+
+def init_one_rank_group(device):
+    """A one-rank RCCL process group on `device` (127.0.0.1 rendezvous) for the one-GPU proxies."""
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        dist.init_process_group(backend="nccl", init_method="env://", rank=0, world_size=1, device_id=device)
+    return dist.group.WORLD
+
+
 def tp_proxy(args, base, layers):
-    """One TP rank's compute for a micro-batch (no collectives): `layers` decoder layers with the
-    shard widths (heads / tp, I / tp; the layer kernels read shards exactly like this inside the
-    TP model) and the launch forms of a tp > 1 group (its all-reduces no-ops), the embedding lookup
+    """One TP rank's compute for a micro-batch: `layers` decoder layers with the shard widths
+    (heads / tp, I / tp; the layer kernels read shards exactly like this inside the TP model) and the
+    launch forms of a tp > 1 group -- the sequence-parallel layout in its chunks, each collective a
+    real RCCL launch on a one-rank group (OneRankTP: no xGMI transfer time) -- the embedding lookup
     and the lm_head's vocab shard (ColumnParallel, V / tp) plus the cross-entropy -- on the vocab
     shard (functional.VocabParallelCEFunction, the shipped form) or, with PICOTRON_VP_CE=0, over the
-    gathered vocabulary as the reference -- fwd + bwd.  Returns the JSON line."""
+    gathered vocabulary as the reference -- fwd + bwd, eager and (--graph 1, how the product TP path
+    runs: train.GraphedTrainStep) replayed as one HIP graph.  Returns the JSON line."""
     import math
     from picotron_amd import functional as FN
     from picotron_amd import kernels as K
     from picotron_amd import process_group_manager as pgm
+    from picotron_amd.tensor_parallel import sequence_parallel as SPM
     from picotron_amd.train import MI355X_BF16_DENSE_PEAK, make_config
     pgm.setup_process_group_manager(1, 1, 1, 1)
     tp = args.tp_proxy
@@ -129,6 +188,7 @@ def tp_proxy(args, base, layers):
     nh, nkv, d = cfg.num_attention_heads // tp, cfg.num_key_value_heads // tp, cfg.hidden_size // cfg.num_attention_heads
     T = args.mbs * args.seq
     dev = torch.device("cuda")
+    group = init_one_rank_group(dev)
     g = torch.Generator(device=dev).manual_seed(0)
 
     def u(o, i):
@@ -155,60 +215,32 @@ def tp_proxy(args, base, layers):
         def backward(ctx, g):
             return g[:, :g.shape[1] // tp]
 
-    class _RowGatherStandIn(torch.autograd.Function):
-        """sequence_parallel.GatherFromSequenceRegion (the exit all-gather) as one rank sees it:
-        forward a [T, H] buffer (the no-op collective's, filled once), backward this rank's rows of
-        the gradient -- the autograd edge back into the layers must stay."""
-
-        @staticmethod
-        def forward(ctx, x):
-            return _TPNoComm(None, tp, 0).all_gather_rows(x).clone()
-
-        @staticmethod
-        def backward(ctx, g):
-            return g[:g.shape[0] // tp]
-
     from picotron_amd.switches import S as SW
-    sp = tp > 1 and SW.tp_sp != 0 and args.seq % tp == 0   # sequence parallelism (sequence_parallel.py)
+    # sequence parallelism (sequence_parallel.py) in the layout's chunks (0: not shardable)
+    chunks = SPM.layout_chunks(args.mbs, args.seq, tp) if tp > 1 and SW.tp_sp != 0 else 0
     vp = tp > 1 and FN.vp_ce_shape_ok(T, V // tp, H)          # the lm_head's vocab-parallel CE
 
     def micro_batch():
         x = FN.embedding(ids, emb)
-        if sp:   # this rank's token rows of the residual stream (the entry hook's slice)
-            x = x.view(T, H)[:T // tp].view(args.mbs, args.seq // tp, H)
+        if chunks:   # the entry: this rank's rows of the summed lookups (reduce-scatter)
+            x = SPM.ReduceScatterToSequenceRegion.apply(x, chunks)
+        else:
+            FN.TPContext.current().all_reduce(x)
         for w in stack:
-            x = FN.DecoderLayerFunction.apply(x, *w, cos, sin, cfg.rms_norm_eps, 0, nh, nkv, d, False, sp)
-        if sp:   # the exit hook's all-gather before the final norm
-            x = _RowGatherStandIn.apply(x.reshape(T // tp, H))
+            x = FN.DecoderLayerFunction.apply(x, *w, cos, sin, cfg.rms_norm_eps, 0, nh, nkv, d, False, chunks)
+        if chunks:   # the exit's all-gather before the final norm
+            x = SPM.GatherFromSequenceRegion.apply(x, chunks)
         if vp:   # the vocab-parallel CE (functional.VocabParallelCEFunction): no logits gather
-            lg, stats = FN.lm_head_shard(x.view(T, H), head)
+            lg, stats = FN.lm_head_shard(x.reshape(T, H), head)
             full = FN.vp_logits(lg, stats, 0, V, lambda: _GatherStandIn.apply(lg))
         else:
-            lg = FN.linear(x.view(T, H), head)                     # this rank's vocab shard
+            lg = FN.linear(x.reshape(T, H), head)                  # this rank's vocab shard
             full = _GatherStandIn.apply(lg) if tp > 1 else lg       # stands in for the all-gather
         FN.cross_entropy(full, tgt).backward()
-    # the layers see a tp group of `tp` ranks whose all-reduces are no-ops, so they take the TP
-    # launch forms (dX and dW as separate launches around the dX all-reduce), not tp = 1's duals
-    gathered = {}
-
-    class _TPNoComm(FN.TPContext):
-        """The tp group's collectives as no-ops, as the compute-only proxy treats the all-reduces:
-        the all-gather hands back a [T, H] buffer of this shape (filled once, then reused -- the
-        values do not matter to the timing), the reduce-scatter this rank's rows of its input."""
-
-        def all_reduce(self, t, async_op=False):
-            return None
-
-        def all_gather_rows(self, t):
-            key = (tuple(t.shape), t.dtype)
-            if key not in gathered:
-                gathered[key] = torch.cat([t] * self.world_size)
-            return gathered[key]
-
-        def reduce_scatter_rows(self, t, async_op=False):
-            return t[:t.shape[0] // self.world_size], None
+    # the layers see a tp group of `tp` ranks (one-rank RCCL collectives), so they take the TP
+    # launch forms (dX and dW as separate launches around the dX reduce-scatter), not tp = 1's duals
     current = FN.TPContext.current
-    FN.TPContext.current = staticmethod(lambda: _TPNoComm(None, tp, 0))
+    FN.TPContext.current = staticmethod(lambda: OneRankTP(group, tp))
     try:
         probe = K.GemmProbe()
         for _ in range(args.warmup + 1):
@@ -219,15 +251,16 @@ def tp_proxy(args, base, layers):
         t = t_eager = _events_time(micro_batch, args.steps)
         graph_note = None
         if args.graph:
-            # at the shard widths the ~425 launches of a micro-batch outrun their kernels on the host
-            # (Python + autograd + ctypes per launch): capture the micro-batch (fwd, CE, bwd) as one
-            # HIP graph and replay it -- how a TP deployment issues this fixed sequence
+            # the product TP path's launch mode (train.GraphedTrainStep): the micro-batch (fwd, CE,
+            # bwd, the RCCL collectives) captured as one HIP graph and replayed
             try:
                 side = torch.cuda.Stream()
                 side.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(side):
                     micro_batch()
                 torch.cuda.current_stream().wait_stream(side)
+                from picotron_amd.train import quiesce_collectives
+                quiesce_collectives(dev)
                 graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(graph):
                     micro_batch()
@@ -243,16 +276,19 @@ def tp_proxy(args, base, layers):
     fpt_rank = 6 * sum(p.numel() for w in stack for p in w) + 6 * head.numel() + 12 * layers * nh * d * args.seq
     ach = s["avg_flop"] / (s["avg_ms"] * 1e-3) / 1e12
     tok_gpu = T / t / tp          # tp ranks share these tokens
-    from picotron_amd.train import SMOLLM_1_7B  # noqa: F401
-    return {"metric": f"TP={tp} per-rank compute proxy (1 GPU, no collectives)", "value": tok_gpu,
-            "unit": "tokens/s/GPU (compute-only upper bound)", "ms_per_microbatch": t * 1e3,
-            "launch": "hip graph replay" if (args.graph and graph_note is None) else "eager",
-            "eager_ms_per_microbatch": t_eager * 1e3, **({"graph_note": graph_note} if graph_note else {}),
+    dist.destroy_process_group()
+    return {"metric": f"TP={tp} per-rank compute proxy (1 GPU, one-rank RCCL collectives: no xGMI transfer time)",
+            "value": tok_gpu, "unit": "tokens/s/GPU (compute + collective launches, no link time)",
+            "ms_per_microbatch": t * 1e3,
+            "launch": "hip graph replay (as train.GraphedTrainStep runs the TP path)"
+            if (args.graph and graph_note is None) else "eager",
+            "eager_ms_per_microbatch": t_eager * 1e3, "eager_tokens_per_s_per_gpu": T / t_eager / tp,
+            **({"graph_note": graph_note} if graph_note else {}),
             "mfu_upper_bound": tok_gpu * (fpt_rank * tp) / MI355X_BF16_DENSE_PEAK,
             "config": {"model": cfg_name(base), "layers": layers, "micro_batch": args.mbs, "seq_len": args.seq,
                        "shard": {"q|k|v": 3 * nh * d, "I": I, "heads": nh, "vocab": V // tp},
-                       "sequence_parallel": sp, "vocab_parallel_ce": vp},
-            "roofline": {"bound": "mfma", "kernel": "gemm (every GEMM launch of one micro-batch)", "achieved": ach,
+                       "sequence_parallel": bool(chunks), "sp_chunks": chunks, "vocab_parallel_ce": vp},
+            "roofline": {"bound": "mfma", "kernel": "gemm (every GEMM launch of one eager micro-batch)", "achieved": ach,
                          "peak": MI355X_BF16_DENSE_PEAK / 1e12, "unit": "TFLOP/s",
                          "frac": ach / (MI355X_BF16_DENSE_PEAK / 1e12), "launches": s["launches"],
                          "gemm_share": s["total_ms"] * 1e-3 / t},
@@ -535,8 +571,8 @@ def build_parser():
     ap.add_argument("--pp-engine", choices=["1f1b", "afab"], default="1f1b", help="pipeline schedule (train.py:222-225)")
     ap.add_argument("--tp-proxy", type=int, default=0, help="1 GPU: one TP rank's compute at this degree")
     ap.add_argument("--cp-proxy", type=int, default=0, help="1 GPU: the CP ring's critical rank at this degree")
-    ap.add_argument("--graph", type=int, default=1, help="--tp-proxy: time the micro-batch as a captured HIP graph "
-                                                         "(0: eager launches only)")
+    ap.add_argument("--graph", type=int, default=1, help="tp > 1 (and --tp-proxy): run each micro-batch as a "
+                                                         "replayed HIP graph (train.GraphedTrainStep; 0: eager)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo: rehearse an N-rank grid with every rank on cuda:0 (one-GPU box); timing meaningless")
     ap.add_argument("--mbs", type=int, default=4)
@@ -654,6 +690,10 @@ def main():
         # on all ~550 GEMM launches of a step costs ~5 % of the step on ROCm
         K._PROBE = probe if (probe is not None and i == probe_mb) else None
 
+    # tensor parallelism: the micro-batch replayed as one HIP graph (its RCCL collectives inside)
+    graphed = None
+    if args.graph and tp > 1 and args.backend == "nccl" and TR.GraphedTrainStep.supported(model):
+        graphed = TR.GraphedTrainStep(model, loader, device)
     if pp > 1:
         from picotron_amd.pipeline_parallel import pipeline_parallel as PPE
         pp_step = PPE.train_step_pipeline_1f1b if args.pp_engine == "1f1b" else PPE.train_step_pipeline_afab
@@ -671,7 +711,10 @@ def main():
         # is enqueued behind the backward before the host reads the loss (train_step(read_loss=False)),
         # and the next step's zero_grad (set_to_none: drops the gradients, stream-ordered) runs while
         # the AdamW launch does -- same work, no GPU idle gap at the boundary
-        loss = train_step(model, loader, device, on_microbatch=sample, read_loss=False)
+        if graphed is not None:
+            loss = graphed(read_loss=False)
+        else:
+            loss = train_step(model, loader, device, on_microbatch=sample, read_loss=False)
         optimizer.step()
         if hasattr(model, "reset"):
             model.reset()
@@ -690,7 +733,7 @@ def main():
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     losses = []
-    probe = K.GemmProbe() if not (args.no_probe or pp > 1) else None
+    probe = K.GemmProbe() if not (args.no_probe or pp > 1 or graphed is not None) else None
     for i in range(args.steps):
         losses.append(step())
         log(f"step {i}: loss {losses[-1]:.4f}")
@@ -763,6 +806,7 @@ def main():
                           "model": model_name, "layers": layers, "micro_batch": args.mbs,
                           "grad_acc": args.grad_acc, "global_batch": args.mbs * args.grad_acc * dp,
                           "seq_len": args.seq, "parallelism": par + ("-bucket" if force_dp else ""),
+                          "launch": "hip graph replay per micro-batch" if graphed is not None else "eager",
                           **({"bucket_mb": args.bucket_mb, "grad_type": args.grad_type}
                              if (m.cp_dp_world_size > 1 or force_dp) else {})},
                "roofline": roofline, "cpu_baseline": cpu}

@@ -61,15 +61,17 @@ def _grad_ready(p):
         hook(p)
 
 
-def wgrad(dy2d, x2d, params):
+def wgrad(dy2d, x2d, params, notify=True):
     """dW_i = dY_i^T X for the column segments of dY; one launch when the sinks agree.  Parameters
-    with requires_grad=False get no gradient (autograd leaves their .grad alone)."""
+    with requires_grad=False get no gradient (autograd leaves their .grad alone).  notify=False: a
+    partial gradient (one token chunk of a chunked sequence-parallel layer, the sum is not complete
+    yet): the owner is not told."""
     if not all(p.requires_grad for p in params):
         lo = 0
         for p in params:
             n = p.shape[0]
             if p.requires_grad:
-                wgrad(dy2d[:, lo:lo + n], x2d, [p])
+                wgrad(dy2d[:, lo:lo + n], x2d, [p], notify)
             lo += n
         return
     targets = [_wgrad_target(p) for p in params]
@@ -82,11 +84,12 @@ def wgrad(dy2d, x2d, params):
             n = p.shape[0]
             K.linear_wgrad(dy2d[:, lo:lo + n], x2d, [t], epilogue=e)
             lo += n
-    for p in params:
-        _grad_ready(p)
+    if notify:
+        for p in params:
+            _grad_ready(p)
 
 
-def wgrad_group(jobs):
+def wgrad_group(jobs, notify=True):
     """Several wgrads [(dy2d, x2d, params), ...] in one grouped launch when every sink takes the
     same epilogue (else one wgrad() per job)."""
     frozen = any(not p.requires_grad for _, _, params in jobs for p in params)
@@ -94,16 +97,17 @@ def wgrad_group(jobs):
     epis = {e for tg in targets for _, e in tg}
     if frozen or len(epis) != 1:
         for dy2d, x2d, params in jobs:
-            wgrad(dy2d, x2d, params)
+            wgrad(dy2d, x2d, params, notify)
         return
     K.linear_wgrad_grouped([(dy2d, x2d, [t for t, _ in tg]) for (dy2d, x2d, _), tg in zip(jobs, targets)],
                            epilogue=epis.pop())
-    for _, _, params in jobs:
-        for p in params:
-            _grad_ready(p)
+    if notify:
+        for _, _, params in jobs:
+            for p in params:
+                _grad_ready(p)
 
 
-def dgrad_with_wgrad(dy2d, weights, wjobs, gu=None, keep_parts=False, split_min=None, order=None):
+def dgrad_with_wgrad(dy2d, weights, wjobs, gu=None, keep_parts=False, split_min=None, order=None, notify=True):
     """dX = dY . [W_0; ...] (with gu: the down_proj dX's SwiGLU backward, dg|du) AND the wgrads
     wjobs [(dy2d, x2d, params)] of the same layer in ONE launch (K.linear_dgrad_dual) when the
     shapes tile for it and every sink takes one epilogue; otherwise the separate launches.
@@ -129,12 +133,13 @@ def dgrad_with_wgrad(dy2d, weights, wjobs, gu=None, keep_parts=False, split_min=
                 for p, (t, e) in zip(params, tg):
                     K.linear_wgrad(dy[:, lo:lo + p.shape[0]], x, [t], epilogue=e)
                     lo += p.shape[0]
-        for _, _, params in wjobs:
-            for p in params:
-                _grad_ready(p)
+        if notify:
+            for _, _, params in wjobs:
+                for p in params:
+                    _grad_ready(p)
         return dx
     dx = K.linear_dgrad_swiglu(dy2d, weights[0], gu) if gu is not None else K.linear_dgrad(dy2d, weights)
-    wgrad_group(wjobs)
+    wgrad_group(wjobs, notify)
     return dx
 
 
@@ -285,11 +290,17 @@ class TPContext:
             return t
         t = t.contiguous()
         out = torch.empty((self.world_size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        if self._nccl():
-            dist.all_gather_into_tensor(out, t, group=self.group)
-        else:   # gloo (CPU tests, one-GPU rehearsals): the list form
-            dist.all_gather(list(out.chunk(self.world_size)), t, group=self.group)
+        self.all_gather_rows_into(out, t)
         return out
+
+    def all_gather_rows_into(self, out, t, async_op=False):
+        """t [n, ...] (this rank's rows) -> out [world * n, ...] (a contiguous buffer or row block of
+        one; rank i's rows at i * n).  Returns the work handle (async_op, RCCL) or None (done)."""
+        if self._nccl():
+            return dist.all_gather_into_tensor(out, t.contiguous(), group=self.group, async_op=async_op)
+        # gloo (CPU tests, one-GPU rehearsals): the list form, synchronous
+        dist.all_gather(list(out.chunk(self.world_size)), t.contiguous(), group=self.group)
+        return None
 
     def reduce_scatter_rows(self, t, async_op=False):
         """[world * n, ...] partial sums -> (this rank's [n, ...] rows of their sum, handle or None)."""
@@ -303,6 +314,41 @@ class TPContext:
             return out, h
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)   # gloo: the sum, then my rows
         return t[self.rank * n:(self.rank + 1) * n], None
+
+    def reduce_scatter_rows_into(self, out, t, async_op=False):
+        """t [world * n, ...] partial sums -> out [n, ...] (a contiguous buffer or row block of one) =
+        this rank's rows of their sum.  Returns the work handle (async_op, RCCL) or None (done)."""
+        if self._nccl():
+            return dist.reduce_scatter_tensor(out, t.contiguous(), op=dist.ReduceOp.SUM, group=self.group,
+                                              async_op=async_op)
+        n = out.shape[0]
+        t = t.clone()
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)   # gloo: the sum, then my rows
+        out.copy_(t[self.rank * n:(self.rank + 1) * n])
+        return None
+
+    # the chunked token-row layout (sequence parallelism with c chunks, tensor_parallel/
+    # sequence_parallel.py): the flattened [T, ...] rows are c chunks of T / c rows (whole sequences);
+    # rank r holds rows [r n, (r + 1) n) of every chunk (n = T / (c world)), chunk after chunk, so
+    # chunk j's all-gather / reduce-scatter is one collective of its own that the layer issues as
+    # soon as chunk j's producer is done and waits for only where chunk j's consumer starts
+    def gather_chunk(self, full, shard, c, j, async_op=False):
+        """Chunk j of the shard [T / world, ...] -> rows of chunk j of full [T, ...]; handle or None."""
+        n = shard.shape[0] // c
+        return self.all_gather_rows_into(full[j * n * self.world_size:(j + 1) * n * self.world_size],
+                                         shard[j * n:(j + 1) * n], async_op=async_op)
+
+    def scatter_chunk(self, shard, part, c, j, async_op=False):
+        """Partial sums of chunk j's rows (part [T / c, ...]) -> chunk j's rows of the shard
+        [T / world, ...] (their sum over the group); handle or None."""
+        n = shard.shape[0] // c
+        return self.reduce_scatter_rows_into(shard[j * n:(j + 1) * n], part, async_op=async_op)
+
+
+def wait_all(handles):
+    for h in handles:
+        if h is not None:
+            h.wait()
 
 
 def _contig2d(x):
@@ -487,13 +533,22 @@ class _VPInfo:
         return self.full
 
 
+def _standin(info, shape, path, requires_grad):
+    """A data-less [shape] HipLogits (a 0-dim tensor expanded: no storage of that size) carrying the
+    vocab shards `info` and the view path from the gathered logits.  It requires grad when the
+    shard does (its own autograd history is a dummy: F.cross_entropy on it differentiates the shard
+    through VocabParallelCEFunction, any other op through the gathered logits)."""
+    ph = torch.empty((), dtype=info.shard.dtype, device=info.shard.device, requires_grad=requires_grad)
+    out = ph.expand(*shape).as_subclass(HipLogits)
+    out._pt_vp, out._pt_vp_path = info, path
+    return out
+
+
 def vp_logits(shard, stats, vocab_lo, vocab, materialize):
     """The stand-in for the gathered [..., vocab] logits of the vocab shard `shard` [..., Vs]
     (columns vocab_lo ..); `materialize()` gathers the real logits (GatherFromModelParallelRegion)."""
-    ph = torch.empty((), dtype=shard.dtype, device=shard.device).expand(*shard.shape[:-1], vocab)
-    out = ph.as_subclass(HipLogits)
-    out._pt_vp, out._pt_vp_path = _VPInfo(shard, stats, vocab_lo, vocab, materialize), ()
-    return out
+    return _standin(_VPInfo(shard, stats, vocab_lo, vocab, materialize), tuple(shard.shape[:-1]) + (vocab,), (),
+                    shard.requires_grad)
 
 
 def _vp_real(t):
@@ -548,6 +603,34 @@ class VocabParallelCEFunction(torch.autograd.Function):
         return dl.view(ctx.shape), None, None, None, None, None, None
 
 
+_ROW_VIEWS = (torch.Tensor.view, torch.Tensor.reshape, torch.Tensor.flatten)
+
+
+def _vp_path_form(path, ndim):
+    """Which of the reference's two cross-entropy call forms the view path from the gathered
+    [..., V] logits (ndim dims) is, so that the shard rows meet their targets in order: 'rows' --
+    only view / reshape / flatten (on the contiguous gathered logits they never reorder rows:
+    train.py:49's view(-1, V)) -- or 'bvs' -- exactly one transpose(1, 2) / permute(0, 2, 1) of a 3-D
+    [B, S, V] (pipeline_parallel.py:103,153); None for any other path (rows possibly reordered: the
+    caller gathers the logits and runs on them, as the reference does).  contiguous() reorders
+    nothing and is skipped."""
+    ops = [(f, a, kw) for f, a, kw in path if f is not torch.Tensor.contiguous]
+    if all(f in _ROW_VIEWS for f, _, _ in ops):
+        return "rows"
+    if len(ops) != 1 or ndim != 3:
+        return None
+    f, a, kw = ops[0]
+    dims = tuple(a) + tuple(kw.values())
+    if len(dims) == 1 and isinstance(dims[0], (tuple, list)):
+        dims = tuple(dims[0])
+    dims = tuple(int(x) % 3 for x in dims)
+    if f is torch.Tensor.transpose and sorted(dims) == [1, 2]:
+        return "bvs"
+    if f is torch.Tensor.permute and dims == (0, 2, 1):
+        return "bvs"
+    return None
+
+
 def _vp_cross_entropy(input, target, reduction, ignore_index):
     """cross_entropy on a stand-in in one of the reference's two forms -- [N, V] rows (train.py:49)
     or [B, V, S] = transpose(1, 2) of [B, S, V] (pipeline_parallel.py:103,153) -- else None."""
@@ -556,9 +639,11 @@ def _vp_cross_entropy(input, target, reduction, ignore_index):
     lead = tuple(shard.shape[:-1])
     rows = shard.numel() // shard.shape[-1]
     target = _plain(target)
-    if input.dim() == 2 and tuple(input.shape) == (rows, V) and target.dim() == 1 and target.numel() == rows:
+    form = _vp_path_form(input._pt_vp_path, shard.dim())
+    if form == "rows" and input.dim() == 2 and tuple(input.shape) == (rows, V) and target.dim() == 1 and \
+            target.numel() == rows:
         out_shape = (rows,)
-    elif input.dim() == 3 and len(lead) == 2 and tuple(input.shape) == (lead[0], V, lead[1]) and \
+    elif form == "bvs" and input.dim() == 3 and len(lead) == 2 and tuple(input.shape) == (lead[0], V, lead[1]) and \
             tuple(target.shape) == lead:
         out_shape = lead
     else:
@@ -642,10 +727,14 @@ def _dual_qkv_enabled():
     return SW.dual_qkv != 0
 
 
-def attn_block_bwd(da, h2, saved, wq, wk, wv, wo, cos, sin, sh, tp, need_dx=True, keep_parts=False, sp=False):
+def attn_block_bwd(da, h2, saved, wq, wk, wv, wo, cos, sin, sh, tp, need_dx=True, keep_parts=False, sp=False,
+                   rs_out=None, notify=True):
     """keep_parts: the q|k|v dX may come back as K.SplitKParts (two f32 K halves) for a following
     rmsnorm backward to sum.  sp: the column-parallel dX is reduce-scattered onto this rank's token
-    rows (sequence parallelism) instead of all-reduced."""
+    rows (sequence parallelism) instead of all-reduced.  rs_out: one token chunk of the chunked
+    sequence-parallel layer -- the dX reduce-scatter writes rs_out and is NOT waited for: its handle
+    is returned (the next chunk's work runs under it); notify=False: this chunk's weight gradients
+    are partial sums (wgrad)."""
     qkv, o, lse = saved
     scale = 1.0 / math.sqrt(sh.d)
     do2 = K.linear_dgrad(da, [wo])
@@ -660,14 +749,18 @@ def attn_block_bwd(da, h2, saved, wq, wk, wv, wo, cos, sin, sh, tp, need_dx=True
     dh = handle = None
     if need_dx:
         dh = K.linear_dgrad(dqkv, [wq, wk, wv])
-        if sp:
+        if rs_out is not None:
+            handle = tp.reduce_scatter_rows_into(rs_out, dh, async_op=True)
+        elif sp:
             dh, handle = tp.reduce_scatter_rows(dh, async_op=True)
         else:
             handle = tp.all_reduce(dh, async_op=True)
     # dW of q|k|v and of o_proj in one launch: 192 + 64 tiles of 256x256 at SmolLM-1.7B dims,
     # where either alone leaves CUs idle (o_proj's wgrad was deferred from above; its inputs
     # da and o stay alive until here anyway)
-    wgrad_group([(dqkv, h2, [wq, wk, wv]), (da, o.view(sh.T, sh.wq), [wo])])
+    wgrad_group([(dqkv, h2, [wq, wk, wv]), (da, o.view(sh.T, sh.wq), [wo])], notify)
+    if rs_out is not None:
+        return handle
     if handle is not None:
         handle.wait()
     return dh
@@ -722,21 +815,23 @@ def _dual_gu_enabled():
 GU_DUAL_ORDER = 1
 
 
-def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True, keep_parts=False, sp=False):
+def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True, keep_parts=False, sp=False, rs_out=None,
+                  notify=True):
     """keep_parts: the gate|up dX may come back as K.SplitKParts (its split-K halves unsummed) for a
     following rmsnorm backward to sum.  sp: the column-parallel dX is reduce-scattered onto this
-    rank's token rows instead of all-reduced."""
+    rank's token rows instead of all-reduced.  rs_out / notify: one token chunk of the chunked
+    sequence-parallel layer (attn_block_bwd): returns the reduce-scatter's handle, not waited for."""
     gu, hh = saved
     I = wg.shape[0]
     if _fuse() and K.swiglu_fuse_pays(dm.shape[0], I, backward=True):   # SwiGLU bwd in the down dX epilogue
         # ... in one launch with the down_proj dW: the epilogue's HBM-bound g|u / dg|du tail
         # overlaps the dW's MFMA work (K.linear_dgrad_dual)
-        dgu = dgrad_with_wgrad(dm, [wd], [(dm, hh, [wd])], gu=gu)
+        dgu = dgrad_with_wgrad(dm, [wd], [(dm, hh, [wd])], gu=gu, notify=notify)
     else:
         dhh = K.linear_dgrad(dm, [wd])
         dgu = torch.empty_like(gu)
         K.swiglu_bwd(dhh, gu[:, :I], gu[:, I:], dg=dgu[:, :I], du=dgu[:, I:])
-        wgrad(dm, hh, [wd])
+        wgrad(dm, hh, [wd], notify)
     dh = handle = None
     split = SW.gu_splitk != 0
     if need_dx and tp.world_size == 1 and _dual_gu_enabled() and \
@@ -751,11 +846,15 @@ def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True, keep_parts=False,
                                 split_min=None if split else 1 << 30, order=GU_DUAL_ORDER)
     if need_dx:
         dh = K.linear_dgrad(dgu, [wg, wu])
-        if sp:
+        if rs_out is not None:
+            handle = tp.reduce_scatter_rows_into(rs_out, dh, async_op=True)
+        elif sp:
             dh, handle = tp.reduce_scatter_rows(dh, async_op=True)
         else:
             handle = tp.all_reduce(dh, async_op=True)
-    wgrad(dgu, h2, [wg, wu])
+    wgrad(dgu, h2, [wg, wu], notify)
+    if rs_out is not None:
+        return handle
     if handle is not None:
         handle.wait()
     return dh
@@ -792,10 +891,10 @@ class DecoderLayerFunction(torch.autograd.Function):
     shard (cos / sin its positions' tables): the ring runs on it with no re-lay."""
 
     @staticmethod
-    def forward(ctx, x, w1, w2, wq, wk, wv, wo, wg, wu, wd, cos, sin, eps, mode, nh, nkv, d, zz=False, sp=False):
-        if sp:
+    def forward(ctx, x, w1, w2, wq, wk, wv, wo, wg, wu, wd, cos, sin, eps, mode, nh, nkv, d, zz=False, sp=0):
+        if sp:   # sp = the chunk count of the sequence-parallel layout (0: the replicated stream)
             return DecoderLayerFunction._forward_sp(ctx, x, w1, w2, wq, wk, wv, wo, wg, wu, wd, cos, sin, eps, mode,
-                                                    nh, nkv, d)
+                                                    nh, nkv, d, int(sp))
         ctx.sp = False
         B, S, H = x.shape
         sh = AttnShape(B, S, nh, nkv, d, zz)
@@ -811,49 +910,91 @@ class DecoderLayerFunction(torch.autograd.Function):
         return out.view(B, S, H)
 
     @staticmethod
-    def _forward_sp(ctx, x, w1, w2, wq, wk, wv, wo, wg, wu, wd, cos, sin, eps, mode, nh, nkv, d):
+    def _forward_sp(ctx, x, w1, w2, wq, wk, wv, wo, wg, wu, wd, cos, sin, eps, mode, nh, nkv, d, c):
         """Sequence-parallel TP layer (tensor_parallel/sequence_parallel.py): x is this rank's shard
-        of the residual stream, token rows [r T/tp, (r+1) T/tp) of the flattened [B*S, H] batch, viewed
-        as [B, S/tp, H].  The norms and residual adds run on the shard; the column-parallel inputs
-        are all-gathered ([T, H], as the reference's replicated norm output), the row-parallel outputs
-        reduce-scattered onto the shards (the reference's all-reduce, keeping only this rank's rows):
+        of the residual stream in the chunked token-row layout (TPContext.gather_chunk: c chunks of
+        B / c whole sequences; rank r holds rows [r n, (r + 1) n) of each), viewed [B, S/tp, H].  The
+        norms and residual adds run on the shard; the column-parallel inputs are all-gathered (the
+        reference's replicated norm output), the row-parallel outputs reduce-scattered onto the shards
+        (the reference's all-reduce, keeping this rank's rows):
 
             h1 = AG(norm1(x));  a = RS(attn(h1));  z = x + a (fused into norm2);  h2 = AG(norm2(z))
             out = z + RS(mlp(h2))
 
-        The same values as the reference's layer (model.py:204-209 with tp_communications.py:35-49),
-        row by row; per rank the norms / adds touch T/tp rows instead of T."""
+        chunk by chunk: every chunk's all-gather is issued at once (RCCL runs them in order on its
+        stream), chunk j's block waits only for chunk j's rows, and its reduce-scatter is issued as
+        soon as its GEMM is done -- so chunk j + 1's all-gather runs under chunk j's GEMMs and
+        attention, chunk j's reduce-scatter under chunk j + 1's (tp_communications.py:35-49 moves the
+        same bytes with nothing beside them).  The same values as the reference's layer
+        (model.py:204-209), row by row; per rank the norms / adds touch T/tp rows instead of T."""
         tp = TPContext.current()
         B, Sl, H = x.shape
-        S = Sl * tp.world_size
-        sh = AttnShape(B, S, nh, nkv, d)
+        W = tp.world_size
+        S = Sl * W
+        Tc = B // c * S                                # gathered rows per chunk
+        sh = AttnShape(B // c, S, nh, nkv, d)
         x2 = _contig2d(x)
         h1r, rstd1, _ = K.rmsnorm_fwd(x2, w1, eps, mode)
-        h1 = tp.all_gather_rows(h1r)
-        a, asaved = attn_block_fwd(h1, wq, wk, wv, wo, cos, sin, sh, tp, reduce=False)
-        ar, _ = tp.reduce_scatter_rows(a)
+        h1 = torch.empty(B * S, H, dtype=x2.dtype, device=x2.device)
+        ag = [tp.gather_chunk(h1, h1r, c, j, async_op=True) for j in range(c)]
+        ar = torch.empty_like(x2)
+        asaved, rs = [], []
+        for j in range(c):
+            wait_all(ag[j:j + 1])
+            a, sv = attn_block_fwd(h1[j * Tc:(j + 1) * Tc], wq, wk, wv, wo, cos, sin, sh, tp, reduce=False)
+            asaved += list(sv)
+            rs.append(tp.scatter_chunk(ar, a, c, j, async_op=True))
+        wait_all(rs)
         h2r, rstd2, z = K.rmsnorm_fwd(ar, w2, eps, mode, residual=x2)
-        h2 = tp.all_gather_rows(h2r)
-        m, msaved = mlp_block_fwd(h2, wg, wu, wd, tp, reduce=False)
-        mr, _ = tp.reduce_scatter_rows(m)
-        out = K.residual_add(z, mr.contiguous())
-        ctx.save_for_backward(x2, h1, rstd1, *asaved, z, h2, rstd2, *msaved,
-                              w1, w2, wq, wk, wv, wo, wg, wu, wd, cos, sin)
-        ctx.sh, ctx.mode, ctx.sp = sh, mode, True
+        h2 = torch.empty_like(h1)
+        ag = [tp.gather_chunk(h2, h2r, c, j, async_op=True) for j in range(c)]
+        mr = torch.empty_like(x2)
+        msaved, rs = [], []
+        for j in range(c):
+            wait_all(ag[j:j + 1])
+            m, sv = mlp_block_fwd(h2[j * Tc:(j + 1) * Tc], wg, wu, wd, tp, reduce=False)
+            msaved += list(sv)
+            rs.append(tp.scatter_chunk(mr, m, c, j, async_op=True))
+        wait_all(rs)
+        out = K.residual_add(z, mr)
+        ctx.save_for_backward(x2, h1, rstd1, z, h2, rstd2, w1, w2, wq, wk, wv, wo, wg, wu, wd, cos, sin,
+                              *asaved, *msaved)
+        ctx.sh, ctx.mode, ctx.sp, ctx.c = sh, mode, True, c
         return out.view(B, Sl, H)
 
     @staticmethod
     def _backward_sp(ctx, dout):
-        (x2, h1, rstd1, qkv, o, lse, z, h2, rstd2, gu, hh,
-         w1, w2, wq, wk, wv, wo, wg, wu, wd, cos, sin) = ctx.saved_tensors
-        sh, mode = ctx.sh, ctx.mode
+        x2, h1, rstd1, z, h2, rstd2, w1, w2, wq, wk, wv, wo, wg, wu, wd, cos, sin, *rest = ctx.saved_tensors
+        sh, mode, c = ctx.sh, ctx.mode, ctx.c
+        asaved, msaved = rest[:3 * c], rest[3 * c:]
         tp = TPContext.current()
+        Tc = sh.T
         dout2 = _contig2d(dout)                       # [T/tp, H]: the residual's gradient rows
-        dm = tp.all_gather_rows(dout2)                # the row-parallel down_proj sees every row
-        dh2 = mlp_block_bwd(dm, h2, (gu, hh), wg, wu, wd, tp, sp=True)
+        # the row-parallel down_proj sees every row: chunk j's rows gathered while chunk j - 1's MLP
+        # backward runs; chunk j's dX reduce-scatter runs under chunk j + 1's
+        dm = torch.empty_like(h2)
+        ag = [tp.gather_chunk(dm, dout2, c, j, async_op=True) for j in range(c)]
+        dh2 = torch.empty_like(dout2)
+        rs = []
+        for j in range(c):
+            wait_all(ag[j:j + 1])
+            rows = slice(j * Tc, (j + 1) * Tc)
+            n = dout2.shape[0] // c
+            rs.append(mlp_block_bwd(dm[rows], h2[rows], msaved[2 * j:2 * j + 2], wg, wu, wd, tp,
+                                    rs_out=dh2[j * n:(j + 1) * n], notify=j == c - 1))
+        wait_all(rs)
         dz = norm_bwd(dh2, z, w2, rstd2, mode, dres=dout2, sp=tp)
-        da = tp.all_gather_rows(dz)
-        dh1 = attn_block_bwd(da, h1, (qkv, o, lse), wq, wk, wv, wo, cos, sin, sh, tp, sp=True)
+        da = torch.empty_like(h1)
+        ag = [tp.gather_chunk(da, dz, c, j, async_op=True) for j in range(c)]
+        dh1 = torch.empty_like(dout2)
+        rs = []
+        for j in range(c):
+            wait_all(ag[j:j + 1])
+            rows = slice(j * Tc, (j + 1) * Tc)
+            n = dout2.shape[0] // c
+            rs.append(attn_block_bwd(da[rows], h1[rows], asaved[3 * j:3 * j + 3], wq, wk, wv, wo, cos, sin, sh, tp,
+                                     rs_out=dh1[j * n:(j + 1) * n], notify=j == c - 1))
+        wait_all(rs)
         dx = norm_bwd(dh1, x2, w1, rstd1, mode, dres=dz, sp=tp)
         return (dx.view(dout.shape),) + (None,) * 18
 
@@ -968,6 +1109,12 @@ class HipLogits(torch.Tensor):
         kwargs = kwargs or {}
         if func is torch.nn.functional.cross_entropy:
             return _dispatch_cross_entropy(*args, **kwargs)
+        if func is torch.Tensor.contiguous and args and _is_vp(args[0]):
+            # the stand-in stays one: recorded on its path (replayed on a gather, if ever), nothing
+            # allocated -- a real contiguous() of the expanded stand-in would write a [T, V] buffer
+            t = args[0]
+            return _standin(t._pt_vp, tuple(t.shape), t._pt_vp_path + ((func, tuple(args[1:]), dict(kwargs)),),
+                            t.requires_grad)
         if args and _is_vp(args[0]) and (func in cls._KEEP or func in _VP_META or
                                          getattr(func, "__name__", "") == "__get__"):
             # a view of the vocab-parallel stand-in stays one (its path replayed on a gather, if ever);

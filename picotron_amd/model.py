@@ -26,7 +26,6 @@ from . import functional as FN
 from . import kernels as K
 from . import process_group_manager as pgm
 from .context_parallel import context_parallel
-from .tensor_parallel import sequence_parallel
 
 
 def _flash():
@@ -264,7 +263,7 @@ class DecoderLayer(nn.Module):
         # the residual stream (RoPE rows: that shard's positions, _tables) whenever its length tiles
         self.cp_zigzag_residual = False
         # set by tensor_parallel.apply_tensor_parallel at tp > 1: the input is this rank's token-row
-        # shard of the residual stream whenever the batch was sharded (sequence_parallel.local_len)
+        # shard of the residual stream whenever the batch was sharded (the model's SPState)
         self.tp_sequence_parallel = False
 
     def _tables(self, device, zz_len=0):
@@ -289,8 +288,11 @@ class DecoderLayer(nn.Module):
         n1, n2, at, mlp = self.input_layernorm, self.post_attention_layernorm, self.attention, self.mlp
         if _norm_mode(n1) != _norm_mode(n2) or _norm_eps(n1) != _norm_eps(n2):
             raise ValueError("DecoderLayer: both norms must be the same flavour")
-        # a token-row shard of the residual stream (tensor_parallel/sequence_parallel.py)?
-        sp = self.tp_sequence_parallel and sequence_parallel.local_len() == x.shape[1]
+        # a token-row shard of the residual stream (tensor_parallel/sequence_parallel.py)?  Then
+        # sp = its layout's chunk count (the model's SPState, set by this forward's entry)
+        st = getattr(self, "_pt_sp_state", None)
+        sp = st.chunks if (self.tp_sequence_parallel and st is not None and st.local_len and
+                           st.local_len == x.shape[1]) else 0
         return FN.DecoderLayerFunction.apply(
             x, n1.weight, n2.weight, *at.weights(), mlp.gate_proj.weight, mlp.up_proj.weight, mlp.down_proj.weight,
             cos, sin, _norm_eps(n1), _norm_mode(n1), at.num_local_heads, at.num_local_kv_heads, at.head_dim, zz, sp)

@@ -30,8 +30,10 @@ DEFAULTS = {
     # context_parallel.py: the zig-zag (load-balanced) ring where it tiles, the residual stream kept
     # in that layout across the decoder stack, the full-mesh K|V / dK|dV exchange instead of the ring
     "ring_zigzag": 1, "zigzag_residual": 1, "ring_mesh": 1,
-    # tensor_parallel/sequence_parallel.py: the residual stream sharded by token rows over the tp group
-    "tp_sp": 1,
+    # tensor_parallel/sequence_parallel.py: the residual stream sharded by token rows over the tp group,
+    # in a layout of (up to) this many chunks, whose collectives overlap the other chunks' GEMMs
+    # (0 = auto: chunks of >= 4096 token rows)
+    "tp_sp": 1, "tp_sp_chunks": 0,
     # functional.py: the TP lm_head's F.cross_entropy on the vocab shards (no logits all-gather)
     "vp_ce": 1,
     # native (libpicotron_hip.so, pt_set_variant)

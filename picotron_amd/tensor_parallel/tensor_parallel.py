@@ -175,4 +175,8 @@ class VocabParallelEmbedding(nn.Module):
         # the masked lookup (ids outside this rank's slice -> zero rows, no gradient) in one kernel
         output_parallel = FN.embedding(x, self.weight, self.vocab_start_index, self.vocab_end_index,
                                        self.padding_idx)
+        state = getattr(self, "_pt_sp_state", None)
+        if state is not None:   # sequence parallelism: reduce-scatter the partial lookups into the shards
+            from .sequence_parallel import enter
+            return enter(state, output_parallel, partial=True)
         return ReduceFromModelParallelRegion.apply(output_parallel)

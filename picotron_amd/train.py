@@ -89,7 +89,11 @@ def train_step(model, data_loader, device, on_microbatch=None, read_loss=True):
     read_loss=False: return the loss as a device scalar instead, so that the caller can enqueue the
     optimizer step before the host waits for the backward (`read_step_loss` reads it then): reading it
     here idles the GPU for the optimizer's host work (~1.5 ms at SmolLM-1.7B), and the AdamW launch that
-    follows an idle gap runs at the idle clocks, 3.4 vs 2.8 ms (profiles/r05/notes_r05.md)."""
+    follows an idle gap runs at the idle clocks, 3.4 vs 2.8 ms (profiles/r05/notes_r05.md).  Note that
+    read_loss=False also postpones the device-status check (a bad cross-entropy target: NaN rows and
+    gradients) to `read_step_loss`, i.e. after an optimizer step enqueued in between has already
+    applied those gradients -- bench.py's ordering; a training loop that must not update weights
+    from a flagged step reads the loss (read_loss=True) before its optimizer step."""
     acc_loss = torch.zeros((), dtype=torch.float32, device=device)
     # (bench.py --dp-bucket: a 1-rank DataParallelBucket syncs like N > 1 would)
     requires_grad_sync = pgm.current().cp_dp_world_size > 1 or getattr(model, "_force_grad_sync", False)
@@ -111,8 +115,121 @@ def train_step(model, data_loader, device, on_microbatch=None, read_loss=True):
     return read_step_loss(acc_loss, device) if read_loss else acc_loss
 
 
+def quiesce_collectives(device, poll_s=0.35):
+    """Before a HIP-graph capture that contains RCCL collectives: wait for the device to drain, then
+    for torch's NCCL watchdog thread (it polls its list of in-flight works about every 100 ms) to
+    retire the works the eager collectives left in it, so that it queries no event of RCCL's stream
+    while that stream is part of the capture (GraphedTrainStep's docstring).  One-time cost per
+    capture."""
+    import time
+    torch.cuda.synchronize(device)
+    if torch.distributed.is_initialized():
+        time.sleep(poll_s)
+
+
+class GraphedTrainStep:
+    """train_step (train.py:29-55) with the micro-batch -- forward, F.cross_entropy / grad_acc on the
+    fused HIP kernel, backward, the loss accumulation -- captured ONCE as a HIP graph and replayed for
+    every later micro-batch.  For tensor parallelism: at the TP = 8 shard widths a micro-batch is
+    ~425 short kernels plus its RCCL collectives, and launching them from Python + autograd + ctypes
+    costs more host time than the GPU spends on them (bench.py --tp-proxy: 9.8 ms eager vs 6.5 ms
+    replayed per SmolLM-1.7B micro-batch); a replay issues the same launches -- the collectives
+    included, each on RCCL's stream with its fork / join edges as the eager layer issues them --
+    from one call.
+
+    Contract (what a replay can and cannot re-decide):
+      * the micro-batch's input / target ids are copied into static device buffers before each
+        replay; every micro-batch has the shape of the first;
+      * the gradients are this object's: the captured weight-gradient epilogues accumulate into
+        fixed .grad buffers, so each call re-attaches them to the parameters (an optimizer's
+        zero_grad(set_to_none=True) in between is fine) and zeroes them in place before its first
+        micro-batch (one multi-tensor launch);
+      * no data-parallel wrapper, no CP / PP (their per-micro-batch host decisions -- the bucket
+        all-reduce on the last micro-batch, the ring's host-side schedule, the pipeline's p2p
+        order -- would be frozen into the graph): `supported(model)` says whether it applies;
+      * on RCCL, the capture starts only after torch's NCCL watchdog has retired every eager
+        collective (`quiesce_collectives`): once the first captured collective joins RCCL's stream
+        to the capture, HIP refuses a query of any event recorded on that stream ("operation not
+        permitted on an event last recorded in a capturing stream") -- and the watchdog thread polls
+        the end events of the works still in its list (seen intermittently on the one-rank tests
+        before this wait).
+    The first call runs its first `warmup` micro-batches eagerly on a side stream (they are real
+    micro-batches: their gradients count), captures the next, replays it, and replays the rest;
+    later calls only replay."""
+
+    def __init__(self, model, data_loader, device, warmup=2):
+        if not GraphedTrainStep.supported(model):
+            raise ValueError("GraphedTrainStep: data-parallel wrappers, CP and PP are not captured")
+        self.model, self.loader, self.device = model, data_loader, torch.device(device)
+        self.warmup = max(1, warmup)
+        self.graph = None
+        self.params = [p for p in model.parameters() if p.requires_grad]
+        self.grads = None
+        self.acc = torch.zeros((), dtype=torch.float32, device=self.device)
+
+    @staticmethod
+    def supported(model):
+        m = pgm.current()
+        return not hasattr(model, "bucket_manager") and not getattr(model, "_force_grad_sync", False) and \
+            m.cp_world_size == 1 and m.pp_world_size == 1 and m.cp_dp_world_size == 1
+
+    def _micro_batch(self, input_ids, target_ids):
+        outputs = self.model(input_ids=input_ids)
+        batch_size, seq_len = input_ids.shape
+        outputs = outputs.view(seq_len * batch_size, -1)
+        loss = FN.cross_entropy(outputs, target_ids.reshape(-1), reduction="mean") / self.loader.grad_acc_steps
+        loss.backward()
+        self.acc += loss.detach().float()
+
+    def _capture(self, batch):
+        self.ids = batch["input_ids"].to(self.device).clone()
+        self.tgt = batch["target_ids"].to(self.device).clone()
+        # every parameter's gradient must exist (allocated eagerly, outside the graph's pool) so the
+        # captured epilogues accumulate into buffers this object keeps
+        missing = [p for p in self.params if p.grad is None]
+        if missing:
+            raise RuntimeError(f"GraphedTrainStep: {len(missing)} parameters got no gradient in the warm-up")
+        self.grads = [p.grad for p in self.params]
+        quiesce_collectives(self.device)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._micro_batch(self.ids, self.tgt)
+
+    def __call__(self, on_microbatch=None, read_loss=True):
+        """One optimizer step's worth of micro-batches; returns the accumulated loss (float, or the
+        device scalar with read_loss=False: see train_step)."""
+        ga = self.loader.grad_acc_steps
+        self.acc.zero_()
+        if self.grads is not None:
+            for p, g in zip(self.params, self.grads):
+                if p.grad is not g:
+                    p.grad = g
+            torch._foreach_zero_(self.grads)
+        for i in range(ga):
+            if on_microbatch is not None:
+                on_microbatch(i)
+            batch = next(self.loader)
+            if self.graph is None and i < self.warmup:
+                side = torch.cuda.Stream(self.device)
+                side.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(side):
+                    self._micro_batch(batch["input_ids"].to(self.device), batch["target_ids"].to(self.device))
+                torch.cuda.current_stream(self.device).wait_stream(side)
+                continue
+            if self.graph is None:
+                self._capture(batch)
+            else:
+                self.ids.copy_(batch["input_ids"])
+                self.tgt.copy_(batch["target_ids"])
+            self.graph.replay()
+        loss = self.acc.clone()
+        return read_step_loss(loss, self.device) if read_loss else loss
+
+
 def read_step_loss(acc_loss, device):
-    """The step's loss as a float (one host <-> device synchronisation), then the device status check."""
+    """The step's loss as a float (one host <-> device synchronisation), then the device status check
+    (HipKernelError on a bad cross-entropy target) -- called after an optimizer step that was enqueued
+    first (train_step(read_loss=False)), the check comes after that update."""
     out = acc_loss.item()
     K.check_device_status(torch.device(device))   # the host has synchronised: surface device asserts
     return out

@@ -669,7 +669,44 @@ def _sp_host(rank, world):
     for (n, p), q in zip(toy.named_parameters(), ref_toy.parameters()):
         assert torch.allclose(p.grad, q.grad), n
     toy(torch.randn(B, S + 1, H))
-    assert toy.seen == (B, S + 1, H) and SPM.local_len() == 0
+    assert toy.seen == (B, S + 1, H) and toy._pt_sp_state.local_len == 0
+    # a forward that raised between the entry and the exit: the next model forward starts unsharded
+    toy._pt_sp_state.local_len = S // world
+    toy(torch.randn(B, S + 1, H))
+    assert toy._pt_sp_state.local_len == 0
+    # the chunked layout (c = 2 chunks of one sequence each): rank r holds rows [r n, (r+1) n) of
+    # every chunk; the per-chunk collectives, the entry reduce-scatter and the exit gather
+    c, n2 = 2, B * S // (2 * world)
+    mine2 = torch.cat([full[j * B * S // c + rank * n2: j * B * S // c + (rank + 1) * n2] for j in range(c)])
+    from picotron_amd import switches
+    with switches.override(tp_sp_chunks=2):
+        assert SPM.layout_chunks(B, S, world) == 2 and SPM.layout_chunks(B, S + 1, world) == 0
+        assert SPM.layout_chunks(1, S, world) == 1 and SPM.layout_chunks(3, S, world) == 1
+    # auto: chunks of >= 4096 rows (BASELINE's mbs 4 x seq 1024: one chunk; mbs 8: two)
+    assert SPM.layout_chunks(B, S, world) == 1 and SPM.layout_chunks(4, 1024, 8) == 1
+    assert SPM.layout_chunks(8, 1024, 8) == 2 and SPM.layout_chunks(16, 1024, 8) == 4
+    assert torch.equal(SPM.shard_rows(full, tp, c), mine2)
+    assert torch.equal(SPM.gather_rows(mine2, tp, c), full)
+    out = torch.empty_like(full)
+    for j in range(c):
+        assert tp.gather_chunk(out, mine2, c, j, async_op=True) is None   # gloo: synchronous
+    assert torch.equal(out, full)
+    shard = torch.empty_like(mine2)
+    for j in range(c):
+        tp.scatter_chunk(shard, (full * (rank + 1))[j * B * S // c:(j + 1) * B * S // c], c, j)
+    assert torch.equal(shard, mine2 * sum(range(1, world + 1)))
+    xp = (full * (rank + 1)).view(B, S, H).requires_grad_(True)     # this rank's partial lookups
+    sh2 = SPM.ReduceScatterToSequenceRegion.apply(xp, c)
+    assert torch.equal(sh2.reshape(-1, H), mine2 * sum(range(1, world + 1)))
+    y2 = SPM.GatherFromSequenceRegion.apply(sh2 * 2, c)
+    assert torch.equal(y2, 2 * full.view(B, S, H) * sum(range(1, world + 1)))
+    y2.backward(g)
+    assert torch.equal(xp.grad, 2 * g)
+    x3 = full.view(B, S, H).clone().requires_grad_(True)
+    sh3 = SPM.ScatterToSequenceRegion.apply(x3, c)
+    assert torch.equal(sh3.reshape(-1, H), mine2)
+    SPM.GatherFromSequenceRegion.apply(sh3, c).backward(g)
+    assert torch.equal(x3.grad, g)
 
 
 @pytest.mark.parametrize("world", [2, 4])

@@ -65,25 +65,25 @@ def _setup(tp, cp, seq=256, cfg_over=None):
         for n, p in names.items():
             p.copy_(_shard(full[n], p, m.tp_rank))
     g = torch.Generator().manual_seed(11)
-    ids = torch.randint(0, CFG["vocab_size"], (2, seq + 1), generator=g)
+    ids = torch.randint(0, base["vocab_size"], (2, seq + 1), generator=g)
     # the oracle on the full model, fp32 from the same bf16 weights
     pf = {k: v.float().requires_grad_(True) for k, v in full.items()}
     cos, sin = O.get_cos_sin(seq, 64, base=CFG["rope_theta"])
     lo = O.llama_forward(ids[:, :-1], pf, dict(base), cos.float(), sin.float(), norm=O.rmsnorm_flash_semantics)
-    loss_r = F.cross_entropy(lo.reshape(-1, CFG["vocab_size"]), ids[:, 1:].reshape(-1))
+    loss_r = F.cross_entropy(lo.reshape(-1, base["vocab_size"]), ids[:, 1:].reshape(-1))
     loss_r.backward()
     return m, model, names, pf, ids, lo, loss_r
 
 
 def _llama(rank, world, tp, cp, seq=256, zigzag=False, residual=1, mesh=1, production_thresholds=False, sp=1,
-           cfg_over=None):
+           cfg_over=None, chunks=2):
     from picotron_amd import switches
     # conftest.py zeroes the RoPE / SwiGLU fusion tile thresholds for the small test shapes;
     # production_thresholds restores the shipped ones (96 / 192 / 0), under which these TP-shard
     # widths take the split (GEMM + separate rope / swiglu kernel) paths
     thr = dict(rope_fuse_min_tiles=96, swiglu_fuse_min_tiles=192, swiglu_bwd_min_tiles=0) \
         if production_thresholds else {}
-    with switches.override(zigzag_residual=residual, ring_mesh=mesh, tp_sp=sp, **thr):
+    with switches.override(zigzag_residual=residual, ring_mesh=mesh, tp_sp=sp, tp_sp_chunks=chunks, **thr):
         _llama_body(rank, world, tp, cp, seq, zigzag, residual, cfg_over)
 
 
@@ -92,16 +92,17 @@ def _llama_body(rank, world, tp, cp, seq, zigzag, residual, cfg_over=None):
     from picotron_amd import switches
     from picotron_amd.context_parallel import context_parallel as CP
     m, model, names, pf, ids, lo, loss_r = _setup(tp, cp, seq, cfg_over)
+    V = dict(CFG, **(cfg_over or {}))["vocab_size"]
     # sequence parallelism (tensor_parallel/sequence_parallel.py): on at tp > 1 without cp, by default
     sp_on = tp > 1 and cp == 1 and switches.S.tp_sp != 0
     assert all(layer.tp_sequence_parallel == sp_on for layer in model.decoder_layers)
     gathers = []
-    orig_ag = FN.TPContext.all_gather_rows
+    orig_ag = FN.TPContext.all_gather_rows_into
 
-    def counted_ag(self, t):
+    def counted_ag(self, out, t, async_op=False):
         gathers.append(tuple(t.shape))
-        return orig_ag(self, t)
-    FN.TPContext.all_gather_rows = counted_ag
+        return orig_ag(self, out, t, async_op)
+    FN.TPContext.all_gather_rows_into = counted_ag
     if residual:   # what the data-parallel wrappers do at cp > 1 (the grads are checked summed over cp)
         CP.enable_zigzag_residual(model)
     s = seq // cp
@@ -119,22 +120,26 @@ def _llama_body(rank, world, tp, cp, seq, zigzag, residual, cfg_over=None):
         logits = model(x.cuda())
         n_fwd = len(calls)
         n_ag_fwd = len(gathers)
-        assert logits.shape == (2, s, CFG["vocab_size"])             # final_proj gathers its vocab shards
-        loss = FN.cross_entropy(logits.view(-1, CFG["vocab_size"]), t.reshape(-1).cuda())
+        assert logits.shape == (2, s, V)             # final_proj gathers its vocab shards
+        loss = FN.cross_entropy(logits.view(-1, V), t.reshape(-1).cuda())
         loss.backward()
         torch.cuda.synchronize()
     finally:
         CP.zigzag_exchange = orig
-        FN.TPContext.all_gather_rows = orig_ag
+        FN.TPContext.all_gather_rows_into = orig_ag
     L, H = CFG["num_hidden_layers"], dict(CFG, **(cfg_over or {}))["hidden_size"]
     # the vocab-parallel CE (functional.VocabParallelCEFunction): one gather of 16 B per row at tp > 1
     vp = [g for g in gathers if g == (2 * s, 4)]
-    vp_on = tp > 1 and FN.vp_ce_shape_ok(2 * s, CFG["vocab_size"] // tp, H)   # tp 8: V / tp = 64 does not tile
+    vp_on = tp > 1 and FN.vp_ce_shape_ok(2 * s, V // tp, H)   # V 512 at tp 8: V / tp = 64 does not tile
+    assert vp_on == (tp > 1 and (V // tp) % 128 == 0 and switches.S.vp_ce != 0)
     assert len(vp) == (1 if vp_on else 0), gathers
     gathers = [g for g in gathers if g != (2 * s, 4)]
-    if sp_on:   # per layer 2 gathers each way, plus the exit (forward) / the entry (backward)
-        assert n_ag_fwd == 2 * L + 1 and len(gathers) == 4 * L + 2, gathers
-        assert all(g == (2 * s // tp, H) for g in gathers), gathers   # every gather is of T / tp rows
+    if sp_on:   # per layer and chunk 2 gathers each way, plus the exit (forward) / the entry (backward)
+        from picotron_amd.tensor_parallel import sequence_parallel as SPM
+        c = SPM.layout_chunks(2, s, tp)
+        assert c == (min(2, switches.S.tp_sp_chunks) if switches.S.tp_sp_chunks > 0 else 1), c   # B 2
+        assert n_ag_fwd == c * (2 * L + 1) and len(gathers) == c * (4 * L + 2), gathers
+        assert all(g == (2 * s // (tp * c), H) for g in gathers), gathers   # every gather is of T / (tp c) rows
     else:
         assert not gathers
     if zigzag and residual:
@@ -170,6 +175,12 @@ def test_tensor_parallel_llama_tp2_production_thresholds():
     _dist.run(_llama, 2, 2, 1, 256, False, 1, 1, True, device="cuda")
 
 
+def test_tensor_parallel_llama_tp2_one_chunk():
+    """tp2 with the sequence-parallel layout in one chunk (PICOTRON_TP_SP_CHUNKS=1: rank r holds rows
+    [r T/tp, (r+1) T/tp), every collective of a block in one piece)."""
+    _dist.run(_llama, 2, 2, 1, 256, False, 1, 1, False, 1, None, 1, device="cuda")
+
+
 def test_tensor_parallel_llama_tp2_replicated_stream():
     """tp2 without sequence parallelism (PICOTRON_TP_SP=0): the reference's replicated residual
     stream and row-parallel all-reduces."""
@@ -187,6 +198,16 @@ def test_tensor_parallel_llama_tp8():
     """config 3's TP degree: 8 ranks (gloo on cuda:0), one q head and one kv head each, the residual
     stream sharded 64 token rows per rank, against the oracle on the full model."""
     over = dict(hidden_size=512, intermediate_size=1024, num_attention_heads=8, num_key_value_heads=8)
+    _dist.run(_llama, 8, 8, 1, 256, False, 1, 1, False, 1, over, device="cuda")
+
+
+def test_tensor_parallel_llama_tp8_vocab_parallel_ce():
+    """config 3's shipped lm_head path at world 8: V 2048 (V / 8 = 256 columns per rank tile the
+    lm_head GEMM's CE statistics), so the vocab-parallel cross-entropy runs (asserted in the body:
+    one 16-B-per-row gather) with sequence parallelism on -- loss, logits and every gradient against
+    the oracle on the full model."""
+    over = dict(hidden_size=512, intermediate_size=1024, num_attention_heads=8, num_key_value_heads=8,
+                vocab_size=2048)
     _dist.run(_llama, 8, 8, 1, 256, False, 1, 1, False, 1, over, device="cuda")
 
 
@@ -448,7 +469,7 @@ def _vp_ce(rank, world):
     from picotron_amd.tensor_parallel.tensor_parallel import ColumnParallelLinear
     torch.cuda.set_device(0)
     m = pgm.setup_process_group_manager(tp_size=world, cp_size=1, pp_size=1, dp_size=1)
-    B, S, H, V = 2, 256, 128, 1024
+    B, S, H, V = 2, 256, 128, 512 * world      # V / world = 256: the vocab shards tile the CE statistics
     g = torch.Generator().manual_seed(5)
     w_full = (torch.randn(V, H, generator=g) * 0.05).to(torch.bfloat16)
     x_full = torch.randn(B, S, H, generator=g).to(torch.bfloat16)
@@ -460,9 +481,15 @@ def _vp_ce(rank, world):
         lin.weight.copy_(w_full.narrow(0, m.tp_rank * (V // world), V // world))
     ref_loss = F.cross_entropy(x_full.float().reshape(-1, H) @ w_full.float().t(), tgt.reshape(-1))
     res = {}
+    # the reference's two call forms and, through the same views, permute / contiguous spellings of
+    # them; 'seqmajor' reorders the rows (sequence-major) with matching targets -- not a form the shard
+    # rows can serve in order, so the stand-in gathers the logits and runs on them
+    forms = ("rows", "bvs", "permute", "contig", "seqmajor")
     for vp in (1, 0):
-        for form in ("rows", "bvs"):
+        for form in forms:
             for red in ("mean", "sum", "none"):
+                if form in ("permute", "contig", "seqmajor") and red != "mean":
+                    continue
                 with switches.override(vp_ce=vp):
                     x = x_full.cuda().requires_grad_(True)
                     lin.weight.grad = None
@@ -470,8 +497,17 @@ def _vp_ce(rank, world):
                     assert FN._is_vp(logits) == bool(vp) and logits.shape == (B, S, V)
                     if form == "rows":
                         loss = F.cross_entropy(logits.view(-1, V), tgt.reshape(-1).cuda(), reduction=red)
-                    else:
+                    elif form == "bvs":
                         loss = F.cross_entropy(logits.transpose(1, 2), tgt.cuda(), reduction=red)
+                    elif form == "permute":
+                        loss = F.cross_entropy(logits.permute(0, 2, 1), tgt.cuda(), reduction=red)
+                    elif form == "contig":
+                        loss = F.cross_entropy(logits.contiguous().view(-1, V), tgt.reshape(-1).cuda(), reduction=red)
+                    else:
+                        loss = F.cross_entropy(logits.transpose(0, 1).reshape(-1, V), tgt.t().reshape(-1).cuda(),
+                                               reduction=red)
+                    if vp:   # the shard path ran (no gather) exactly where the rows are in order
+                        assert (logits._pt_vp.full is not None) == (form == "seqmajor"), form
                     (loss.float().sum() if red == "none" else loss.float()).backward()
                     torch.cuda.synchronize()
                     res[(vp, form, red)] = (loss.detach().float().cpu(), x.grad.float().cpu(),
@@ -487,5 +523,6 @@ def _vp_ce(rank, world):
         assert _rel(logits.float(), full) < 1e-2 and _rel(logits.view(-1, V)[3], full.view(-1, V)[3]) < 1e-2
 
 
-def test_vocab_parallel_cross_entropy_tp2():
-    _dist.run(_vp_ce, 2, device="cuda")
+@pytest.mark.parametrize("world", [2, 8])
+def test_vocab_parallel_cross_entropy(world):
+    _dist.run(_vp_ce, world, device="cuda")
