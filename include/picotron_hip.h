@@ -339,7 +339,6 @@ int pt_attn_bwd_split(const void* q, const int64_t* q_str, const void* k, const 
  * switches.py reads PICOTRON_<NAME> once at import and pushes them here).  Names and defaults:
  *   "attn_pair"     1   causal attention: pair query/key blocks (i, n-1-i) per workgroup
  *   "attn_split"    2   dK/dV kernel form per head dim: bit 0 = d64, bit 1 = d128 use the wave pair
- *   "gemm_group_m" -1   GEMM tile-rows per group of the tile order (-1 = 6; n > 0: n rows)
  *   "gemm_mix"      1   q|k|v + RoPE GEMM as one mixed 256x256 / 256x128 launch
  *   "gemm_kh"       2   auto-picked 256x128 tiles as tile 14 (K-halves) when K >= 4096; 0 never
  *   "attn_kv_chunk" 4   few-head attention (pt_attn_split_plan): K / Q tiles per work item (even;

@@ -14,7 +14,7 @@
 #include "../../include/picotron_hip.h"
 
 // measurement variants (pt_set_variant, csrc/variants.hip): read by the launchers, never the kernels
-enum PtVariant { PT_VAR_ATTN_PAIR = 0, PT_VAR_ATTN_SPLIT, PT_VAR_GEMM_GROUP_M, PT_VAR_GEMM_MIX, PT_VAR_GEMM_KH,
+enum PtVariant { PT_VAR_ATTN_PAIR = 0, PT_VAR_ATTN_SPLIT, PT_VAR_GEMM_MIX, PT_VAR_GEMM_KH,
                  PT_VAR_ATTN_KV_CHUNK, PT_VAR_COUNT };
 int pt_variant(PtVariant v);
 

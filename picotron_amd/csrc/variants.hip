@@ -7,7 +7,7 @@
 namespace {
 struct VariantDef { const char* name; int value; };
 VariantDef g_variants[PT_VAR_COUNT] = {
-    {"attn_pair", 1}, {"attn_split", 2}, {"gemm_group_m", -1}, {"gemm_mix", 1}, {"gemm_kh", 2}, {"attn_kv_chunk", 4}};
+    {"attn_pair", 1}, {"attn_split", 2}, {"gemm_mix", 1}, {"gemm_kh", 2}, {"attn_kv_chunk", 4}};
 
 int find(const char* name) {
   if (!name) return -1;

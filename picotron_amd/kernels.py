@@ -585,30 +585,6 @@ def swiglu_dx_ksplit(T, I, H):
     return s
 
 
-def fewtile_ksplit(M, N, K):
-    """(ksplit, tile) for a forward / dX GEMM whose output tiles leave most of the 256 CUs idle -- the
-    TP-shard projections (TP = 8 at SmolLM-1.7B: the q|k|v forward 4096 x 768 is 48 tiles of
-    256x256, the o_proj dX 4096 x 256 only 16): K-slices of the phased 256x256 (256x128 when N only
-    tiles by 128) kernel, the largest power of two that keeps the launch within one round of the
-    256 CUs and every slice >= 256 deep, summed by pt_gemm_splitk_reduce through the GEMM's own
-    epilogue (bf16 store / residual add).  The small-tile kernels the unsplit launch would take
-    (128x128, 64x64) run at a third of the phased rate per CU.  (1, -1) = unsplit."""
-    if not _ksplit_enabled() or not SW.fewtile or M % 256 or M < 2048 or K < 1024:
-        return 1, -1
-    if N % 256 == 0:
-        tile, tiles = 12, (M // 256) * (N // 256)
-    elif N % 128 == 0:
-        tile, tiles = 13, (M // 256) * (N // 128)
-    else:
-        return 1, -1
-    if tiles >= 96:
-        return 1, -1
-    s = 1
-    while s < 16 and tiles * s * 2 <= 256 and K % (s * 2 * 64) == 0 and K // (s * 2) >= 256:
-        s *= 2
-    return (s, tile) if s > 1 else (1, -1)
-
-
 def hq_form(mnks, extra_tiles=0):
     """K-slices (1 or 2) for a group of few-tile problems [(M, N, K)] on the 128x128 k-substep tile
     (15), or 0 when it does not apply.  It applies where the phased 256x256 tiles leave most of the 256
@@ -620,7 +596,7 @@ def hq_form(mnks, extra_tiles=0):
     (tools/tp_gemm_ab.py, profiles/r05/tp_gemm_ab_r05c.log), against the 256x256 K-slice forms:
     q|k|v forward 22.1 vs 34.4 us, o_proj dX 20.7 vs 25.8, q|k|v + o dW 34.4 vs 42.6, gate|up dW
     40.6 vs 49.9, down_proj dW 31.6 vs 38.6."""
-    if not _ksplit_enabled() or not SW.fewtile_hq or any(m % 128 or n % 128 for m, n, _ in mnks):
+    if not _ksplit_enabled() or any(m % 128 or n % 128 for m, n, _ in mnks):
         return 0
     t12 = sum((m // 256) * (n // 256) if m % 256 == 0 and n % 256 == 0 else (m * n) // 65536 for m, n, _ in mnks)
     if t12 >= 96 or any(m < 2048 and k < 2048 for m, _, k in mnks):
@@ -785,11 +761,6 @@ def linear_fwd(x2d, weights, out=None, tile=-1, residual=None):
     elif hq == 2 and _reduce_sink_ok(y, residual):
         return _gemm_ksplit(x2d, x2d.stride(0), 1, weights, [K] * len(weights), _bounds(ns), 1, 0, y, T, N, K, 2, 15,
                             epi, residual=residual, ldr=ldr)
-    if tile < 0 and _reduce_sink_ok(y, residual):
-        s, t = fewtile_ksplit(T, N, K)
-        if s > 1 and all(n % (256 if t == 12 else 128) == 0 for n in ns):
-            return _gemm_ksplit(x2d, x2d.stride(0), 1, weights, [K] * len(weights), _bounds(ns), 1, 0, y, T, N, K, s, t,
-                                epi, residual=residual, ldr=ldr)
     _gemm(x2d, x2d.stride(0), 1, weights, [K] * len(weights), _bounds(ns), 1, 0, [y], [y.stride(0)], [0, T],
           T, N, K, epi, tile, residual=residual, ldr=ldr)
     return y
@@ -1103,11 +1074,6 @@ def linear_dgrad(dy2d, weights, out=None, accumulate=False, tile=-1):
     elif hq == 2 and _reduce_sink_ok(dx):
         return _gemm_ksplit(dy2d, dy2d.stride(0), 1, weights, [Kin] * len(weights), _bounds(ns), 0, 1, dx, T, Kin,
                             N, 2, 15, EPI_BF16_ACC if accumulate else EPI_BF16)
-    if tile < 0 and _reduce_sink_ok(dx):
-        s, t = fewtile_ksplit(T, Kin, N)
-        if s > 1 and all(n % 64 == 0 for n in ns):
-            return _gemm_ksplit(dy2d, dy2d.stride(0), 1, weights, [Kin] * len(weights), _bounds(ns), 0, 1, dx, T, Kin,
-                                N, s, t, EPI_BF16_ACC if accumulate else EPI_BF16)
     _gemm(dy2d, dy2d.stride(0), 1, weights, [Kin] * len(weights), _bounds(ns), 0, 1, [dx], [dx.stride(0)],
           [0, T], T, Kin, N, EPI_BF16_ACC if accumulate else EPI_BF16, tile)
     return dx
@@ -1118,11 +1084,10 @@ def dual_enabled():
     return SW.dual != 0
 
 
-def _dual_order():
-    """0: dX tiles first in every XCD, 1: dW first, 2 (default): staggered -- even XCDs dX first, odd XCDs
-    dW first, so half the chip is in the dX tiles' HBM-bound SwiGLU-backward tail at a time (+0.8 %
-    on the step, profiles/r03/dual_order_ab.txt)."""
-    return SW.dual_order
+# the dual launch's XCD order unless a caller picks one: 0 = dX tiles first in every XCD, 1 = dW
+# first, 2 = staggered -- even XCDs dX first, odd XCDs dW first, so half the chip is in the dX tiles'
+# HBM-bound SwiGLU-backward tail at a time (+0.8 % on the step over 0 / 1, profiles/r03/dual_order_ab.txt)
+DUAL_ORDER = 2
 
 
 def dual_fits(dgrad_mn, wgrad_mns):
@@ -1220,7 +1185,7 @@ def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None, keep
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
     if order is None:
-        order = _dual_order()
+        order = DUAL_ORDER
         # unsplit dX tiles longer (in K) than the dW tiles: dX first on every XCD, the dW tiles
         # chaining on the other CUs around them (a dW-first XCD would start its dX tiles last)
         if e0 == EPI_BF16 and wjobs and N > max(dy.shape[0] for dy, _, _ in wjobs):

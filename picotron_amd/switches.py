@@ -25,7 +25,7 @@ DEFAULTS = {
     # launches and their XCD order, the norm backward fed by split-K halves, the attention
     # backward's fused delta, and the tile-count thresholds below which the RoPE / SwiGLU epilogues
     # run as separate kernels (TP shard widths)
-    "ksplit": 1, "fewtile": 1, "fewtile_hq": 1, "swiglu_splitk": 1, "splitk2": 1, "splitk2_min": 8192, "dual": 1, "dual_order": 2, "norm_splitk": 1,
+    "ksplit": 1, "swiglu_splitk": 1, "splitk2": 1, "splitk2_min": 8192, "dual": 1, "norm_splitk": 1,
     "fuse_delta": 1, "rope_fuse_min_tiles": 96, "swiglu_fuse_min_tiles": 192, "swiglu_bwd_min_tiles": 0,
     # context_parallel.py: the zig-zag (load-balanced) ring where it tiles, the residual stream kept
     # in that layout across the decoder stack, the full-mesh K|V / dK|dV exchange instead of the ring
@@ -37,9 +37,9 @@ DEFAULTS = {
     # functional.py: the TP lm_head's F.cross_entropy on the vocab shards (no logits all-gather)
     "vp_ce": 1,
     # native (libpicotron_hip.so, pt_set_variant)
-    "attn_pair": 1, "attn_split": 2, "gemm_group_m": -1, "gemm_mix": 1, "gemm_kh": 2, "attn_kv_chunk": 4,
+    "attn_pair": 1, "attn_split": 2, "gemm_mix": 1, "gemm_kh": 2, "attn_kv_chunk": 4,
 }
-NATIVE = ("attn_pair", "attn_split", "gemm_group_m", "gemm_mix", "gemm_kh", "attn_kv_chunk")
+NATIVE = ("attn_pair", "attn_split", "gemm_mix", "gemm_kh", "attn_kv_chunk")
 
 
 class _Switches:

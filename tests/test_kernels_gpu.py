@@ -979,14 +979,14 @@ def test_cross_entropy_mean_kernel():
 
 @pytest.mark.parametrize("M,N,K,kind,residual", [(4096, 768, 2048, "fwd", False), (4096, 256, 2048, "dgrad", False),
                                                  (4096, 512, 2048, "fwd", True), (2048, 384, 1024, "fwd", False)])
-def test_fewtile_splitk_matches_single_pass(monkeypatch, M, N, K, kind, residual):
+def test_fewtile_forms_match_single_pass(monkeypatch, M, N, K, kind, residual):
     """The TP-shard forward / dX GEMMs whose tiles leave most CUs idle (SmolLM-1.7B at TP = 8: the
-    q|k|v forward 4096 x 768 x 2048, the o_proj dX 4096 x 256 x 2048) run as K-slices of the phased
-    kernel + the reduce pass (kernels.fewtile_ksplit): against an f32 reference and the unsplit
-    launch (PICOTRON_KSPLIT=0), equal up to the f32 summation order (<= 2 bf16 ulps)."""
+    q|k|v forward 4096 x 768 x 2048, the o_proj dX 4096 x 256 x 2048) run on the 128x128 k-substep
+    tile, as 2 K-slices + the reduce pass where its tiles still fill half a round (kernels.hq_form):
+    against an f32 reference and the unsplit launch (PICOTRON_KSPLIT=0), equal up to the f32
+    summation order (<= 2 bf16 ulps)."""
     from picotron_amd import kernels as K_
-    s, t = K_.fewtile_ksplit(M, N, K)
-    assert s > 1, (M, N, K)
+    assert K_.hq_form([(M, N, K) if kind == "fwd" else (M, N, K)]) >= 1, (M, N, K)
     if kind == "fwd":
         x = torch.randn(M, K).to(BF).to(DEV)
         ws = [(torch.randn(n, K) / math.sqrt(K)).to(BF).to(DEV) for n in (N // 2, N // 2)]

@@ -27,13 +27,6 @@ def test_wgrad_ksplit_fills_one_round():
         assert K.wgrad_ksplit([(q, H, T), (H, o, T)]) == 1
 
 
-def test_fewtile_ksplit_for_tp_projections():
-    assert K.fewtile_ksplit(T, 3 * H // 8, H) == (4, 12)   # q|k|v forward: 48 tiles x 4
-    assert K.fewtile_ksplit(T, H // 8, H) == (8, 12)       # o_proj dX: 16 tiles x 8
-    assert K.fewtile_ksplit(T, H, H) == (1, -1)            # 128 tiles: unsplit
-    assert K.fewtile_ksplit(1024, 256, 2048) == (1, -1)    # short M: unsplit
-
-
 def test_splitk_halves_for_long_k_dx():
     assert K._splitk_halves(T, H, 2 * I) == I              # gate|up dX: two K-8192 halves
     assert K._splitk_halves(T, H, V) == V // 2             # lm_head dX
@@ -67,5 +60,5 @@ def test_hq_form_for_tp_shards():
     assert K.hq_form([(T, 3 * H, H)]) == 0                       # TP = 1
     assert K.hq_form([(1024, 256, 1024)]) == 0                   # small shapes keep the old forms
     assert K.hq_form([(T, 192, H)]) == 0                         # not on 128-column tiles
-    with switches.override(fewtile_hq=0):
+    with switches.override(ksplit=0):
         assert K.hq_form([(T, 3 * H // 8, H)]) == 0

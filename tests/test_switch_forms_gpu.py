@@ -23,11 +23,8 @@ CONFIGS = {"a": dict(S=1024, H=1024, I=4096, nh=16, nkv=8, V=2048), "b": dict(S=
 # overrides on top of FORCE; the order is that of tools/switch_kernels.py, which traces what each changes
 CASES = [("a", {})] + [("a", {k: v}) for k, v in (
     ("fuse", 0), ("norm_defer", 0), ("ce_stats", 0), ("dual_qkv", 0), ("dual_gu", 0), ("gu_splitk", 0), ("ksplit", 0),
-    ("fewtile_hq", 0), ("splitk2", 0), ("dual", 0), ("dual_order", 0), ("dual_order", 1), ("norm_splitk", 0),
-    ("fuse_delta", 0), ("attn_pair", 0), ("gemm_group_m", 4), ("gemm_mix", 0))] + [
-    # under the 128x128 few-tile form the K-slice form is not reached
-    ("a", dict(fewtile_hq=0, fewtile=0)),
-    ("b", {}), ("b", dict(swiglu_splitk=0)), ("b", dict(fewtile_hq=0)), ("b", dict(fewtile_hq=0, swiglu_splitk=0)),
+    ("splitk2", 0), ("dual", 0), ("norm_splitk", 0), ("fuse_delta", 0), ("attn_pair", 0), ("gemm_mix", 0))] + [
+    ("b", {}), ("b", dict(swiglu_splitk=0)),
 ]
 # (gemm_kh, the K-halves tile 14 for 256x128 launches at K >= 4096, is not reached at shapes this
 # small: test_kernels_gpu.py covers gemm_kh = 0 on the launch directly)
