@@ -672,9 +672,6 @@ __device__ __forceinline__ const uint16_t* bimg_ptr(const BImg& b, bool bkc, int
 }
 
 // ============================================================================ 8-phase 256x256
-#ifndef PT_SWIGLU_PF_TILES
-#define PT_SWIGLU_PF_TILES 0
-#endif
 // 256x256 tile, BK = 64, 8 waves as 2(M) x 4(N), each wave a 128 x 64 output (8 x 4 accumulators
 // of 16x16).  Each operand tile is held as two "half images" of 128 rows (A) / columns (B) x 64 k,
 // split so that one half holds exactly the fragments every wave reads in one phase:
@@ -804,32 +801,6 @@ __device__ __forceinline__ void gemm_8ph_tile(const GemmArgs& a, const int tile_
   const bool late = __builtin_amdgcn_readfirstlane(wm) == 1;
   if (late) bar();
 
-  // EPI_SWIGLU_BWD: the epilogue's g|u rows (256 KiB per tile) pulled toward the CU during the last
-  // PT_SWIGLU_PF_TILES K-tiles -- LDS-DMA into a scratch KiB past the main loop's images, never read:
-  // the fill is the point -- so the HBM-bound tail reads them from the cache hierarchy while the
-  // main loop had HBM bandwidth to spare.  2 DMA ops per wave per K-tile, issued after phase 4's
-  // stage and retired by the next K-tile's wait (vmcnt(8) instead of 6).
-  constexpr int PF_TILES = EPI == EPI_SWIGLU_BWD ? PT_SWIGLU_PF_TILES : 0;
-  const int pf_t0 = nk - 2 - PF_TILES;
-  auto swiglu_pf = [&](int t) -> bool {
-    if constexpr (PF_TILES == 0) {
-      return false;
-    } else {
-      if (t < pf_t0) return false;
-      constexpr int QPT = 256 / PF_TILES;   // 1-KiB pieces per K-tile (two rows of g or u each)
-      static_assert(QPT == 16, "2 pieces per wave per K-tile");
-#pragma unroll
-      for (int it = 0; it < 2; ++it) {
-        const int q = (t - pf_t0) * QPT + it * 8 + wave;   // 0 .. 255: [g | u] x 128 row pairs
-        const int row = 2 * (q & 127) + (lane >> 5);
-        const uint16_t* gb = a.R + (int64_t)m0 * a.ldr + n0 + ((q >> 7) ? a.N : 0);
-        pt_glds16(gb, (uint32_t)((row * a.ldr + (lane & 31) * 8) * 2),
-                  (__attribute__((address_space(3))) void*)(smem + 8 * HALF));
-      }
-      return true;
-    }
-  };
-
   auto ktile = [&](int t, auto bufc) {
     constexpr int buf = decltype(bufc)::value;
     const lds_u8* sAt = smem + buf * BUF;
@@ -874,11 +845,7 @@ __device__ __forceinline__ void gemm_8ph_tile(const GemmArgs& a, const int tile_
     // phase 4: no reads; stage Br(t+2); retire K-tile t+1; quadrant (1, 0)
     if (n2) {
       stage(t + 2, buf, 2);
-      if (swiglu_pf(t)) {   // 2 more ops in flight, retired by the next K-tile's wait
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      }
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     } else if (n1) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
