@@ -475,6 +475,23 @@ def cp_proxy(args, base, layers):
                          "half_block_frac": (blk_flop / 2 * 3.5) / t_kv0 / MI355X_BF16_DENSE_PEAK}}
 
 
+def pmc_kernel_key(label):
+    """The rocprofv3 kernel (name + workgroup count, tools/traffic_summary.py's key) a GemmProbe
+    label of a dual launch (kernels.linear_dgrad_dual) ran as: gemm_8ph_dual_kernel<AK0 = true,
+    BKC0 = false, dX epilogue, false, false, dW epilogue> with one workgroup per 256x256 tile (the dX
+    split-K halves, epilogue 2, count twice).  Other labels: the label itself."""
+    import re
+    m = re.fullmatch(r"dual dX (\d+)x(\d+)x(\d+) e(\d+) \+ dW ([\dx,]+) e(\d+)", label)
+    if not m:
+        return label
+    T, N, _, e0, dws, e1 = m.groups()
+    wg = (int(T) // 256) * (int(N) // 256) * (2 if e0 == "2" else 1)
+    for dw in dws.split(","):
+        nw, kin, _ = (int(v) for v in dw.split("x"))
+        wg += (nw // 256) * (kin // 256)
+    return f"void gemm_8ph_dual_kernel<true, false, {e0}, false, false, {e1}> [{wg} WG]"
+
+
 def cfg_name(base):
     return {v[1]: v[0] for v in MODELS.values()}.get(base.get("_name"), "custom")
 
@@ -728,13 +745,26 @@ def main():
         loss = step()
         log(f"warmup {i}: loss {loss:.4f} ({time.time() - t:.2f} s)")
 
+    # GEMM timing (HIP events on the launch stream, micro-batch `probe_mb` of a step): the first timed
+    # step times every GEMM launch (the family average, and which launch kind dominates), the later
+    # ones only the dominant kind's launches -- an event pair per launch idles the GPU a few us, ~1.3
+    # ms for a micro-batch's whole family
+    use_probe = not (args.no_probe or pp > 1 or graphed is not None)
+    fam_probe, dom = None, None
+
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     losses = []
-    probe = K.GemmProbe() if not (args.no_probe or pp > 1 or graphed is not None) else None
+    dom_probe = None
     for i in range(args.steps):
+        if use_probe and i == 0:
+            probe = fam_probe = K.GemmProbe()
+        elif use_probe and i == 1:
+            labels = fam_probe.by_label() if fam_probe.records else {}
+            dom = max(labels, key=lambda k: labels[k][1]) if labels else None
+            probe = dom_probe = K.GemmProbe(only=dom) if dom else None
         losses.append(step())
         log(f"step {i}: loss {losses[-1]:.4f}")
     torch.cuda.synchronize()
@@ -758,11 +788,29 @@ def main():
     mfu = per_gpu * fpt / MI355X_BF16_DENSE_PEAK
 
     roofline = None
-    if probe:
-        s = probe.summary()
-        achieved = s["avg_flop"] / (s["avg_ms"] * 1e-3) / 1e12
-        traffic, tsrc, tnote = None, None, "no PMC traffic file"
-        if os.path.exists(TRAFFIC_FILE):   # PMC-measured HBM bytes per GEMM launch (offline passes)
+    probe = None
+    if fam_probe is not None and fam_probe.records:
+        fam = fam_probe
+        s = fam.summary()
+        fam_achieved = s["avg_flop"] / (s["avg_ms"] * 1e-3) / 1e12
+        # the dominant kernel: the GEMM launch kind with the most time in the sampled micro-batch
+        # (SmolLM-1.7B: the gate|up dX split-K halves + gate|up dW dual launch, ~24 % of the step);
+        # its launches of every timed step
+        if dom is None:
+            labels = fam.by_label()
+            dom = max(labels, key=lambda k: labels[k][1])
+        d = fam.label_stats(dom)
+        if dom_probe is not None and dom_probe.records:
+            d2 = dom_probe.label_stats(dom)
+            n = d["launches"] + d2["launches"]
+            d = {"launches": n, "total_ms": d["total_ms"] + d2["total_ms"],
+                 "avg_ms": (d["total_ms"] + d2["total_ms"]) / n,
+                 "avg_flop": (d["avg_flop"] * d["launches"] + d2["avg_flop"] * d2["launches"]) / n,
+                 "avg_alg_bytes": (d["avg_alg_bytes"] * d["launches"] + d2["avg_alg_bytes"] * d2["launches"]) / n}
+        achieved = d["avg_flop"] / (d["avg_ms"] * 1e-3) / 1e12
+        traffic, tsrc, tnote, pmc_key = None, None, "no PMC traffic file", pmc_kernel_key(dom)
+        fam_traffic = None
+        if os.path.exists(TRAFFIC_FILE):   # PMC-measured HBM bytes per launch (offline passes)
             with open(TRAFFIC_FILE) as f:
                 tj = json.load(f)
             # only a measurement of THIS line's workload with THIS library build counts
@@ -773,16 +821,30 @@ def main():
                 tnote = f"{os.path.relpath(TRAFFIC_FILE, ROOT)} measured another workload ({tj.get('workload')})"
             elif tj.get("library_md5") != mine:
                 tnote = f"{os.path.relpath(TRAFFIC_FILE, ROOT)} measured another library build"
+            elif pmc_key not in tj.get("kernels", {}):
+                tnote = f"{os.path.relpath(TRAFFIC_FILE, ROOT)} has no entry {pmc_key!r}"
             else:
-                traffic, tsrc, tnote = tj["gemm_avg_bytes_per_launch"], os.path.relpath(TRAFFIC_FILE, ROOT), None
-        roofline = {"bound": "mfma", "kernel": "gemm (all bf16 MFMA GEMM launches of micro-batch "
-                    f"{probe_mb} of every timed step)", "achieved": achieved,
+                traffic, tsrc, tnote = tj["kernels"][pmc_key]["avg_bytes"], os.path.relpath(TRAFFIC_FILE, ROOT), None
+                fam_traffic = tj["gemm_avg_bytes_per_launch"]
+        roofline = {"bound": "mfma", "kernel": f"{pmc_key} = {dom} (launches of micro-batch {probe_mb} of every "
+                    "timed step)", "achieved": achieved,
                     "peak": MI355X_BF16_DENSE_PEAK / 1e12, "unit": "TFLOP/s",
                     "frac": achieved / (MI355X_BF16_DENSE_PEAK / 1e12), "traffic": traffic,
                     "traffic_unit": "bytes per launch", "traffic_source": tsrc, "traffic_note": tnote,
-                    "algorithmic_bytes_per_launch": s["avg_alg_bytes"],
-                    "launches": s["launches"], "avg_launch_ms": s["avg_ms"], "avg_launch_gflop": s["avg_flop"] / 1e9,
-                    "gemm_share_of_step": s["total_ms"] * 1e-3 * args.grad_acc / elapsed}
+                    "algorithmic_bytes_per_launch": d["avg_alg_bytes"], "algorithmic_flop_per_launch": d["avg_flop"],
+                    "launches": d["launches"], "avg_launch_ms": d["avg_ms"],
+                    "share_of_step": d["avg_ms"] * (d["launches"] / max(args.steps, 1)) * 1e-3 * args.grad_acc /
+                    (elapsed / args.steps),
+                    # every bf16 MFMA GEMM launch of one micro-batch (rounds 1-5 reported this as the
+                    # roofline), sampled in the last warm-up step
+                    "gemm_family": {"sampled": "micro-batch %d of the first timed step" % probe_mb,
+                                    "achieved": fam_achieved, "frac": fam_achieved / (MI355X_BF16_DENSE_PEAK / 1e12),
+                                    "launches": s["launches"], "avg_launch_ms": s["avg_ms"],
+                                    "avg_launch_gflop": s["avg_flop"] / 1e9,
+                                    "algorithmic_bytes_per_launch": s["avg_alg_bytes"], "traffic": fam_traffic,
+                                    "share_of_step": s["total_ms"] * 1e-3 * args.grad_acc / (elapsed / args.steps),
+                                    "by_launch_kind": {k: {"launches": v[0], "ms": v[1], "tflops": v[2]}
+                                                       for k, v in fam.by_label().items()}}}
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_tokens > 0 and args.model == "smollm-1.7b":

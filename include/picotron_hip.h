@@ -228,6 +228,13 @@ typedef struct {
   int64_t ldr;
   int ksplit;              /* 0 / 1: not split */
   int64_t kpart_stride;    /* elements between two slices' f32 partials */
+  /* A K-segmented: k >= a_k2 (a multiple of 64 inside K) reads A2 (same lda) -- a weight gradient
+   * over two micro-batches' token rows (dY of both; B K-segmented the same way through b_seg_dim 1,
+   * b_bounds {0, a_k2, K}): one K = 2 T launch instead of two accumulating ones (data_parallel.py:
+   * 122-144's main_grad read-modify-written once per two micro-batches).  NULL: not segmented.  The
+   * 256x256 8-phase tile only (pt_gemm_grouped tile 12 / auto, pt_gemm_dual). */
+  const void* A2;
+  int64_t a_k2;
 } pt_gemm_problem;
 int pt_gemm_grouped(const pt_gemm_problem* probs, int nprob, int a_kcontig, int b_kcontig, int epilogue, int tile,
                     hipStream_t stream);

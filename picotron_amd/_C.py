@@ -24,7 +24,7 @@ class GemmProblem(ctypes.Structure):
     _fields_ = [("A", _vp), ("lda", _i64), ("B", _vp * 4), ("ldb", _i64 * 4), ("b_bounds", _i64 * 5), ("nb", _i32),
                 ("b_seg_dim", _i32), ("C", _vp * 4), ("ldc", _i64 * 4), ("c_bounds", _i64 * 5), ("nc", _i32),
                 ("M", _i64), ("N", _i64), ("K", _i64), ("residual", _vp), ("ldr", _i64), ("ksplit", _i32),
-                ("kpart_stride", _i64)]
+                ("kpart_stride", _i64), ("A2", _vp), ("a_k2", _i64)]
 
 
 # name -> (restype, argtypes); mirrors include/picotron_hip.h one to one

@@ -83,6 +83,10 @@ __device__ __forceinline__ float silu_sig(float x) { return pt_sigmoid(x); }
 struct GemmArgs {
   const uint16_t* A;
   int64_t lda;
+  // A's second K-segment: k >= ak2 reads A2 (same lda) -- a weight gradient over two micro-batches'
+  // token rows (dY of both, K = 2 T); ak2 = INT32_MAX: none.  The 256x256 8-phase kernel only.
+  const uint16_t* A2;
+  int ak2;
   const uint16_t* B[4];
   int64_t ldb[4];
   int64_t bseg[5];  // boundaries along N (bdim 0) or K (bdim 1)
@@ -746,7 +750,16 @@ __device__ __forceinline__ void gemm_8ph_tile(const GemmArgs& a, const int tile_
   }
   const int kb = kslice_begin(a, ks);        // this split-K slice's first k (0 unsplit)
   const uint16_t* Ab0 = AK ? a.A + (int64_t)m0 * lda + kb : a.A + m0 + (int64_t)kb * lda;
-  auto a_ptr = [&](int t) { return AK ? Ab0 + t * BK : Ab0 + (int64_t)t * BK * lda; };
+  // A's second K-segment (a two-micro-batch weight gradient): from k = ak2 on, element (k, m) is
+  // A2's (k - ak2, m): the same address plus one element offset, read once into registers
+  const int ak2 = a.ak2;
+  const int64_t a_d2 = a.A2 ? ((int64_t)(intptr_t)a.A2 - (int64_t)(intptr_t)a.A) / 2 -
+                                  (AK ? (int64_t)ak2 : (int64_t)ak2 * lda)
+                            : 0;
+  auto a_ptr = [&](int t) {
+    const int64_t e2 = kb + t * BK >= ak2 ? a_d2 : 0;
+    return (AK ? Ab0 + t * BK : Ab0 + (int64_t)t * BK * lda) + e2;
+  };
   auto b_ptr = [&](int t) { return bimg_ptr(bi, BKC, kb + t * BK); };
   // paired: rows tile_n * 128 .. +127 of W_gate (Bl) and W_up (Br), K-contiguous
   auto pair_ptr = [&](int t, int which) {
@@ -1721,6 +1734,14 @@ namespace {
 // split-K fields of a grouped problem: ksplit slices of K / ksplit (a multiple of BK) written as f32
 // partials kpart_stride elements apart (EPI_F32 only).
 int fill_split(GemmArgs& a, const pt_gemm_problem& q, int epilogue) {
+  a.A2 = nullptr;
+  a.ak2 = INT32_MAX;
+  if (q.A2) {   // A K-segmented at a_k2 (a BK multiple inside K; A2 aligned like A)
+    if (q.a_k2 <= 0 || q.a_k2 >= a.K || q.a_k2 % BK) return PT_EINVAL;
+    if (!pt_aligned16(q.A2)) return PT_EALIGN;
+    a.A2 = (const uint16_t*)q.A2;
+    a.ak2 = (int)q.a_k2;
+  }
   a.ksplit = q.ksplit > 1 ? q.ksplit : 1;
   a.kpart_stride = q.kpart_stride;
   if (a.ksplit == 1) return PT_OK;
@@ -1928,7 +1949,7 @@ int launch_group(GemmGroup& g, int a_kcontig, int b_kcontig, int epilogue, int t
     return PT_EUNSUPPORTED;
   }
   for (int i = 0; i < g.nprob; ++i)
-    if (!args_fit(g.p[i], tile)) return PT_EUNSUPPORTED;
+    if (!args_fit(g.p[i], tile) || (g.p[i].A2 && tile != 12)) return PT_EUNSUPPORTED;
   switch (epilogue) {
     case EPI_BF16: return launch_epi<EPI_BF16>(g, a_kcontig, b_kcontig, tile, stream);
     case EPI_BF16_ACC: return launch_epi<EPI_BF16_ACC>(g, a_kcontig, b_kcontig, tile, stream);

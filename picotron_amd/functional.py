@@ -61,11 +61,79 @@ def _grad_ready(p):
         hook(p)
 
 
+# ------------------------------------------------------------------------ paired weight gradients
+# The weight-gradient epilogues read-modify-write the gradient sink once per micro-batch: at
+# SmolLM-1.7B 2.4 GB of bf16 .grad (DP = 1) or 4.8 GB of f32 main_grad (DataParallelBucket,
+# data_parallel.py:122-144) read AND written 32 times per step.  Paired, micro-batch 2 i defers its
+# weight gradients -- keeps their dY and X alive -- and micro-batch 2 i + 1 launches each as ONE GEMM
+# over both micro-batches' tokens (K = 2 T, kernels.KPair: the A and B operands K-segmented), so the
+# sinks are read-modify-written once per pair.  Same sums (the f32 accumulator covers both
+# micro-batches before the one rounding into the sink: the same or closer to the fp32 sum).  The
+# training loop drives it (train.train_step: `wgrad_pairing(phase)` around each backward at tp = 1;
+# None = off, the reference's one-backward-at-a-time behaviour for any other caller).
+class WgradPairing:
+    phase = None   # None: launch now; 0: defer this backward's weight gradients; 1: pair them
+    pending = {}   # parameter ids -> (dy2d, x2d, params) deferred by the previous micro-batch
+
+
+def wgrad_pairing(phase):
+    """Set the pairing phase of the next backward (train.train_step); returns the previous one."""
+    old, WgradPairing.phase = WgradPairing.phase, phase
+    return old
+
+
+def flush_wgrad_pairs():
+    """Launch (unpaired) every weight gradient a micro-batch deferred and no pair completed."""
+    pend, WgradPairing.pending = WgradPairing.pending, {}
+    ph, WgradPairing.phase = WgradPairing.phase, None
+    try:
+        for dy, x, params in pend.values():
+            wgrad(dy, x, params)
+    finally:
+        WgradPairing.phase = ph
+
+
+def pair_jobs(wjobs):
+    """wjobs [(dy2d, x2d, params)] -> the jobs to launch in this backward: [] when it defers them
+    (phase 0), each paired with the previous micro-batch's job of the same parameters (phase 1)."""
+    ph = WgradPairing.phase
+    if ph is None or not wjobs:
+        return wjobs
+    if ph == 0:
+        for dy, x, params in wjobs:
+            key = tuple(id(p) for p in params)
+            if key in WgradPairing.pending:   # deferred twice without a pair: the older one now
+                odx, ox, op = WgradPairing.pending.pop(key)
+                wgrad(odx, ox, op)
+            WgradPairing.pending[key] = (dy, x, params)
+        return []
+    out = []
+    for dy, x, params in wjobs:
+        prev = WgradPairing.pending.pop(tuple(id(p) for p in params), None)
+        if prev is not None and (prev[0].shape != dy.shape or prev[1].shape != x.shape or
+                                 prev[0].stride() != dy.stride() or prev[1].stride() != x.stride()):
+            wgrad(*prev)            # not the same layout: the older one on its own first
+            prev = None
+        out.append((dy, x, params) if prev is None else (K.KPair(prev[0], dy), K.KPair(prev[1], x), params))
+    return out
+
+
 def wgrad(dy2d, x2d, params, notify=True):
     """dW_i = dY_i^T X for the column segments of dY; one launch when the sinks agree.  Parameters
     with requires_grad=False get no gradient (autograd leaves their .grad alone).  notify=False: a
     partial gradient (one token chunk of a chunked sequence-parallel layer, the sum is not complete
-    yet): the owner is not told."""
+    yet): the owner is not told.  Under weight-gradient pairing (WgradPairing) the job may be
+    deferred to, or paired with, the other micro-batch of its pair."""
+    if WgradPairing.phase is not None:
+        jobs = pair_jobs([(dy2d, x2d, params)])
+        if not jobs:
+            return
+        (dy2d, x2d, params), = jobs
+        ph = wgrad_pairing(None)   # settled: the per-parameter fallbacks launch it as it is
+        try:
+            return wgrad(dy2d, x2d, params, notify)
+        finally:
+            wgrad_pairing(ph)
     if not all(p.requires_grad for p in params):
         lo = 0
         for p in params:
@@ -92,6 +160,18 @@ def wgrad(dy2d, x2d, params, notify=True):
 def wgrad_group(jobs, notify=True):
     """Several wgrads [(dy2d, x2d, params), ...] in one grouped launch when every sink takes the
     same epilogue (else one wgrad() per job)."""
+    if WgradPairing.phase is not None:
+        jobs = pair_jobs(jobs)
+        if not jobs:
+            return
+    ph = wgrad_pairing(None)   # the jobs are settled: the per-job fallbacks below launch them as they are
+    try:
+        _wgrad_group(jobs, notify)
+    finally:
+        wgrad_pairing(ph)
+
+
+def _wgrad_group(jobs, notify):
     frozen = any(not p.requires_grad for _, _, params in jobs for p in params)
     targets = [] if frozen else [[_wgrad_target(p) for p in params] for _, _, params in jobs]
     epis = {e for tg in targets for _, e in tg}
@@ -111,7 +191,23 @@ def dgrad_with_wgrad(dy2d, weights, wjobs, gu=None, keep_parts=False, split_min=
     """dX = dY . [W_0; ...] (with gu: the down_proj dX's SwiGLU backward, dg|du) AND the wgrads
     wjobs [(dy2d, x2d, params)] of the same layer in ONE launch (K.linear_dgrad_dual) when the
     shapes tile for it and every sink takes one epilogue; otherwise the separate launches.
-    Returns dX / dg|du."""
+    Returns dX / dg|du.  Under weight-gradient pairing a deferring micro-batch launches the dX alone
+    (the split-K halves kept for the consumer as in the dual), the completing one the dual with the
+    paired (K = 2 T) weight gradients."""
+    if WgradPairing.phase is not None:
+        wjobs = pair_jobs(wjobs)
+        if not wjobs:
+            if gu is not None:
+                return K.linear_dgrad_swiglu(dy2d, weights[0], gu)
+            return K.linear_dgrad(dy2d, weights, keep_parts=keep_parts, split_min=split_min)
+    ph = wgrad_pairing(None)
+    try:
+        return _dgrad_with_wgrad(dy2d, weights, wjobs, gu, keep_parts, split_min, order, notify)
+    finally:
+        wgrad_pairing(ph)
+
+
+def _dgrad_with_wgrad(dy2d, weights, wjobs, gu, keep_parts, split_min, order, notify):
     frozen = any(not p.requires_grad for _, _, params in wjobs for p in params)
     mns = [(dy.shape[1], x.shape[1]) for dy, x, _ in wjobs]
     dmn = (dy2d.shape[0], gu.shape[1] // 2 if gu is not None else weights[0].shape[1])

@@ -28,6 +28,10 @@ def _req(cond, msg):
 
 
 def _bf16_rowmajor(t, name):
+    if isinstance(t, KPair):
+        _bf16_rowmajor(t.a, name)
+        _bf16_rowmajor(t.b, name)
+        return
     _req(t.dtype == BF16, f"{name}: expected bfloat16, got {t.dtype}")
     _req(t.is_cuda, f"{name}: expected a device tensor")
     _req(t.dim() == 2 and t.stride(1) == 1, f"{name}: expected a 2-D row-major view")
@@ -75,6 +79,26 @@ class SplitKParts:
                                          _C.stream_ptr(self.device))
         _C.check(rc, "pt_gemm_splitk_sum")
         return out
+
+
+class KPair:
+    """Two [T, n] row blocks a, b of one layout standing for their concatenation [2 T, n] along the
+    token (K) dimension of a weight gradient: two micro-batches' dY (or X).  The wgrad launches take
+    it as a K-segmented operand (pt_gemm_problem.A2 / b_seg_dim 1): dW = dY_a^T X_a + dY_b^T X_b in
+    one K = 2 T GEMM (functional.pair_jobs).  Column slices stay pairs."""
+
+    def __init__(self, a, b):
+        _req(a.shape == b.shape and a.stride() == b.stride() and a.dtype == b.dtype and a.device == b.device,
+             "KPair: two row blocks of one shape and layout")
+        self.a, self.b = a, b
+        self.shape = (2 * a.shape[0], a.shape[1])
+        self.dtype, self.device = a.dtype, a.device
+
+    def stride(self, i=None):
+        return self.a.stride() if i is None else self.a.stride(i)
+
+    def __getitem__(self, idx):
+        return KPair(self.a[idx], self.b[idx])
 
 
 def rmsnorm_bwd(dy, z, weight, rstd, mode=MODE_TRITON, dres=None, dw_out=None, dw_sink=0, defer_dw=False):
@@ -453,8 +477,9 @@ class GemmProbe:
     """Live timing of every GEMM launch (bench.py's roofline): a pair of HIP events recorded on
     the launch stream around each pt_gemm call, plus its algorithmic FLOPs (2*M*N*K)."""
 
-    def __init__(self):
+    def __init__(self, only=None):
         self.records = []
+        self.only = only   # a launch label: time only launches of that kind (bench.py's timed steps)
 
     def __enter__(self):
         global _PROBE
@@ -474,6 +499,15 @@ class GemmProbe:
         return {"launches": n, "total_ms": sum(ms), "total_flop": sum(flops),
                 "avg_ms": sum(ms) / max(n, 1), "avg_flop": sum(flops) / max(n, 1),
                 "avg_alg_bytes": sum(byts) / max(n, 1)}
+
+    def label_stats(self, label):
+        """Launches of one label: {launches, total_ms, avg_ms, avg_flop, avg_alg_bytes}."""
+        torch.cuda.synchronize()
+        rs = [r for r in self.records if r[4] == label]
+        n = max(len(rs), 1)
+        ms = [r[0].elapsed_time(r[1]) for r in rs]
+        return {"launches": len(rs), "total_ms": sum(ms), "avg_ms": sum(ms) / n,
+                "avg_flop": sum(r[2] for r in rs) / n, "avg_alg_bytes": sum(r[3] for r in rs) / n}
 
     def by_label(self):
         """{label: (launches, total ms, TF/s)} -- which GEMM shapes / launch kinds take the time."""
@@ -502,11 +536,18 @@ def _alg_bytes(M, N, K, epilogue):
 _PROBE = None
 
 
+def _probe_for(label):
+    """The active GemmProbe if it times launches of this label, else None."""
+    p = _PROBE
+    return p if p is not None and (p.only is None or p.only == label) else None
+
+
 def _gemm(A, lda, a_kcontig, Bs, ldbs, b_bounds, b_kcontig, b_seg_dim, Cs, ldcs, c_bounds, M, N, K, epilogue,
           tile=-1, residual=None, ldr=0):
     lib = _C.lib()
     nb, nc = len(Bs), len(Cs)
-    probe = _PROBE
+    label = f"gemm {M}x{N}x{K} e{epilogue} t{tile}"
+    probe = _probe_for(label)
     if probe is not None:
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
@@ -518,8 +559,7 @@ def _gemm(A, lda, a_kcontig, Bs, ldbs, b_bounds, b_kcontig, b_seg_dim, Cs, ldcs,
     _C.check(rc, f"pt_gemm(M={M}, N={N}, K={K}, a_k={a_kcontig}, b_k={b_kcontig}, epi={epilogue})")
     if probe is not None:
         ev1.record()
-        probe.records.append((ev0, ev1, 2.0 * M * N * K, _alg_bytes(M, N, K, epilogue),
-                              f"gemm {M}x{N}x{K} e{epilogue} t{tile}"))
+        probe.records.append((ev0, ev1, 2.0 * M * N * K, _alg_bytes(M, N, K, epilogue), label))
 
 
 def _bounds(sizes):
@@ -617,14 +657,15 @@ def _gemm_ksplit(A, lda, a_kcontig, Bs, ldbs, b_bounds, b_kcontig, b_seg_dim, ou
     pr = _problem(A, lda, Bs, ldbs, b_bounds, b_seg_dim, [ws], [N], [0, M], M, N, K)
     pr.ksplit, pr.kpart_stride = s, M * N
     probs[0] = pr
-    probe = _PROBE
+    label = f"gemm {M}x{N}x{K} ks{s}"
+    probe = _probe_for(label)
     if probe is not None:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
     _ksplit_launch(probs, 1, a_kcontig, b_kcontig, tile, [_sink([out], [0, M], epilogue, residual, ldr)], dev)
     if probe is not None:
         ev1.record()
-        probe.records.append((ev0, ev1, 2.0 * M * N * K, _alg_bytes(M, N, K, epilogue), f"gemm {M}x{N}x{K} ks{s}"))
+        probe.records.append((ev0, ev1, 2.0 * M * N * K, _alg_bytes(M, N, K, epilogue), label))
     return out
 
 
@@ -683,7 +724,7 @@ def _wgrad_ksplit_run(jobs, epilogue, s, tile=-1):
         base += s * N * Kin
         flops += 2.0 * N * Kin * T
         nbytes += _alg_bytes(N, Kin, T, epilogue)
-    probe = _PROBE
+    probe = _probe_for("_wgrad_ksplit_run")
     if probe is not None:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
@@ -691,13 +732,51 @@ def _wgrad_ksplit_run(jobs, epilogue, s, tile=-1):
     _ksplit_launch(probs, len(jobs), 0, 0, tile, sinks, dev)
     if probe is not None:
         ev1.record()
-        probe.records.append((ev0, ev1, flops, nbytes, sys._getframe().f_code.co_name))
+        probe.records.append((ev0, ev1, flops, nbytes, "_wgrad_ksplit_run"))
+
+
+def _wgrad_problem(dy2d, x2d, outs):
+    """The GemmProblem of dW = dY^T X into outs (row segments of dW): dY and X plain [T, n] or KPair
+    (two micro-batches: A K-segmented at T through A2, B through two K-segments)."""
+    Nw, Kin = dy2d.shape[1], x2d.shape[1]
+    ns = [o.shape[0] for o in outs]
+    _req(sum(ns) == Nw and x2d.shape[0] == dy2d.shape[0], "wgrad: output rows must cover dY's width")
+    Cs, ldcs, cb = outs, [o.stride(0) for o in outs], _bounds(ns)
+    if isinstance(dy2d, KPair):
+        _req(isinstance(x2d, KPair), "wgrad: dY and X paired together")
+        t = dy2d.a.shape[0]
+        pr = _problem(dy2d.a, dy2d.stride(0), [x2d.a, x2d.b], [x2d.stride(0)] * 2, [0, t, 2 * t], 1, Cs, ldcs, cb,
+                      Nw, Kin, 2 * t)
+        pr.A2, pr.a_k2 = _ptr(dy2d.b), t
+        return pr
+    return _problem(dy2d, dy2d.stride(0), [x2d], [x2d.stride(0)], [0, Kin], 0, Cs, ldcs, cb, Nw, Kin, dy2d.shape[0])
+
+
+def _is_paired(jobs):
+    return any(isinstance(dy, KPair) for dy, _, _ in jobs)
+
+
+_ACC_OF = {EPI_BF16: EPI_BF16_ACC, EPI_BF16_ACC: EPI_BF16_ACC, EPI_F32: EPI_F32_ACC, EPI_F32_ACC: EPI_F32_ACC}
+
+
+def _wgrad_unpaired(jobs, epilogue):
+    """Paired wgrad jobs as two launches each: the first micro-batch's half through `epilogue`, the
+    second's accumulating onto it."""
+    for dy, x, outs in jobs:
+        if isinstance(dy, KPair):
+            linear_wgrad_grouped([(dy.a, x.a, outs)], epilogue)
+            linear_wgrad_grouped([(dy.b, x.b, outs)], _ACC_OF[epilogue])
+        else:
+            linear_wgrad_grouped([(dy, x, outs)], epilogue)
 
 
 def linear_wgrad_grouped(jobs, epilogue=EPI_BF16, tile=-1):
     """Several wgrad GEMMs (dW_i = dY_i^T X for each job (dy2d, x2d, outs)) in ONE launch
     (pt_gemm_grouped): e.g. dW of q|k|v (192 tiles) + dW of o_proj (64 tiles) fill 256 CUs.  A group
     that would leave most CUs idle (TP shards) runs split-K (wgrad_ksplit)."""
+    paired = _is_paired(jobs)
+    if paired:
+        tile = 12   # the K-segmented A: the 256x256 8-phase kernel only
     if tile < 0 and epilogue in (EPI_BF16, EPI_BF16_ACC, EPI_F32_ACC):
         mnks = [(dy.shape[1], x.shape[1], dy.shape[0]) for dy, x, _ in jobs]
         hq = hq_form(mnks) if all(o.shape[0] % 128 == 0 for _, _, outs in jobs for o in outs) else 0
@@ -717,21 +796,21 @@ def linear_wgrad_grouped(jobs, epilogue=EPI_BF16, tile=-1):
         _bf16_rowmajor(x2d, "x")
         T, N = dy2d.shape
         Kin = x2d.shape[1]
-        ns = [o.shape[0] for o in outs]
-        _req(sum(ns) == N and x2d.shape[0] == T, "wgrad: output rows must cover dY's width")
-        probs[j] = _problem(dy2d, dy2d.stride(0), [x2d], [x2d.stride(0)], [0, Kin], 0, outs,
-                            [o.stride(0) for o in outs], _bounds(ns), N, Kin, T)
+        probs[j] = _wgrad_problem(dy2d, x2d, outs)
         flops += 2.0 * N * Kin * T
         nbytes += _alg_bytes(N, Kin, T, epilogue)
-    probe = _PROBE
+    probe = _probe_for("linear_wgrad_grouped")
     if probe is not None:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
     rc = _C.lib().pt_gemm_grouped(probs, len(jobs), 0, 0, int(epilogue), int(tile), _C.stream_ptr(jobs[0][0].device))
+    if rc == -3 and paired:   # a shape the 256x256 tile does not cover: each micro-batch's half on its own
+        _wgrad_unpaired(jobs, epilogue)
+        rc = 0
     _C.check(rc, f"pt_gemm_grouped({len(jobs)} problems, epi={epilogue})")
     if probe is not None:
         ev1.record()
-        probe.records.append((ev0, ev1, flops, nbytes, sys._getframe().f_code.co_name))
+        probe.records.append((ev0, ev1, flops, nbytes, "linear_wgrad_grouped"))
 
 
 def linear_fwd(x2d, weights, out=None, tile=-1, residual=None):
@@ -798,7 +877,7 @@ def linear_fwd_rope(x2d, weights, cos, sin, seq_len, rot_heads, head_dim):
         y = linear_fwd(x2d, weights)
         return rope_(y, rot_heads, head_dim, cos, sin, seq_len)
     y = torch.empty(T, N, dtype=BF16, device=x2d.device)
-    probe = _PROBE
+    probe = _probe_for("linear_fwd_rope")
     if probe is not None:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
@@ -808,7 +887,7 @@ def linear_fwd_rope(x2d, weights, cos, sin, seq_len, rot_heads, head_dim):
     _C.check(rc, "pt_gemm_rope")
     if probe is not None:
         ev1.record()
-        probe.records.append((ev0, ev1, 2.0 * T * N * K, _alg_bytes(T, N, K, EPI_BF16), sys._getframe().f_code.co_name))
+        probe.records.append((ev0, ev1, 2.0 * T * N * K, _alg_bytes(T, N, K, EPI_BF16), "linear_fwd_rope"))
     return y
 
 
@@ -839,7 +918,7 @@ def linear_ce_stats(x2d, weight):
     _req(block is not None and K % 64 == 0, "linear_ce_stats: T % 256, V % 128, K % 64")
     y = torch.empty(T, V, dtype=BF16, device=x2d.device)
     stats = torch.empty(V // block, T, 2, dtype=torch.float32, device=x2d.device)
-    probe = _PROBE
+    probe = _probe_for("linear_ce_stats")
     if probe is not None:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
@@ -848,7 +927,7 @@ def linear_ce_stats(x2d, weight):
     _C.check(rc, "pt_gemm_ce_stats")
     if probe is not None:
         ev1.record()
-        probe.records.append((ev0, ev1, 2.0 * T * V * K, _alg_bytes(T, V, K, EPI_BF16), sys._getframe().f_code.co_name))
+        probe.records.append((ev0, ev1, 2.0 * T * V * K, _alg_bytes(T, V, K, EPI_BF16), "linear_ce_stats"))
     return y, stats
 
 
@@ -1010,7 +1089,7 @@ def _segments(sizes, lo, hi):
 
 
 def _splitk_run(probs, b_kcontig, parts, residual, out, flops, nbytes, device):
-    probe = _PROBE
+    probe = _probe_for("_splitk_run")
     if probe is not None:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
@@ -1021,13 +1100,14 @@ def _splitk_run(probs, b_kcontig, parts, residual, out, flops, nbytes, device):
     _C.check(rc, "pt_gemm_splitk_sum")
     if probe is not None:
         ev1.record()
-        probe.records.append((ev0, ev1, flops, nbytes, sys._getframe().f_code.co_name))
+        probe.records.append((ev0, ev1, flops, nbytes, "_splitk_run"))
     return out
 
 
-def _linear_dgrad_splitk(dy2d, weights, h, dx):
+def _linear_dgrad_splitk(dy2d, weights, h, dx, keep_parts=False):
     """dX = bf16(dY[:, :h] . W[:h] + dY[:, h:] . W[h:]) with W = [W_0; W_1; ...] (the halves may cut
-    through a weight): two f32 problems on 256x256 tiles in one grouped launch, then the sum pass."""
+    through a weight): two f32 problems on 256x256 tiles in one grouped launch, then the sum pass
+    (keep_parts: no sum pass, the SplitKParts for a consumer that sums them)."""
     T, N = dy2d.shape
     Kin = weights[0].shape[1]
     ns = [w.shape[0] for w in weights]
@@ -1038,6 +1118,10 @@ def _linear_dgrad_splitk(dy2d, weights, h, dx):
         bs = [weights[j][a:a + n] for j, a, n in segs]
         probs[i] = _problem(dy2d[:, lo:], dy2d.stride(0), bs, [Kin] * len(bs), _bounds([n for _, _, n in segs]), 1,
                             [parts[i]], [Kin], [0, T], T, Kin, hi - lo)
+    if keep_parts:
+        rc = _C.lib().pt_gemm_grouped(probs, 2, 1, 0, EPI_F32, 12, _C.stream_ptr(dy2d.device))
+        _C.check(rc, "pt_gemm_grouped(split-K halves)")
+        return SplitKParts(parts[0], parts[1])
     return _splitk_run(probs, 0, parts, None, dx, 2.0 * T * Kin * N, _alg_bytes(T, Kin, N, EPI_BF16), dy2d.device)
 
 
@@ -1055,18 +1139,20 @@ def _linear_fwd_splitk(x2d, weights, h, y, residual):
     return _splitk_run(probs, 1, parts, residual, y, 2.0 * T * N * K, _alg_bytes(T, N, K, EPI_BF16), x2d.device)
 
 
-def linear_dgrad(dy2d, weights, out=None, accumulate=False, tile=-1):
-    """dX = dY . [W_0; W_1; ...]  where dY = [dY_0 | dY_1 | ...] is [T, sum N_i]."""
+def linear_dgrad(dy2d, weights, out=None, accumulate=False, tile=-1, keep_parts=False, split_min=None):
+    """dX = dY . [W_0; W_1; ...]  where dY = [dY_0 | dY_1 | ...] is [T, sum N_i].  split_min / keep_parts
+    as linear_dgrad_dual's (the dX of a dual launch whose weight gradients were deferred)."""
     _bf16_rowmajor(dy2d, "dy")
     T, N = dy2d.shape
     Kin = weights[0].shape[1]
     ns = [w.shape[0] for w in weights]
     _req(sum(ns) == N, "dgrad: dY width must equal the stacked weight rows")
     if out is None and not accumulate and tile < 0 and _splitk_enabled() and len(weights) <= 3:
-        h = _splitk_halves(T, Kin, N)
+        h = _splitk_halves(T, Kin, N, split_min)
         if h is not None and all(w.dtype == BF16 and w.is_contiguous() for w in weights) and \
                 all(n % 64 == 0 for n in ns):
-            return _linear_dgrad_splitk(dy2d, weights, h, torch.empty(T, Kin, dtype=BF16, device=dy2d.device))
+            return _linear_dgrad_splitk(dy2d, weights, h, torch.empty(T, Kin, dtype=BF16, device=dy2d.device),
+                                        keep_parts=keep_parts)
     dx = out if out is not None else torch.empty(T, Kin, dtype=BF16, device=dy2d.device)
     hq = hq_form([(T, Kin, N)]) if tile < 0 and all(n % 64 == 0 for n in ns) else 0
     if hq == 1:
@@ -1152,11 +1238,14 @@ def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None, keep
             e0 = EPI_F32
     if e0 != EPI_F32 or dxs > 1:
         p0s = (_C.GemmProblem * 1)(p0)
+    # the probe's label of this launch kind (bench.py's roofline picks the dominant kernel by label)
+    label = f"dual dX {T}x{p0s[0].N if e0 != EPI_F32 or dxs > 1 else dx.shape[1]}x{N} e{e0} + dW " + \
+        ",".join(f"{dy.shape[1]}x{x.shape[1]}x{dy.shape[0]}" for dy, x, _ in wjobs) + f" e{wepilogue}"
     p1s = (_C.GemmProblem * len(wjobs))()
     # the TP shards' few-tile dW as split-K slices beside the dX tiles (f32 partials, reduced below)
     dx_tiles = sum(p.M // 256 * (p.N // 256) * max(1, p.ksplit) for p in p0s)
     ws = wgrad_ksplit([(dy.shape[1], x.shape[1], dy.shape[0]) for dy, x, _ in wjobs], extra_tiles=dx_tiles) \
-        if wepilogue in (EPI_BF16, EPI_BF16_ACC, EPI_F32_ACC) else 1
+        if wepilogue in (EPI_BF16, EPI_BF16_ACC, EPI_F32_ACC) and not _is_paired(wjobs) else 1
     # the reduce pass writes 16-B (f32) / 8-B (bf16) row chunks: a sink it cannot address that way (a
     # misaligned .grad / main_grad view) keeps the unsplit dW, decided before anything is launched
     if ws > 1 and not all(_reduce_sink_ok(o) for _, _, outs in wjobs for o in outs):
@@ -1169,7 +1258,9 @@ def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None, keep
         Kin = x2d.shape[1]
         ns = [o.shape[0] for o in outs]
         _req(sum(ns) == Nw and x2d.shape[0] == Tw, "wgrad: output rows must cover dY's width")
-        if ws > 1:
+        if isinstance(wdy, KPair):   # two micro-batches' weight gradient, K = 2 T (the 8-phase tile: A2)
+            p1s[j] = _wgrad_problem(wdy, x2d, outs)
+        elif ws > 1:
             part = torch.empty(ws * Nw * Kin, dtype=torch.float32, device=dy2d.device)
             wparts.append(part)
             p1s[j] = _problem(wdy, wdy.stride(0), [x2d], [x2d.stride(0)], [0, Kin], 0, [part], [Kin], [0, Nw], Nw,
@@ -1180,7 +1271,7 @@ def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None, keep
                               [o.stride(0) for o in outs], _bounds(ns), Nw, Kin, Tw)
         flops += 2.0 * Nw * Kin * Tw
         nbytes += _alg_bytes(Nw, Kin, Tw, wepilogue)
-    probe = _PROBE
+    probe = _probe_for(label)
     if probe is not None:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
@@ -1216,12 +1307,16 @@ def linear_dgrad_dual(dy2d, weights, wjobs, wepilogue, gu=None, order=None, keep
             _C.check(rc, "pt_gemm_splitk_sum")
     if probe is not None:
         ev1.record()
-        probe.records.append((ev0, ev1, flops, nbytes, sys._getframe().f_code.co_name))
+        probe.records.append((ev0, ev1, flops, nbytes, label))
     return dx
 
 
 def linear_wgrad(dy2d, x2d, outs, epilogue=EPI_BF16, tile=-1):
-    """dW_i = dY_i^T . X for the column segments dY_i of dY (widths = outs[i].shape[0]); one launch."""
+    """dW_i = dY_i^T . X for the column segments dY_i of dY (widths = outs[i].shape[0]); one launch.
+    dY / X may be KPair (two micro-batches in one K = 2 T launch)."""
+    if isinstance(dy2d, KPair):
+        linear_wgrad_grouped([(dy2d, x2d, outs)], epilogue)
+        return outs
     _bf16_rowmajor(dy2d, "dy")
     _bf16_rowmajor(x2d, "x")
     T, N = dy2d.shape

@@ -5,7 +5,8 @@ split-K vs one pass, one launch vs two); the defaults are the production path, a
 hot path reads the environment again.  `PICOTRON_<NAME>` (upper case) sets a switch for a whole
 process (an A/B run); tests and tools change one for a block with `override(name=value)`.
 Every non-default form runs through the whole GPU path against the oracle in
-tests/test_switch_forms_gpu.py (ring_zigzag in test_parallel_gpu.py, gemm_kh in test_kernels_gpu.py);
+tests/test_switch_forms_gpu.py (ring_zigzag / tp_sp_chunks in test_parallel_gpu.py, gemm_kh and
+wgrad_pair in test_kernels_gpu.py);
 tools/switch_kernels.py traces which launches each changes (profiles/r05/switch_kernels_r05k.txt).
 
 The native switches (attention causal pairing, dK/dV kernel form, few-head split chunk; GEMM
@@ -36,6 +37,9 @@ DEFAULTS = {
     "tp_sp": 1, "tp_sp_chunks": 0,
     # functional.py: the TP lm_head's F.cross_entropy on the vocab shards (no logits all-gather)
     "vp_ce": 1,
+    # functional.py / train.py: the weight gradients of micro-batch pairs as one K = 2 T launch each
+    # (train_step at tp = pp = 1; 0 = one launch per micro-batch, the reference's order)
+    "wgrad_pair": 1,
     # native (libpicotron_hip.so, pt_set_variant)
     "attn_pair": 1, "attn_split": 2, "gemm_mix": 1, "gemm_kh": 2, "attn_kv_chunk": 4,
 }

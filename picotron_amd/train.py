@@ -97,22 +97,48 @@ def train_step(model, data_loader, device, on_microbatch=None, read_loss=True):
     acc_loss = torch.zeros((), dtype=torch.float32, device=device)
     # (bench.py --dp-bucket: a 1-rank DataParallelBucket syncs like N > 1 would)
     requires_grad_sync = pgm.current().cp_dp_world_size > 1 or getattr(model, "_force_grad_sync", False)
-    for i in range(data_loader.grad_acc_steps):
-        if on_microbatch is not None:
-            on_microbatch(i)
-        batch = next(data_loader)
-        input_ids = batch["input_ids"].to(device)
-        target_ids = batch["target_ids"].to(device)
-        if requires_grad_sync:
-            model.require_backward_grad_sync = (i == data_loader.grad_acc_steps - 1)
-        outputs = model(input_ids=input_ids)
-        batch_size, seq_len = input_ids.shape
-        target_ids = target_ids.reshape(-1)
-        outputs = outputs.view(seq_len * batch_size, -1)
-        loss = FN.cross_entropy(outputs, target_ids, reduction="mean") / data_loader.grad_acc_steps
-        loss.backward()
-        acc_loss += loss.detach().float()
+    ga = data_loader.grad_acc_steps
+    pairing = wgrad_pairing_applies()
+    try:
+        for i in range(ga):
+            if on_microbatch is not None:
+                on_microbatch(i)
+            batch = next(data_loader)
+            input_ids = batch["input_ids"].to(device)
+            target_ids = batch["target_ids"].to(device)
+            if requires_grad_sync:
+                model.require_backward_grad_sync = (i == ga - 1)
+            outputs = model(input_ids=input_ids)
+            batch_size, seq_len = input_ids.shape
+            target_ids = target_ids.reshape(-1)
+            outputs = outputs.view(seq_len * batch_size, -1)
+            loss = FN.cross_entropy(outputs, target_ids, reduction="mean") / ga
+            # micro-batches (2 j, 2 j + 1) share their weight-gradient launches (functional.WgradPairing):
+            # the first defers, the second launches K = 2 T GEMMs; an odd last micro-batch on its own
+            if pairing:
+                FN.wgrad_pairing(pairing_phase(i, ga))
+            loss.backward()
+            acc_loss += loss.detach().float()
+    finally:
+        if pairing:
+            FN.wgrad_pairing(None)
+            FN.flush_wgrad_pairs()
     return read_step_loss(acc_loss, device) if read_loss else acc_loss
+
+
+def pairing_phase(i, ga):
+    """Micro-batch i of ga: 0 = defers its weight gradients, 1 = completes the pair (2 j, 2 j + 1),
+    None = an odd last micro-batch on its own."""
+    return 0 if i % 2 == 0 and i + 1 < ga else (1 if i % 2 == 1 else None)
+
+
+def wgrad_pairing_applies():
+    """Weight-gradient pairing (functional.WgradPairing) runs in train_step at tp = pp = 1 (the TP
+    shards' split-K weight-gradient forms and the pipeline's interleaved micro-batches keep one
+    launch per micro-batch); switch `wgrad_pair`."""
+    from .switches import S as SW
+    m = pgm.current()
+    return SW.wgrad_pair != 0 and m.tp_world_size == 1 and m.pp_world_size == 1
 
 
 def quiesce_collectives(device, poll_s=0.35):

@@ -118,3 +118,17 @@ def test_bench_assembles_the_8_rank_dp2_tp2_pp2_grid_on_cpu():
         assert e["rank"] == ((dp_ * 2 + pp_) * 1 + cp_) * 2 + tp_
         assert e["embedding"] == (pp_ == 0) and e["lm_head"] == (pp_ == 1)
         assert e["layers"] == ([0] if pp_ == 0 else [1]) and e["buckets"] > 0
+
+
+def test_pmc_kernel_key_for_dual_labels():
+    """bench.py's roofline names the dominant kernel by its GemmProbe label; the PMC traffic file keys
+    kernels by rocprofv3 name + workgroup count: the dual launches map onto gemm_8ph_dual_kernel with
+    one workgroup per 256x256 tile (the split-K dX halves counted twice)."""
+    k = bench.pmc_kernel_key
+    assert k("dual dX 4096x2048x16384 e2 + dW 16384x2048x4096 e1") == \
+        "void gemm_8ph_dual_kernel<true, false, 2, false, false, 1> [768 WG]"     # gate|up dX halves + dW
+    assert k("dual dX 4096x2048x6144 e2 + dW 6144x2048x4096,2048x2048x4096 e1") == \
+        "void gemm_8ph_dual_kernel<true, false, 2, false, false, 1> [512 WG]"     # q|k|v halves + q|k|v, o dW
+    assert k("dual dX 4096x8192x2048 e6 + dW 2048x8192x4096 e3") == \
+        "void gemm_8ph_dual_kernel<true, false, 6, false, false, 3> [768 WG]"     # down dX + SwiGLU bwd + dW
+    assert k("linear_wgrad_grouped") == "linear_wgrad_grouped"

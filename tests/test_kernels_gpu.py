@@ -1045,3 +1045,96 @@ def test_attention_few_head_split_forms(B, S, H, HKV, causal, rope, chunk):
         assert rel_err(dv, vv.grad.view(B, HKV, rep, S, D).sum(2).transpose(1, 2)) < 2e-2
 
 
+
+
+@pytest.mark.parametrize("epi", ["bf16", "bf16_acc", "f32_acc"])
+def test_paired_wgrad_k_segments(epi):
+    """Weight-gradient pairing (functional.WgradPairing): dW = dY_a^T X_a + dY_b^T X_b of two
+    micro-batches as ONE K = 2 T GEMM whose A (pt_gemm_problem.A2) and B (two K-segments) operands
+    are the two micro-batches' row blocks (kernels.KPair) -- grouped (q|k|v + o_proj shapes, column
+    slices of one dY buffer as the model passes them) and beside a dX group in the dual launch --
+    against the fp32 sum and against the two separate launches (equal up to the f32 summation order:
+    the pair rounds into the sink once)."""
+    from picotron_amd import kernels as K_
+    T, H = 1024, 512
+    g = torch.Generator().manual_seed(3)
+
+    def rnd(*s, sc=1.0):
+        return (torch.randn(*s, generator=g) * sc).to(BF).to(DEV)
+    dqkv = [rnd(T, 3 * H) for _ in range(2)]             # two micro-batches' dY [T, q|k|v]
+    xs = [rnd(T, H) for _ in range(2)]
+    da = [rnd(T, H) for _ in range(2)]
+    os_ = [rnd(T, H) for _ in range(2)]
+    f32 = epi == "f32_acc"
+    dt = torch.float32 if f32 else BF
+    e = {"bf16": K_.EPI_BF16, "bf16_acc": K_.EPI_BF16_ACC, "f32_acc": K_.EPI_F32_ACC}[epi]
+    base = [(torch.randn(3 * H, H, generator=g) * 0.1).to(dt).to(DEV), (torch.randn(H, H, generator=g) * 0.1).to(dt).to(DEV)]
+    init = [b.clone() if epi != "bf16" else torch.zeros_like(b) for b in base]
+    ref = [init[0].float() + sum(dqkv[i].float().t() @ xs[i].float() for i in range(2)),
+           init[1].float() + sum(da[i].float().t() @ os_[i].float() for i in range(2))]
+    # grouped: q|k|v as three row segments of one output, o_proj beside it
+    outs = [b.clone() for b in base]
+    segs = [outs[0][:H], outs[0][H:2 * H], outs[0][2 * H:]]
+    K_.linear_wgrad_grouped([(K_.KPair(dqkv[0], dqkv[1]), K_.KPair(xs[0], xs[1]), segs),
+                             (K_.KPair(da[0], da[1]), K_.KPair(os_[0], os_[1]), [outs[1]])], epilogue=e)
+    # the separate launches (the unpaired path: first half through e, second accumulating)
+    sep = [b.clone() for b in base]
+    acc = {K_.EPI_BF16: K_.EPI_BF16_ACC}.get(e, e)
+    K_.linear_wgrad_grouped([(dqkv[0], xs[0], [sep[0]]), (da[0], os_[0], [sep[1]])], epilogue=e)
+    K_.linear_wgrad_grouped([(dqkv[1], xs[1], [sep[0]]), (da[1], os_[1], [sep[1]])], epilogue=acc)
+    # dual: a dX group (q|k|v dX: dY . W) beside the paired dW group
+    w = rnd(3 * H, H, sc=0.05)
+    dual = [b.clone() for b in base]
+    dx = K_.linear_dgrad_dual(dqkv[1], [w], [(K_.KPair(dqkv[0], dqkv[1]), K_.KPair(xs[0], xs[1]), [dual[0]]),
+                                             (K_.KPair(da[0], da[1]), K_.KPair(os_[0], os_[1]), [dual[1]])], e)
+    torch.cuda.synchronize()
+    assert dx is not None and rel_err(dx, dqkv[1].float() @ w.float()) < 4e-3
+    tol = 2e-3 if f32 else 6e-3
+    for got in (outs, dual):
+        for o, r in zip(got, ref):
+            assert rel_err(o, r) < tol, epi
+    for o, s_, r in zip(outs, sep, ref):   # the pair is no further from the fp32 sum than two launches
+        assert rel_err(o, r) <= rel_err(s_, r) * 1.05 + 1e-6
+    for a, b in zip(outs, dual):
+        assert torch.equal(a, b)               # the same tiles, the same K order
+
+
+def test_paired_wgrad_training_matches_unpaired_and_oracle():
+    """train_step with weight-gradient pairing (default) vs without (PICOTRON_WGRAD_PAIR=0) on a small
+    Llama, 4 micro-batches (2 pairs) of one step, bf16 .grad sinks and fp32 main_grad (a one-rank
+    DataParallelBucket is not needed: the main_grad sink is exercised by test_golden_gpu's G8): the
+    loss is identical and every gradient agrees to bf16 rounding; both agree with the fp32 oracle's
+    accumulated gradients at north_star's tolerance."""
+    import types
+    import torch.nn.functional as F
+    from picotron_amd import process_group_manager as pgm
+    from picotron_amd.model import Llama
+    from picotron_amd.train import SyntheticMicroBatchDataLoader, train_step
+    pgm.setup_process_group_manager(1, 1, 1, 1)
+    cfg = types.SimpleNamespace(hidden_size=256, intermediate_size=512, num_attention_heads=4, num_key_value_heads=2,
+                                vocab_size=512, rms_norm_eps=1e-5, rope_theta=10000.0, num_hidden_layers=2,
+                                max_position_embeddings=256)
+    res = {}
+    for pair in (1, 0):
+        torch.manual_seed(0)
+        with torch.device(DEV):
+            model = Llama(cfg)
+        model.to(BF)
+        loader = SyntheticMicroBatchDataLoader(2, 256, 4, cfg.vocab_size, torch.device(DEV), seed=5)
+        with switches.override(wgrad_pair=pair):
+            loss = train_step(model, loader, DEV)
+        torch.cuda.synchronize()
+        res[pair] = (loss, {n: p.grad.float().cpu() for n, p in model.named_parameters()})
+        if pair:
+            params = {n: p.detach().float().cpu().requires_grad_(True) for n, p in model.named_parameters()}
+            ids_all = [(loader._inputs[i].cpu(), loader._targets[i].cpu()) for i in range(4)]
+    assert abs(res[1][0] - res[0][0]) < 1e-6 * abs(res[0][0])
+    for n in res[0][1]:
+        assert rel_err(res[1][1][n], res[0][1][n]) < 1e-2, n
+    c = dict(vars(cfg))
+    cos, sin = O.get_cos_sin(256, 64, base=10000.0)
+    for x, t in ids_all:
+        lo = O.llama_forward(x, params, c, cos.float(), sin.float(), norm=O.rmsnorm_flash_semantics)
+        (F.cross_entropy(lo.reshape(-1, cfg.vocab_size), t.reshape(-1)) / 4).backward()
+    for n, p in params.items():
+        assert rel_err(res[1][1][n], p.grad) < 2e-2, n
