@@ -86,7 +86,7 @@ def test_tp_modules_match_reference_g7():
     _dist.run(_tp_modules, 2, device="cuda")
 
 
-def _dp_g8(rank, world, wrapper, grad_type):
+def _dp_g8(rank, world, wrapper, grad_type, pair=False):
     os.environ["FLASH_ATTEN"] = "0"   # the fixture is the reference's eager path (LlamaRMSNorm)
     torch.cuda.set_device(0)
     import torch.nn.functional as F
@@ -111,12 +111,18 @@ def _dp_g8(rank, world, wrapper, grad_type):
         dp = DataParallelNaive(model)
     ids = g[f"rank{rank}.ids"]
     ga = ids.shape[1]
+    from picotron_amd import functional as FN
+    from picotron_amd.train import pairing_phase
     for i in range(ga):
         dp.require_backward_grad_sync = (i == ga - 1)
         t = ids[rank, i].to(dev)
         lo = dp(input_ids=t[:, :-1])
         loss = F.cross_entropy(lo.reshape(-1, 256), t[:, 1:].reshape(-1)) / ga   # HipLogits -> HIP CE
+        if pair:   # train_step's weight-gradient pairing: micro-batch 0 defers, 1 launches K = 2 T
+            FN.wgrad_pairing(pairing_phase(i, ga))
         loss.backward()
+    FN.wgrad_pairing(None)
+    assert not FN.WgradPairing.pending
     torch.cuda.synchronize()
     tol = TOL if grad_type == torch.float32 else 3e-2
     for n, p in model.named_parameters():
@@ -124,13 +130,16 @@ def _dp_g8(rank, world, wrapper, grad_type):
         assert _rel(p.grad, g[f"rank{rank}.grad.{n}"]) < tol, (n, _rel(p.grad, g[f"rank{rank}.grad.{n}"]))
 
 
-@pytest.mark.parametrize("wrapper,grad_type", [("bucket", torch.float32), ("bucket", torch.bfloat16),
-                                               ("naive", torch.float32)])
-def test_data_parallel_matches_reference_g8(wrapper, grad_type):
-    _dist.run(_dp_g8, 2, wrapper, grad_type, device="cuda")
+@pytest.mark.parametrize("wrapper,grad_type,pair", [("bucket", torch.float32, False), ("bucket", torch.bfloat16, False),
+                                                    ("naive", torch.float32, False), ("bucket", torch.float32, True),
+                                                    ("bucket", torch.bfloat16, True)])
+def test_data_parallel_matches_reference_g8(wrapper, grad_type, pair):
+    """pair: the two micro-batches' weight gradients as one K = 2 T launch each (train_step's
+    default, functional.WgradPairing) into the fp32 / bf16 main_grad buckets."""
+    _dist.run(_dp_g8, 2, wrapper, grad_type, pair, device="cuda")
 
 
-def _train_curve(rank, world, tp, cp, dp, out_q, kind="G10m", seq=256, avg=False):
+def _train_curve(rank, world, tp, cp, dp, out_q, kind="G10m", seq=256, avg=False, pair=False):
     """train.py's loop (train_step 29-55, steps 219-240) on the GPU path at the given tp / cp / dp from
     the fixtures' full initial weights (G10m's): the reference's wrapping rule (DataParallelBucket only
     for dp > 1, train.py:194-195), picotron_amd's fused AdamW, HipLogits -> HIP CE, the logged loss
@@ -198,7 +207,13 @@ def _train_curve(rank, world, tp, cp, dp, out_q, kind="G10m", seq=256, avg=False
             x, y = t[:, :-1][:, sl].contiguous().to(dev), t[:, 1:][:, sl].contiguous().to(dev)
             out = model(input_ids=x)
             loss = F.cross_entropy(out.reshape(-1, V), y.reshape(-1), reduction="mean") / 2
+            if pair:   # train_step's weight-gradient pairing (functional.WgradPairing)
+                from picotron_amd import functional as FN
+                from picotron_amd.train import pairing_phase
+                FN.wgrad_pairing(pairing_phase(i, 2))
             loss.backward()
+            if pair:
+                FN.wgrad_pairing(None)
             acc += loss.item()
         if world > 1:
             red = torch.tensor([acc], dtype=torch.float32)
@@ -229,9 +244,11 @@ def test_multirank_loss_curve_matches_reference_g10m(tp, cp, dp):
     print(tag, [round(x, 4) for x in losses], [round(x, 4) for x in ref])
 
 
-@pytest.mark.parametrize("tp,cp,dp,seq,avg", [(1, 1, 1, 256, False), (2, 1, 1, 256, False), (1, 2, 1, 256, False),
-                                             (1, 1, 2, 256, False), (1, 2, 1, 512, False), (1, 2, 1, 512, True)])
-def test_50_step_loss_curve_matches_reference_g11(tp, cp, dp, seq, avg):
+@pytest.mark.parametrize("tp,cp,dp,seq,avg,pair", [(1, 1, 1, 256, False, False), (2, 1, 1, 256, False, False),
+                                                  (1, 2, 1, 256, False, False), (1, 1, 2, 256, False, False),
+                                                  (1, 2, 1, 512, False, False), (1, 2, 1, 512, True, False),
+                                                  (1, 1, 1, 256, False, True), (1, 1, 2, 256, False, True)])
+def test_50_step_loss_curve_matches_reference_g11(tp, cp, dp, seq, avg, pair):
     """north_star: "the loss curve within 1 % over 50 steps", against the REFERENCE's own curves
     (G11, make_golden.g11_curve: train.py's loop run by the reference on gloo/CPU in its GPU training
     precision -- bf16 model and AdamW states, train.py:76,190 -- 50 AdamW steps at lr 1e-3, a fresh
@@ -242,10 +259,11 @@ def test_50_step_loss_curve_matches_reference_g11(tp, cp, dp, seq, avg):
     mesh, pinned to the reference's own ring -- as train.py runs it at dp 1 (G11_cp2s512: no gradient
     averaging, each cp rank steps on its own chunk's gradient; the build re-lays inside each
     attention call) and with the reference's DataParallelBucket averaging the cp ranks
-    (G11_cp2s512avg; the build keeps the whole residual stream zig-zag)."""
+    (G11_cp2s512avg; the build keeps the whole residual stream zig-zag).  pair: the step's two
+    micro-batches' weight gradients as one K = 2 T launch each (train_step's default at tp 1)."""
     import torch.multiprocessing as mp
     q = mp.get_context("spawn").SimpleQueue()
-    _dist.run(_train_curve, tp * cp * dp, tp, cp, dp, q, "G11", seq, avg, device="cuda")
+    _dist.run(_train_curve, tp * cp * dp, tp, cp, dp, q, "G11", seq, avg, pair, device="cuda")
     tag, losses, ref = q.get()
     print(tag, "max rel dev", max(abs(a - b) / b for a, b in zip(losses, ref)))
 
