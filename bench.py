@@ -46,7 +46,7 @@ if ROOT not in sys.path:
 
 # HBM bytes per GEMM launch from rocprofv3 PMC passes (tools/gpu.sh counters: bench.py --grad-acc 2, then
 # tools/traffic_summary.py); read for the roofline's `traffic`
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r05", "gemm_traffic_r05e3.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r06", "gemm_traffic_r06j.json")
 
 
 def log(*a):
@@ -706,7 +706,9 @@ def main():
     log(f"rank {rank}/{world}: model {num_params / 1e9:.3f} B params built in {time.time() - t0:.1f} s")
 
     probe = None
-    probe_mb = 1 if args.grad_acc > 1 else 0   # a steady-state micro-batch (grads accumulate)
+    # a steady-state micro-batch: the gradients accumulate (the ACC epilogues) and, with the weight-
+    # gradient pairing of train_step, the pair (2, 3) completes in it (its K = 2 T weight gradients)
+    probe_mb = 3 if args.grad_acc >= 4 else (1 if args.grad_acc > 1 else 0)
 
     def sample(i):
         # GEMM timing events only around the launches of one micro-batch per step: an event pair
@@ -839,8 +841,8 @@ def main():
                     "traffic_unit": "bytes per launch", "traffic_source": tsrc, "traffic_note": tnote,
                     "algorithmic_bytes_per_launch": d["avg_alg_bytes"], "algorithmic_flop_per_launch": d["avg_flop"],
                     "launches": d["launches"], "avg_launch_ms": d["avg_ms"],
-                    "share_of_step": d["avg_ms"] * (d["launches"] / max(args.steps, 1)) * 1e-3 * args.grad_acc /
-                    (elapsed / args.steps),
+                    # of the GEMM time of the micro-batch the family was sampled in
+                    "share_of_sampled_microbatch_gemm": fam.label_stats(dom)["total_ms"] / max(s["total_ms"], 1e-9),
                     # every bf16 MFMA GEMM launch of one micro-batch (rounds 1-5 reported this as the
                     # roofline), sampled in the last warm-up step
                     "gemm_family": {"sampled": "micro-batch %d of the first timed step" % probe_mb,
@@ -848,7 +850,7 @@ def main():
                                     "launches": s["launches"], "avg_launch_ms": s["avg_ms"],
                                     "avg_launch_gflop": s["avg_flop"] / 1e9,
                                     "algorithmic_bytes_per_launch": s["avg_alg_bytes"], "traffic": fam_traffic,
-                                    "share_of_step": s["total_ms"] * 1e-3 * args.grad_acc / (elapsed / args.steps),
+                                    "sampled_microbatch_gemm_ms": s["total_ms"],
                                     "by_launch_kind": {k: {"launches": v[0], "ms": v[1], "tflops": v[2]}
                                                        for k, v in fam.by_label().items()}}}
 

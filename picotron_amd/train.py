@@ -170,6 +170,8 @@ class GraphedTrainStep:
         fixed .grad buffers, so each call re-attaches them to the parameters (an optimizer's
         zero_grad(set_to_none=True) in between is fine) and zeroes them in place before its first
         micro-batch (one multi-tensor launch);
+      * one weight-gradient launch per micro-batch (train_step's pairing, a two-micro-batch pattern,
+        is a tp = 1 optimisation and does not apply to a replayed micro-batch);
       * no data-parallel wrapper, no CP / PP (their per-micro-batch host decisions -- the bucket
         all-reduce on the last micro-batch, the ring's host-side schedule, the pipeline's p2p
         order -- would be frozen into the graph): `supported(model)` says whether it applies;

@@ -41,10 +41,14 @@ def _step_graph_vs_eager(rank, world):
         loader = SyntheticMicroBatchDataLoader(2, 256, 4, CFG["vocab_size"], dev, seed=7, fresh=True)
         step = GraphedTrainStep(model, loader, dev) if mode == "graph" else None
         losses = []
-        for _ in range(3):
-            opt.zero_grad()
-            losses.append(step() if step is not None else train_step(model, loader, dev))
-            opt.step()
+        from picotron_amd import switches
+        # one weight-gradient launch per micro-batch on both sides: a replay repeats one captured
+        # micro-batch, so train_step's pairing (tp = 1 only) does not apply to the graphed step
+        with switches.override(wgrad_pair=0):
+            for _ in range(3):
+                opt.zero_grad()
+                losses.append(step() if step is not None else train_step(model, loader, dev))
+                opt.step()
         torch.cuda.synchronize()
         runs[mode] = (losses, [p.detach().clone() for p in model.parameters()])
         if step is not None:

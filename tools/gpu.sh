@@ -56,8 +56,8 @@ step_prof() {
 }
 
 step_pmc() {
-  timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O.pmc1 -o f -- python -u bench.py --steps 1 --warmup 0 --grad-acc 2 --cpu-tokens 0 --no-probe > $O.pmc1.log 2>&1 || { echo pmc1 failed; return 1; }
-  timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O.pmc2 -o w -- python -u bench.py --steps 1 --warmup 0 --grad-acc 2 --cpu-tokens 0 --no-probe > $O.pmc2.log 2>&1 || { echo pmc2 failed; return 1; }
+  timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O.pmc1 -o f -- python -u bench.py --steps 1 --warmup 0 --grad-acc 4 --cpu-tokens 0 --no-probe > $O.pmc1.log 2>&1 || { echo pmc1 failed; return 1; }
+  timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O.pmc2 -o w -- python -u bench.py --steps 1 --warmup 0 --grad-acc 4 --cpu-tokens 0 --no-probe > $O.pmc2.log 2>&1 || { echo pmc2 failed; return 1; }
   python tools/traffic_summary.py $O.pmc1/f_counter_collection.csv $O.pmc2/w_counter_collection.csv $O.gemm_traffic.json \
     '{"model": "SmolLM-1.7B", "layers": 15, "micro_batch": 4, "seq_len": 1024, "parallelism": "dp1"}' $LIB
 }

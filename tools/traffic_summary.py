@@ -1,6 +1,6 @@
 """HBM traffic per GEMM launch from the rocprofv3 PMC passes of one bench.py step
-(tools/gpu_round.sh <tag> pmc: `--pmc FETCH_SIZE` and `--pmc WRITE_SIZE` in separate runs of
-`bench.py --steps 1 --warmup 0 --grad-acc 1`).  Bytes = FETCH_SIZE x 2 (MI355X_MICROARCH.md: on
+(tools/gpu.sh <tag> pmc: `--pmc FETCH_SIZE` and `--pmc WRITE_SIZE` in separate runs of
+`bench.py --steps 1 --warmup 0 --grad-acc 4`).  Bytes = FETCH_SIZE x 2 (MI355X_MICROARCH.md: on
 gfx950 FETCH_SIZE reports half the bytes of wide streaming reads) + WRITE_SIZE, both counted in
 KiB.  Writes profiles/<name>.json, which bench.py reads for its roofline `traffic` (HBM bytes per
 GEMM launch, averaged over the GEMM launches of the sampled micro-batch like `achieved`).
@@ -31,7 +31,7 @@ def short(name):
     return name.split("(")[0] if "<" not in name else name.split(">")[0] + ">"
 
 
-GRAD_ACC = 2
+GRAD_ACC = 4   # tools/gpu.sh pmc: micro-batch 3 completes a weight-gradient pair with accumulating sinks
 
 
 def lib_md5(path):
