@@ -598,9 +598,11 @@ def build_parser():
                                                          "replayed HIP graph (train.GraphedTrainStep; 0: eager)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo: rehearse an N-rank grid with every rank on cuda:0 (one-GPU box); timing meaningless")
-    ap.add_argument("--mbs", type=int, default=4)
+    ap.add_argument("--mbs", type=int, default=None,
+                    help="micro-batch (default 4; 32 with --tp / --tp-proxy > 1, see resolve_batch)")
     ap.add_argument("--seq", type=int, default=1024)
-    ap.add_argument("--grad-acc", type=int, default=32)
+    ap.add_argument("--grad-acc", type=int, default=None,
+                    help="micro-batches per step (default 32; 4 with the TP micro-batch default)")
     ap.add_argument("--cpu-tokens", type=int, default=1024, help="tokens in the cpu_baseline sample (0 = skip)")
     ap.add_argument("--no-probe", action="store_true", help="do not time GEMM launches with events")
     ap.add_argument("--bucket-mb", type=float, default=25, help="DataParallelBucket bucket_cap_mb (reference: 25)")
@@ -615,8 +617,26 @@ def build_parser():
     return ap
 
 
+def resolve_batch(args):
+    """Fill in --mbs / --grad-acc.  Defaults: mbs 4 x grad_acc 32 (BASELINE's config 2).  Pure tensor
+    parallelism (--tp or --tp-proxy > 1 without cp / pp: config 3, which names no micro-batch) with
+    neither given: mbs 32 x grad_acc 4 -- the same 128 sequences and the same gradient per step --
+    because a TP = 8 rank's shard GEMMs starve at 4096 rows (64 k tokens/s/GPU of compute at mbs 4,
+    101 k at mbs 32) and a micro-batch of 32 sequences runs the chunked layout in 4 chunks, 3/4 of
+    its collectives under the other chunks' compute (sequence_parallel.CHUNK_MIN_ROWS; the
+    measurements and the projection in profiles/r06/notes_r06.md)."""
+    pure_tp = max(args.tp, args.tp_proxy) > 1 and args.cp == 1 and args.pp == 1
+    if pure_tp and args.mbs is None and args.grad_acc is None:
+        args.mbs, args.grad_acc = 32, 4
+    if args.mbs is None:
+        args.mbs = 4
+    if args.grad_acc is None:
+        args.grad_acc = 32
+    return args
+
+
 def main():
-    args = build_parser().parse_args()
+    args = resolve_batch(build_parser().parse_args())
     proxy = bool(args.tp_proxy or args.cp_proxy)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1 and not proxy:
         # `python bench.py --gpus N`: start the N ranks ourselves (before any GPU call in this process)

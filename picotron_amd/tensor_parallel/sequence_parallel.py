@@ -16,9 +16,9 @@ sequences, and rank r holds rows [r n, (r + 1) n) of every chunk (n = B S / (c t
 chunk, viewed [B, S/tp, H].  Each chunk's collective is its own, so a layer overlaps chunk j + 1's
 all-gather with chunk j's GEMMs and chunk j's reduce-scatter with chunk j + 1's
 (functional.DecoderLayerFunction._forward_sp).  c = `layout_chunks`: by default as many chunks (up
-to 4) as keep >= 4096 token rows each -- the shard GEMMs at fewer rows cost more than the hidden
-collectives save -- so one chunk at BASELINE's mbs 4 x seq 1024 (rank r then holds rows
-[r T/tp, (r+1) T/tp)); the `tp_sp_chunks` switch forces a count (tests, A/B).
+to 8) as keep >= 8192 token rows each -- the shard GEMMs at fewer rows cost more than the hidden
+collectives save -- so one chunk at mbs 4 or 8 x seq 1024 (rank r then holds rows
+[r T/tp, (r+1) T/tp)), two at mbs 16, four at mbs 32; the `tp_sp_chunks` switch forces a count.
 
 Entry / exit, as the zig-zag CP residual (context_parallel.enable_zigzag_residual): the vocab-parallel
 embedding's masked lookup is reduce-scattered straight into the shards (the reference all-reduces it,
@@ -55,19 +55,22 @@ def sp_supported():
 
 
 # auto chunking keeps every chunk at least this many token rows: the TP-shard GEMMs lose too much
-# below it (TP = 8 SmolLM-1.7B proxy, 2 chunks of 2048 rows: 10.5 vs 6.45 ms of GEMMs per micro-batch
-# against the ~2.7 ms of collectives the chunks could hide; profiles/r06/notes_r06.md)
-CHUNK_MIN_ROWS = 4096
+# below it.  TP = 8 SmolLM-1.7B proxy, replayed ms per micro-batch (profiles/r06/notes_r06.md):
+# mbs 8 (8192 rows) 10.2 in one chunk, 15.6 in two; mbs 16: 19.3 / 20.8; mbs 32: 35.7 / 39.0 / 40.5
+# in 1 / 2 / 4 chunks -- a chunk of 4096 rows costs half again, one of >= 8192 rows 8-14 %, against the
+# (c - 1) / c of the exposed collectives (~5.4 ms per 4096 tokens at 250 GB/s) it takes off the path
+CHUNK_MIN_ROWS = 8192
+CHUNK_MAX = 8
 
 
 def layout_chunks(B, S, tp):
     """Chunks of the token-row layout for a [B, S] batch over tp ranks: 0 = not shardable (S % tp),
-    else the largest power of two c <= the tp_sp_chunks switch (0 = auto: <= 4, and each chunk >=
-    CHUNK_MIN_ROWS rows) dividing B with (B / c) S % tp == 0."""
+    else the largest power of two c <= the tp_sp_chunks switch (0 = auto: <= CHUNK_MAX, and each
+    chunk >= CHUNK_MIN_ROWS rows) dividing B with (B / c) S % tp == 0."""
     if S % tp:
         return 0
     auto = SW.tp_sp_chunks <= 0
-    c = 4 if auto else SW.tp_sp_chunks
+    c = CHUNK_MAX if auto else SW.tp_sp_chunks
     while c > 1 and (B % c or (B // c * S) % tp or (auto and B // c * S < CHUNK_MIN_ROWS)):
         c //= 2
     return c

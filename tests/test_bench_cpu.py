@@ -132,3 +132,18 @@ def test_pmc_kernel_key_for_dual_labels():
     assert k("dual dX 4096x8192x2048 e6 + dW 2048x8192x4096 e3") == \
         "void gemm_8ph_dual_kernel<true, false, 6, false, false, 3> [768 WG]"     # down dX + SwiGLU bwd + dW
     assert k("linear_wgrad_grouped") == "linear_wgrad_grouped"
+
+
+def test_resolve_batch_defaults():
+    """Config 2's mbs 4 x grad_acc 32 by default; pure TP (config 3) mbs 32 x grad_acc 4 -- the same
+    128 sequences per step -- unless either is given; cp / pp keep the config-2 defaults."""
+    import bench
+
+    def r(*a):
+        x = bench.resolve_batch(bench.build_parser().parse_args(list(a)))
+        return x.mbs, x.grad_acc
+    assert r() == (4, 32)
+    assert r("--tp", "8") == (32, 4) and r("--tp-proxy", "8") == (32, 4)
+    assert r("--tp", "8", "--mbs", "4") == (4, 32) and r("--tp", "8", "--grad-acc", "4") == (4, 4)
+    assert r("--model", "llama2-7b", "--tp", "2", "--pp", "2", "--gpus", "8") == (4, 32)
+    assert r("--cp", "8", "--mbs", "1") == (1, 32)

@@ -682,9 +682,11 @@ def _sp_host(rank, world):
     with switches.override(tp_sp_chunks=2):
         assert SPM.layout_chunks(B, S, world) == 2 and SPM.layout_chunks(B, S + 1, world) == 0
         assert SPM.layout_chunks(1, S, world) == 1 and SPM.layout_chunks(3, S, world) == 1
-    # auto: chunks of >= 4096 rows (BASELINE's mbs 4 x seq 1024: one chunk; mbs 8: two)
+    # auto: chunks of >= 8192 rows, at most 8 (mbs 4 / 8 x seq 1024: one chunk; 16: two; 32: four)
     assert SPM.layout_chunks(B, S, world) == 1 and SPM.layout_chunks(4, 1024, 8) == 1
-    assert SPM.layout_chunks(8, 1024, 8) == 2 and SPM.layout_chunks(16, 1024, 8) == 4
+    assert SPM.layout_chunks(8, 1024, 8) == 1 and SPM.layout_chunks(16, 1024, 8) == 2
+    assert SPM.layout_chunks(32, 1024, 8) == 4 and SPM.layout_chunks(128, 1024, 8) == 8
+    assert SPM.layout_chunks(12, 1024, 8) == 1
     assert torch.equal(SPM.shard_rows(full, tp, c), mine2)
     assert torch.equal(SPM.gather_rows(mine2, tp, c), full)
     out = torch.empty_like(full)

@@ -38,7 +38,7 @@ def _shard(full, local, rank):
     return full.narrow(d, rank * n, n)
 
 
-def _setup(tp, cp, seq=256, cfg_over=None):
+def _setup(tp, cp, seq=256, cfg_over=None, batch=2):
     import types
     os.environ["FLASH_ATTEN"] = "1"
     torch.cuda.set_device(0)
@@ -65,7 +65,7 @@ def _setup(tp, cp, seq=256, cfg_over=None):
         for n, p in names.items():
             p.copy_(_shard(full[n], p, m.tp_rank))
     g = torch.Generator().manual_seed(11)
-    ids = torch.randint(0, base["vocab_size"], (2, seq + 1), generator=g)
+    ids = torch.randint(0, base["vocab_size"], (batch, seq + 1), generator=g)
     # the oracle on the full model, fp32 from the same bf16 weights
     pf = {k: v.float().requires_grad_(True) for k, v in full.items()}
     cos, sin = O.get_cos_sin(seq, 64, base=CFG["rope_theta"])
@@ -76,7 +76,7 @@ def _setup(tp, cp, seq=256, cfg_over=None):
 
 
 def _llama(rank, world, tp, cp, seq=256, zigzag=False, residual=1, mesh=1, production_thresholds=False, sp=1,
-           cfg_over=None, chunks=2):
+           cfg_over=None, chunks=2, batch=2):
     from picotron_amd import switches
     # conftest.py zeroes the RoPE / SwiGLU fusion tile thresholds for the small test shapes;
     # production_thresholds restores the shipped ones (96 / 192 / 0), under which these TP-shard
@@ -84,14 +84,15 @@ def _llama(rank, world, tp, cp, seq=256, zigzag=False, residual=1, mesh=1, produ
     thr = dict(rope_fuse_min_tiles=96, swiglu_fuse_min_tiles=192, swiglu_bwd_min_tiles=0) \
         if production_thresholds else {}
     with switches.override(zigzag_residual=residual, ring_mesh=mesh, tp_sp=sp, tp_sp_chunks=chunks, **thr):
-        _llama_body(rank, world, tp, cp, seq, zigzag, residual, cfg_over)
+        _llama_body(rank, world, tp, cp, seq, zigzag, residual, cfg_over, batch)
 
 
-def _llama_body(rank, world, tp, cp, seq, zigzag, residual, cfg_over=None):
+def _llama_body(rank, world, tp, cp, seq, zigzag, residual, cfg_over=None, batch=2):
     from picotron_amd import functional as FN
     from picotron_amd import switches
     from picotron_amd.context_parallel import context_parallel as CP
-    m, model, names, pf, ids, lo, loss_r = _setup(tp, cp, seq, cfg_over)
+    m, model, names, pf, ids, lo, loss_r = _setup(tp, cp, seq, cfg_over, batch)
+    B = batch
     V = dict(CFG, **(cfg_over or {}))["vocab_size"]
     # sequence parallelism (tensor_parallel/sequence_parallel.py): on at tp > 1 without cp, by default
     sp_on = tp > 1 and cp == 1 and switches.S.tp_sp != 0
@@ -120,7 +121,7 @@ def _llama_body(rank, world, tp, cp, seq, zigzag, residual, cfg_over=None):
         logits = model(x.cuda())
         n_fwd = len(calls)
         n_ag_fwd = len(gathers)
-        assert logits.shape == (2, s, V)             # final_proj gathers its vocab shards
+        assert logits.shape == (B, s, V)             # final_proj gathers its vocab shards
         loss = FN.cross_entropy(logits.view(-1, V), t.reshape(-1).cuda())
         loss.backward()
         torch.cuda.synchronize()
@@ -129,17 +130,17 @@ def _llama_body(rank, world, tp, cp, seq, zigzag, residual, cfg_over=None):
         FN.TPContext.all_gather_rows_into = orig_ag
     L, H = CFG["num_hidden_layers"], dict(CFG, **(cfg_over or {}))["hidden_size"]
     # the vocab-parallel CE (functional.VocabParallelCEFunction): one gather of 16 B per row at tp > 1
-    vp = [g for g in gathers if g == (2 * s, 4)]
-    vp_on = tp > 1 and FN.vp_ce_shape_ok(2 * s, V // tp, H)   # V 512 at tp 8: V / tp = 64 does not tile
+    vp = [g for g in gathers if g == (B * s, 4)]
+    vp_on = tp > 1 and FN.vp_ce_shape_ok(B * s, V // tp, H)   # V 512 at tp 8: V / tp = 64 does not tile
     assert vp_on == (tp > 1 and (V // tp) % 128 == 0 and switches.S.vp_ce != 0)
     assert len(vp) == (1 if vp_on else 0), gathers
-    gathers = [g for g in gathers if g != (2 * s, 4)]
+    gathers = [g for g in gathers if g != (B * s, 4)]
     if sp_on:   # per layer and chunk 2 gathers each way, plus the exit (forward) / the entry (backward)
         from picotron_amd.tensor_parallel import sequence_parallel as SPM
-        c = SPM.layout_chunks(2, s, tp)
-        assert c == (min(2, switches.S.tp_sp_chunks) if switches.S.tp_sp_chunks > 0 else 1), c   # B 2
+        c = SPM.layout_chunks(B, s, tp)
+        assert c == (min(B, switches.S.tp_sp_chunks) if switches.S.tp_sp_chunks > 0 else 1), c
         assert n_ag_fwd == c * (2 * L + 1) and len(gathers) == c * (4 * L + 2), gathers
-        assert all(g == (2 * s // (tp * c), H) for g in gathers), gathers   # every gather is of T / (tp c) rows
+        assert all(g == (B * s // (tp * c), H) for g in gathers), gathers   # every gather is of T / (tp c) rows
     else:
         assert not gathers
     if zigzag and residual:
@@ -179,6 +180,13 @@ def test_tensor_parallel_llama_tp2_one_chunk():
     """tp2 with the sequence-parallel layout in one chunk (PICOTRON_TP_SP_CHUNKS=1: rank r holds rows
     [r T/tp, (r+1) T/tp), every collective of a block in one piece)."""
     _dist.run(_llama, 2, 2, 1, 256, False, 1, 1, False, 1, None, 1, device="cuda")
+
+
+def test_tensor_parallel_llama_tp8_four_chunks():
+    """tp8 in the layout bench.py's config-3 default runs (mbs 32: 4 chunks): batch 4, each sequence a
+    chunk, 32 token rows per rank and chunk -- every chunk's collectives its own -- against the oracle."""
+    over = dict(hidden_size=512, intermediate_size=1024, num_attention_heads=8, num_key_value_heads=8)
+    _dist.run(_llama, 8, 8, 1, 256, False, 1, 1, False, 1, over, 4, 4, device="cuda")
 
 
 def test_tensor_parallel_llama_tp2_replicated_stream():
