@@ -33,7 +33,7 @@ DEFAULTS = {
     "ring_zigzag": 1, "zigzag_residual": 1, "ring_mesh": 1,
     # tensor_parallel/sequence_parallel.py: the residual stream sharded by token rows over the tp group,
     # in a layout of (up to) this many chunks, whose collectives overlap the other chunks' GEMMs
-    # (0 = auto: chunks of >= 4096 token rows)
+    # (0 = auto: chunks of >= 8192 token rows, at most 8)
     "tp_sp": 1, "tp_sp_chunks": 0,
     # functional.py: the TP lm_head's F.cross_entropy on the vocab shards (no logits all-gather)
     "vp_ce": 1,
