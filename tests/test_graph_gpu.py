@@ -135,6 +135,6 @@ def _tp_graph_vs_eager(rank, world, chunks):
         assert torch.equal(a, b), i
 
 
-@pytest.mark.parametrize("chunks", [2, 1])
+@pytest.mark.parametrize("chunks", [4, 2, 1])   # 4: the layout of bench.py's TP default (mbs 32)
 def test_graphed_tp_layers_equal_eager(chunks):
     _dist.run(_tp_graph_vs_eager, 1, chunks, device="cuda", backend="nccl")
