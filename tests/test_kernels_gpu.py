@@ -1099,9 +1099,11 @@ def test_paired_wgrad_k_segments(epi):
         assert torch.equal(a, b)               # the same tiles, the same K order
 
 
-def test_paired_wgrad_training_matches_unpaired_and_oracle():
+@pytest.mark.parametrize("ga", [4, 3])
+def test_paired_wgrad_training_matches_unpaired_and_oracle(ga):
     """train_step with weight-gradient pairing (default) vs without (PICOTRON_WGRAD_PAIR=0) on a small
-    Llama, 4 micro-batches (2 pairs) of one step, bf16 .grad sinks and fp32 main_grad (a one-rank
+    Llama, ga micro-batches of one step (4: 2 pairs; 3: a pair and a last micro-batch launched on its
+    own), bf16 .grad sinks and fp32 main_grad (a one-rank
     DataParallelBucket is not needed: the main_grad sink is exercised by test_golden_gpu's G8): the
     loss is identical and every gradient agrees to bf16 rounding; both agree with the fp32 oracle's
     accumulated gradients at north_star's tolerance."""
@@ -1120,14 +1122,14 @@ def test_paired_wgrad_training_matches_unpaired_and_oracle():
         with torch.device(DEV):
             model = Llama(cfg)
         model.to(BF)
-        loader = SyntheticMicroBatchDataLoader(2, 256, 4, cfg.vocab_size, torch.device(DEV), seed=5)
+        loader = SyntheticMicroBatchDataLoader(2, 256, ga, cfg.vocab_size, torch.device(DEV), seed=5)
         with switches.override(wgrad_pair=pair):
             loss = train_step(model, loader, DEV)
         torch.cuda.synchronize()
         res[pair] = (loss, {n: p.grad.float().cpu() for n, p in model.named_parameters()})
         if pair:
             params = {n: p.detach().float().cpu().requires_grad_(True) for n, p in model.named_parameters()}
-            ids_all = [(loader._inputs[i].cpu(), loader._targets[i].cpu()) for i in range(4)]
+            ids_all = [(loader._inputs[i].cpu(), loader._targets[i].cpu()) for i in range(ga)]
     assert abs(res[1][0] - res[0][0]) < 1e-6 * abs(res[0][0])
     for n in res[0][1]:
         assert rel_err(res[1][1][n], res[0][1][n]) < 1e-2, n
@@ -1135,6 +1137,6 @@ def test_paired_wgrad_training_matches_unpaired_and_oracle():
     cos, sin = O.get_cos_sin(256, 64, base=10000.0)
     for x, t in ids_all:
         lo = O.llama_forward(x, params, c, cos.float(), sin.float(), norm=O.rmsnorm_flash_semantics)
-        (F.cross_entropy(lo.reshape(-1, cfg.vocab_size), t.reshape(-1)) / 4).backward()
+        (F.cross_entropy(lo.reshape(-1, cfg.vocab_size), t.reshape(-1)) / ga).backward()
     for n, p in params.items():
         assert rel_err(res[1][1][n], p.grad) < 2e-2, n
