@@ -139,12 +139,13 @@ def test_data_parallel_matches_reference_g8(wrapper, grad_type, pair):
     _dist.run(_dp_g8, 2, wrapper, grad_type, pair, device="cuda")
 
 
-def _train_curve(rank, world, tp, cp, dp, out_q, kind="G10m", seq=256, avg=False, pair=False):
+def _train_curve(rank, world, tp, cp, dp, out_q, kind="G10m", seq=256, avg=False, pair=False, chunks=0):
     """train.py's loop (train_step 29-55, steps 219-240) on the GPU path at the given tp / cp / dp from
     the fixtures' full initial weights (G10m's): the reference's wrapping rule (DataParallelBucket only
     for dp > 1, train.py:194-195), picotron_amd's fused AdamW, HipLogits -> HIP CE, the logged loss
     averaged over cp_dp (utils.py:93-98).  kind G10m: 4 steps on one batch, lr 1e-2; G11: 50 steps,
-    a fresh bigram batch per step (the fixture's token stream), lr 1e-3."""
+    a fresh bigram batch per step (the fixture's token stream), lr 1e-3.  chunks > 0: the
+    sequence-parallel layout forced to that many chunks (tp > 1)."""
     os.environ["FLASH_ATTEN"] = "0"   # the fixture is the reference's eager path (LlamaRMSNorm, SDPA)
     torch.cuda.set_device(0)
     import torch.distributed as dist
@@ -197,6 +198,20 @@ def _train_curve(rank, world, tp, cp, dp, out_q, kind="G10m", seq=256, avg=False
     opt = AdamW(model.parameters(), lr=lr)
     sl = slice(m.cp_rank * S // cp, (m.cp_rank + 1) * S // cp)
     losses = []
+    from picotron_amd import switches
+    force = switches.override(tp_sp_chunks=chunks)
+    force.__enter__()
+    seen_c = set()
+    if chunks:
+        from picotron_amd import functional as FN_
+        from picotron_amd.tensor_parallel import sequence_parallel as SPM
+        assert SPM.layout_chunks(ids.shape[-2], S // cp, tp) == chunks
+        orig_gc = FN_.TPContext.gather_chunk
+
+        def gc(self, full, shard, c, j, async_op=False):
+            seen_c.add(c)
+            return orig_gc(self, full, shard, c, j, async_op)
+        FN_.TPContext.gather_chunk = gc
     for step in range(g["rank0.losses"].numel()):
         opt.zero_grad()
         acc = 0.0
@@ -223,9 +238,13 @@ def _train_curve(rank, world, tp, cp, dp, out_q, kind="G10m", seq=256, avg=False
         opt.step()
         if hasattr(model, "reset"):
             model.reset()
+    force.__exit__(None, None, None)
+    if chunks:
+        FN_.TPContext.gather_chunk = orig_gc
+        assert seen_c == {chunks}, seen_c   # every sharded collective ran in the forced layout
     ref = g["rank0.losses"].tolist()
     if rank == 0:
-        out_q.put((tag, losses, ref))
+        out_q.put((tag + (f"c{chunks}" if chunks else ""), losses, ref))
     for k, (a, b) in enumerate(zip(losses, ref)):
         assert abs(a - b) <= 0.01 * abs(b), (tag, k, losses, ref)   # north_star: within 1 %
 
@@ -244,11 +263,12 @@ def test_multirank_loss_curve_matches_reference_g10m(tp, cp, dp):
     print(tag, [round(x, 4) for x in losses], [round(x, 4) for x in ref])
 
 
-@pytest.mark.parametrize("tp,cp,dp,seq,avg,pair", [(1, 1, 1, 256, False, False), (2, 1, 1, 256, False, False),
-                                                  (1, 2, 1, 256, False, False), (1, 1, 2, 256, False, False),
-                                                  (1, 2, 1, 512, False, False), (1, 2, 1, 512, True, False),
-                                                  (1, 1, 1, 256, False, True), (1, 1, 2, 256, False, True)])
-def test_50_step_loss_curve_matches_reference_g11(tp, cp, dp, seq, avg, pair):
+@pytest.mark.parametrize("tp,cp,dp,seq,avg,pair,chunks", [
+    (1, 1, 1, 256, False, False, 0), (2, 1, 1, 256, False, False, 0), (2, 1, 1, 256, False, False, 2),
+    (1, 2, 1, 256, False, False, 0), (1, 1, 2, 256, False, False, 0),
+    (1, 2, 1, 512, False, False, 0), (1, 2, 1, 512, True, False, 0),
+    (1, 1, 1, 256, False, True, 0), (1, 1, 2, 256, False, True, 0)])
+def test_50_step_loss_curve_matches_reference_g11(tp, cp, dp, seq, avg, pair, chunks):
     """north_star: "the loss curve within 1 % over 50 steps", against the REFERENCE's own curves
     (G11, make_golden.g11_curve: train.py's loop run by the reference on gloo/CPU in its GPU training
     precision -- bf16 model and AdamW states, train.py:76,190 -- 50 AdamW steps at lr 1e-3, a fresh
@@ -260,12 +280,13 @@ def test_50_step_loss_curve_matches_reference_g11(tp, cp, dp, seq, avg, pair):
     averaging, each cp rank steps on its own chunk's gradient; the build re-lays inside each
     attention call) and with the reference's DataParallelBucket averaging the cp ranks
     (G11_cp2s512avg; the build keeps the whole residual stream zig-zag).  pair: the step's two
-    micro-batches' weight gradients as one K = 2 T launch each (train_step's default at tp 1)."""
+    micro-batches' weight gradients as one K = 2 T launch each (train_step's default at tp 1).
+    chunks 2 at tp2: the sequence-parallel layer in two token chunks, each with its own collectives."""
     import torch.multiprocessing as mp
     q = mp.get_context("spawn").SimpleQueue()
-    _dist.run(_train_curve, tp * cp * dp, tp, cp, dp, q, "G11", seq, avg, pair, device="cuda")
+    _dist.run(_train_curve, tp * cp * dp, tp, cp, dp, q, "G11", seq, avg, pair, chunks, device="cuda")
     tag, losses, ref = q.get()
-    print(tag, "max rel dev", max(abs(a - b) / b for a, b in zip(losses, ref)))
+    print(tag, "max rel dev", max(abs(a - b) / b for a, b in zip(losses, ref)), "last", losses[-1], "ref", ref[-1])
 
 
 def _pp_curve(rank, world, engine, out_q):
