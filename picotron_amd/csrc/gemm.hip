@@ -1562,9 +1562,14 @@ void set_smem_once(Kern k, int smem) {
 // profiles/r04/group_m/, two boxes, interleaved): 6 -> 156.6-157.5 k, 5 / 7 -> 156.2-157.8 k,
 // 4 -> 155.4-155.9 k, the previous 8 (256x256) / 4 (256x128) -> 154.9-155.0 k tokens/s
 // (the A/B variant that overrode it is retired: every other count measured slower)
+// round 6 (weight-gradient pairing on), same box, 2 interleaved rounds (profiles/r06/notes_r06.md):
+// 6 -> 164.7 / 165.4 k, 4 -> 165.4 / 165.0 k, 8 -> 163.7 / 164.0 k.  -DPT_GROUP_M=n builds the A/B form.
+#ifndef PT_GROUP_M
+#define PT_GROUP_M 6
+#endif
 int group_m_for(int bm, int bn) {
   (void)bm; (void)bn;
-  return 6;
+  return PT_GROUP_M;
 }
 
 inline int group_tiles(GemmGroup& g, int bm, int bn) {
