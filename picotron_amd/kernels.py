@@ -569,6 +569,101 @@ def _bounds(sizes):
     return out
 
 
+# ------------------------------------------------------------------ shapes off the 64-element grid
+# Every GEMM tile is a multiple of 64 in M, N and K (the smallest tile is 64x64, the K-tile 64), so a
+# projection whose T, width or K is not (Llama-2-7B at tp 8: a vocab shard of 4000, an intermediate
+# shard of 1376; an odd token count) runs on zero-padded copies: the padding adds zero products
+# (the real outputs are the unpadded kernel's, bit for bit, K-order unchanged) and is sliced off.  The
+# layer shapes of picotron's configs tile and never take this path.
+GRID = 64
+
+
+def _up(n):
+    return -(-int(n) // GRID) * GRID
+
+
+def _on_grid(*dims):
+    return all(int(d) % GRID == 0 for d in dims)
+
+
+def _pad2(t, rows, cols):
+    """A zero-padded contiguous [rows, cols] copy of a 2-D tensor (or the tensor when it fits)."""
+    if tuple(t.shape) == (rows, cols) and t.is_contiguous():
+        return t
+    out = torch.zeros(rows, cols, dtype=t.dtype, device=t.device)
+    out[:t.shape[0], :t.shape[1]] = t
+    return out
+
+
+def _pad_cols_segments(t, rows, ns):
+    """[r, sum ns] with column segments of widths ns -> [rows, sum _up(n)], each segment at its
+    padded offset (the segments of a stacked q|k|v or gate|up output)."""
+    out = torch.zeros(rows, sum(_up(n) for n in ns), dtype=t.dtype, device=t.device)
+    src = dst = 0
+    for n in ns:
+        out[:t.shape[0], dst:dst + n] = t[:, src:src + n]
+        src, dst = src + n, dst + _up(n)
+    return out
+
+
+def _unpad_cols_segments(tp, rows, ns):
+    """Inverse of _pad_cols_segments: the real columns of every segment, [rows, sum ns] (a copy)."""
+    if len(ns) == 1:
+        return tp[:rows, :ns[0]]
+    parts, off = [], 0
+    for n in ns:
+        parts.append(tp[:rows, off:off + n])
+        off += _up(n)
+    return torch.cat(parts, dim=1)
+
+
+def _linear_fwd_padded(x2d, weights, out, residual):
+    T, K = x2d.shape
+    ns = [w.shape[0] for w in weights]
+    Tp, Kp = _up(T), _up(K)
+    rp = None if residual is None else _pad_cols_segments(residual, Tp, ns)
+    yp = linear_fwd(_pad2(x2d, Tp, Kp), [_pad2(w, _up(n), Kp) for w, n in zip(weights, ns)], residual=rp)
+    y = _unpad_cols_segments(yp, T, ns)
+    if out is None:
+        return y.contiguous()
+    out.copy_(y)
+    return out
+
+
+def _linear_dgrad_padded(dy2d, weights, out, accumulate):
+    T = dy2d.shape[0]
+    Kin = weights[0].shape[1]
+    ns = [w.shape[0] for w in weights]
+    Tp, Kp = _up(T), _up(Kin)
+    dxp = linear_dgrad(_pad_cols_segments(dy2d, Tp, ns), [_pad2(w, _up(n), Kp) for w, n in zip(weights, ns)])
+    dx = dxp[:T, :Kin]
+    if out is None:
+        return dx.contiguous()
+    if accumulate:   # EPI_BF16_ACC's bf16(old + bf16(new)): dx is already the bf16 product
+        out.copy_(out + dx)
+    else:
+        out.copy_(dx)
+    return out
+
+
+def _linear_wgrad_padded(dy2d, x2d, outs, epilogue):
+    """dW_i into the sinks outs with the epilogue's semantics: EPI_BF16 store, EPI_BF16_ACC
+    bf16(old + bf16(new)), EPI_F32 store / EPI_F32_ACC old + new in f32 (the f32 product, unrounded)."""
+    T = dy2d.shape[0]
+    Kin = x2d.shape[1]
+    ns = [o.shape[0] for o in outs]
+    Tp, Kp = _up(T), _up(Kin)
+    f32 = epilogue in (EPI_F32, EPI_F32_ACC)
+    tmp = [torch.empty(_up(n), Kp, dtype=torch.float32 if f32 else BF16, device=dy2d.device) for n in ns]
+    linear_wgrad(_pad_cols_segments(dy2d, Tp, ns), _pad2(x2d, Tp, Kp), tmp, EPI_F32 if f32 else EPI_BF16)
+    for o, t, n in zip(outs, tmp, ns):
+        if epilogue in (EPI_BF16_ACC, EPI_F32_ACC):
+            o.copy_(o + t[:n, :Kin])
+        else:
+            o.copy_(t[:n, :Kin])
+    return outs
+
+
 def _problem(A, lda, Bs, ldbs, b_bounds, b_seg_dim, Cs, ldcs, c_bounds, M, N, K):
     pr = _C.GemmProblem()
     pr.A, pr.lda = _ptr(A), int(lda)
@@ -774,6 +869,14 @@ def linear_wgrad_grouped(jobs, epilogue=EPI_BF16, tile=-1):
     """Several wgrad GEMMs (dW_i = dY_i^T X for each job (dy2d, x2d, outs)) in ONE launch
     (pt_gemm_grouped): e.g. dW of q|k|v (192 tiles) + dW of o_proj (64 tiles) fill 256 CUs.  A group
     that would leave most CUs idle (TP shards) runs split-K (wgrad_ksplit)."""
+    if not all(_on_grid(dy.shape[0], x.shape[1], *[o.shape[0] for o in outs]) for dy, x, outs in jobs):
+        # a job off the 64-grid: every job on its own (linear_wgrad pads; a pair as its two halves)
+        if _is_paired(jobs):
+            _wgrad_unpaired(jobs, epilogue)
+        else:
+            for dy, x, outs in jobs:
+                linear_wgrad(dy, x, outs, epilogue)
+        return
     paired = _is_paired(jobs)
     if paired:
         tile = 12   # the K-segmented A: the 256x256 8-phase kernel only
@@ -822,6 +925,10 @@ def linear_fwd(x2d, weights, out=None, tile=-1, residual=None):
         _req(w.dtype == BF16 and w.is_contiguous() and w.shape[1] == K, "weight must be contiguous [N, K] bf16")
     ns = [w.shape[0] for w in weights]
     N = sum(ns)
+    if not _on_grid(T, K, *ns):
+        if residual is not None:
+            _req(tuple(residual.shape) == (T, N), "residual shape")
+        return _linear_fwd_padded(x2d, weights, out, residual)
     y = out if out is not None else torch.empty(T, N, dtype=BF16, device=x2d.device)
     _req(y.stride(1) == 1 and y.shape == (T, N), "out shape")
     epi, ldr = EPI_BF16, 0
@@ -1147,6 +1254,8 @@ def linear_dgrad(dy2d, weights, out=None, accumulate=False, tile=-1, keep_parts=
     Kin = weights[0].shape[1]
     ns = [w.shape[0] for w in weights]
     _req(sum(ns) == N, "dgrad: dY width must equal the stacked weight rows")
+    if not _on_grid(T, Kin, *ns):
+        return _linear_dgrad_padded(dy2d, weights, out, accumulate)
     if out is None and not accumulate and tile < 0 and _splitk_enabled() and len(weights) <= 3:
         h = _splitk_halves(T, Kin, N, split_min)
         if h is not None and all(w.dtype == BF16 and w.is_contiguous() for w in weights) and \
@@ -1323,6 +1432,8 @@ def linear_wgrad(dy2d, x2d, outs, epilogue=EPI_BF16, tile=-1):
     Kin = x2d.shape[1]
     ns = [o.shape[0] for o in outs]
     _req(sum(ns) == N, "wgrad: output rows must cover dY's width")
+    if not _on_grid(T, Kin, *ns):
+        return _linear_wgrad_padded(dy2d, x2d, outs, epilogue)
     if tile < 0 and epilogue in (EPI_BF16, EPI_BF16_ACC, EPI_F32_ACC):
         hq = hq_form([(N, Kin, T)]) if all(n % 128 == 0 for n in ns) else 0
         sinks_ok = all(_reduce_sink_ok(o) for o in outs)

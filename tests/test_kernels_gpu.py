@@ -264,6 +264,45 @@ def test_gemm_every_tile_every_layout(tile):
     assert rel_err(dw, _ref_mm(dy.t(), a)) < 1e-2
 
 
+@pytest.mark.parametrize("T,K,ns", [(100, 72, [40, 24]), (4000 // 8, 1376 // 8, [4000 // 8]), (192, 1376, [96]),
+                                    (256, 256, [200])])
+def test_gemm_off_grid_shapes_run_padded(T, K, ns):
+    """Projections whose T, K or output widths are not multiples of 64 (no GEMM tile covers them:
+    Llama-2-7B at tp 8 has a vocab shard of 4000 and an intermediate shard of 1376) run on
+    zero-padded copies (kernels._linear_*_padded): forward with stacked segments and the residual
+    epilogue, dX plain and accumulated, dW stored / bf16-accumulated / f32-accumulated, and a
+    micro-batch pair's dW (KPair) -- each against torch fp32 on the same bf16 inputs."""
+    from picotron_amd import kernels as K_
+    N = sum(ns)
+    x = torch.randn(T, K).to(BF)
+    ws = [(torch.randn(n, K) / math.sqrt(K)).to(BF) for n in ns]
+    res = torch.randn(T, N).to(BF)
+    dy = torch.randn(T, N).to(BF)
+    W = torch.cat([w.float() for w in ws])
+    y = K_.linear_fwd(x.to(DEV), [w.to(DEV) for w in ws])
+    assert y.shape == (T, N) and rel_err(y, x.float() @ W.t()) < 1e-2
+    yr = K_.linear_fwd(x.to(DEV), [w.to(DEV) for w in ws], residual=res.to(DEV))
+    assert rel_err(yr, res.float() + x.float() @ W.t()) < 1e-2
+    dx = K_.linear_dgrad(dy.to(DEV), [w.to(DEV) for w in ws])
+    assert dx.shape == (T, K) and rel_err(dx, dy.float() @ W) < 1e-2
+    acc = torch.randn(T, K).to(BF).to(DEV)
+    want = acc.float().cpu() + dy.float() @ W
+    K_.linear_dgrad(dy.to(DEV), [w.to(DEV) for w in ws], out=acc, accumulate=True)
+    assert rel_err(acc, want) < 1e-2
+    ref = dy.float().t() @ x.float()
+    for epi, dt in ((K_.EPI_BF16, BF), (K_.EPI_BF16_ACC, BF), (K_.EPI_F32_ACC, torch.float32)):
+        outs = [torch.randn(n, K).to(dt).to(DEV) for n in ns]
+        base = torch.cat([o.float().cpu() for o in outs]) if epi != K_.EPI_BF16 else 0
+        K_.linear_wgrad(dy.to(DEV), x.to(DEV), outs, epi)
+        got = torch.cat([o.float().cpu() for o in outs])
+        assert rel_err(got, base + ref) < 1e-2, epi
+    # a micro-batch pair's weight gradient (train_step's pairing) off the grid: its two halves
+    dy2, x2 = torch.randn(T, N).to(BF), torch.randn(T, K).to(BF)
+    outs = [torch.zeros(n, K, dtype=BF, device=DEV) for n in ns]
+    K_.linear_wgrad(K_.KPair(dy.to(DEV), dy2.to(DEV)), K_.KPair(x.to(DEV), x2.to(DEV)), outs, K_.EPI_BF16)
+    assert rel_err(torch.cat([o.float().cpu() for o in outs]), ref + dy2.float().t() @ x2.float()) < 1e-2
+
+
 def test_gemm_retired_tiles_are_refused():
     """Tile ids 4, 5, 8, 9 (the simple 256-row kernels, never auto-picked, spilling at 256x256) are
     not in the library: asking for one is PT_EUNSUPPORTED, not a silent other kernel."""

@@ -189,6 +189,16 @@ def test_tensor_parallel_llama_tp8_four_chunks():
     _dist.run(_llama, 8, 8, 1, 256, False, 1, 1, False, 1, over, 4, 4, device="cuda")
 
 
+@pytest.mark.parametrize("tp", [1, 2])
+def test_llama_off_grid_widths(tp):
+    """An intermediate (344 per rank) and a vocabulary (1000; 500 per rank at tp2) off the GEMM tiles'
+    64-element grid -- as Llama-2-7B's shards at tp 8 (1376, 4000) -- run on the padded projections
+    (kernels._linear_*_padded) with the separate SwiGLU / cross-entropy kernels: the full model's
+    logits, loss and every gradient against the oracle."""
+    over = dict(intermediate_size=344 * tp, vocab_size=1000)
+    _dist.run(_llama, tp, tp, 1, 256, False, 1, 1, False, 1, over, device="cuda")
+
+
 def test_tensor_parallel_llama_tp2_replicated_stream():
     """tp2 without sequence parallelism (PICOTRON_TP_SP=0): the reference's replicated residual
     stream and row-parallel all-reduces."""
