@@ -265,7 +265,7 @@ def test_gemm_every_tile_every_layout(tile):
 
 
 @pytest.mark.parametrize("T,K,ns", [(100, 72, [40, 24]), (4000 // 8, 1376 // 8, [4000 // 8]), (192, 1376, [96]),
-                                    (256, 256, [200])])
+                                    (256, 256, [200]), (512, 4096, [4000]), (512, 1376, [4096])])
 def test_gemm_off_grid_shapes_run_padded(T, K, ns):
     """Projections whose T, K or output widths are not multiples of 64 (no GEMM tile covers them:
     Llama-2-7B at tp 8 has a vocab shard of 4000 and an intermediate shard of 1376) run on

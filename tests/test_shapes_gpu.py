@@ -175,6 +175,12 @@ def test_smollm_1_7b_tp8_shard_layer():
     _layer_parity(B=4, S=1024, H=2048, I=8192 // 8, nh=4, nkv=4, d=64, seed=5)
 
 
+def test_llama2_7b_tp8_shard_layer():
+    """Llama-2-7B at TP 8: 4 heads of 128 and an intermediate shard of 1376, off the GEMM tiles'
+    64-grid -- the gate|up / down projections on the padded GEMMs (kernels._linear_*_padded)."""
+    _layer_parity(B=2, S=1024, H=4096, I=11008 // 8, nh=4, nkv=4, d=128, seed=11)
+
+
 def test_cp8_ring_block_s4096_d128():
     """Rank 1 of a ring at S_local 4096, d 128 (Llama-2-7B CP = 8 at 32k, one head group): step 0 is
     the causal diagonal block, step 1 the full block of rank 0's K/V, merged into the running f32
