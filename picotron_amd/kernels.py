@@ -1485,12 +1485,47 @@ def _lse_ld(t, B, H, Sq, name="lse"):
     return t.stride(1) if H > 1 else (t.stride(0) if B > 1 else Sq)
 
 
+# causal attention over a sequence length off the kernels' 128-row query blocks (attention.hip
+# check_common: Sq % 128): q / k / v zero-padded to the next multiple.  Causality keeps the padded
+# keys out of every real query's softmax, and the padded queries' rows are sliced off (forward) or
+# carry dO = 0 and LSE = +inf, so P = 0 and they add nothing to dK / dV (backward): the real rows'
+# results are the kernels' own on the real data.
+ATTN_Q_BLOCK = 128
+
+
+def _attn_padded_len(S):
+    return -(-int(S) // ATTN_Q_BLOCK) * ATTN_Q_BLOCK
+
+
+def _pad_seq(t, Sp, fill=0.0):
+    """[B, S, ...] -> a contiguous [B, Sp, ...] copy whose rows past S are `fill`."""
+    out = torch.full((t.shape[0], Sp) + tuple(t.shape[2:]), fill, dtype=t.dtype, device=t.device)
+    out[:, :t.shape[1]] = t
+    return out
+
+
+def _attn_off_block(causal, Sq, Sk, lse, B, H):
+    return causal and Sq == Sk and Sq % ATTN_Q_BLOCK != 0 and (lse is None or _lse_ld(lse, B, H, Sq) == Sq)
+
+
 def attn_fwd(q, k, v, scale, causal, out=None, lse=None, merge=False):
     """q [B,Sq,H,D], k/v [B,Sk,Hkv,D] (token-major views).  Returns (out, lse[B,H,Sq] f32).
     merge=True: `out` is an f32 accumulator and `lse` the running LSE; this block is merged in.
     lse may be the Sq-column slice of a longer [B, H, S] LSE (rows evenly spaced)."""
     B, Sq, H, D = q.shape
     Sk, HKV = k.shape[1], k.shape[2]
+    if not merge and _attn_off_block(causal, Sq, Sk, lse, B, H):
+        Sp = _attn_padded_len(Sq)
+        op, lp = attn_fwd(_pad_seq(q, Sp), _pad_seq(k, Sp), _pad_seq(v, Sp), scale, True)
+        if out is None:
+            out = op[:, :Sq].contiguous()
+        else:
+            out.copy_(op[:, :Sq])
+        if lse is None:
+            lse = lp[:, :, :Sq].contiguous()
+        else:
+            lse.copy_(lp[:, :, :Sq])
+        return out, lse
     if out is None:
         out = torch.empty(B, Sq, H, D, dtype=BF16, device=q.device)
     if lse is None:
@@ -1556,6 +1591,28 @@ def attn_bwd(dout, q, k, v, out, lse, scale, causal, dq=None, dk=None, dv=None, 
     backward fused into the attention backward; positions = sequence index)."""
     B, Sq, H, D = q.shape
     Sk, HKV = k.shape[1], k.shape[2]
+    if not grad_f32 and _attn_off_block(causal, Sq, Sk, lse, B, H) and \
+            (delta is None or _lse_ld(delta, B, H, Sq, "delta") == Sq):
+        Sp = _attn_padded_len(Sq)
+        lsep = torch.full((B, H, Sp), float("inf"), dtype=torch.float32, device=q.device)
+        lsep[:, :, :Sq] = lse
+        dlp = None
+        if delta is not None:
+            dlp = torch.zeros(B, H, Sp, dtype=torch.float32, device=q.device)
+            dlp[:, :, :Sq] = delta
+        rp = None
+        if rope is not None:   # tables long enough for the padded rows (their values are never used)
+            rp = tuple(t if t.shape[0] >= Sp else _pad_seq(t.unsqueeze(0), Sp)[0] for t in rope)
+        dqp, dkp, dvp, dlt = attn_bwd(_pad_seq(dout, Sp), _pad_seq(q, Sp), _pad_seq(k, Sp), _pad_seq(v, Sp),
+                                      _pad_seq(out, Sp), lsep, scale, True, delta=dlp, rope=rp)
+        res = []
+        for given, got in ((dq, dqp), (dk, dkp), (dv, dvp)):
+            if given is None:
+                res.append(got[:, :Sq].contiguous())
+            else:
+                given.copy_(got[:, :Sq])
+                res.append(given)
+        return res[0], res[1], res[2], dlt[:, :, :Sq]
     lib = _C.lib()
     fuse_delta = delta is None and not grad_f32 and out.dtype == BF16 and SW.fuse_delta != 0
     if delta is None and not fuse_delta:

@@ -819,6 +819,31 @@ def test_attention_fwd_bwd(B, S, H, HKV, D, causal):
     assert rel_err(dv, dv_ref) < 2e-2
 
 
+@pytest.mark.parametrize("B,S,H,HKV,D", [(2, 200, 4, 2, 64), (1, 1000, 4, 4, 128), (2, 72, 2, 1, 64)])
+def test_attention_off_block_sequence_lengths(B, S, H, HKV, D):
+    """Causal attention at sequence lengths off the kernels' 128-row query blocks (kernels.attn_fwd /
+    attn_bwd zero-pad q / k / v; the padded keys are causally invisible, the padded queries carry
+    dO = 0 and LSE = +inf): out, lse and dq / dk / dv against the oracle."""
+    from picotron_amd import kernels as K_
+    q, k, v = _qkv(B, S, H, HKV, D)
+    scale = 1 / math.sqrt(D)
+    o, lse = K_.attn_fwd(q, k, v, scale, True)
+    assert o.shape == (B, S, H, D) and lse.shape == (B, H, S)
+    qq, kk, vv = _ref_attn(q, k, v, True, scale)
+    qq.requires_grad_(True); kk.requires_grad_(True); vv.requires_grad_(True)
+    o_ref, lse_ref = O.attention_lse(qq, kk, vv, scale, True)
+    assert rel_err(o, o_ref.transpose(1, 2)) < 1e-2
+    assert maxabs(lse, lse_ref) < 1e-2
+    do = torch.randn(o.shape).to(BF)
+    (o_ref * do.float().transpose(1, 2)).sum().backward()
+    dq, dk, dv, _ = K_.attn_bwd(do.to(DEV), q, k, v, o, lse, scale, True)
+    torch.cuda.synchronize()
+    rep = H // HKV
+    assert rel_err(dq, qq.grad.transpose(1, 2)) < 2e-2
+    assert rel_err(dk, kk.grad.view(B, HKV, rep, S, D).sum(2).transpose(1, 2)) < 2e-2
+    assert rel_err(dv, vv.grad.view(B, HKV, rep, S, D).sum(2).transpose(1, 2)) < 2e-2
+
+
 @pytest.mark.parametrize("B,S,H,HKV,D,causal,f32,rope", [
     (2, 1024, 4, 4, 64, True, False, True), (1, 512, 4, 2, 64, True, False, False),
     (1, 384, 2, 1, 64, True, False, False), (1, 512, 2, 2, 128, True, False, True),

@@ -132,7 +132,7 @@ def _llama_body(rank, world, tp, cp, seq, zigzag, residual, cfg_over=None, batch
     # the vocab-parallel CE (functional.VocabParallelCEFunction): one gather of 16 B per row at tp > 1
     vp = [g for g in gathers if g == (B * s, 4)]
     vp_on = tp > 1 and FN.vp_ce_shape_ok(B * s, V // tp, H)   # V 512 at tp 8: V / tp = 64 does not tile
-    assert vp_on == (tp > 1 and (V // tp) % 128 == 0 and switches.S.vp_ce != 0)
+    assert vp_on == (tp > 1 and (V // tp) % 128 == 0 and (B * s) % 256 == 0 and switches.S.vp_ce != 0)
     assert len(vp) == (1 if vp_on else 0), gathers
     gathers = [g for g in gathers if g != (B * s, 4)]
     if sp_on:   # per layer and chunk 2 gathers each way, plus the exit (forward) / the entry (backward)
@@ -197,6 +197,14 @@ def test_llama_off_grid_widths(tp):
     logits, loss and every gradient against the oracle."""
     over = dict(intermediate_size=344 * tp, vocab_size=1000)
     _dist.run(_llama, tp, tp, 1, 256, False, 1, 1, False, 1, over, device="cuda")
+
+
+@pytest.mark.parametrize("tp", [1, 2])
+def test_llama_off_block_sequence(tp):
+    """seq 200: off the attention kernels' 128-row query blocks (padded attention) and, with T = 400
+    token rows, off the GEMM tiles' 64-grid (padded projections); at tp2 the sequence-parallel layout
+    in 2 chunks of 100 rows per rank -- the full model against the oracle."""
+    _dist.run(_llama, tp, tp, 1, 200, False, 1, 1, False, 1, None, device="cuda")
 
 
 def test_tensor_parallel_llama_tp2_replicated_stream():

@@ -1,5 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
 O=gpurun_out/$1
-timeout -k 10 500 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_kernels_gpu.py tests/test_shapes_gpu.py -k "off_grid or llama2_7b_tp8" > $O.og_tests.log 2>&1 || { echo tests failed; tail -40 $O.og_tests.log; exit 1; }
-grep -E "passed|failed" $O.og_tests.log | tail -1
+timeout -k 10 500 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_kernels_gpu.py tests/test_parallel_gpu.py -k "off_block" > $O.ob_tests.log 2>&1 || { echo tests failed; tail -50 $O.ob_tests.log; exit 1; }
+grep -E "passed|failed" $O.ob_tests.log | tail -1
