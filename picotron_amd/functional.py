@@ -774,10 +774,75 @@ class AttnShape:
         return t[:, self.wq + self.wkv:].view(self.B, self.S, self.nkv, self.d)
 
 
+# head dims the attention kernels do not take (64 / 128; e.g. 60 = SmolLM-360M with 16 heads, as
+# create_config.py's own example builds it): every head zero-padded to the next kernel width, each
+# rotary half separately -- [x1 | 0 | x2 | 0] -- so that RoPE's (d, d + d/2) pairs stay pairs and the
+# padded columns add nothing to q . k or to o (the scale stays 1/sqrt(d) of the real d).
+ATTN_HEAD_DIMS = (64, 128)
+
+
+def _head_pad_dim(d):
+    return next((w for w in ATTN_HEAD_DIMS if d <= w), None)
+
+
+def _pad_heads(t2d, heads, d, dp):
+    """[T, heads * d] -> [T, heads, dp]: each head's halves at 0 and dp / 2, zeros between."""
+    T, h, hp = t2d.shape[0], d // 2, dp // 2
+    x = t2d.reshape(T, heads, d)
+    out = torch.zeros(T, heads, dp, dtype=t2d.dtype, device=t2d.device)
+    out[..., :h] = x[..., :h]
+    out[..., hp:hp + h] = x[..., h:]
+    return out
+
+
+def _unpad_heads(tp, d):
+    """Inverse of _pad_heads: [T, heads, dp] -> [T, heads * d] (contiguous)."""
+    T, heads, dp = tp.shape
+    h, hp = d // 2, dp // 2
+    return torch.cat([tp[..., :h], tp[..., hp:hp + h]], dim=-1).reshape(T, heads * d)
+
+
+def _pad_rope_table(t, d, dp):
+    return _pad_heads(t, 1, d, dp).view(t.shape[0], dp)
+
+
+def _attention_core_fwd_padded(qkv, sh, cos, sin, scale):
+    d, dp = sh.d, _head_pad_dim(sh.d)
+    heads = sh.nh + 2 * sh.nkv
+    x = _pad_heads(qkv, heads, d, dp).view(sh.T, heads * dp)
+    K.rope_(x, sh.nh + sh.nkv, dp, _pad_rope_table(cos, d, dp), _pad_rope_table(sin, d, dp), sh.S)
+    # the rotated q|k back into qkv (in place, as the kernel-width path leaves them for the backward)
+    qkv[:, :sh.wq + sh.wkv].copy_(_unpad_heads(x.view(sh.T, heads, dp)[:, :sh.nh + sh.nkv], d))
+    shp = AttnShape(sh.B, sh.S, sh.nh, sh.nkv, dp)
+    o, lse = K.attn_fwd(shp.q(x), shp.k(x), shp.v(x), scale, True)
+    return _unpad_heads(o.view(sh.T, sh.nh, dp), d).view(sh.B, sh.S, sh.nh, d), lse
+
+
+def _attention_core_bwd_padded(do, qkv, o, lse, sh, cos, sin, scale):
+    d, dp = sh.d, _head_pad_dim(sh.d)
+    heads = sh.nh + 2 * sh.nkv
+    x = _pad_heads(qkv, heads, d, dp).view(sh.T, heads * dp)   # q|k already rotated (the forward)
+    shp = AttnShape(sh.B, sh.S, sh.nh, sh.nkv, dp)
+    dop = _pad_heads(do.reshape(sh.T, sh.wq), sh.nh, d, dp).view(sh.B, sh.S, sh.nh, dp)
+    op = _pad_heads(o.reshape(sh.T, sh.wq), sh.nh, d, dp).view(sh.B, sh.S, sh.nh, dp)
+    dxp = torch.empty_like(x)
+    K.attn_bwd(dop, shp.q(x), shp.k(x), shp.v(x), op, lse, scale, True, dq=shp.q(dxp), dk=shp.k(dxp), dv=shp.v(dxp))
+    K.rope_(dxp, sh.nh + sh.nkv, dp, _pad_rope_table(cos, d, dp), _pad_rope_table(sin, d, dp), sh.S, inverse=True)
+    return _unpad_heads(dxp.view(sh.T, heads, dp), d)
+
+
+def _req_head_dim(d, roped):
+    if _head_pad_dim(d) is None or d % 2 or roped:
+        raise RuntimeError(f"attention: head_dim {d} -- the kernels take 64 / 128 and pad even dims below 128")
+
+
 def attention_core_fwd(qkv, sh, cos, sin, scale, roped=False):
     """RoPE on q|k in place (model.py:136-137; skipped when the projection epilogue already
     rotated them: roped), then causal flash attention (model.py:154) or the ring
     (model.py:148-151).  Returns (o [B,S,nh,d] bf16, lse f32 [B,nh,S])."""
+    if sh.d not in ATTN_HEAD_DIMS and not ring_enabled():
+        _req_head_dim(sh.d, roped)
+        return _attention_core_fwd_padded(qkv, sh, cos, sin, scale)
     if not roped:
         K.rope_(qkv, sh.nh + sh.nkv, sh.d, cos, sin, sh.S)
     if ring_enabled():
@@ -788,6 +853,8 @@ def attention_core_fwd(qkv, sh, cos, sin, scale, roped=False):
 
 def attention_core_bwd(do, qkv, o, lse, sh, cos, sin, scale):
     """dq|dk|dv written into one [T, q|k|v] buffer, then the inverse rotation of dq|dk."""
+    if sh.d not in ATTN_HEAD_DIMS and not ring_enabled():
+        return _attention_core_bwd_padded(do, qkv, o, lse, sh, cos, sin, scale)
     dqkv = torch.empty_like(qkv)
     if ring_enabled():
         from .context_parallel.context_parallel import ring_attention_tokens_bwd
@@ -890,7 +957,7 @@ def mlp_block_fwd(h2, wg, wu, wd, tp, residual=None, reduce=True):
     """h2 [T,H] -> down(silu(gate) * up) (+ residual, entering the tp sum once, from tp rank 0;
     reduce=False: this rank's partial, no residual, for the sequence-parallel reduce-scatter)."""
     I = wg.shape[0]
-    if _fuse() and K.swiglu_fuse_pays(h2.shape[0], I):   # SwiGLU in the gate|up GEMM's epilogue
+    if _fuse() and K.swiglu_fuse_pays(h2.shape[0], I, H=h2.shape[1]):   # SwiGLU in the gate|up GEMM's epilogue
         gu, hh = K.linear_swiglu_fwd(h2, wg, wu)
     else:
         gu = K.linear_fwd(h2, [wg, wu])
@@ -919,7 +986,7 @@ def mlp_block_bwd(dm, h2, saved, wg, wu, wd, tp, need_dx=True, keep_parts=False,
     sequence-parallel layer (attn_block_bwd): returns the reduce-scatter's handle, not waited for."""
     gu, hh = saved
     I = wg.shape[0]
-    if _fuse() and K.swiglu_fuse_pays(dm.shape[0], I, backward=True):   # SwiGLU bwd in the down dX epilogue
+    if _fuse() and K.swiglu_fuse_pays(dm.shape[0], I, backward=True, H=dm.shape[1]):   # SwiGLU bwd in the down dX epilogue
         # ... in one launch with the down_proj dW: the epilogue's HBM-bound g|u / dg|du tail
         # overlaps the dW's MFMA work (K.linear_dgrad_dual)
         dgu = dgrad_with_wgrad(dm, [wd], [(dm, hh, [wd])], gu=gu, notify=notify)

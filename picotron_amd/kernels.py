@@ -1115,9 +1115,10 @@ def cross_entropy_grad_lse_shard(logits_shard, targets, row_lse, scale_dev, voca
     return dl
 
 
-def swiglu_fusable(T, I, backward=False):
-    """Shapes the SwiGLU-fused projections tile (8-phase kernel: T % 256, I % 128 (fwd) / 256 (bwd))."""
-    return T % 256 == 0 and I % (256 if backward else 128) == 0
+def swiglu_fusable(T, I, backward=False, H=None):
+    """Shapes the SwiGLU-fused projections tile (8-phase kernel: T % 256, I % 128 (fwd) / 256 (bwd),
+    and the hidden size H -- the GEMM's K -- on the 64 K-tile grid)."""
+    return T % 256 == 0 and I % (256 if backward else 128) == 0 and (H is None or H % GRID == 0)
 
 
 # fewer 256-row x (128 fwd / 256 bwd)-column tiles than this: the SwiGLU runs as its own kernel
@@ -1126,10 +1127,11 @@ def swiglu_fusable(T, I, backward=False):
 # (TP = 8 proxy: 8.95 vs 9.08 ms per micro-batch split).  PICOTRON_SWIGLU_FUSE_MIN_TILES / _BWD_MIN_TILES.
 
 
-def swiglu_fuse_pays(T, I, backward=False):
+def swiglu_fuse_pays(T, I, backward=False, H=None):
     """swiglu_fusable and enough tiles that the fused (8-phase 256x256) launch fills the CUs."""
     tiles = (T // 256) * (I // (256 if backward else 128))
-    return swiglu_fusable(T, I, backward) and tiles >= (SW.swiglu_bwd_min_tiles if backward else SW.swiglu_fuse_min_tiles)
+    return swiglu_fusable(T, I, backward, H) and \
+        tiles >= (SW.swiglu_bwd_min_tiles if backward else SW.swiglu_fuse_min_tiles)
 
 
 def linear_swiglu_fwd(x2d, wg, wu):
@@ -1140,7 +1142,7 @@ def linear_swiglu_fwd(x2d, wg, wu):
     I = wg.shape[0]
     for w in (wg, wu):
         _req(w.dtype == BF16 and w.is_contiguous() and tuple(w.shape) == (I, K), "gate/up weights [I, K] bf16")
-    _req(swiglu_fusable(T, I), "linear_swiglu_fwd: T % 256 and I % 128 required")
+    _req(swiglu_fusable(T, I, H=x2d.shape[1]), "linear_swiglu_fwd: T % 256, I % 128 and H % 64 required")
     gu = torch.empty(T, 2 * I, dtype=BF16, device=x2d.device)
     h = torch.empty(T, I, dtype=BF16, device=x2d.device)
     _gemm(x2d, x2d.stride(0), 1, [wg, wu], [K, K], [0, I, 2 * I], 1, 0, [h, gu], [I, 2 * I], [0, T], T, 2 * I, K,
@@ -1157,7 +1159,7 @@ def linear_dgrad_swiglu(dy2d, wd, gu):
     I = wd.shape[1]
     _req(wd.dtype == BF16 and wd.is_contiguous() and wd.shape[0] == H, "down weight [H, I] bf16")
     _req(tuple(gu.shape) == (T, 2 * I), "gu must be [T, 2I]")
-    _req(swiglu_fusable(T, I, backward=True), "linear_dgrad_swiglu: T % 256 and I % 256 required")
+    _req(swiglu_fusable(T, I, backward=True, H=dy2d.shape[1]), "linear_dgrad_swiglu: T % 256, I % 256 and H % 64 required")
     dgu = torch.empty(T, 2 * I, dtype=BF16, device=dy2d.device)
     _gemm(dy2d, dy2d.stride(0), 1, [wd], [I], [0, I], 0, 0, [dgu], [dgu.stride(0)], [0, T], T, I, H, EPI_SWIGLU_BWD,
           residual=gu, ldr=gu.stride(0))

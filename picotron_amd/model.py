@@ -72,22 +72,37 @@ def get_cos_sin(seq_length, head_dim, base=500000.0):
     return torch.cos(ang).to(dtype).repeat(1, 2), torch.sin(ang).to(dtype).repeat(1, 2)
 
 
+def _pad_d(t, dp):
+    """[..., D] -> [..., dp] zero-padded (a head dim the kernels do not take: no RoPE pairing here)."""
+    return t if t.shape[-1] == dp else torch.nn.functional.pad(t, (0, dp - t.shape[-1]))
+
+
 class _FlashAttention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, causal):
-        # q/k/v: [B, S, H, D] views (d contiguous)
-        scale = 1.0 / math.sqrt(q.shape[-1])
-        o, lse = K.attn_fwd(q, k, v, scale, causal)
-        ctx.save_for_backward(q, k, v, o, lse)
-        ctx.scale, ctx.causal = scale, causal
-        return o
+        # q/k/v: [B, S, H, D] views (d contiguous); a D other than 64 / 128 runs zero-padded (the
+        # padded columns add nothing to q . k and are sliced off o; the scale is the real D's)
+        D = q.shape[-1]
+        scale = 1.0 / math.sqrt(D)
+        dp = FN._head_pad_dim(D) if D not in FN.ATTN_HEAD_DIMS else D
+        if dp is None:
+            raise RuntimeError(f"flash_attention: head_dim {D} -- the kernels take 64 / 128 and pad dims below 128")
+        qp, kp, vp = (_pad_d(t, dp) for t in (q, k, v))
+        o, lse = K.attn_fwd(qp, kp, vp, scale, causal)
+        ctx.save_for_backward(qp, kp, vp, o, lse)
+        ctx.scale, ctx.causal, ctx.D = scale, causal, D
+        return o[..., :D] if dp != D else o
 
     @staticmethod
     def backward(ctx, do):
         q, k, v, o, lse = ctx.saved_tensors
+        D = ctx.D
+        do = _pad_d(do, o.shape[-1])
         if do.stride(-1) != 1:
             do = do.contiguous()
         dq, dk, dv, _ = K.attn_bwd(do, q, k, v, o, lse, ctx.scale, ctx.causal)
+        if o.shape[-1] != D:
+            dq, dk, dv = dq[..., :D], dk[..., :D], dv[..., :D]
         return dq, dk, dv, None
 
 

@@ -819,6 +819,25 @@ def test_attention_fwd_bwd(B, S, H, HKV, D, causal):
     assert rel_err(dv, dv_ref) < 2e-2
 
 
+@pytest.mark.parametrize("D,causal", [(60, True), (80, False), (96, True)])
+def test_flash_attention_api_padded_head_dims(D, causal):
+    """model.flash_attention (flash_attn_func's call form) at head dims the kernels do not take:
+    zero-padded to 64 / 128 (scale of the real D), out and dq / dk / dv against the oracle."""
+    from picotron_amd.model import flash_attention
+    B, S, H = 2, 256, 4
+    g = torch.Generator().manual_seed(3)
+    q, k, v, do = (torch.randn(B, H, S, D, generator=g).to(BF) for _ in range(4))
+    qd, kd, vd = (t.to(DEV).requires_grad_(True) for t in (q, k, v))
+    out = flash_attention(qd, kd, vd, causal)                        # [B, S, H, D]
+    out.backward(do.transpose(1, 2).to(DEV))
+    qr, kr, vr = (t.float().requires_grad_(True) for t in (q, k, v))
+    o_ref, _ = O.attention_lse(qr, kr, vr, 1 / math.sqrt(D), causal)
+    o_ref.backward(do.float())
+    assert out.shape == (B, S, H, D) and rel_err(out, o_ref.transpose(1, 2)) < 1e-2
+    for got, ref in ((qd.grad, qr.grad), (kd.grad, kr.grad), (vd.grad, vr.grad)):
+        assert rel_err(got, ref) < 2e-2
+
+
 @pytest.mark.parametrize("B,S,H,HKV,D", [(2, 200, 4, 2, 64), (1, 1000, 4, 4, 128), (2, 72, 2, 1, 64)])
 def test_attention_off_block_sequence_lengths(B, S, H, HKV, D):
     """Causal attention at sequence lengths off the kernels' 128-row query blocks (kernels.attn_fwd /

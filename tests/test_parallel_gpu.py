@@ -68,7 +68,7 @@ def _setup(tp, cp, seq=256, cfg_over=None, batch=2):
     ids = torch.randint(0, base["vocab_size"], (batch, seq + 1), generator=g)
     # the oracle on the full model, fp32 from the same bf16 weights
     pf = {k: v.float().requires_grad_(True) for k, v in full.items()}
-    cos, sin = O.get_cos_sin(seq, 64, base=CFG["rope_theta"])
+    cos, sin = O.get_cos_sin(seq, base["hidden_size"] // base["num_attention_heads"], base=CFG["rope_theta"])
     lo = O.llama_forward(ids[:, :-1], pf, dict(base), cos.float(), sin.float(), norm=O.rmsnorm_flash_semantics)
     loss_r = F.cross_entropy(lo.reshape(-1, base["vocab_size"]), ids[:, 1:].reshape(-1))
     loss_r.backward()
@@ -132,7 +132,7 @@ def _llama_body(rank, world, tp, cp, seq, zigzag, residual, cfg_over=None, batch
     # the vocab-parallel CE (functional.VocabParallelCEFunction): one gather of 16 B per row at tp > 1
     vp = [g for g in gathers if g == (B * s, 4)]
     vp_on = tp > 1 and FN.vp_ce_shape_ok(B * s, V // tp, H)   # V 512 at tp 8: V / tp = 64 does not tile
-    assert vp_on == (tp > 1 and (V // tp) % 128 == 0 and (B * s) % 256 == 0 and switches.S.vp_ce != 0)
+    assert vp_on == (tp > 1 and (V // tp) % 128 == 0 and (B * s) % 256 == 0 and H % 64 == 0 and switches.S.vp_ce != 0)
     assert len(vp) == (1 if vp_on else 0), gathers
     gathers = [g for g in gathers if g != (B * s, 4)]
     if sp_on:   # per layer and chunk 2 gathers each way, plus the exit (forward) / the entry (backward)
@@ -205,6 +205,16 @@ def test_llama_off_block_sequence(tp):
     token rows, off the GEMM tiles' 64-grid (padded projections); at tp2 the sequence-parallel layout
     in 2 chunks of 100 rows per rank -- the full model against the oracle."""
     _dist.run(_llama, tp, tp, 1, 200, False, 1, 1, False, 1, None, device="cuda")
+
+
+@pytest.mark.parametrize("tp", [1, 2])
+def test_llama_head_dim_60(tp):
+    """head_dim 60 (hidden 240, 4 heads; create_config.py's own example gives SmolLM-360M 16 heads of
+    60): every head zero-padded to the kernels' 64 in its two rotary halves (functional.
+    _attention_core_*_padded), the projections off the 64-grid padded too -- the full model against
+    the oracle."""
+    over = dict(hidden_size=240, num_attention_heads=4, num_key_value_heads=2)
+    _dist.run(_llama, tp, tp, 1, 256, False, 1, 1, False, 1, over, device="cuda")
 
 
 def test_tensor_parallel_llama_tp2_replicated_stream():
