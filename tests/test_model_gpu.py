@@ -318,13 +318,20 @@ def test_cross_entropy_edge_cases_match_torch():
 
 
 def test_unsupported_shapes_fail_loudly():
-    """Shapes outside the kernels' tiling raise HipKernelError / ValueError -- never a silent
-    fallback (S % 128 for the flash kernels, head_dim 64 / 128)."""
+    """Shapes outside what the kernels and the host padding cover raise HipKernelError / ValueError /
+    RuntimeError -- never a silent fallback: a non-causal block off the 128-row query blocks (only
+    causal self-attention is padded), a head dim the kernel entry points do not take (the model's
+    attention pads even dims below 128; the kernels themselves take 64 / 128), a head dim above 128."""
     from picotron_amd import kernels as K
     from picotron_amd._C import HipKernelError
+    from picotron_amd.model import flash_attention
     q = torch.randn(1, 100, 2, 64, device="cuda").to(BF)
     with pytest.raises((HipKernelError, ValueError)):
-        K.attn_fwd(q, q, q, 0.125, True)
+        K.attn_fwd(q, q, q, 0.125, False)
+    K.attn_fwd(q, q, q, 0.125, True)   # causal: zero-padded to 128 rows (test_kernels_gpu's off-block test)
     q = torch.randn(1, 128, 2, 32, device="cuda").to(BF)
     with pytest.raises((HipKernelError, ValueError)):
         K.attn_fwd(q, q, q, 0.125, True)
+    q = torch.randn(1, 2, 128, 160, device="cuda").to(BF)
+    with pytest.raises((HipKernelError, ValueError, RuntimeError)):
+        flash_attention(q, q, q, True)
