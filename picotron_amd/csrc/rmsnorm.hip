@@ -238,6 +238,155 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(min_wa
   }
 }
 
+// ------------------------------------------------------------------ rows wider than 4096 columns
+// (Llama-2-13B 5120, 70B 8192: more 16-byte chunks per lane than the register-resident kernels
+// hold).  One wave per row, the row streamed in 512-column passes twice: the sum of squares (the
+// backward's dot) first, then the output from a second read of the same bytes (L2-resident by then;
+// the residual form re-reads the z it wrote).  The backward's dW partial stays one LDS row per wave
+// (planar, as above), combined per block in a fixed order: one partial row per block.
+constexpr int kWideWpb = 4;   // waves per block; 2 above 8192 columns (LDS: WPB x cols x 4 B)
+constexpr int kWideMax = 16384;
+inline int wide_wpb(int cols) { return cols > 8192 ? 2 : kWideWpb; }
+
+__global__ __launch_bounds__(kWideWpb * 64) void rmsnorm_fwd_wide_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ res, const uint16_t* __restrict__ w,
+    uint16_t* __restrict__ y, uint16_t* z_out, float* __restrict__ rstd_out, int64_t rows, int cols, float eps,
+    int mode) {
+  const int lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
+  const int nchunk = cols >> 3;
+  const float inv_cols = 1.0f / (float)cols;
+  for (int64_t row = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); row < rows; row += (int64_t)gridDim.x * wpb) {
+    float ss = 0.f;
+    for (int c = lane; c < nchunk; c += PT_WAVE) {
+      float v[8];
+      unpack8(ld8(x + row * cols + c * 8), v);
+      if (res) {
+        float r[8];
+        unpack8(ld8(res + row * cols + c * 8), r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = round_bf(v[j] + r[j]);   // bf16 residual stream
+        st8(z_out + row * cols + c * 8, pack8(v));
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
+    }
+    ss = wave_sum(ss);
+    const float rstd = rsqrtf(ss * inv_cols + eps);
+    if (lane == 0) rstd_out[row] = rstd;
+    const uint16_t* src = res ? z_out : x;   // the lane re-reads what it read (or wrote) above
+    for (int c = lane; c < nchunk; c += PT_WAVE) {
+      float v[8], wf[8], o[8];
+      unpack8(ld8(src + row * cols + c * 8), v);
+      unpack8(ld8(w + c * 8), wf);
+      if (mode == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = v[j] * rstd * wf[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = wf[j] * round_bf(v[j] * rstd);
+      }
+      st8(y + row * cols + c * 8, pack8(o));
+    }
+  }
+}
+
+template <bool SPLIT>
+__global__ __launch_bounds__(kWideWpb * 64) void rmsnorm_bwd_wide_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ z, const uint16_t* __restrict__ w,
+    const float* __restrict__ rstd_in, const uint16_t* __restrict__ dres, uint16_t* __restrict__ dx,
+    float* __restrict__ dw_partial, int64_t rows, int cols, int mode, const float* __restrict__ dy_p1) {
+  extern __shared__ float red[];  // [wpb][cols], planar as rmsnorm_bwd_kernel's
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+  const int nchunk = cols >> 3, half = cols >> 1;
+  const float inv_cols = 1.0f / (float)cols;
+  float* dwrow = red + wid * cols;
+  for (int c = lane; c < nchunk; c += PT_WAVE) {
+    *(float4*)(dwrow + c * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+    *(float4*)(dwrow + half + c * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  auto load_dy = [&](int64_t row, int c, float (&d)[8]) {
+    if constexpr (SPLIT) {
+      const float* p0 = (const float*)dy + row * cols + c * 8;
+      const float* p1 = dy_p1 + row * cols + c * 8;
+      const float4 a0 = *(const float4*)p0, a1 = *(const float4*)(p0 + 4);
+      const float4 b0 = *(const float4*)p1, b1 = *(const float4*)(p1 + 4);
+      float f[8] = {a0.x + b0.x, a0.y + b0.y, a0.z + b0.z, a0.w + b0.w,
+                    a1.x + b1.x, a1.y + b1.y, a1.z + b1.z, a1.w + b1.w};
+      unpack8(pack8(f), d);   // bf16(p0 + p1): the split-K sum pass's own rounding
+    } else {
+      unpack8(ld8(dy + row * cols + c * 8), d);
+    }
+  };
+  for (int64_t row = (int64_t)blockIdx.x * wpb + wid; row < rows; row += (int64_t)gridDim.x * wpb) {
+    const float rstd = rstd_in[row];
+    float dot = 0.f;
+    for (int c = lane; c < nchunk; c += PT_WAVE) {
+      float zz[8], d[8], wf[8];
+      unpack8(ld8(z + row * cols + c * 8), zz);
+      load_dy(row, c, d);
+      unpack8(ld8(w + c * 8), wf);
+      float4* acc0 = (float4*)(dwrow + c * 4);
+      float4* acc1 = (float4*)(dwrow + half + c * 4);
+      float g[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xh = zz[j] * rstd;
+        dot += d[j] * wf[j] * xh;
+        g[j] = d[j] * (mode == 0 ? xh : round_bf(xh));
+      }
+      float4 a0 = *acc0, a1 = *acc1;
+      a0.x += g[0]; a0.y += g[1]; a0.z += g[2]; a0.w += g[3];
+      a1.x += g[4]; a1.y += g[5]; a1.z += g[6]; a1.w += g[7];
+      *acc0 = a0; *acc1 = a1;
+    }
+    dot = wave_sum(dot) * inv_cols;
+    for (int c = lane; c < nchunk; c += PT_WAVE) {
+      float zz[8], d[8], wf[8], o[8];
+      unpack8(ld8(z + row * cols + c * 8), zz);
+      load_dy(row, c, d);
+      unpack8(ld8(w + c * 8), wf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = rstd * (d[j] * wf[j] - zz[j] * rstd * dot);
+      if (dres) {
+        float r[8];
+        unpack8(ld8(dres + row * cols + c * 8), r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += r[j];
+      }
+      st8(dx + row * cols + c * 8, pack8(o));
+    }
+  }
+  __syncthreads();
+  for (int col = threadIdx.x; col < cols; col += blockDim.x) {
+    const int at = ((col & 7) >> 2) * half + (col >> 3) * 4 + (col & 3);
+    float s = 0.f;
+    for (int k = 0; k < wpb; ++k) s += red[k * cols + at];
+    dw_partial[(int64_t)blockIdx.x * cols + col] = s;
+  }
+}
+
+int wide_grid(int64_t rows, int wpb, int bpc) {
+  const int64_t g = (rows + wpb - 1) / wpb, cap = (int64_t)kCUs * bpc;
+  return (int)(g < cap ? g : cap);
+}
+
+void launch_bwd_wide(bool split, int grid, hipStream_t s, const uint16_t* DY, const uint16_t* Z, const uint16_t* W,
+                     const float* rstd, const uint16_t* DR, uint16_t* DX, float* part, int64_t rows, int cols,
+                     int mode, const float* P1) {
+  const int wpb = wide_wpb(cols);
+  const size_t lds = (size_t)wpb * cols * sizeof(float);
+  static bool attr[2] = {false, false};
+  if (!attr[split]) {
+    (void)hipFuncSetAttribute(split ? (const void*)rmsnorm_bwd_wide_kernel<true> : (const void*)rmsnorm_bwd_wide_kernel<false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr[split] = true;
+  }
+  if (split)
+    rmsnorm_bwd_wide_kernel<true><<<grid, wpb * 64, lds, s>>>(DY, Z, W, rstd, DR, DX, part, rows, cols, mode, P1);
+  else
+    rmsnorm_bwd_wide_kernel<false><<<grid, wpb * 64, lds, s>>>(DY, Z, W, rstd, DR, DX, part, rows, cols, mode, P1);
+}
+
 // dw[col] = sum_p partial[p][col]  -- fixed summation order, deterministic.  One block per 32
 // columns: 8 lanes x 16 B cover a partial row's 32 columns (128 contiguous bytes per row), the 128
 // lane groups of the 1024-thread block take every 128th partial row (all of a thread's rows loaded
@@ -375,7 +524,10 @@ extern "C" {
 
 int pt_rmsnorm_bwd_partials(int64_t rows, int cols) {
   const int nch = nch_for(cols);
-  if (nch < 0) return PT_EUNSUPPORTED;
+  if (nch < 0) {
+    if (cols > kWideMax || (cols & 7)) return PT_EUNSUPPORTED;
+    return wide_grid(rows, wide_wpb(cols), 1);   // the wide-row backward: one partial row per block
+  }
   return grid_for(rows, bwd_wpb(nch, rows), kBwdBpc);  // one partial row per bwd block
 }
 
@@ -395,7 +547,11 @@ int pt_rmsnorm_fwd(const void* x, const void* residual, const void* weight, void
     case 2: launch_fwd<2>(stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
     case 4: launch_fwd<4>(stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
     case 8: launch_fwd<8>(stream, X, R, W, Y, Z, rstd, rows, (int)cols, eps, mode); break;
-    default: return PT_EUNSUPPORTED;
+    default:
+      if (cols > kWideMax) return PT_EUNSUPPORTED;
+      rmsnorm_fwd_wide_kernel<<<wide_grid(rows, kWideWpb, 4), kWideWpb * 64, 0, stream>>>(X, R, W, Y, Z, rstd, rows,
+                                                                                         (int)cols, eps, mode);
+      break;
   }
   PT_CHECK_LAUNCH();
   return PT_OK;
@@ -409,10 +565,10 @@ int pt_rmsnorm_bwd(const void* dy, const void* z, const void* weight, const floa
   if (!pt_aligned16(dy) || !pt_aligned16(z) || !pt_aligned16(dx) || (dres && !pt_aligned16(dres)))
     return PT_EALIGN;
   const int nch = nch_for((int)cols);
-  if (nch < 0) return PT_EUNSUPPORTED;
+  if (nch < 0 && cols > kWideMax) return PT_EUNSUPPORTED;
   const int nmode = mode & 3;
   if (nmode > 1 || (mode & PT_DW_ACC_BF16 && mode & PT_DW_ACC_F32)) return PT_EINVAL;
-  const int grid = grid_for(rows, bwd_wpb(nch, rows), kBwdBpc);
+  const int grid = nch < 0 ? wide_grid(rows, wide_wpb((int)cols), 1) : grid_for(rows, bwd_wpb(nch, rows), kBwdBpc);
   const auto* DY = (const uint16_t*)dy;
   const auto* Z = (const uint16_t*)z;
   const auto* W = (const uint16_t*)weight;
@@ -423,7 +579,7 @@ int pt_rmsnorm_bwd(const void* dy, const void* z, const void* weight, const floa
     case 2: launch_bwd<2>(grid, stream, DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
     case 4: launch_bwd<4>(grid, stream, DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
     case 8: launch_bwd<8>(grid, stream, DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode); break;
-    default: return PT_EUNSUPPORTED;
+    default: launch_bwd_wide(false, grid, stream, DY, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode, nullptr);
   }
   PT_CHECK_LAUNCH();
   if (dweight) {
@@ -446,10 +602,10 @@ int pt_rmsnorm_bwd_splitk(const float* dy_p0, const float* dy_p1, const void* z,
       (dres && !pt_aligned16(dres)))
     return PT_EALIGN;
   const int nch = nch_for((int)cols);
-  if (nch < 0) return PT_EUNSUPPORTED;
+  if (nch < 0 && cols > kWideMax) return PT_EUNSUPPORTED;
   const int nmode = mode & 3;
   if (nmode > 1 || (mode & PT_DW_ACC_BF16 && mode & PT_DW_ACC_F32)) return PT_EINVAL;
-  const int grid = grid_for(rows, bwd_wpb(nch, rows), kBwdBpc);
+  const int grid = nch < 0 ? wide_grid(rows, wide_wpb((int)cols), 1) : grid_for(rows, bwd_wpb(nch, rows), kBwdBpc);
   const auto* P0 = (const uint16_t*)dy_p0;  // reinterpreted as float inside the SPLIT kernel
   const auto* Z = (const uint16_t*)z;
   const auto* W = (const uint16_t*)weight;
@@ -460,7 +616,7 @@ int pt_rmsnorm_bwd_splitk(const float* dy_p0, const float* dy_p1, const void* z,
     case 2: launch_bwd<2, true>(grid, stream, P0, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode, dy_p1); break;
     case 4: launch_bwd<4, true>(grid, stream, P0, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode, dy_p1); break;
     case 8: launch_bwd<8, true>(grid, stream, P0, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode, dy_p1); break;
-    default: return PT_EUNSUPPORTED;
+    default: launch_bwd_wide(true, grid, stream, P0, Z, W, rstd, DR, DX, dw_partial, rows, (int)cols, nmode, dy_p1);
   }
   PT_CHECK_LAUNCH();
   if (dweight) {

@@ -30,9 +30,11 @@ def _seed():
 
 
 # --------------------------------------------------------------------------- RMSNorm
-@pytest.mark.parametrize("rows,cols", [(64, 64), (300, 2048), (128, 4096), (8, 512)])
+@pytest.mark.parametrize("rows,cols", [(64, 64), (300, 2048), (128, 4096), (8, 512), (64, 5120), (300, 8192),
+                                       (16, 16384), (1000, 4104)])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_rmsnorm_fwd_bwd(rows, cols, mode):
+    """(the rows wider than 4096: rmsnorm.hip's wide-row kernels -- Llama-2-13B 5120, 70B 8192)"""
     from picotron_amd import kernels as K
     x = torch.randn(rows, cols).to(BF)
     w = (1 + 0.1 * torch.randn(cols)).to(BF)
@@ -50,7 +52,8 @@ def test_rmsnorm_fwd_bwd(rows, cols, mode):
     assert rel_err(dw, wr.grad) < 1e-2
 
 
-@pytest.mark.parametrize("rows,cols,mode", [(4096, 2048, 0), (300, 2048, 1), (256, 512, 0), (64, 4096, 0)])
+@pytest.mark.parametrize("rows,cols,mode", [(4096, 2048, 0), (300, 2048, 1), (256, 512, 0), (64, 4096, 0),
+                                            (300, 5120, 0), (64, 8192, 1)])
 def test_rmsnorm_bwd_from_splitk_parts(rows, cols, mode):
     """dy given as two f32 split-K halves (pt_rmsnorm_bwd_splitk) == their bf16 sum pass followed
     by the plain backward, bit for bit (dx with the residual gradient, dweight)."""
@@ -66,9 +69,10 @@ def test_rmsnorm_bwd_from_splitk_parts(rows, cols, mode):
     assert torch.equal(dx1, dx2) and torch.equal(dw1, dw2)
 
 
-def test_rmsnorm_fused_residual():
+@pytest.mark.parametrize("cols", [2048, 8192])
+def test_rmsnorm_fused_residual(cols):
     from picotron_amd import kernels as K
-    rows, cols = 256, 2048
+    rows = 256
     x, r = torch.randn(rows, cols).to(BF), torch.randn(rows, cols).to(BF)
     w = torch.ones(cols).to(BF)
     y, rstd, z = K.rmsnorm_fwd(x.to(DEV), w.to(DEV), 1e-5, 0, residual=r.to(DEV))

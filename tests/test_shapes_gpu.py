@@ -175,6 +175,12 @@ def test_smollm_1_7b_tp8_shard_layer():
     _layer_parity(B=4, S=1024, H=2048, I=8192 // 8, nh=4, nkv=4, d=64, seed=5)
 
 
+def test_llama2_13b_layer():
+    """Llama-2-13B's layer dims (H 5120: the wide-row RMSNorm kernels; I 13824, 40 heads of 128) at
+    mbs 1 x seq 512."""
+    _layer_parity(B=1, S=512, H=5120, I=13824, nh=40, nkv=40, d=128, seed=13)
+
+
 def test_llama2_7b_tp8_shard_layer():
     """Llama-2-7B at TP 8: 4 heads of 128 and an intermediate shard of 1376, off the GEMM tiles'
     64-grid -- the gate|up / down projections on the padded GEMMs (kernels._linear_*_padded)."""
