@@ -1226,6 +1226,15 @@ class CrossEntropyFunction(torch.autograd.Function):
         lg = _contig2d(logits)
         tg = targets.reshape(-1)
         stats = _take_ce_stats(lg)   # the lm_head GEMM's statistics of exactly these logits, if any
+        V = lg.shape[1]
+        if V % 8:
+            # the CE kernels stream 16-byte row chunks: a vocabulary off the 8-column grid (50257,
+            # 32001) is padded with -inf columns -- exp(-inf - max) = 0 adds nothing to any row's sum;
+            # their gradient columns are sliced off in the backward
+            lgp = torch.full((lg.shape[0], (V + 7) // 8 * 8), float("-inf"), dtype=lg.dtype, device=lg.device)
+            lgp[:, :V] = lg
+            lg, stats = lgp, None
+        ctx.vocab = V
         odt = logits.dtype if logits.dtype in (torch.bfloat16, torch.float32) else torch.float32
         if stats is not None:
             loss, inv_count, row_lse = K.cross_entropy_loss_lse_stats(lg, tg, stats, ignore_index, out_dtype=odt,
@@ -1247,7 +1256,9 @@ class CrossEntropyFunction(torch.autograd.Function):
         else:
             scale = g.float().reshape(1) * inv[0]
         dl = K.cross_entropy_grad_lse(lg, tg, row_lse, scale, ctx.ignore_index)
-        return dl.view(ctx.shape), None, None, None
+        if dl.shape[1] != ctx.vocab:
+            dl = dl[:, :ctx.vocab]
+        return dl.reshape(ctx.shape), None, None, None
 
 
 def _plain(t):

@@ -169,6 +169,52 @@ def test_cross_entropy_function_matches_torch():
     assert lg.grad[3].float().abs().max().item() == 0.0
 
 
+@pytest.mark.parametrize("reduction", ["mean", "sum", "none"])
+def test_cross_entropy_vocab_off_8_columns(reduction):
+    """A vocabulary off the CE kernels' 8-column grid (GPT-2's 50257): the logits padded with -inf
+    columns (nothing added to any row's softmax), the gradient's padded columns dropped -- loss and
+    dlogits against torch, with an ignored row."""
+    from picotron_amd import functional as FN
+    T, V = 128, 50257
+    logits = (2 * torch.randn(T, V)).to(BF)
+    tgt = torch.randint(0, V, (T,))
+    tgt[7] = -100
+    lg = logits.cuda().requires_grad_(True)
+    out = FN.cross_entropy(lg, tgt.cuda(), reduction=reduction)
+    lr = logits.float().requires_grad_(True)
+    ref = F.cross_entropy(lr, tgt, reduction=reduction)
+    g = torch.randn(ref.shape) if reduction == "none" else torch.tensor(0.25)
+    out.backward(g.to(out.dtype).cuda())
+    ref.backward(g)
+    assert rel(out.float(), ref) < 1e-2
+    assert lg.grad.shape == (T, V) and rel(lg.grad, lr.grad) < TOL
+
+
+def test_llama_vocab_off_8_columns(monkeypatch):
+    """The full model at vocab 1001: the lm_head GEMM padded (off the 64-grid), the CE padded (off
+    the 8-column grid) -- loss and every gradient against the oracle."""
+    monkeypatch.setenv("FLASH_ATTEN", "1")
+    from picotron_amd import functional as FN
+    from picotron_amd.model import Llama
+    cfg = cfg_tiny(layers=1, V=1001)
+    with torch.device("cuda"):
+        model = Llama(cfg)
+    model.to(BF)
+    g = torch.Generator().manual_seed(4)
+    ids = torch.randint(0, cfg.vocab_size, (2, 129), generator=g)
+    logits = model(ids[:, :-1].cuda())
+    loss = FN.cross_entropy(logits.view(-1, cfg.vocab_size), ids[:, 1:].reshape(-1).cuda())
+    loss.backward()
+    p = _params_f32(model)
+    cos, sin = O.get_cos_sin(128, 64, base=10000.0)
+    lr = O.llama_forward(ids[:, :-1], p, dict(vars(cfg)), cos.float(), sin.float(), norm=O.rmsnorm_flash_semantics)
+    loss_r = F.cross_entropy(lr.reshape(-1, cfg.vocab_size), ids[:, 1:].reshape(-1))
+    loss_r.backward()
+    assert abs(loss.float().item() - loss_r.item()) < TOL * abs(loss_r.item())
+    for n, q in model.named_parameters():
+        assert rel(q.grad, p[n].grad) < TOL, n
+
+
 def test_residual_epilogue_exact():
     """GEMM residual epilogue == bf16(residual + bf16(x W^T)) bit for bit (torch's bf16 add)."""
     from picotron_amd import kernels as K
