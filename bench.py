@@ -46,7 +46,7 @@ if ROOT not in sys.path:
 
 # HBM bytes per GEMM launch from rocprofv3 PMC passes (tools/gpu.sh counters: bench.py --grad-acc 2, then
 # tools/traffic_summary.py); read for the roofline's `traffic`
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r06", "gemm_traffic_r06j.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r06", "gemm_traffic_r06pm.json")
 
 
 def log(*a):
